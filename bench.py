@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ICA-LSTM dSGD training throughput, one site per GPU.
+
+BASELINE.json metric: "samples/sec/site ICA-LSTM dSGD at 1/2/4/8 sites".  Config = the
+reference's ICA single-site runner (``comps/icalstm/site_run.py:6-8``: batch_size 32) on the
+inputspec geometry (``datasets/icalstm/inputspec.json``: C=100 components, T=980, W=10 -> S=98
+windows) with the compspec hidden size 384 (``compspec.json:251-281``), input_size 256.  Each
+timed step is a complete training step: fused encoder GEMM, persistent bi-LSTM forward,
+classifier + softmax-CE, full backward, dSGD all-reduce (RCCL over xGMI for N>1), fused Adam.
+Synthetic data (the ICA dataset is not shipped, ``.gitignore:123``) and random-init weights.
+
+Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
+--master-addr 127.0.0.1 bench.py --gpus N``.  Rank 0 prints ONE JSON line; ``value`` is the
+whole-job aggregate (samples/s summed over all sites), ``per_site`` the per-GPU rate.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+# reference CPU throughput of the same step (172.7 samples/s, B=32, H=384)
+BASELINE_SAMPLES_PER_SEC_PER_SITE = 172.7
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=32, help="per-site batch (reference site_run: 32)")
+    ap.add_argument("--engine", default="dSGD", choices=["dSGD", "rankDAD", "powerSGD"])
+    ap.add_argument("--hidden", type=int, default=384)
+    ap.add_argument("--input-size", type=int, default=256)
+    ap.add_argument("--comps", type=int, default=100)
+    ap.add_argument("--window", type=int, default=10)
+    ap.add_argument("--temporal", type=int, default=980)
+    ap.add_argument("--precision-bits", default="32", choices=["16", "32"])
+    ap.add_argument("--graph", type=int, default=1, help="capture fwd+bwd(+opt) in a HIP graph")
+    ap.add_argument("--pool", type=int, default=8, help="distinct synthetic batches resident in HBM")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from dinunet_implementations_amd.parallel import init_sites, make_engine
+    from dinunet_implementations_amd.runtime.step import TrainStep
+    from dinunet_implementations_amd.models import ICALstm
+    from dinunet_implementations_amd.ops import FlatParams, FusedAdam
+
+    grp = init_sites()
+    dev = grp.device
+    if dev.type != "cuda":
+        print("bench.py needs a GPU", file=sys.stderr)
+        return 2
+    torch.manual_seed(1234)
+    S = args.temporal // args.window
+    model = ICALstm(input_size=args.input_size, hidden_size=args.hidden, num_comps=args.comps,
+                    window_size=args.window, num_cls=2).to(dev).train()
+    flat = FlatParams(model.parameters())
+    grp.broadcast(flat.data, 0)
+    opt = FusedAdam(flat, lr=1e-3)
+    cfg = {"precision_bits": args.precision_bits, "seed": 0}
+    engine = make_engine(args.engine, model, flat, grp, cfg)
+    step = TrainStep(model, flat, opt, engine, task="ica", use_graph=bool(args.graph))
+
+    g = torch.Generator(device=dev).manual_seed(100 + grp.rank)
+    xs = torch.randn(args.pool, args.batch, S, args.comps, args.window, device=dev, generator=g)
+    ys = torch.randint(0, 2, (args.pool, args.batch), device=dev, generator=g)
+
+    for i in range(args.warmup):
+        step(xs[i % args.pool], ys[i % args.pool])
+    torch.cuda.synchronize()
+    grp.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(xs[i % args.pool], ys[i % args.pool])
+    torch.cuda.synchronize()
+    grp.barrier()
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    grp.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
+    dt = float(dt.item())
+    loss = float(step.last_loss)
+    n = grp.world
+    total = n * args.batch * args.steps / dt
+    if grp.is_master:
+        rec = {
+            "metric": "ICA-LSTM dSGD training samples/sec (sum over sites)",
+            "value": round(total, 2),
+            "unit": "samples/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * dt / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round((total / n) / BASELINE_SAMPLES_PER_SEC_PER_SITE, 2),
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"model": f"ICA-LSTM (C={args.comps}, W={args.window}, S={S}, "
+                                f"I={args.input_size}, H={args.hidden}, bi-dir)",
+                       "global_batch": args.batch * n, "seq_len": S,
+                       "parallelism": f"dp{n}", "engine": args.engine,
+                       "precision_bits": args.precision_bits, "hip_graph": bool(args.graph)},
+            "per_site": round(total / n, 2),
+            "baseline_metric": "samples/sec/site ICA-LSTM dSGD (BASELINE.json)",
+            "baseline_note": "vs_baseline = per-site samples/s / 172.7 (reference step, B=32, "
+                             "measured on CPU in BASELINE.md; no published GPU number)",
+            "final_loss": round(loss, 5),
+        }
+        print(json.dumps(rec), flush=True)
+    from dinunet_implementations_amd.parallel import shutdown
+    shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,129 @@
+"""Build the gfx950 kernel library in-tree.
+
+Every ``csrc/kernels/*.hip`` file is compiled with ``hipcc --offload-arch=gfx950`` and linked
+into ONE shared object, ``dinunet_implementations_amd/_native/libdinunet_kernels.so``, exposing a
+plain C ABI (raw device pointers + ``hipStream_t``).  Python binds it with ``ctypes`` *after*
+``import torch``, so the library resolves ``libamdhip64.so.7`` to the runtime torch already
+loaded: one HIP runtime, one set of streams, graph capture works.
+
+The host-side runtime pieces (``csrc/host/*.cpp``: data preprocessing, metric kernels for the
+CPU) are compiled into ``libdinunet_host.so`` with the system C++ compiler.
+
+Usage: ``python -m dinunet_implementations_amd.csrc.build [--force] [--jobs N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+OUT_DIR = os.path.join(PKG, "_native")
+KERNEL_LIB = os.path.join(OUT_DIR, "libdinunet_kernels.so")
+HOST_LIB = os.path.join(OUT_DIR, "libdinunet_host.so")
+ARCH = os.environ.get("DINUNET_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", shutil.which("g++") or "c++")
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
+             "-munsafe-fp-atomics", "-Wno-unused-result"]
+
+
+def _sources(kind: str):
+    if kind == "hip":
+        return sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip")))
+    return sorted(glob.glob(os.path.join(HERE, "host", "*.cpp")))
+
+
+def _digest(paths, extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    deps = set(paths)
+    for d in ("kernels", "host"):
+        deps.update(glob.glob(os.path.join(HERE, d, "*.h")))
+    for p in sorted(deps):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stamp_ok(lib: str, digest: str) -> bool:
+    stamp = lib + ".sha256"
+    return os.path.exists(lib) and os.path.exists(stamp) and open(stamp).read().strip() == digest
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stderr[-6000:]}")
+    return r
+
+
+def build_kernels(force: bool = False, jobs: int = 4, verbose: bool = True) -> str:
+    srcs = _sources("hip")
+    os.makedirs(OUT_DIR, exist_ok=True)
+    digest = _digest(srcs, " ".join(HIP_FLAGS) + ARCH)
+    if not force and _stamp_ok(KERNEL_LIB, digest):
+        return KERNEL_LIB
+    objdir = os.path.join(OUT_DIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        _run([HIPCC, *HIP_FLAGS, "-I", os.path.join(HERE, "kernels"), "-c", src, "-o", obj])
+        if verbose:
+            print(f"[build] {os.path.relpath(src, PKG)}", flush=True)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = KERNEL_LIB + ".tmp"
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
+    os.replace(tmp, KERNEL_LIB)
+    with open(KERNEL_LIB + ".sha256", "w") as f:
+        f.write(digest)
+    return KERNEL_LIB
+
+
+def build_host(force: bool = False, verbose: bool = True) -> str:
+    srcs = _sources("cpp")
+    if not srcs:
+        return ""
+    os.makedirs(OUT_DIR, exist_ok=True)
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp"]
+    digest = _digest(srcs, " ".join(flags))
+    if not force and _stamp_ok(HOST_LIB, digest):
+        return HOST_LIB
+    tmp = HOST_LIB + ".tmp"
+    _run([CXX, *flags, "-I", os.path.join(HERE, "host"), *srcs, "-o", tmp])
+    os.replace(tmp, HOST_LIB)
+    with open(HOST_LIB + ".sha256", "w") as f:
+        f.write(digest)
+    if verbose:
+        print(f"[build] host runtime -> {os.path.relpath(HOST_LIB, PKG)}", flush=True)
+    return HOST_LIB
+
+
+def build_all(force: bool = False, jobs: int = 4, verbose: bool = True):
+    return build_kernels(force, jobs, verbose), build_host(force, verbose)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args(argv)
+    k, h = build_all(a.force, a.jobs)
+    print(k)
+    if h:
+        print(h)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

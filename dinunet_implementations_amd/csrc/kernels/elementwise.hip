@@ -1,0 +1,83 @@
+// Small fused memory-bound kernels (vectorised 16 B per lane, deterministic reductions).
+#include "common.h"
+
+namespace {
+
+constexpr int RB_SLABS = 64;  // row slabs for column reductions (>= 64 workgroups in flight)
+
+// dym = dy * (y > 0) and per-slab column sums of dym.  y = ReLU output, all bf16 [N][O].
+// block = 256 threads = 8 rows x 32 column-groups of 8 (16 B vectors); grid = (col strips, slabs)
+__global__ void __launch_bounds__(256)
+relu_bwd_colsum_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                       bf16* __restrict__ dym, float* __restrict__ part, int N, int O) {
+  const int cg = blockIdx.x * 32 + (threadIdx.x & 31);  // column group
+  const int rl = threadIdx.x >> 5;                       // 0..7
+  const int c0 = cg * 8;
+  const int rows_per = (N + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool vec = (O & 7) == 0 && c0 + 8 <= O;
+  for (int r = r0 + rl; r < r1; r += 8) {
+    const long i = (long)r * O + c0;
+    if (vec) {
+      const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + i);
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(y + i);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = (float)a[e] > 0.f ? g[e] : (bf16)0.f;
+        s[e] += (float)o[e];
+      }
+      *reinterpret_cast<bf16x8*>(dym + i) = o;
+    } else {
+      for (int e = 0; e < 8 && c0 + e < O; ++e) {
+        const bf16 o = (float)y[i + e] > 0.f ? dy[i + e] : (bf16)0.f;
+        dym[i + e] = o;
+        s[e] += (float)o;
+      }
+    }
+  }
+  __shared__ float red[8][32 * 8 + 4];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][(threadIdx.x & 31) * 8 + e] = s[e];
+  __syncthreads();
+  // 256 threads: each finalises one column of this strip
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col < O) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) t += red[r][threadIdx.x];
+    part[(long)blockIdx.y * O + col] = t;
+  }
+}
+
+// out[c] = sum_s part[s][c]  (fixed order -> bit-reproducible)
+__global__ void colsum_slabs_kernel(const float* __restrict__ part, int slabs, int O,
+                                    float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= O) return;
+  // 8 independent partial chains: the slab loads are issued back to back
+  float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= slabs; s += 8)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] += part[(long)(s + k) * O + c];
+  for (; s < slabs; ++s) t[0] += part[(long)s * O + c];
+  const float v = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+  out[c] = accumulate ? out[c] + v : v;
+}
+
+}  // namespace
+
+DN_API long dn_relu_bwd_colsum_workspace(int N, int O) { return (long)RB_SLABS * O; }
+
+DN_API int dn_relu_bwd_colsum(const void* dy, const void* y, void* dym, float* db, float* ws,
+                              int N, int O, int accumulate, hipStream_t st) {
+  if (N <= 0 || O <= 0) return DN_BAD_SHAPE;
+  const int slabs = N < RB_SLABS ? N : RB_SLABS;
+  hipLaunchKernelGGL(relu_bwd_colsum_kernel, dim3((O + 255) / 256, slabs), dim3(256), 0, st,
+                     (const bf16*)dy, (const bf16*)y, (bf16*)dym, ws, N, O);
+  hipLaunchKernelGGL(colsum_slabs_kernel, dim3((O + 255) / 256), dim3(256), 0, st, ws, slabs, O, db,
+                     accumulate);
+  return dn_launch_status();
+}

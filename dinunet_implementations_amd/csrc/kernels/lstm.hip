@@ -1,0 +1,511 @@
+// Persistent bidirectional LSTM recurrence for gfx950 (MI355X).
+//
+// Replaces the reference's per-time-step Python loop (comps/icalstm/models.py:30-41, ~12 kernel
+// launches per step and direction) with ONE launch per pass:
+//
+//   grid  = (ceil(B/16) batch chunks, ndir directions)        -> independent workgroups
+//   block = HD/16 waves; wave w owns hidden units [16w, 16w+16)
+//
+// * The recurrent weights W_hh of a direction (4*HD x HD bf16, 295 KB at HD=192) stay RESIDENT in
+//   VGPRs for all S steps as MFMA A-fragments (96 VGPRs per lane at HD=192, 12 waves): nothing is
+//   re-read from L2 inside the time loop.
+// * Gate rows are permuted to m = 4*u + g (g = i,f,o,g) so one 16x16x32 MFMA output tile holds,
+//   per lane, all four gate pre-activations of ONE (unit, batch-row): the cell update is entirely
+//   lane-local, no shuffles, no LDS round trip for gates.
+// * h_t (bf16) is exchanged between waves through a double-buffered, bank-conflict-free LDS tile:
+//   exactly one workgroup barrier per time step.
+// * The input projection x_t W_ih^T (time-parallel) is hoisted into one large GEMM before the
+//   kernel; its per-step loads are issued before the step's MFMAs so their latency hides under
+//   the recurrent GEMM.
+// * Reference numerics: i,f,o = sigmoid(sigmoid(pre)), g = tanh(pre),
+//   reverse direction consumes x[S-1-t]; its outputs stay in processing order.
+//
+// The backward kernel runs the reverse-time recurrence dh_{t-1} = W_hh^T dpre_t with W_hh^T
+// resident the same way (one unit-quad per lane), recomputes the gates from the saved
+// pre-activations, and writes dpre (bf16, original time order) for the weight-gradient GEMMs
+// dW_ih = dpre^T x, dW_hh = dpre^T h_{t-1} that run after it on the full chip.
+#include "common.h"
+
+namespace {
+
+template <typename XT> struct Gate4Raw;
+template <> struct Gate4Raw<float> { typedef f32x4 type; };
+template <> struct Gate4Raw<bf16> { typedef bf16x4 type; };
+
+// raw (unconverted) 4-gate load: keeps bf16 inputs packed in 2 VGPRs across the MFMA phase
+template <typename XT>
+__device__ __forceinline__ typename Gate4Raw<XT>::type load_raw4(const XT* p, bool ok) {
+  typedef typename Gate4Raw<XT>::type R;
+  if (ok) return *reinterpret_cast<const R*>(p);
+  R z;
+  z[0] = z[1] = z[2] = z[3] = (XT)0.f;
+  return z;
+}
+
+__device__ __forceinline__ void load_gate4(const float* p, bool ok, float (&v)[4]) {
+  f32x4 x = load_raw4<float>(p, ok);
+  v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------------
+// m-tiles (of 4 per wave) whose W fragments live in LDS instead of VGPRs (fwd), and k-steps
+// (of 4*HD/32) of W^T kept in LDS (bwd): sized so HD=192 fits 168 VGPRs (3 waves/SIMD) spill-free.
+template <int HD> struct LdsSplit { static constexpr int FWD_MT = 0, BWD_KS = 0; };
+template <> struct LdsSplit<192> { static constexpr int FWD_MT = 1, BWD_KS = 9; };
+
+// All per-step global traffic is UNCONDITIONAL (internal buffers are padded to Bp = 16*chunks
+// rows and HD units; loads of padded batch rows are clamped to row B-1): no divergent branches
+// around memory ops, so hipcc emits counted s_waitcnt vmcnt(N) and a step never waits for the
+// previous step's stores.  The x-projection of step t+1 is issued before step t's MFMAs.
+template <int HD, bool SEQ>
+__global__ void __launch_bounds__(HD / 16 * 64)
+lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted cols, no bias
+                const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
+                const bf16* __restrict__ whh,    // [ndir][4*HD][HD] permuted rows, zero padded
+                int B, int S, int Hd, int ndir,
+                float* __restrict__ c_save,      // [ndir][Bp][S][HD]   c_t at original time idx
+                bf16* __restrict__ hprev,        // [ndir][Bp][S][HD]   h_{t-1} at original time idx
+                float* __restrict__ hseq,        // SEQ: [Bp][S][ndir*HD] (processing order)
+                float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
+                float* __restrict__ hT, float* __restrict__ cT) {  // [B][ndir*Hd]
+  constexpr int NT = HD / 16 * 64;
+  constexpr int KS = HD / 32;
+  constexpr int LDH = HD + 8;  // +16 B per row: the 16 rows land on distinct bank quads
+  constexpr int NLM = LdsSplit<HD>::FWD_MT, NRM = 4 - NLM;
+  constexpr int NW = HD / 16;
+  __shared__ __attribute__((aligned(16))) bf16 hbuf[2][16][LDH];
+  __shared__ __attribute__((aligned(16))) float bias_s[4 * HD];
+  // lane-linear fragment image: one 1 KiB row per (wave, m-tile, k-step) -> conflict-free b128
+  __shared__ __attribute__((aligned(16))) bf16x8 wlds[NW][NLM > 0 ? NLM : 1][KS][64];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q = lane >> 4, bl = lane & 15;
+  const int dir = blockIdx.y;
+  const int Bp = gridDim.x * 16;
+  const int b = blockIdx.x * 16 + bl;          // padded row (always < Bp)
+  const int bc = b < B ? b : B - 1;             // clamped row for loads
+  const long rowX = (long)ndir * 4 * HD;
+
+  bf16x8 wf[NRM][KS];
+  {
+    const bf16* wd = whh + (long)dir * 4 * HD * HD;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int row = 16 * (4 * w + mt) + bl;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(wd + (long)row * HD + 32 * ks + 8 * q);
+        if (mt < NRM) wf[mt < NRM ? mt : 0][ks] = v;
+        else wlds[w][mt - NRM][ks][lane] = v;
+      }
+  }
+  for (int i = tid; i < 4 * HD; i += NT) bias_s[i] = bias[dir * 4 * HD + i];
+  for (int i = tid; i < 2 * 16 * LDH; i += NT) (&hbuf[0][0][0])[i] = (bf16)0.f;
+  __syncthreads();
+
+  const float* xrow = xp + (long)bc * S * rowX + (long)dir * 4 * HD + 4 * (16 * w + q);
+  const long hplane = (long)dir * Bp * S * HD;
+  // cooperative h_{t-1} copy: thread -> 4 consecutive bf16 of the [16][HD] tile
+  const int cp_r = (tid * 4) / HD, cp_c = (tid * 4) % HD;
+  bf16* hcp = hprev + hplane + ((long)(blockIdx.x * 16 + cp_r) * S) * HD + cp_c;
+  float* csv = c_save + hplane + (long)b * S * HD + 16 * w + q;
+
+  float c[4] = {0.f, 0.f, 0.f, 0.f}, hs[4] = {0.f, 0.f, 0.f, 0.f}, hl[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 xn[4];
+  {
+    const int tau0 = dir == 0 ? 0 : S - 1;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) xn[mt] = *reinterpret_cast<const f32x4*>(xrow + (long)tau0 * rowX + 16 * mt);
+  }
+  int cur = 0;
+  for (int t = 0; t < S; ++t) {
+    const int tau = dir == 0 ? t : S - 1 - t;
+    const int t1 = t + 1 < S ? t + 1 : t;
+    const int tau1 = dir == 0 ? t1 : S - 1 - t1;
+    // h_{t-1} (the tile every wave reads below) -> global for the weight-gradient GEMMs
+    *reinterpret_cast<bf16x4*>(hcp + (long)tau * HD) = *reinterpret_cast<const bf16x4*>(&hbuf[cur][cp_r][cp_c]);
+    // recurrent GEMM  pre^T[m][b] = sum_k W[m][k] h[b][k]  (W resident)
+    f32x4 acc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][bl][32 * ks + 8 * q]);
+#pragma unroll
+      for (int mt = 0; mt < NRM; ++mt) acc[mt] = mfma16(wf[mt][ks], hb, acc[mt]);
+#pragma unroll
+      for (int mt = NRM; mt < 4; ++mt) acc[mt] = mfma16(wlds[w][mt - NRM][ks][lane], hb, acc[mt]);
+    }
+    // gates + cell update: lane-local (unit u = 16w + 4mt + q, row b), 4 gates in acc regs
+    const int nxt = cur ^ 1;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int u = 16 * w + 4 * mt + q;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(&bias_s[4 * u]);
+      const float p0 = acc[mt][0] + xn[mt][0] + bb[0];
+      const float p1 = acc[mt][1] + xn[mt][1] + bb[1];
+      const float p2 = acc[mt][2] + xn[mt][2] + bb[2];
+      const float p3 = acc[mt][3] + xn[mt][3] + bb[3];
+      // this m-tile's projection is consumed: issue step t+1's (hidden by its MFMA phase)
+      xn[mt] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 16 * mt);
+      const float gi = dn_sigmoid(dn_sigmoid(p0));
+      const float gf = dn_sigmoid(dn_sigmoid(p1));
+      const float go = dn_sigmoid(dn_sigmoid(p2));
+      const float gg = dn_tanh(p3);
+      c[mt] = gf * c[mt] + gi * gg;
+      const float h = go * dn_tanh(c[mt]);
+      csv[(long)tau * HD + 4 * mt] = c[mt];
+      if constexpr (SEQ) hseq[((long)b * S + t) * ndir * HD + dir * HD + u] = h;
+      hs[mt] += h;
+      hl[mt] = h;
+      hbuf[nxt][bl][u] = (bf16)h;
+    }
+    __syncthreads();
+    cur = nxt;
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int u = 16 * w + 4 * mt + q;
+    if (b < B && u < Hd) {
+      const long o = (long)b * ndir * Hd + dir * Hd + u;
+      if (hmean) hmean[o] = hs[mt] * mean_scale;
+      if (hT) hT[o] = hl[mt];
+      if (cT) cT[o] = c[mt];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward (reverse-time recurrence)
+// ---------------------------------------------------------------------------------------------
+// pre: the gate pre-activations, recomputed time-parallel after the forward by one GEMM
+// (pre = x W_ih^T + h_{t-1} W_hh^T + b) instead of being stored per step by the forward kernel.
+template <int HD, bool DSEQ>
+__global__ void __launch_bounds__(HD / 16 * 64)
+lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time order
+                const float* __restrict__ c_save,  // [ndir][Bp][S][HD]
+                const bf16* __restrict__ whhT,     // [ndir][HD][4*HD]
+                const float* __restrict__ dh_ext, long dh_sb, long dh_st, float dh_scale,
+                const float* __restrict__ dhT, const float* __restrict__ dcT,  // optional [B][ndir*Hd]
+                int B, int S, int Hd, int ndir,
+                bf16* __restrict__ dpre) {          // [Bp*S][ndir][4*HD] permuted, original time
+  constexpr int KS = 4 * HD / 32;
+  constexpr int LDD = 4 * HD + 8;
+  constexpr int NLK = LdsSplit<HD>::BWD_KS, NRK = KS - NLK;
+  constexpr int NW = HD / 16;
+  constexpr int NT = NW * 64;
+  __shared__ __attribute__((aligned(16))) bf16 dbuf[2][16][LDD];
+  __shared__ __attribute__((aligned(16))) bf16x8 wlds[NW][NLK > 0 ? NLK : 1][64];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q = lane >> 4, bl = lane & 15;
+  const int dir = blockIdx.y;
+  const int Bp = gridDim.x * 16;
+  const int b = blockIdx.x * 16 + bl;
+  const bool vb = b < B;
+  const int bc = vb ? b : B - 1;
+  const long rowX = (long)ndir * 4 * HD;
+
+  bf16x8 af[NRK];
+  {
+    const bf16* wt = whhT + (long)dir * HD * 4 * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 v =
+          *reinterpret_cast<const bf16x8*>(wt + (long)(16 * w + bl) * 4 * HD + 32 * ks + 8 * q);
+      if (ks < NRK) af[ks < NRK ? ks : 0] = v;
+      else wlds[w][ks - NRK][lane] = v;
+    }
+  }
+  for (int i = tid; i < 2 * 16 * LDD; i += NT) (&dbuf[0][0][0])[i] = (bf16)0.f;
+
+  const int u0 = 16 * w + 4 * q;  // this lane's 4 consecutive units u0..u0+3
+  const float* prow = pre + (long)bc * S * rowX + (long)dir * 4 * HD + 4 * u0;
+  const float* crow = c_save + (long)dir * Bp * S * HD + (long)b * S * HD + u0;
+  bf16* drow = dpre + (long)b * S * rowX + (long)dir * 4 * HD + 4 * u0;
+  // external grads: lanes of padded rows / units read a clamped address and are zeroed
+  float msk[4], dhx[4], dcc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int u = u0 + j;
+    msk[j] = (vb && u < Hd) ? 1.f : 0.f;
+    const long eo = (long)bc * dh_sb + dir * Hd + (u < Hd ? u : Hd - 1);
+    dhx[j] = DSEQ ? 0.f : dh_ext[eo] * dh_scale * msk[j];
+    const long fo = (long)bc * ndir * Hd + dir * Hd + (u < Hd ? u : Hd - 1);
+    dcc[j] = dcT ? dcT[fo] * msk[j] : 0.f;
+  }
+  const float* dhrow = dh_ext + (long)bc * dh_sb + dir * Hd;
+  // state of step t (processing order) and prefetch of step t-1
+  const int tauL = dir == 0 ? S - 1 : 0;
+  f32x4 cc = *reinterpret_cast<const f32x4*>(crow + (long)tauL * HD);
+  f32x4 pn[4], cpn;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pn[j] = *reinterpret_cast<const f32x4*>(prow + (long)tauL * rowX + 4 * j);
+  {
+    const int tp = S >= 2 ? S - 2 : 0;
+    const int taup = dir == 0 ? tp : S - 1 - tp;
+    cpn = *reinterpret_cast<const f32x4*>(crow + (long)taup * HD);
+  }
+  __syncthreads();
+
+  int cur = 0;
+  for (int t = S - 1; t >= 0; --t) {
+    const int tau = dir == 0 ? t : S - 1 - t;
+    f32x4 pc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pc[j] = pn[j];
+    f32x4 cp = t > 0 ? cpn : f32x4{0.f, 0.f, 0.f, 0.f};
+    {  // prefetch step t-1 (pre) and t-2 (c_{t-2} = c_prev of step t-1), clamped at 0
+      const int t1 = t > 0 ? t - 1 : 0;
+      const int tau1 = dir == 0 ? t1 : S - 1 - t1;
+      const int t2 = t > 1 ? t - 2 : 0;
+      const int tau2 = dir == 0 ? t2 : S - 1 - t2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pn[j] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * j);
+      cpn = *reinterpret_cast<const f32x4*>(crow + (long)tau2 * HD);
+    }
+    float dx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dx[j] = dhx[j];
+    if constexpr (DSEQ) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = u0 + j < Hd ? u0 + j : Hd - 1;
+        dx[j] = dhrow[(long)t * dh_st + u] * dh_scale * msk[j];
+      }
+    }
+    if (t == S - 1 && dhT) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = u0 + j;
+        dx[j] += dhT[(long)bc * ndir * Hd + dir * Hd + (u < Hd ? u : Hd - 1)] * msk[j];
+      }
+    }
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][bl][32 * ks + 8 * q]);
+      acc = mfma16(ks < NRK ? af[ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db, acc);
+    }
+    const int nxt = cur ^ 1;
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float si = dn_sigmoid(pc[j][0]), sf = dn_sigmoid(pc[j][1]), so = dn_sigmoid(pc[j][2]);
+      const float gi = dn_sigmoid(si), gf = dn_sigmoid(sf), go = dn_sigmoid(so);
+      const float gg = dn_tanh(pc[j][3]);
+      const float tc = dn_tanh(cc[j]);
+      const float dh = acc[j] + dx[j];
+      const float dc = dcc[j] + dh * go * (1.f - tc * tc);
+      const float d_o = dh * tc;
+      const float d_i = dc * gg, d_g = dc * gi, d_f = dc * cp[j];
+      dcc[j] = dc * gf * msk[j];
+      const float m = msk[j];
+      const bf16 e0 = (bf16)(m * d_i * gi * (1.f - gi) * si * (1.f - si));
+      const bf16 e1 = (bf16)(m * d_f * gf * (1.f - gf) * sf * (1.f - sf));
+      const bf16 e2 = (bf16)(m * d_o * go * (1.f - go) * so * (1.f - so));
+      const bf16 e3 = (bf16)(m * d_g * (1.f - gg * gg));
+      if (j < 2) { lo[4 * j] = e0; lo[4 * j + 1] = e1; lo[4 * j + 2] = e2; lo[4 * j + 3] = e3; }
+      else { hi[4 * j - 8] = e0; hi[4 * j - 7] = e1; hi[4 * j - 6] = e2; hi[4 * j - 5] = e3; }
+    }
+    cc = cp;
+    // gate cols of this lane's 4 units are contiguous: 4*u0 .. 4*u0+15
+    *reinterpret_cast<bf16x8*>(&dbuf[nxt][bl][4 * u0]) = lo;
+    *reinterpret_cast<bf16x8*>(&dbuf[nxt][bl][4 * u0 + 8]) = hi;
+    *reinterpret_cast<bf16x8*>(drow + (long)tau * rowX) = lo;
+    *reinterpret_cast<bf16x8*>(drow + (long)tau * rowX + 8) = hi;
+    __syncthreads();
+    cur = nxt;
+  }
+}
+
+// deterministic column sums of a bf16 [N][C] matrix into slab partials [slabs][C] (fp32)
+__global__ void __launch_bounds__(256)
+colsum_bf16_kernel(const bf16* __restrict__ x, int N, int C, float* __restrict__ part) {
+  const int cg = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rl = threadIdx.x >> 5;
+  const int c0 = cg * 8;
+  const int rows_per = (N + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 + 8 <= C) {
+    for (int r = r0 + rl; r < r1; r += 8) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (long)r * C + c0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
+    }
+  }
+  __shared__ float red[8][32 * 8 + 4];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][(threadIdx.x & 31) * 8 + e] = s[e];
+  __syncthreads();
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) t += red[r][threadIdx.x];
+    part[(long)blockIdx.y * C + col] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight pack: reference layout ([i|f|o|g] rows, fp32) -> kernel layouts (bf16, m = 4u+g,
+// units zero-padded to HD)
+// ---------------------------------------------------------------------------------------------
+struct LstmParams {
+  const float* wih[2];
+  const float* bih[2];
+  const float* whh[2];
+  const float* bhh[2];
+};
+
+__global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
+                                 bf16* __restrict__ wih_p,    // [ndir*4HD][I]
+                                 float* __restrict__ bias_p,  // [ndir*4HD]
+                                 bf16* __restrict__ whh_p,    // [ndir][4HD][HD]
+                                 bf16* __restrict__ whhT_p) { // [ndir][HD][4HD]
+  const long GP = 4L * HD;
+  const long n_wih = ndir * GP * I, n_b = ndir * GP, n_whh = ndir * GP * HD;
+  const long total = n_wih + n_b + 2 * n_whh;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    if (idx < n_wih) {
+      const long k = idx % I, r = idx / I;
+      const int d = (int)(r / GP), m = (int)(r % GP), u = m >> 2, g = m & 3;
+      wih_p[idx] = (bf16)(u < Hd ? p.wih[d][((long)g * Hd + u) * I + k] : 0.f);
+    } else if (idx < n_wih + n_b) {
+      const long r = idx - n_wih;
+      const int d = (int)(r / GP), m = (int)(r % GP), u = m >> 2, g = m & 3;
+      float v = 0.f;
+      if (u < Hd) {
+        if (p.bih[d]) v += p.bih[d][g * Hd + u];
+        if (p.bhh[d]) v += p.bhh[d][g * Hd + u];
+      }
+      bias_p[r] = v;
+    } else if (idx < n_wih + n_b + n_whh) {
+      const long r = idx - n_wih - n_b;  // [d][m][k]
+      const int k = (int)(r % HD);
+      const long dm = r / HD;
+      const int d = (int)(dm / GP), m = (int)(dm % GP), u = m >> 2, g = m & 3;
+      whh_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][((long)g * Hd + u) * Hd + k] : 0.f);
+    } else {
+      const long r = idx - n_wih - n_b - n_whh;  // [d][k][m]
+      const int m = (int)(r % GP);
+      const long dk = r / GP;
+      const int d = (int)(dk / HD), k = (int)(dk % HD), u = m >> 2, g = m & 3;
+      whhT_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][((long)g * Hd + u) * Hd + k] : 0.f);
+    }
+  }
+}
+
+// bias grads: sum the column-sum slabs of dpre and ACCUMULATE into b_ih and b_hh (same grad)
+__global__ void lstm_bias_grad_kernel(const float* __restrict__ part, int slabs, int Hd, int HD,
+                                      int ndir, LstmParams out) {
+  const int G = 4 * Hd;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= ndir * G) return;
+  const int d = idx / G, r = idx % G, g = r / Hd, u = r % Hd;
+  const int col = d * 4 * HD + 4 * u + g;
+  float s = 0.f;
+  for (int k = 0; k < slabs; ++k) s += part[(long)k * ndir * 4 * HD + col];
+  if (out.bih[d]) const_cast<float*>(out.bih[d])[r] += s;
+  if (out.bhh[d]) const_cast<float*>(out.bhh[d])[r] += s;
+}
+
+template <int HD>
+int launch_fwd(const float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
+               float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
+               float* cT, hipStream_t st) {
+  dim3 grid((B + 15) / 16, ndir), block(HD / 16 * 64);
+  if (hseq)
+    hipLaunchKernelGGL((lstm_fwd_kernel<HD, true>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
+                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT);
+  else
+    hipLaunchKernelGGL((lstm_fwd_kernel<HD, false>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
+                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT);
+  return dn_launch_status();
+}
+
+template <int HD>
+int launch_bwd(const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
+               long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
+               int Hd, int ndir, bf16* dpre, hipStream_t st) {
+  dim3 grid((B + 15) / 16, ndir), block(HD / 16 * 64);
+  if (st_ != 0)
+    hipLaunchKernelGGL((lstm_bwd_kernel<HD, true>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
+                       sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
+  else
+    hipLaunchKernelGGL((lstm_bwd_kernel<HD, false>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
+                       sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
+  return dn_launch_status();
+}
+
+}  // namespace
+
+// padded per-direction hidden the kernels are instantiated for
+DN_API int dn_lstm_padded_hidden(int Hd) {
+  if (Hd <= 0) return 0;
+  if (Hd <= 64) return 64;
+  if (Hd <= 128) return 128;
+  if (Hd <= 192) return 192;
+  return 0;
+}
+
+DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0, const float* bhh0,
+                        const float* wih1, const float* bih1, const float* whh1, const float* bhh1,
+                        int I, int Hd, int ndir, void* wih_p, float* bias_p, void* whh_p,
+                        void* whhT_p, hipStream_t st) {
+  const int HD = dn_lstm_padded_hidden(Hd);
+  if (!HD || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
+  LstmParams p{{wih0, wih1}, {bih0, bih1}, {whh0, whh1}, {bhh0, bhh1}};
+  const long total = ndir * 4L * HD * I + ndir * 4L * HD + 2L * ndir * 4 * HD * HD;
+  const int blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+  hipLaunchKernelGGL(lstm_pack_kernel, dim3(blocks), dim3(256), 0, st, p, I, Hd, HD, ndir,
+                     (bf16*)wih_p, bias_p, (bf16*)whh_p, (bf16*)whhT_p);
+  return dn_launch_status();
+}
+
+DN_API int dn_lstm_fwd(const float* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
+                       int ndir, float* c_save, void* hprev, float* hseq, float* hmean,
+                       float mean_scale, float* hT, float* cT, hipStream_t st) {
+  const int HD = dn_lstm_padded_hidden(Hd);
+  if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
+  switch (HD) {
+    case 64: return launch_fwd<64>(xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
+    case 128: return launch_fwd<128>(xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
+    case 192: return launch_fwd<192>(xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
+  }
+  return DN_UNSUPPORTED;
+}
+
+DN_API int dn_lstm_bwd(const float* pre, const float* c_save, const void* whhT_p,
+                       const float* dh_ext, long dh_sb, long dh_st, float dh_scale,
+                       const float* dhT, const float* dcT, int B, int S, int Hd, int ndir,
+                       void* dpre, hipStream_t st) {
+  const int HD = dn_lstm_padded_hidden(Hd);
+  if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
+  switch (HD) {
+    case 64: return launch_bwd<64>(pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 128: return launch_bwd<128>(pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 192: return launch_bwd<192>(pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+  }
+  return DN_UNSUPPORTED;
+}
+
+// bias grads from dpre [N][ndir*4HD] bf16: slab column sums (ws: [64][ndir*4HD] fp32), then
+// accumulate into b_ih / b_hh of each direction (reference layout)
+DN_API int dn_lstm_bias_grad(const void* dpre, int N, int Hd, int ndir, float* ws, float* dbih0,
+                             float* dbhh0, float* dbih1, float* dbhh1, hipStream_t st) {
+  const int HD = dn_lstm_padded_hidden(Hd);
+  if (!HD || N <= 0) return DN_BAD_SHAPE;
+  const int C = ndir * 4 * HD;
+  const int slabs = N < 64 ? N : 64;
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((C + 255) / 256, slabs), dim3(256), 0, st,
+                     (const bf16*)dpre, N, C, ws);
+  LstmParams o{{nullptr, nullptr}, {dbih0, dbih1}, {nullptr, nullptr}, {dbhh0, dbhh1}};
+  hipLaunchKernelGGL(lstm_bias_grad_kernel, dim3((ndir * 4 * Hd + 255) / 256), dim3(256), 0, st,
+                     ws, slabs, Hd, HD, ndir, o);
+  return dn_launch_status();
+}

@@ -1,0 +1,60 @@
+"""HBM-resident batch loader.
+
+The reference iterates a torch ``DataLoader`` whose workers parse files and collate float64
+batches that are then copied host->device every step (``comps/fs/__init__.py:51``).  Here the
+split already sits in device memory as one ``[N, ...]`` tensor; an epoch is a device-side
+permutation and every batch is a single gather (or a contiguous slice when not shuffling).
+``drop_last`` follows ``dataloader_args`` (the reference sets it for train: ``local.py:29``,
+BatchNorm cannot take a 1-sample batch).
+"""
+from __future__ import annotations
+
+from typing import Iterator, Optional, Tuple
+
+import torch
+
+
+class DeviceLoader:
+    def __init__(self, inputs: torch.Tensor, labels: torch.Tensor, batch_size: int,
+                 shuffle: bool = False, drop_last: bool = False, seed: int = 0,
+                 index: Optional[torch.Tensor] = None):
+        self.inputs = inputs
+        self.labels = labels
+        self.index = index  # global sample ids (for logging predictions), same order as inputs
+        self.batch_size = max(1, int(batch_size))
+        self.shuffle = shuffle
+        self.drop_last = drop_last
+        self.epoch = 0
+        self.seed = seed
+        self._gen = torch.Generator(device="cpu")
+
+    def __len__(self):
+        n = self.inputs.shape[0]
+        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+
+    @property
+    def num_samples(self) -> int:
+        return int(self.inputs.shape[0])
+
+    def set_epoch(self, epoch: int):
+        self.epoch = epoch
+
+    def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+        n = self.inputs.shape[0]
+        dev = self.inputs.device
+        if self.shuffle:
+            self._gen.manual_seed(self.seed * 100003 + self.epoch)
+            perm = torch.randperm(n, generator=self._gen).to(dev, non_blocking=True)
+        else:
+            perm = None
+        self.epoch += 1
+        nb = len(self)
+        for b in range(nb):
+            s = b * self.batch_size
+            e = min(n, s + self.batch_size)
+            if perm is None:
+                ix = torch.arange(s, e, device=dev)
+                yield self.inputs[s:e], self.labels[s:e], ix
+            else:
+                ix = perm[s:e]
+                yield self.inputs.index_select(0, ix), self.labels.index_select(0, ix), ix

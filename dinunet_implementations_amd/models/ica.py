@@ -1,0 +1,132 @@
+"""ICA bi-LSTM classifier, reference ``comps/icalstm/models.py:5-110``.
+
+Module tree and ``state_dict`` keys are identical to the reference:
+``encoder.0.*``, ``lstm.lstms.{0,1}.{i2h,h2h}.*``, ``classifier.{1,2,4,6}.*`` (``classifier.2``
+is a BatchNorm1d *with* running stats).  Numerics follow the reference quirks (double sigmoid on
+i/f/o, per-direction hidden = hidden_size // 2, reverse outputs in processing order,
+``num_layers`` ignored: SURVEY.md A1-A4).
+
+Execution is MI355X-first: on a GPU the encoder runs as one ``[B*S, C*W] x [C*W, I]`` bf16 MFMA
+GEMM with a fused bias+ReLU epilogue (no per-sample Python loop, reference ``models.py:107``),
+the input projection of both directions is one GEMM hoisted out of the recurrence, and the
+recurrence of both directions runs in one persistent HIP kernel whose recurrent weights stay
+resident in VGPRs for all time steps (``ops.lstm``).  On CPU the module runs the reference math
+(``ops.reference``), which is also the test oracle.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..ops import reference as ref
+
+
+class LSTMCell(nn.Module):
+    """One LSTM direction built from two ``nn.Linear`` (``models.py:5-45``).
+
+    Keeping ``i2h``/``h2h`` as real Linear modules matters for rank-dAD: the engine sees every
+    Linear's inputs and output-gradients.
+    """
+
+    def __init__(self, input_size: int, hidden_size: int, bias: bool = True):
+        super().__init__()
+        self.input_size = input_size
+        self.hidden_size = hidden_size
+        self.bias = bias
+        self.i2h = nn.Linear(input_size, 4 * hidden_size, bias=bias)
+        self.h2h = nn.Linear(hidden_size, 4 * hidden_size, bias=bias)
+
+    def init_hidden(self, bz: int, device="cpu"):
+        return (torch.zeros(bz, self.hidden_size, device=device),
+                torch.zeros(bz, self.hidden_size, device=device))
+
+    def params(self):
+        return (self.i2h.weight, self.i2h.bias, self.h2h.weight, self.h2h.bias)
+
+    def forward(self, x: torch.Tensor, h=None):
+        return ref.lstm_cell_seq(x, *self.params(), h0=h)
+
+
+class LSTM(nn.Module):
+    """Bi-directional wrapper (``models.py:48-66``)."""
+
+    def __init__(self, input_size: int, hidden_size: int, bidirectional: bool = True,
+                 num_layers: int = 1, bias: bool = True):
+        super().__init__()
+        self.input_size = input_size
+        self.num_layers = num_layers  # stored, ignored (reference quirk A3)
+        self.bidirectional = bidirectional
+        self.num_direction = 2 if bidirectional else 1
+        self.hidden_size = hidden_size // self.num_direction
+        self.bias = bias
+        self.lstms = nn.ModuleList([LSTMCell(input_size, self.hidden_size, bias=bias)
+                                    for _ in range(self.num_direction)])
+        self.use_fused = True
+
+    def fused_ok(self, x: torch.Tensor) -> bool:
+        return (self.use_fused and x.is_cuda and self.bias
+                and ops.lstm_supported(x.shape[0], self.input_size, self.hidden_size,
+                                       self.num_direction))
+
+    def forward(self, x: torch.Tensor, h=None, reduce: str = "none"):
+        """``reduce='none'`` returns ``(hidden_seq [B,S,H*dirs], (h, c))`` like the reference;
+        ``reduce='mean'`` returns the temporal mean ``[B, H*dirs]`` instead of the sequence
+        (what ``ICALstm`` consumes) so the fused kernel never materialises the sequence."""
+        if h is None and self.fused_ok(x):
+            params = [cell.params() for cell in self.lstms]
+            return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms))
+        if h is not None:
+            hs, (h_t, c_t) = self.lstms[0](x, h)
+            if self.bidirectional:
+                rhs, (rh, rc) = self.lstms[1](torch.flip(x, (1,)), h)
+                hs = torch.cat([hs, rhs], 2)
+                h_t, c_t = torch.cat([h_t, rh], 1), torch.cat([c_t, rc], 1)
+        else:
+            hs, (h_t, c_t) = ref.bilstm(x, [c.params() for c in self.lstms], self.bidirectional,
+                                        modules=list(self.lstms))
+        if reduce == "mean":
+            return hs.mean(1), (h_t, c_t)
+        return hs, (h_t, c_t)
+
+
+class ICALstm(nn.Module):
+    def __init__(self, input_size: int = 256, hidden_size: int = 256, bidirectional: bool = True,
+                 num_cls: int = 2, num_comps: int = 53, window_size: int = 20,
+                 num_layers: int = 1):
+        super().__init__()
+        self.input_size = input_size
+        self.hidden_size = hidden_size
+        self.num_comp = num_comps
+        self.window_size = window_size
+        self.encoder = nn.Sequential(nn.Linear(num_comps * window_size, input_size), nn.ReLU())
+        self.lstm = LSTM(input_size=input_size, hidden_size=hidden_size,
+                         bidirectional=bidirectional, num_layers=num_layers)
+        self.classifier = nn.Sequential(
+            nn.Dropout(0.25),
+            nn.Linear(hidden_size, 256),
+            nn.BatchNorm1d(256),
+            nn.ReLU(),
+            nn.Linear(256, 64),
+            nn.ReLU(),
+            nn.Linear(64, num_cls),
+        )
+        self.use_fused = True
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        """``[B, S, C, W] -> [B, S, I]``: one batched GEMM instead of the per-sample loop."""
+        B, S = x.shape[:2]
+        flat = x.reshape(B * S, -1)
+        lin = self.encoder[0]
+        if self.use_fused and x.is_cuda:
+            enc = ops.linear_bias_relu(flat, lin.weight, lin.bias, module=lin)
+        else:
+            enc = torch.relu(lin(flat))  # module call: rank-dAD hooks see it
+        return enc.view(B, S, -1)
+
+    def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
+        enc = self.encode(x)
+        o, h = self.lstm(enc, reduce="mean")
+        return self.classifier(o.flatten(1).to(self.classifier[1].weight.dtype)), h

@@ -1,0 +1,20 @@
+"""Hot ops.  On a GPU every op below runs hand-written gfx950 kernels from the in-tree library
+(``_native/libdinunet_kernels.so``); on CPU they run the reference math (``ops.reference``)."""
+from . import _lib, capture, reference
+from ._lib import native_available
+from .gemm import mm
+from .linear import linear_bias_relu
+from .lstm import bilstm as _bilstm_fused, lstm_supported, padded_hidden
+from .optim import FlatParams, FusedAdam, cast_bf16_to_f32, cast_f32_to_bf16
+from .heads import fs_mlp, fs_mlp_supported, softmax_ce, log_softmax_nll
+
+
+def bilstm(x, params, reduce: str = "none", modules=None):
+    return _bilstm_fused(x, params, reduce=reduce, modules=modules)
+
+
+__all__ = [
+    "mm", "linear_bias_relu", "bilstm", "lstm_supported", "padded_hidden", "FlatParams",
+    "FusedAdam", "cast_bf16_to_f32", "cast_f32_to_bf16", "fs_mlp", "fs_mlp_supported",
+    "softmax_ce", "log_softmax_nll", "native_available", "capture", "reference",
+]

@@ -1,0 +1,112 @@
+"""Python face of the hand-written gfx950 GEMM (``csrc/kernels/gemm.hip``).
+
+``mm(a, b)`` computes ``op(a) @ op(b)`` with bf16 MFMA and fp32 accumulation for fp32 or bf16
+operands of any 2-D stride pattern that is contiguous along one axis (both transposes are free:
+the kernel stages either layout).  Fused epilogue: ``alpha``, ``bias``, ``relu``, ``beta``
+accumulate, output row remap, fp32 or bf16 store.  Long-K / few-tile problems split K over
+workgroups with a deterministic fp32 slab reduction.
+
+On CPU tensors the same call runs ``torch.matmul`` in fp32 (oracle / plumbing path).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+Tensor = torch.Tensor
+
+_lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _lib.c_void_p,
+                          _lib.c_int, _lib.c_int, _lib.c_long, _lib.c_void_p, _lib.c_int,
+                          _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_float,
+                          _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
+                          _lib.c_int, _lib.c_void_p, _lib.c_void_p])
+
+_NCU = 256
+
+
+def _layout(t: Tensor, rows_first: bool):
+    """Return (tensor, transposed_flag, leading_dim) for a logical 2-D operand.
+
+    For A (logical [M,K]) ``rows_first`` is True: k-contiguous -> flag 0.
+    For B (logical [K,N]) ``rows_first`` is False: k-contiguous -> flag 1.
+    """
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        t = t.float()
+    s0, s1 = t.stride()
+    # axis 1 contiguous: A -> [M][lda] (k contiguous), B -> [K][ldb] (n contiguous): flag 0
+    if t.shape[1] == 1 or s1 == 1:
+        return t, 0, (s0 if t.shape[0] > 1 else max(t.shape[1], 1))
+    # axis 0 contiguous: A -> stored [K][M], B -> stored [N][K]: flag 1
+    if t.shape[0] == 1 or s0 == 1:
+        return t, 1, (s1 if t.shape[1] > 1 else max(t.shape[0], 1))
+    t = t.contiguous()
+    return t, 0, t.stride(0)
+
+
+def choose_tiling(M: int, N: int, K: int):
+    t128 = ((M + 127) // 128) * ((N + 127) // 128)
+    t64 = ((M + 63) // 64) * ((N + 63) // 64)
+    if t128 >= 2 * _NCU:
+        return 1, 1
+    splits = 1
+    if t64 < _NCU // 2 and K >= 1024:
+        splits = max(1, min(8, _NCU // max(t64, 1), K // 256))
+    return 0, splits
+
+
+def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
+       out_dtype: torch.dtype = torch.float32, out: Optional[Tensor] = None,
+       bias: Optional[Tensor] = None, relu: bool = False, alpha: float = 1.0, beta: float = 0.0,
+       row_map: Optional[Tensor] = None, splits: Optional[int] = None) -> Tensor:
+    A = a.t() if trans_a else a
+    B = b.t() if trans_b else b
+    M, K = A.shape
+    K2, N = B.shape
+    if K != K2:
+        raise ValueError(f"mm shape mismatch {tuple(A.shape)} x {tuple(B.shape)}")
+    if not A.is_cuda:
+        res = alpha * (A.float() @ B.float())
+        if bias is not None:
+            res = res + bias.float()
+        if relu:
+            res = torch.relu(res)
+        if out is None:
+            out = torch.zeros(M if row_map is None else int(row_map.max()) + 1, N,
+                              dtype=out_dtype) if row_map is not None else None
+        if row_map is not None:
+            if beta != 0:
+                res = res + beta * out[row_map.long()].float()
+            out[row_map.long()] = res.to(out.dtype)
+            return out
+        if out is not None:
+            if beta != 0:
+                res = res + beta * out.float()
+            out.copy_(res.to(out.dtype))
+            return out
+        return res.to(out_dtype)
+    A, ta, lda = _layout(A, True)
+    B, tb, ldb = _layout(B, False)
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=a.device)
+        if beta != 0:
+            raise ValueError("beta != 0 needs an existing `out`")
+    if out.stride(1) != 1:
+        raise ValueError("mm output must be row-contiguous")
+    tile, auto_splits = choose_tiling(M, N, K)
+    sp = auto_splits if splits is None else max(1, int(splits))
+    slab = None
+    if sp > 1:
+        slab = torch.empty(sp * M * N, dtype=torch.float32, device=a.device)
+    if bias is not None:
+        bias = bias.float().contiguous()
+    if row_map is not None:
+        row_map = row_map.to(device=a.device, dtype=torch.int32).contiguous()
+    _lib.call("dn_gemm", A.data_ptr(), int(A.dtype == torch.bfloat16), ta, lda, B.data_ptr(),
+              int(B.dtype == torch.bfloat16), tb, ldb, out.data_ptr(),
+              int(out.dtype == torch.bfloat16), out.stride(0), M, N, K, float(alpha), float(beta),
+              _lib.ptr(bias), int(relu), _lib.ptr(row_map), tile, sp, _lib.ptr(slab),
+              _lib.stream())
+    return out

@@ -1,0 +1,64 @@
+"""Fused ``relu(x W^T + b)`` (the ICA encoder, reference ``comps/icalstm/models.py:87,107``).
+
+Forward is ONE MFMA GEMM with the bias+ReLU epilogue, reading the fp32 input windows and fp32
+master weights directly (rounded to bf16 while staging) and storing bf16 activations.  Backward
+masks the incoming gradient with the stored activations, then runs the weight-gradient GEMM
+(split-K over the B*S rows) and, only when required, the input-gradient GEMM.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import _grad
+from . import _lib
+from . import capture as _cap
+from .gemm import mm
+
+_lib.register("dn_relu_bwd_colsum", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                                     _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
+                                     _lib.c_void_p])
+_RB_SLABS = 64
+
+
+class _LinearBiasReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, weight, bias, module):
+        y = mm(x2d, weight, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16)
+        ctx.save_for_backward(x2d, y)
+        ctx.weight, ctx.bias = weight, bias
+        ctx.module = module
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, y = ctx.saved_tensors
+        weight, bias = ctx.weight, ctx.bias
+        N, O = y.shape
+        dy = dy.to(torch.bfloat16).contiguous()
+        dym = torch.empty_like(dy)
+        ws = torch.empty(_RB_SLABS * O, dtype=torch.float32, device=dy.device)
+        # bias grad accumulated straight into .grad; weight grad by a beta=1 GEMM epilogue
+        db = _grad.grad_buffer(bias) if bias is not None else \
+            torch.empty(O, dtype=torch.float32, device=dy.device)
+        _lib.call("dn_relu_bwd_colsum", dy.data_ptr(), y.data_ptr(), dym.data_ptr(),
+                  db.data_ptr(), ws.data_ptr(), N, O, int(bias is not None), _lib.stream())
+        mm(dym, x2d, trans_a=True, out=_grad.grad_buffer(weight), beta=1.0)
+        _grad.notify([weight] + ([bias] if bias is not None else []))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = mm(dym, weight, out_dtype=x2d.dtype)
+        if ctx.module is not None and _cap.active() is not None:
+            _cap.record(ctx.module, x2d, dym)
+        return dx, None, None, None
+
+
+def linear_bias_relu(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                     module: Optional[nn.Module] = None) -> torch.Tensor:
+    if not x2d.is_cuda:
+        return torch.relu(torch.nn.functional.linear(x2d, weight, bias))
+    if not _lib.native_available():
+        raise RuntimeError("linear_bias_relu on GPU needs the gfx950 kernel library")
+    return _LinearBiasReLU.apply(x2d.contiguous(), weight, bias, module)

@@ -1,0 +1,192 @@
+"""Fused bidirectional LSTM (forward + backward) on the persistent gfx950 kernels.
+
+Per training step (both directions together):
+
+forward
+  1. ``dn_lstm_pack``: fp32 reference-layout params -> bf16 kernel layouts (gate rows permuted to
+     ``m = 4u + g``, units zero-padded to HD in {64,128,192}), fused bias ``b_ih + b_hh``.
+  2. input projection of both directions as ONE GEMM ``[B*S, I] x [I, ndir*4*HD]`` (fp32 out).
+  3. ``dn_lstm_fwd``: persistent recurrence (grid = 16-row batch chunks x directions), stores
+     only ``c_t`` and ``h_{t-1}`` per step.
+backward
+  4. gate pre-activations for every step at once, in place on the projection buffer:
+     ``pre = xp + h_{t-1} W_hh^T + b`` (one GEMM per direction, full chip, time-parallel).
+  5. ``dn_lstm_bwd``: reverse-time recurrence -> gate grads ``dpre`` (bf16, original time order).
+  6. parameter grads ACCUMULATED straight into ``.grad`` (flat buffer) by GEMM epilogues with a
+     row map back to the reference ``[i|f|o|g]`` layout: ``dW_ih += dpre^T x``,
+     ``dW_hh += dpre^T h_{t-1}``; bias grads from a deterministic column sum of ``dpre``.
+  7. ``dx = dpre W_ih`` only when the input needs a gradient.
+
+Reference math: ``comps/icalstm/models.py:5-66`` (oracle: ``ops.reference.bilstm``).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _grad
+from . import _lib
+from . import capture as _cap
+from .gemm import mm
+
+Tensor = torch.Tensor
+
+_lib.register("dn_lstm_pack", [_lib.c_void_p] * 8 + [_lib.c_int] * 3 + [_lib.c_void_p] * 5)
+_lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
+                              _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                              _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
+                              _lib.c_void_p])
+_lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                              _lib.c_long, _lib.c_long, _lib.c_float, _lib.c_void_p,
+                              _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
+                              _lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_lstm_bias_grad", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
+                                    _lib.c_void_p] + [_lib.c_void_p] * 4 + [_lib.c_void_p])
+
+_ROWMAP_CACHE: Dict[Tuple[int, int, str], Tensor] = {}
+
+
+def padded_hidden(hd: int) -> int:
+    if hd <= 0:
+        return 0
+    for p in (64, 128, 192):
+        if hd <= p:
+            return p
+    return 0
+
+
+def lstm_supported(batch: int, input_size: int, hidden: int, ndir: int) -> bool:
+    return padded_hidden(hidden) > 0 and ndir in (1, 2) and batch > 0 and input_size > 0
+
+
+def _row_map(Hd: int, HD: int, device) -> Tensor:
+    """kernel gate row m = 4u+g (u < HD) -> reference row g*Hd + u, or -1 for padded units."""
+    key = (Hd, HD, str(device))
+    rm = _ROWMAP_CACHE.get(key)
+    if rm is None:
+        m = torch.arange(4 * HD)
+        u, g = m // 4, m % 4
+        rm = torch.where(u < Hd, g * Hd + u, torch.full_like(m, -1)).to(torch.int32).to(device)
+        _ROWMAP_CACHE[key] = rm
+    return rm
+
+
+class _BiLSTMFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, enc: Tensor, mode: str, modules, *params: Tensor):
+        ctx.set_materialize_grads(False)  # unused hT / cT -> None (no zero tensors, no syncs)
+        B, S, I = enc.shape
+        ndir = len(params) // 4
+        Hd = params[2].shape[1]
+        HD = padded_hidden(Hd)
+        GP = 4 * HD
+        nch = (B + 15) // 16
+        Bp = nch * 16
+        dev = enc.device
+        st = _lib.stream()
+        wih_p = torch.empty(ndir * GP, I, dtype=torch.bfloat16, device=dev)
+        bias_p = torch.empty(ndir * GP, dtype=torch.float32, device=dev)
+        whh_p = torch.empty(ndir, GP, HD, dtype=torch.bfloat16, device=dev)
+        whhT_p = torch.empty(ndir, HD, GP, dtype=torch.bfloat16, device=dev)
+        ps = [p.detach().contiguous() for p in params] + [None] * (8 - len(params))
+        _lib.call("dn_lstm_pack", *[_lib.ptr(p) for p in ps], I, Hd, ndir, wih_p.data_ptr(),
+                  bias_p.data_ptr(), whh_p.data_ptr(), whhT_p.data_ptr(), st)
+        x2d = enc.reshape(B * S, I)
+        if x2d.dtype != torch.bfloat16:
+            x2d = x2d.to(torch.bfloat16)
+        x2d = x2d.contiguous()
+        xp = mm(x2d, wih_p, trans_b=True, out_dtype=torch.float32)       # [B*S, ndir*GP]
+        c_save = torch.empty(ndir, Bp, S, HD, dtype=torch.float32, device=dev)
+        hprev = torch.empty(ndir, Bp, S, HD, dtype=torch.bfloat16, device=dev)
+        hT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
+        cT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
+        hmean = hseq = None
+        if mode == "mean":
+            hmean = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
+        else:
+            hseq = torch.empty(Bp, S, ndir * HD, dtype=torch.float32, device=dev)
+        _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
+                  ndir, c_save.data_ptr(), hprev.data_ptr(), _lib.ptr(hseq), _lib.ptr(hmean),
+                  1.0 / S, hT.data_ptr(), cT.data_ptr(), st)
+        if mode == "mean":
+            out = hmean
+        else:
+            out = hseq.view(Bp, S, ndir, HD)[:B, :, :, :Hd].reshape(B, S, ndir * Hd)
+        ctx.save_for_backward(x2d, wih_p, whh_p, whhT_p, bias_p, xp, c_save, hprev)
+        ctx.params = params
+        ctx.meta = (B, S, I, Hd, HD, ndir, mode, enc.dtype)
+        ctx.modules = modules
+        return out, hT, cT
+
+    @staticmethod
+    def backward(ctx, dout: Optional[Tensor], dhT: Optional[Tensor], dcT: Optional[Tensor]):
+        x2d, wih_p, whh_p, whhT_p, bias_p, xp, c_save, hprev = ctx.saved_tensors
+        params = ctx.params
+        B, S, I, Hd, HD, ndir, mode, enc_dtype = ctx.meta
+        GP = 4 * HD
+        N = B * S
+        Bp = c_save.shape[1]
+        dev = x2d.device
+        st = _lib.stream()
+        # (4) time-parallel pre-activations, in place on the projection buffer
+        for d in range(ndir):
+            mm(hprev[d].view(Bp * S, HD)[:N], whh_p[d], trans_b=True, out=xp[:, d * GP:(d + 1) * GP],
+               beta=1.0, bias=bias_p[d * GP:(d + 1) * GP])
+        # (5) reverse-time recurrence
+        if dout is None:
+            dout = torch.zeros((B, ndir * Hd) if mode == "mean" else (B, S, ndir * Hd),
+                               dtype=torch.float32, device=dev)
+        dout = dout.float().contiguous()
+        if mode == "mean":
+            sb, stt, scale = ndir * Hd, 0, 1.0 / S
+        else:
+            sb, stt, scale = S * ndir * Hd, ndir * Hd, 1.0
+        dhT = None if dhT is None else dhT.float().contiguous()
+        dcT = None if dcT is None else dcT.float().contiguous()
+        dpre = torch.empty(Bp * S, ndir * GP, dtype=torch.bfloat16, device=dev)
+        _lib.call("dn_lstm_bwd", xp.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
+                  dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir,
+                  dpre.data_ptr(), st)
+        dpre_v = dpre[:N]
+        # (6) parameter grads accumulated into .grad (reference layout via row map)
+        rmap = _row_map(Hd, HD, dev)
+        ws = torch.empty(64 * ndir * GP, dtype=torch.float32, device=dev)
+        gb = [None] * 8
+        for d in range(ndir):
+            w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
+            gb[4 * d + 1] = _grad.grad_buffer(b_ih) if b_ih is not None else None
+            gb[4 * d + 3] = _grad.grad_buffer(b_hh) if b_hh is not None else None
+        _lib.call("dn_lstm_bias_grad", dpre_v.data_ptr(), N, Hd, ndir, ws.data_ptr(),
+                  _lib.ptr(gb[1]), _lib.ptr(gb[3]), _lib.ptr(gb[5]), _lib.ptr(gb[7]), st)
+        for d in range(ndir):
+            w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
+            dsl = dpre_v[:, d * GP:(d + 1) * GP]
+            mm(dsl, x2d, trans_a=True, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap)
+            mm(dsl, hprev[d].view(Bp * S, HD)[:N, :Hd], trans_a=True, out=_grad.grad_buffer(w_hh),
+               beta=1.0, row_map=rmap)
+        _grad.notify([p for p in params if p is not None])
+        # (7) input grad
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = mm(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
+            if enc_dtype != torch.bfloat16:
+                dx = dx.to(enc_dtype)
+        if _cap.active() is not None and ctx.modules is not None:
+            dref = dpre_v.view(N, ndir, HD, 4)[:, :, :Hd, :].transpose(2, 3).reshape(N, ndir, 4 * Hd)
+            for d, cell in enumerate(ctx.modules):
+                _cap.record(cell.i2h, x2d, dref[:, d])
+                _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
+        return (dx, None, None) + (None,) * len(params)
+
+
+def bilstm(x: Tensor, params: Sequence[Tuple[Tensor, Tensor, Tensor, Tensor]],
+           reduce: str = "none", modules=None):
+    """Fused bi-LSTM: returns ``(hmean [B, ndir*Hd] | hseq [B, S, ndir*Hd], (hT, cT))``."""
+    if not _lib.native_available():
+        raise RuntimeError("fused LSTM requested but the gfx950 kernel library is not built")
+    flat: List[Tensor] = []
+    for p in params:
+        flat.extend(p)
+    out, hT, cT = _BiLSTMFn.apply(x, "mean" if reduce == "mean" else "seq", modules, *flat)
+    return out, (hT, cT)

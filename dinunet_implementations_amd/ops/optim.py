@@ -1,0 +1,140 @@
+"""Flat-buffer parameters and fused optimizers.
+
+All parameters of the site's model(s) are re-homed into ONE contiguous fp32 buffer (16-byte
+aligned per tensor) and their ``.grad`` into a matching flat gradient buffer.  Consequences:
+
+* the dSGD all-reduce is one collective on one buffer (or a few buckets) with zero packing;
+* Adam is a single fused HIP launch over the whole model (``csrc/kernels/optim.hip``);
+* checkpoints still save per-module ``state_dict``s with the reference key names.
+
+Semantics match ``torch.optim.Adam`` / ``torch.optim.SGD`` (checked against them in tests).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Iterable, List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+_lib.register("dn_adam", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                          _lib.c_long] + [_lib.c_float] * 8 + [_lib.c_void_p])
+_lib.register("dn_sgd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                         _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_int,
+                         _lib.c_void_p])
+_lib.register("dn_cast_f32_bf16", [_lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_float,
+                                   _lib.c_void_p])
+_lib.register("dn_cast_bf16_f32", [_lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_float,
+                                   _lib.c_void_p])
+
+ALIGN = 4  # elements (16 bytes)
+
+
+class FlatParams:
+    """Re-home ``params`` into one flat buffer; ``.grad`` of each becomes a view of ``self.grad``."""
+
+    def __init__(self, params: Iterable[nn.Parameter], device=None):
+        self.params: List[nn.Parameter] = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("no trainable parameters")
+        device = device or self.params[0].device
+        self.offsets: List[int] = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        for p, o in zip(self.params, self.offsets):
+            n = p.numel()
+            self.data[o:o + n].copy_(p.detach().reshape(-1).float())
+            p.data = self.data[o:o + n].view_as(p)
+            p.grad = self.grad[o:o + n].view_as(p)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def rebind_grads(self):
+        """Autograd may replace ``.grad`` with a fresh tensor when it was None; keep views."""
+        for p, o in zip(self.params, self.offsets):
+            n = p.numel()
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
+                g = p.grad
+                p.grad = self.grad[o:o + n].view_as(p)
+                if g is not None:
+                    p.grad.copy_(g)
+
+    def segments(self):
+        for p, o in zip(self.params, self.offsets):
+            yield p, o, p.numel()
+
+    def numel_of(self, ps) -> int:
+        return sum(p.numel() for p in ps)
+
+
+class FusedAdam:
+    """``torch.optim.Adam`` on a :class:`FlatParams` buffer in one kernel launch per step."""
+
+    def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0):
+        self.flat = flat
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.exp_avg = torch.zeros_like(flat.data)
+        self.exp_avg_sq = torch.zeros_like(flat.data)
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    def step(self, grad_scale: float = 1.0):
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
+        d = self.flat.data
+        if d.is_cuda:
+            _lib.call("dn_adam", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
+                      self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
+                      self.weight_decay, bc1, 1.0 / math.sqrt(bc2), grad_scale, _lib.stream())
+            return
+        g = self.flat.grad * grad_scale
+        if self.weight_decay:
+            g = g + self.weight_decay * d
+        self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
+        self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(self.eps)
+        d.addcdiv_(self.exp_avg, denom, value=-self.lr / bc1)
+
+    def state_dict(self) -> Dict:
+        return {"lr": self.lr, "betas": self.betas, "eps": self.eps,
+                "weight_decay": self.weight_decay, "step": self.step_count,
+                "exp_avg": self.exp_avg.detach().cpu(), "exp_avg_sq": self.exp_avg_sq.detach().cpu()}
+
+    def load_state_dict(self, sd: Dict):
+        self.lr = sd.get("lr", self.lr)
+        self.betas = tuple(sd.get("betas", self.betas))
+        self.eps = sd.get("eps", self.eps)
+        self.weight_decay = sd.get("weight_decay", self.weight_decay)
+        self.step_count = int(sd.get("step", 0))
+        if "exp_avg" in sd:
+            self.exp_avg.copy_(sd["exp_avg"].to(self.exp_avg.device))
+            self.exp_avg_sq.copy_(sd["exp_avg_sq"].to(self.exp_avg_sq.device))
+
+
+def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
+    if src.is_cuda:
+        _lib.call("dn_cast_f32_bf16", src.data_ptr(), dst.data_ptr(), src.numel(), scale,
+                  _lib.stream())
+    else:
+        dst.copy_((src * scale).to(dst.dtype))
+
+
+def cast_bf16_to_f32(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
+    if src.is_cuda:
+        _lib.call("dn_cast_bf16_f32", src.data_ptr(), dst.data_ptr(), src.numel(), scale,
+                  _lib.stream())
+    else:
+        dst.copy_(src.float() * scale)

@@ -1,0 +1,448 @@
+"""Gradient-aggregation engines: dSGD, rank-dAD, PowerSGD (reference ``comps/__init__.py:13-16``).
+
+Each engine turns every site's local gradient (living in the flat grad buffer of
+``ops.FlatParams``) into the *global* update all sites apply with their own optimizer, so
+replicas stay identical:
+
+* ``dSGD``     mean of site gradients — one (bucketed, backward-overlapped) RCCL all-reduce.
+* ``rankDAD``  for every ``nn.Linear``: rank-r factors of ``Delta^T A`` from a structured power
+  iteration (``lowrank.dad_factors``), all-gathered (a few KB per layer), reconstructed as
+  ``mean_s P_s Q_s^T``; exact dAD (raw ``A``, ``Delta`` exchange) when r covers the full rank.
+  Every other parameter (biases, BatchNorm) falls back to the dSGD mean.
+* ``powerSGD`` rank-r ``P = M Q`` / ``Q = M^T P`` with two all-reduces, warm-started ``Q`` and
+  per-site error feedback (Vogels et al. 2019); vectors use the dSGD mean.
+
+Every engine also exposes the three pieces the COINSTAC file transport needs
+(``payload`` on a site, ``aggregate`` on the remote, ``apply`` back on the site) with the same
+arithmetic as the collective path (``compat/``).
+
+``reduce()`` returns the scale the optimizer must apply to the flat gradient (dSGD leaves the
+all-reduce SUM in place and folds ``1/world`` into the fused Adam launch).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops import _grad as _gradreg
+from ..ops import capture as _cap
+from ..ops.optim import FlatParams, cast_bf16_to_f32, cast_f32_to_bf16
+from .group import SiteGroup
+from .lowrank import dad_factors, orthonormalize_
+
+Tensor = torch.Tensor
+
+
+class Engine:
+    name = "base"
+
+    def __init__(self, model: nn.Module, flat: FlatParams, group: SiteGroup, cfg: Optional[dict] = None):
+        self.model = model
+        self.flat = flat
+        self.group = group
+        self.cfg = dict(cfg or {})
+        self.half = str(self.cfg.get("precision_bits", "32")) == "16"
+        self.comm_bytes = 0  # payload bytes this site sent in the last reduce (observability)
+
+    # collective path -------------------------------------------------------------------------
+    def step_context(self):
+        return contextlib.nullcontext()
+
+    def reduce(self) -> float:
+        raise NotImplementedError
+
+    # file-transport path (COINSTAC compat) ---------------------------------------------------
+    def payload(self) -> Dict[str, Tensor]:
+        raise NotImplementedError
+
+    @classmethod
+    def aggregate(cls, payloads: Sequence[Dict[str, Tensor]], cfg: Optional[dict] = None) -> Dict[str, Tensor]:
+        raise NotImplementedError
+
+    def apply(self, agg: Dict[str, Tensor]) -> float:
+        raise NotImplementedError
+
+    # helpers ---------------------------------------------------------------------------------
+    def _allreduce_mean_(self, buf: Tensor):
+        """In-place mean over sites, honouring ``precision_bits``."""
+        g = self.group
+        if not g.distributed:
+            return
+        if self.half:
+            tmp = torch.empty(buf.numel(), dtype=torch.bfloat16, device=buf.device)
+            cast_f32_to_bf16(buf.reshape(-1), tmp)
+            g.all_reduce(tmp)
+            cast_bf16_to_f32(tmp, buf.reshape(-1), 1.0 / g.world)
+            self.comm_bytes += tmp.numel() * 2
+        else:
+            g.all_reduce(buf)
+            buf.mul_(1.0 / g.world)
+            self.comm_bytes += buf.numel() * 4
+
+
+# =============================================================================================
+# dSGD
+# =============================================================================================
+class DSGDEngine(Engine):
+    """Bucketed all-reduce of the flat gradient, overlapped with the backward pass.
+
+    Buckets are contiguous ranges of the flat buffer formed in REVERSE parameter order (the
+    order gradients become ready: classifier, then LSTM, then encoder for ICA).  A bucket's
+    all-reduce is launched from the post-accumulate-grad hook of its last parameter, on RCCL's
+    own stream, while autograd keeps computing earlier layers.
+    """
+    name = "dSGD"
+
+    def __init__(self, model, flat, group, cfg=None, bucket_mb: float = 4.0, overlap: bool = True):
+        super().__init__(model, flat, group, cfg)
+        self.overlap = overlap and group.distributed
+        self.sync_enabled = True
+        cap = int(bucket_mb * (1 << 20) / 4)
+        self.buckets: List[Tuple[int, int]] = []
+        self._param_bucket: Dict[int, int] = {}
+        cur_end, cur_start = None, None
+        segs = list(flat.segments())
+        for p, o, n in reversed(segs):
+            end = o + ((n + 3) // 4) * 4
+            if cur_end is None:
+                cur_end, cur_start = end, o
+            elif cur_end - o > cap and cur_end - cur_start > 0:
+                self.buckets.append((cur_start, cur_end))
+                cur_end, cur_start = cur_start, o
+            else:
+                cur_start = o
+            self._param_bucket[id(p)] = len(self.buckets)
+        if cur_end is not None:
+            self.buckets.append((cur_start, cur_end))
+        self._pending = [0] * len(self.buckets)
+        self._expected = [0] * len(self.buckets)
+        for p, _, _ in segs:
+            self._expected[self._param_bucket[id(p)]] += 1
+        self._handles: Dict[int, object] = {}
+        self._half_bufs: Dict[int, Tensor] = {}
+        self._hooks = []
+        if self.overlap:
+            for p, _, _ in segs:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            _gradreg.register(self._on_grad)  # fused ops write .grad directly and notify
+        self._reset()
+
+    def _reset(self):
+        self._pending = list(self._expected)
+        self._handles.clear()
+
+    def _launch(self, b: int):
+        s, e = self.buckets[b]
+        view = self.flat.grad[s:e]
+        if self.half:
+            buf = self._half_bufs.get(b)
+            if buf is None:
+                buf = self._half_bufs[b] = torch.empty(e - s, dtype=torch.bfloat16, device=view.device)
+            cast_f32_to_bf16(view, buf)
+            self._handles[b] = self.group.all_reduce(buf, async_op=True)
+            self.comm_bytes += buf.numel() * 2
+        else:
+            self._handles[b] = self.group.all_reduce(view, async_op=True)
+            self.comm_bytes += view.numel() * 4
+
+    def _on_grad(self, p):
+        if not self.sync_enabled:
+            return
+        b = self._param_bucket.get(id(p))
+        if b is None:
+            return
+        self._pending[b] -= 1
+        if self._pending[b] == 0 and b not in self._handles:
+            self._launch(b)
+
+    def reduce(self) -> float:
+        g = self.group
+        if not g.distributed:
+            self._reset()
+            return 1.0
+        self.comm_bytes = 0 if not self._handles else self.comm_bytes
+        for b in range(len(self.buckets)):
+            if b not in self._handles:
+                self._launch(b)
+        for b, h in self._handles.items():
+            h.wait()
+            if self.half:
+                s, e = self.buckets[b]
+                cast_bf16_to_f32(self._half_bufs[b], self.flat.grad[s:e])
+        self._reset()
+        return 1.0 / g.world
+
+    def close(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+        _gradreg.unregister(self._on_grad)
+
+    # file transport
+    def payload(self):
+        g = self.flat.grad
+        return {"grad": g.to(torch.bfloat16) if self.half else g.clone()}
+
+    @classmethod
+    def aggregate(cls, payloads, cfg=None):
+        acc = None
+        for p in payloads:
+            v = p["grad"].float()
+            acc = v.clone() if acc is None else acc.add_(v)
+        return {"grad": acc / len(payloads)}
+
+    def apply(self, agg):
+        self.flat.grad.copy_(agg["grad"].to(self.flat.grad.device, torch.float32))
+        return 1.0
+
+
+# =============================================================================================
+# rank-dAD
+# =============================================================================================
+class RankDADEngine(Engine):
+    name = "rankDAD"
+
+    def __init__(self, model, flat, group, cfg=None):
+        super().__init__(model, flat, group, cfg)
+        self.rank = int(self.cfg.get("dad_reduction_rank", 10))
+        self.iters = int(self.cfg.get("dad_num_pow_iters", 5))
+        self.tol = float(self.cfg.get("dad_tol", 1e-3))
+        self.linears: List[nn.Linear] = [m for m in model.modules() if isinstance(m, nn.Linear)]
+        self._weight_ids = {id(m.weight) for m in self.linears}
+        self.dense_segs = [(o, n) for p, o, n in flat.segments() if id(p) not in self._weight_ids]
+        self._cap: Optional[_cap.DADCapture] = None
+        self._gen = None
+
+    def step_context(self):
+        self._cap = _cap.DADCapture(modules=self.linears)
+        return self._cap
+
+    def _dense_pack(self) -> Tensor:
+        g = self.flat.grad
+        return torch.cat([g[o:o + n] for o, n in self.dense_segs]) if self.dense_segs else g[:0].clone()
+
+    def _dense_unpack(self, buf: Tensor):
+        g = self.flat.grad
+        off = 0
+        for o, n in self.dense_segs:
+            g[o:o + n].copy_(buf[off:off + n])
+            off += n
+
+    def _layer_inputs(self):
+        """Per captured Linear: concatenated ``(A [N, in], Delta [N, out])``."""
+        recs = self._cap.records if self._cap is not None else {}
+        out = []
+        for m in self.linears:
+            r = recs.get(m)
+            if not r:
+                continue
+            A = torch.cat([a.reshape(-1, a.shape[-1]) for a, _ in r]).float()
+            D = torch.cat([d.reshape(-1, d.shape[-1]) for _, d in r]).float()
+            out.append((m, A, D))
+        return out
+
+    def _exact(self, A: Tensor, D: Tensor) -> bool:
+        # decided from the layer shape only, so every site picks the same mode (the collective
+        # layouts must agree); at r >= rank(G) the power iteration is exact anyway
+        return self.rank >= min(A.shape[1], D.shape[1])
+
+    def local_factors(self):
+        """[(module, mode, X, Y)] with mode 'exact' (X=Delta, Y=A) or 'lowrank' (X=P, Y=Q)."""
+        res = []
+        for m, A, D in self._layer_inputs():
+            if self._exact(A, D):
+                res.append((m, "exact", D, A))
+            else:
+                P, Q = dad_factors(D, A, self.rank, self.iters, self.tol)
+                res.append((m, "lowrank", P, Q))
+        return res
+
+    def reduce(self) -> float:
+        g = self.group
+        self.comm_bytes = 0
+        dense = self._dense_pack()
+        self._allreduce_mean_(dense)
+        self._dense_unpack(dense)
+        facs = self.local_factors()
+        W = g.world
+        low = [(m, X, Y) for m, mode, X, Y in facs if mode == "lowrank"]
+        if low:
+            flat = torch.cat([torch.cat([X.reshape(-1), Y.reshape(-1)]) for _, X, Y in low])
+            gathered = torch.empty(W * flat.numel(), dtype=flat.dtype, device=flat.device)
+            g.all_gather_into(gathered, flat)
+            self.comm_bytes += flat.numel() * 4
+            gathered = gathered.view(W, -1)
+            off = 0
+            for m, X, Y in low:
+                nx, ny = X.numel(), Y.numel()
+                Ps = gathered[:, off:off + nx].reshape(W, *X.shape)
+                Qs = gathered[:, off + nx:off + nx + ny].reshape(W, *Y.shape)
+                off += nx + ny
+                # mean_s P_s Q_s^T  ==  [P_1..P_W] [Q_1..Q_W]^T / W  (one GEMM)
+                Pc = Ps.permute(1, 0, 2).reshape(X.shape[0], -1)
+                Qc = Qs.permute(1, 0, 2).reshape(Y.shape[0], -1)
+                m.weight.grad.copy_((Pc @ Qc.t()).div_(W).view_as(m.weight))
+        for m, mode, D, A in facs:
+            if mode != "exact":
+                continue
+            Dc = g.all_gather_varlen(D)
+            Ac = g.all_gather_varlen(A)
+            self.comm_bytes += (D.numel() + A.numel()) * 4
+            m.weight.grad.copy_((Dc.t() @ Ac).div_(W).view_as(m.weight))
+        if self._cap is not None:
+            self._cap.clear()
+        return 1.0
+
+    # file transport
+    def payload(self):
+        out = {"dense": self._dense_pack()}
+        facs = self.local_factors()
+        self._captured_order = [m for m, _, _, _ in facs]
+        for i, (m, mode, X, Y) in enumerate(facs):
+            out[f"L{i:03d}.{mode}.X"] = X
+            out[f"L{i:03d}.{mode}.Y"] = Y
+        if self._cap is not None:
+            self._cap.clear()
+        return out
+
+    @classmethod
+    def aggregate(cls, payloads, cfg=None):
+        W = len(payloads)
+        agg = {"dense": sum(p["dense"].float() for p in payloads) / W}
+        keys = sorted({k.rsplit(".", 1)[0] for p in payloads for k in p if k != "dense"})
+        for k in keys:
+            X = torch.cat([p[k + ".X"].float() for p in payloads], 1 if ".lowrank" in k else 0)
+            Y = torch.cat([p[k + ".Y"].float() for p in payloads], 1 if ".lowrank" in k else 0)
+            agg[k] = (X @ Y.t() / W) if ".lowrank" in k else (X.t() @ Y / W)
+        return agg
+
+    def apply(self, agg):
+        self._dense_unpack(agg["dense"].to(self.flat.grad.device))
+        by_layer = {int(k.split(".")[0][1:]): k for k in agg if k != "dense"}
+        for i, k in sorted(by_layer.items()):
+            m = self._captured_order[i]
+            m.weight.grad.copy_(agg[k].to(m.weight.grad.device).view_as(m.weight))
+        return 1.0
+
+
+# =============================================================================================
+# PowerSGD
+# =============================================================================================
+class PowerSGDEngine(Engine):
+    name = "powerSGD"
+
+    def __init__(self, model, flat, group, cfg=None):
+        super().__init__(model, flat, group, cfg)
+        self.rank = int(self.cfg.get("powersgd_rank", 4))
+        self.warm = bool(self.cfg.get("powersgd_warm_start", True))
+        self.mats = []   # (param, n, m, r)
+        dense = []
+        for p, o, n in flat.segments():
+            if p.dim() >= 2:
+                rows, cols = p.shape[0], p.numel() // p.shape[0]
+                r = min(self.rank, rows, cols)
+                if (rows + cols) * r < rows * cols:
+                    self.mats.append((p, rows, cols, r))
+                    continue
+            dense.append((o, n))
+        self.dense_segs = dense
+        gen = torch.Generator(device="cpu").manual_seed(int(self.cfg.get("seed", 0)) + 12345)
+        dev = flat.data.device
+        self.Q = [torch.randn(c, r, generator=gen).to(dev) for _, _, c, r in self.mats]
+        self.err = [torch.zeros(rw, c, device=dev) for _, rw, c, _ in self.mats]
+
+    def _dense_pack(self):
+        g = self.flat.grad
+        return torch.cat([g[o:o + n] for o, n in self.dense_segs]) if self.dense_segs else g[:0].clone()
+
+    def _dense_unpack(self, buf):
+        g = self.flat.grad
+        off = 0
+        for o, n in self.dense_segs:
+            g[o:o + n].copy_(buf[off:off + n])
+            off += n
+
+    def reduce(self) -> float:
+        g = self.group
+        W = g.world
+        self.comm_bytes = 0
+        dense = self._dense_pack()
+        self._allreduce_mean_(dense)
+        self._dense_unpack(dense)
+        if not self.mats:
+            return 1.0
+        Ms = []
+        for (p, rows, cols, r), e in zip(self.mats, self.err):
+            M = p.grad.reshape(rows, cols) + e
+            Ms.append(M)
+        if not self.warm:
+            for q in self.Q:
+                q.normal_()
+        Ps = [M @ q for M, q in zip(Ms, self.Q)]
+        pbuf = torch.cat([P.reshape(-1) for P in Ps])
+        if g.distributed:
+            g.all_reduce(pbuf)
+            pbuf.div_(W)
+            self.comm_bytes += pbuf.numel() * 4
+        off = 0
+        for i, P in enumerate(Ps):
+            Ps[i] = pbuf[off:off + P.numel()].view_as(P)
+            off += P.numel()
+        orthonormalize_(Ps)
+        Qs = [M.t() @ P for M, P in zip(Ms, Ps)]
+        qbuf = torch.cat([Q.reshape(-1) for Q in Qs])
+        if g.distributed:
+            g.all_reduce(qbuf)
+            qbuf.div_(W)
+            self.comm_bytes += qbuf.numel() * 4
+        off = 0
+        for i, (Q, M, P) in enumerate(zip(Qs, Ms, Ps)):
+            Qn = qbuf[off:off + Q.numel()].view_as(Q)
+            off += Q.numel()
+            self.Q[i].copy_(Qn)
+            Mh = P @ Qn.t()
+            self.err[i].copy_(M - Mh)
+            p = self.mats[i][0]
+            p.grad.copy_(Mh.view_as(p))
+        return 1.0
+
+    # file transport: two rounds (P then Q) are modelled as one call sequence by the compat layer
+    def payload_p(self):
+        self._Ms = [p.grad.reshape(rw, c) + e for (p, rw, c, _), e in zip(self.mats, self.err)]
+        return {"dense": self._dense_pack(), **{f"P{i}": M @ q for i, (M, q) in enumerate(zip(self._Ms, self.Q))}}
+
+    def payload_q(self, agg_p):
+        Ps = [agg_p[f"P{i}"].to(self.flat.data.device).clone() for i in range(len(self.mats))]
+        orthonormalize_(Ps)
+        self._Ps = Ps
+        return {f"Q{i}": M.t() @ P for i, (M, P) in enumerate(zip(self._Ms, Ps))}
+
+    def apply_pq(self, agg_p, agg_q):
+        self._dense_unpack(agg_p["dense"].to(self.flat.grad.device))
+        for i, ((p, rw, c, _), P) in enumerate(zip(self.mats, self._Ps)):
+            Qn = agg_q[f"Q{i}"].to(P.device)
+            self.Q[i].copy_(Qn)
+            Mh = P @ Qn.t()
+            self.err[i].copy_(self._Ms[i] - Mh)
+            p.grad.copy_(Mh.view_as(p))
+        return 1.0
+
+    @classmethod
+    def aggregate(cls, payloads, cfg=None):
+        W = len(payloads)
+        return {k: sum(p[k].float() for p in payloads) / W for k in payloads[0]}
+
+
+ENGINES = {"dSGD": DSGDEngine, "rankDAD": RankDADEngine, "powerSGD": PowerSGDEngine}
+
+
+def make_engine(name: str, model: nn.Module, flat: FlatParams, group: SiteGroup, cfg: dict) -> Engine:
+    try:
+        cls = ENGINES[name]
+    except KeyError:
+        raise ValueError(f"unknown agg_engine {name!r}; expected one of {sorted(ENGINES)}")
+    return cls(model, flat, group, cfg)

@@ -1,0 +1,142 @@
+"""Site group: one process per GPU, each GPU plays one COINSTAC site (rank == site index).
+
+The reference routes every update through a remote aggregator over files + JSON (star topology,
+SURVEY.md §2.4).  Here all sites form one ``torch.distributed`` process group — backend ``nccl``
+(= RCCL on ROCm, point-to-point xGMI between the 8 MI355X of a node) on GPUs, ``gloo`` on CPU for
+tests — and every "remote" reduction is a collective whose result every rank holds.  Decisions
+the remote used to make (best epoch, early stop) are computed redundantly and identically on all
+ranks from collectively-reduced inputs.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class SiteGroup:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+    pg: Any = None
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    @property
+    def is_master(self) -> bool:
+        return self.rank == 0
+
+    # ---- thin collective helpers (no-ops at world 1) ----------------------------------------
+    def barrier(self):
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(group=self.pg, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.pg)
+
+    def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
+        if not self.distributed:
+            return None
+        return dist.all_reduce(t, op=op, group=self.pg, async_op=async_op)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False):
+        if not self.distributed:
+            return None
+        return dist.broadcast(t, src=src, group=self.pg, async_op=async_op)
+
+    def all_gather(self, t: torch.Tensor) -> List[torch.Tensor]:
+        if not self.distributed:
+            return [t]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t.contiguous(), group=self.pg)
+        return out
+
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor, async_op: bool = False):
+        """Gather equal-size tensors into one flat ``[world * numel]`` buffer (one collective)."""
+        if not self.distributed:
+            out.copy_(t.reshape(-1))
+            return None
+        return dist.all_gather_into_tensor(out, t.contiguous().reshape(-1), group=self.pg,
+                                           async_op=async_op)
+
+    def all_gather_object(self, obj) -> List[Any]:
+        if not self.distributed:
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.pg)
+        return out
+
+    def broadcast_object(self, obj, src: int = 0):
+        if not self.distributed:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, group=self.pg)
+        return box[0]
+
+    def all_gather_varlen(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate variable-length 1-D/2-D tensors from all ranks (rank order)."""
+        if not self.distributed:
+            return t
+        n = torch.tensor([t.shape[0]], device=t.device, dtype=torch.long)
+        sizes = [int(s.item()) for s in self.all_gather(n)]
+        mx = max(sizes) if sizes else 0
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if t.shape[0]:
+            pad[:t.shape[0]] = t
+        parts = self.all_gather(pad)
+        return torch.cat([p[:s] for p, s in zip(parts, sizes)], 0)
+
+
+_GROUP: Optional[SiteGroup] = None
+
+
+def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
+               timeout_s: int = 1800) -> SiteGroup:
+    """Initialise from torchrun-style env vars; world 1 when they are absent."""
+    global _GROUP
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    want_gpu = device != "cpu" and torch.cuda.is_available()
+    if want_gpu:
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+    pg = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not dist.is_initialized():
+            kw = dict(backend=be, rank=rank, world_size=world,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+            if be == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+        pg = dist.group.WORLD
+    _GROUP = SiteGroup(rank=rank, world=world, local_rank=local, device=dev,
+                       backend=be if world > 1 else None, pg=pg)
+    return _GROUP
+
+
+def current() -> SiteGroup:
+    global _GROUP
+    if _GROUP is None:
+        _GROUP = SiteGroup()
+    return _GROUP
+
+
+def shutdown():
+    global _GROUP
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _GROUP = None

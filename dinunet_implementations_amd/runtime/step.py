@@ -1,0 +1,105 @@
+"""The training step of one site: forward, loss, backward, aggregation, optimizer.
+
+The launch-bound part (encoder GEMM, persistent LSTM, classifier, loss head, full backward,
+gradient zeroing) is captured once into a HIP graph and replayed every step; gradient
+aggregation (RCCL collectives) and the single fused Adam launch run after the replay, because the
+optimizer's bias-correction scalars change every step and collective capture is not needed for a
+handful of bucketed all-reduces.  Engines whose reduction needs host-side logic (rank-dAD,
+PowerSGD) or that capture activations run eagerly.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+from .. import ops
+
+
+def ica_forward_loss(model, x, y):
+    logits, _ = model(x)
+    return ops.softmax_ce(logits, y)
+
+
+def fs_forward_loss(model, x, y):
+    logits = model(x)
+    return ops.log_softmax_nll(logits, y)
+
+
+HEADS = {"ica": ica_forward_loss, "fs": fs_forward_loss}
+
+
+class TrainStep:
+    def __init__(self, model, flat, opt, engine, task: str = "ica", use_graph: bool = True,
+                 eager_warmup: int = 3, forward_loss: Optional[Callable] = None):
+        self.model = model
+        self.flat = flat
+        self.opt = opt
+        self.engine = engine
+        self.forward_loss = forward_loss or HEADS[task]
+        self.use_graph = (use_graph and flat.data.is_cuda and engine.name == "dSGD")
+        self.eager_warmup = eager_warmup
+        self.calls = 0
+        self.graph = None
+        self.static = None
+        self.last_loss = torch.zeros(())
+        self.last_out = None
+        self.last_pred = None
+
+    def _fwd_bwd(self, x, y):
+        with self.engine.step_context():
+            out, loss, pred = self.forward_loss(self.model, x, y)
+            loss.backward()
+        return out, loss, pred
+
+    def _eager(self, x, y):
+        self.flat.zero_grad()
+        out, loss, pred = self._fwd_bwd(x, y)
+        scale = self.engine.reduce()
+        self.opt.step(grad_scale=scale)
+        self.last_out, self.last_loss, self.last_pred = out.detach(), loss.detach(), pred
+        return loss
+
+    def _capture(self, x, y):
+        sx = torch.empty_like(x)
+        sy = torch.empty_like(y)
+        sx.copy_(x)
+        sy.copy_(y)
+        g = torch.cuda.CUDAGraph()
+        prev = getattr(self.engine, "sync_enabled", None)
+        if prev is not None:
+            self.engine.sync_enabled = False  # no collectives inside the captured region
+        try:
+            with torch.cuda.graph(g):
+                self.flat.grad.zero_()
+                out, loss, pred = self._fwd_bwd(sx, sy)
+        finally:
+            if prev is not None:
+                self.engine.sync_enabled = prev
+        self.graph = g
+        self.static = (sx, sy, out, loss, pred)
+
+    def __call__(self, x, y):
+        self.calls += 1
+        if not self.use_graph:
+            return self._eager(x, y)
+        if self.graph is None:
+            if self.calls <= self.eager_warmup:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    loss = self._eager(x, y)
+                torch.cuda.current_stream().wait_stream(s)
+                return loss
+            self._capture(x, y)
+        sx, sy, out, loss, pred = self.static
+        if sx.data_ptr() != x.data_ptr():
+            sx.copy_(x, non_blocking=True)
+            sy.copy_(y, non_blocking=True)
+        self.graph.replay()
+        if hasattr(self.engine, "sync_enabled"):
+            self.engine.sync_enabled = True
+        scale = self.engine.reduce()
+        self.opt.step(grad_scale=scale)
+        self.last_out, self.last_loss, self.last_pred = out, loss, pred
+        return loss

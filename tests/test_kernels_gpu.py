@@ -1,0 +1,169 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-12)
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from dinunet_implementations_amd.ops import _lib
+    assert _lib.native_available(), "kernel library must load on a GPU box"
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(3136, 256, 1000), (3136, 1536, 256), (77, 45, 33), (1536, 256, 3136)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_layouts(M, N, K, ta, tb):
+    from dinunet_implementations_amd.ops import mm
+    a = torch.randn(K, M, device=DEV) if ta else torch.randn(M, K, device=DEV)
+    b = torch.randn(N, K, device=DEV) if tb else torch.randn(K, N, device=DEV)
+    A = a.t() if ta else a
+    B = b.t() if tb else b
+    ref = bf(A) @ bf(B)
+    out = mm(a, b, trans_a=ta, trans_b=tb)
+    assert out.shape == (M, N)
+    assert rel(out, ref) < 2e-3
+
+
+def test_gemm_epilogue_bias_relu_bf16_out_and_beta():
+    from dinunet_implementations_amd.ops import mm
+    M, N, K = 300, 200, 128
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    y = mm(a, w, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16)
+    ref = torch.relu(a.float() @ bf(w).t() + bias)
+    assert y.dtype == torch.bfloat16 and rel(y, ref) < 1e-2
+    c = torch.randn(M, N, device=DEV)
+    c0 = c.clone()
+    mm(a, w, trans_b=True, out=c, beta=1.0, alpha=0.5)
+    assert rel(c, c0 + 0.5 * (a.float() @ bf(w).t())) < 2e-3
+
+
+def test_gemm_splitk_deterministic():
+    from dinunet_implementations_amd.ops import mm
+    a = torch.randn(4096, 96, device=DEV)
+    b = torch.randn(4096, 80, device=DEV)
+    r1 = mm(a, b, trans_a=True, splits=8)
+    r2 = mm(a, b, trans_a=True, splits=8)
+    assert torch.equal(r1, r2)
+    assert rel(r1, bf(a).t() @ bf(b)) < 2e-3
+
+
+def _lstm_params(I, Hd, ndir, scale=0.1):
+    ps = []
+    for _ in range(ndir):
+        ps.append(tuple(t.to(DEV).requires_grad_() for t in (
+            torch.randn(4 * Hd, I) * scale, torch.randn(4 * Hd) * scale,
+            torch.randn(4 * Hd, Hd) * scale, torch.randn(4 * Hd) * scale)))
+    return ps
+
+
+@pytest.mark.parametrize("B,S,I,Hd,ndir,mode", [
+    (32, 98, 256, 192, 2, "mean"),
+    (20, 17, 64, 174, 2, "mean"),
+    (5, 9, 32, 64, 1, "seq"),
+    (40, 12, 48, 100, 2, "seq"),
+])
+def test_lstm_fwd_bwd_matches_reference(B, S, I, Hd, ndir, mode):
+    from dinunet_implementations_amd.ops import reference as ref
+    from dinunet_implementations_amd.ops.lstm import bilstm
+    ps = _lstm_params(I, Hd, ndir)
+    x = torch.randn(B, S, I, device=DEV).requires_grad_()
+    out, (hT, cT) = bilstm(x, ps, reduce=mode)
+    # fp32 oracle on the same bf16-rounded inputs
+    ps_r = [tuple(bf(t.detach()).requires_grad_() for t in p) for p in ps]
+    xr = bf(x.detach()).requires_grad_()
+    hs, (rh, rc) = ref.bilstm(xr, ps_r, bidirectional=ndir == 2)
+    ro = hs.mean(1) if mode == "mean" else hs
+    assert out.shape == ro.shape
+    assert rel(out, ro) < 2e-2
+    assert rel(hT, rh) < 3e-2 and rel(cT, rc) < 3e-2
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    (ro * g).sum().backward()
+    assert rel(x.grad, xr.grad) < 5e-2
+    for p, pr in zip(ps, ps_r):
+        for t, tr in zip(p, pr):
+            assert rel(t.grad, tr.grad) < 5e-2, (t.shape, rel(t.grad, tr.grad))
+
+
+def test_linear_bias_relu_grad():
+    from dinunet_implementations_amd.ops import linear_bias_relu
+    x = torch.randn(500, 120, device=DEV)
+    w = (torch.randn(64, 120, device=DEV) * 0.1).requires_grad_()
+    b = (torch.randn(64, device=DEV) * 0.1).requires_grad_()
+    y = linear_bias_relu(x, w, b)
+    wr, br = bf(w.detach()).requires_grad_(), b.detach().clone().requires_grad_()
+    yr = torch.relu(bf(x) @ wr.t() + br)
+    assert rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    (y.float() * g).sum().backward()
+    (yr * g).sum().backward()
+    assert rel(w.grad, wr.grad) < 2e-2 and rel(b.grad, br.grad) < 2e-2
+
+
+def test_fused_adam_matches_torch():
+    from dinunet_implementations_amd.ops import FlatParams, FusedAdam
+    torch.manual_seed(1)
+    mods = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.Linear(17, 5)).to(DEV)
+    ref_mods = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.Linear(17, 5)).to(DEV)
+    ref_mods.load_state_dict(mods.state_dict())
+    flat = FlatParams(mods.parameters())
+    opt = FusedAdam(flat, lr=1e-2, weight_decay=1e-4)
+    ropt = torch.optim.Adam(ref_mods.parameters(), lr=1e-2, weight_decay=1e-4)
+    for _ in range(5):
+        x = torch.randn(8, 33, device=DEV)
+        opt.zero_grad()
+        mods(x).square().sum().backward()
+        opt.step()
+        ropt.zero_grad()
+        ref_mods(x).square().sum().backward()
+        ropt.step()
+    for p, q in zip(mods.parameters(), ref_mods.parameters()):
+        assert torch.allclose(p, q, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("log_out", [False, True])
+def test_softmax_xent(log_out):
+    from dinunet_implementations_amd.ops import heads, reference as ref
+    z = torch.randn(37, 2, device=DEV, requires_grad=True)
+    y = torch.randint(0, 2, (37,), device=DEV)
+    fn = heads.log_softmax_nll if log_out else heads.softmax_ce
+    rfn = ref.log_softmax_nll if log_out else ref.softmax_ce
+    out, loss, pred = fn(z, y)
+    zr = z.detach().clone().requires_grad_()
+    ro, rl, rp = rfn(zr, y)
+    assert torch.allclose(out, ro, atol=1e-5) and abs(loss.item() - rl.item()) < 1e-5
+    assert torch.equal(pred, rp)
+    loss.backward()
+    rl.backward()
+    assert torch.allclose(z.grad, zr.grad, atol=1e-6)
+
+
+def test_ica_model_gpu_matches_cpu_oracle():
+    from dinunet_implementations_amd.models import ICALstm
+    torch.manual_seed(3)
+    m = ICALstm(input_size=64, hidden_size=96, num_comps=20, window_size=5, num_cls=2)
+    mc = ICALstm(input_size=64, hidden_size=96, num_comps=20, window_size=5, num_cls=2)
+    mc.load_state_dict(m.state_dict())
+    m = m.to(DEV).eval()
+    mc = mc.eval()
+    x = torch.randn(24, 11, 20, 5)
+    out, _ = m(x.to(DEV))
+    ref, _ = mc(x)
+    assert rel(out.cpu(), ref) < 3e-2
