@@ -17,7 +17,7 @@ import torch
 class DeviceLoader:
     def __init__(self, inputs: torch.Tensor, labels: torch.Tensor, batch_size: int,
                  shuffle: bool = False, drop_last: bool = False, seed: int = 0,
-                 index: Optional[torch.Tensor] = None):
+                 index: Optional[torch.Tensor] = None, merge_singleton: bool = True):
         self.inputs = inputs
         self.labels = labels
         self.index = index  # global sample ids (for logging predictions), same order as inputs
@@ -26,11 +26,19 @@ class DeviceLoader:
         self.drop_last = drop_last
         self.epoch = 0
         self.seed = seed
+        # a trailing 1-sample batch breaks batch-statistics BatchNorm (the FS model normalises
+        # with batch stats even in eval): fold it into the previous batch instead
+        self.merge_singleton = merge_singleton
         self._gen = torch.Generator(device="cpu")
 
     def __len__(self):
         n = self.inputs.shape[0]
-        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+        if self.drop_last:
+            return n // self.batch_size
+        nb = (n + self.batch_size - 1) // self.batch_size
+        if self.merge_singleton and nb > 1 and n % self.batch_size == 1:
+            nb -= 1
+        return nb
 
     @property
     def num_samples(self) -> int:
@@ -51,7 +59,7 @@ class DeviceLoader:
         nb = len(self)
         for b in range(nb):
             s = b * self.batch_size
-            e = min(n, s + self.batch_size)
+            e = n if b == nb - 1 and not self.drop_last else min(n, s + self.batch_size)
             if perm is None:
                 ix = torch.arange(s, e, device=dev)
                 yield self.inputs[s:e], self.labels[s:e], ix

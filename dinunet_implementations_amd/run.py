@@ -1,0 +1,60 @@
+"""Launch a decentralized run: one process per site (GPU), e.g.
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+        -m dinunet_implementations_amd.run --data-path datasets/icalstm --out out/
+
+Rank r is site ``local<r>``: its inputs are ``inputspec.json[r]`` (the simulator convention of
+``datasets/*/inputspec.json``, one object per site) and its data directory is
+``<data-path>/input/local<r>/simulatorRun``.  ``--set key=value`` overrides any config key
+(JSON-parsed values), e.g. ``--set agg_engine=rankDAD --set epochs=5``.
+Without a launcher it runs a single site on one device.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from typing import Any, Dict, List
+
+
+def parse_sets(items: List[str]) -> Dict[str, Any]:
+    out = {}
+    for it in items or []:
+        k, _, v = it.partition("=")
+        try:
+            out[k] = json.loads(v)
+        except json.JSONDecodeError:
+            out[k] = v
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data-path", required=True)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--device", default=None, choices=[None, "cpu", "cuda"])
+    ap.add_argument("--set", action="append", default=[])
+    a = ap.parse_args(argv)
+    from .config import build_config, load_inputspec
+    from .parallel import init_sites, shutdown
+    from .runtime.site import FederatedSite
+    from .tasks import get_task
+
+    grp = init_sites(device=a.device)
+    specs = load_inputspec(os.path.join(a.data_path, "inputspec.json"))
+    site_in = specs[grp.rank % len(specs)]
+    cfg = build_config(site_input=site_in, overrides=parse_sets(a.set))
+    base = os.path.join(a.data_path, "input", f"local{grp.rank}", "simulatorRun")
+    if not os.path.isdir(base):
+        base = os.path.join(a.data_path, "input", f"local{grp.rank % len(specs)}", "simulatorRun")
+    state = {"baseDirectory": base, "clientId": f"local{grp.rank}"}
+    out = a.out or os.path.join(a.data_path, "output")
+    T, D, H = get_task(cfg["task_id"])
+    FederatedSite(cfg, grp, T, D, H, state, out, site_name=f"local{grp.rank}").run()
+    shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

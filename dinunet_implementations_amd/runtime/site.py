@@ -1,0 +1,327 @@
+"""One site of a decentralized run — what ``COINNLocal`` + ``COINNRemote`` did together
+(SURVEY.md E2, E3, E13-E16), executed as one rank of a process group.
+
+Phases per fold (``fold_0 .. fold_{k-1}``):
+
+1. list files (plugin ``DataHandle``) -> deterministic per-site split (ratio / k-fold / files)
+   -> plugin ``Dataset`` -> ONE preprocessing pass into HBM-resident tensors.
+2. model init with a seed shared by all sites + broadcast from rank 0 (identical replicas); or,
+   with ``pretrain``, the site holding the most training data trains alone with
+   ``pretrain_args`` and its best weights are broadcast as the common init (config 5).
+3. training in lockstep: every site contributes a gradient at every step (``steps_per_epoch``
+   = max over sites; sites with less data cycle their reshuffled loader), ``local_iterations``
+   micro-batches per step, aggregation by the engine (dSGD / rank-dAD / PowerSGD), fused Adam.
+4. every ``validation_epochs``: each site scores its validation split, scores+labels are
+   all-gathered, the *global* metric (``monitor_metric``, ``metric_direction``) drives the
+   best-epoch checkpoint and ``patience`` early stopping identically on every rank (the
+   remote's decisions, made redundantly instead of by a separate process).
+5. test: reload the best checkpoint, score the test split, write global + local test metrics.
+
+Outputs: ``logs.json`` / ``test_metrics.csv`` per site and for the global "remote" view, remote
+results zip, ``checkpoint_best.pt`` / ``checkpoint_last.pt`` (resume with ``resume=True``).
+"""
+from __future__ import annotations
+
+import copy
+import math
+import os
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+
+from ..config import site_seed
+from ..data.loader import DeviceLoader
+from ..data.splits import make_splits
+from ..parallel import SiteGroup, make_engine
+from ..utils import logs as L
+from ..utils.metrics import Averages, Metrics, improved, metric_value
+from .step import TrainStep
+from .trainer import NNTrainer, set_seed
+
+
+class FederatedSite:
+    def __init__(self, cfg: Dict[str, Any], group: SiteGroup, trainer_cls, dataset_cls,
+                 datahandle_cls, state: Dict[str, Any], out_dir: str, site_name: Optional[str] = None,
+                 verbose: bool = True):
+        self.cfg = cfg
+        self.group = group
+        self.Trainer, self.Dataset, self.DataHandle = trainer_cls, dataset_cls, datahandle_cls
+        self.state = state
+        self.out_dir = out_dir
+        self.site = site_name or f"local{group.rank}"
+        self.device = group.device
+        self.verbose = verbose
+        self.task_id = str(cfg.get("task_id"))
+
+    # ---------------------------------------------------------------------------------------
+    def log(self, *a):
+        if self.verbose:
+            print(f"[{self.site}]", *a, flush=True)
+
+    def _global_max(self, v: int) -> int:
+        t = torch.tensor([int(v)], device=self.device)
+        self.group.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return int(t.item())
+
+    def _datasets(self, split: Dict[str, List[Any]]) -> Dict[str, Tuple[torch.Tensor, torch.Tensor]]:
+        cache = self.cfg
+        out = {}
+        for key in ("train", "validation", "test"):
+            ds = self.Dataset(cache=cache, state=self.state, mode=key)
+            if split.get(key):
+                ds.add(split[key])
+            out[key] = ds.materialize(self.device)
+        return out
+
+    def _loader(self, X, y, key: str, batch_size: int, seed: int) -> DeviceLoader:
+        dl_args = (self.cfg.get("dataloader_args") or {}).get(key, {})
+        drop_last = bool(dl_args.get("drop_last", False))
+        shuffle = key == "train"
+        if drop_last and X.shape[0] < batch_size:
+            drop_last = False  # keep at least one batch on tiny splits
+        return DeviceLoader(X, y, batch_size, shuffle=shuffle, drop_last=drop_last, seed=seed)
+
+    # ---- global evaluation ------------------------------------------------------------------
+    def global_eval(self, trainer: NNTrainer, loader: DeviceLoader):
+        res = trainer.evaluate(loader)
+        avg: Averages = res["averages"]
+        met: Metrics = res["metrics"]
+        s, l = met.tensors()
+        s = s.to(self.device).float()
+        l = l.to(self.device).long()
+        S = self.group.all_gather_varlen(s)
+        Lb = self.group.all_gather_varlen(l)
+        st = avg.to_state()
+        tot = torch.tensor([st["sum"], float(st["n"])], device=self.device, dtype=torch.float64)
+        self.group.all_reduce(tot)
+        gloss = float(tot[0] / tot[1]) if float(tot[1]) > 0 else 0.0
+        gm = Metrics.from_tensors(S, Lb, met.num_class)
+        return {"loss": gloss, "scores": gm.scores(), "local_loss": avg.average,
+                "local_scores": met.scores(), "n": int(tot[1])}
+
+    def _broadcast_model(self, trainer: NNTrainer, src: int = 0):
+        if not self.group.distributed:
+            return
+        self.group.broadcast(trainer.flat.data, src)
+        for m in trainer.nn.values():
+            for b in m.buffers():
+                self.group.broadcast(b, src)
+
+    def _replica_checksum(self, trainer: NNTrainer) -> bool:
+        """Debug race/sync check: are all sites' parameters bit-identical?"""
+        v = trainer.flat.data.double().sum().reshape(1)
+        allv = self.group.all_gather(v)
+        return all(bool(torch.equal(x, allv[0])) for x in allv)
+
+    # ---- train loops ------------------------------------------------------------------------
+    def _train_epochs(self, trainer: NNTrainer, engine, data, cfg: Dict[str, Any], group: SiteGroup,
+                      fold_dir: str, seed: int, logs: Dict[str, Any], tag: str = "",
+                      start_epoch: int = 1, best: Optional[Dict[str, Any]] = None):
+        bs = int(cfg.get("batch_size", 16))
+        li = max(1, int(cfg.get("local_iterations", 1)))
+        tr = self._loader(*data["train"], "train", bs, seed)
+        va = self._loader(*data["validation"], "validation", bs, seed)
+        local_steps = max(1, math.ceil(len(tr) / li)) if tr.num_samples else 0
+        if group is self.group:
+            steps = self._global_max(local_steps)
+        else:
+            steps = local_steps
+        epochs = int(cfg.get("epochs", 1))
+        patience = int(cfg.get("patience", epochs + 1))
+        val_every = max(1, int(cfg.get("validation_epochs", 1)))
+        monitor = str(cfg.get("monitor_metric", "auc"))
+        direction = str(cfg.get("metric_direction", "maximize"))
+        if monitor.lower() == "loss":
+            direction = "minimize"
+        best = best or {"score": None, "epoch": 0, "wait": 0}
+        use_fast = trainer.has_fast_path and li == 1
+        step = TrainStep(trainer.modules(), trainer.flat, trainer.optimizer, engine,
+                         use_graph=bool(cfg.get("use_graph", True)) and self.device.type == "cuda",
+                         forward_loss=lambda m, x, y: trainer.forward_loss(x, y)) \
+            if use_fast else None
+        it = iter(tr)
+        tl = logs.setdefault(f"{tag}train_log", [])
+        vl = logs.setdefault(f"{tag}validation_log", [])
+        lvl = logs.setdefault(f"{tag}local_validation_log", [])
+        comp = logs.setdefault("time_spent_on_computation", [])
+        cum = logs.setdefault("cumulative_total_duration", [])
+        itd = logs.setdefault("local_iter_duration", [])
+        t_run = time.time()
+        trainer.train()
+        for epoch in range(start_epoch, epochs + 1):
+            t0 = time.time()
+            avg, met = trainer.new_averages(), trainer.new_metrics()
+            nsamp = 0
+            for _ in range(steps):
+                if step is not None:
+                    try:
+                        x, y, _ix = next(it)
+                    except StopIteration:
+                        it = iter(tr)
+                        x, y, _ix = next(it)
+                    loss = step(x, y)
+                    avg.add(loss.detach(), len(y))
+                    # clone: a graph replay overwrites its static outputs next step
+                    met.add(trainer.score(step.last_out, step.last_pred).detach().clone(), y)
+                    nsamp += len(y)
+                    continue
+                trainer.flat.zero_grad()
+                if hasattr(engine, "sync_enabled"):
+                    engine.sync_enabled = False
+                with engine.step_context():
+                    for k in range(li):
+                        try:
+                            x, y, ix = next(it)
+                        except StopIteration:
+                            it = iter(tr)
+                            x, y, ix = next(it)
+                        if hasattr(engine, "sync_enabled"):
+                            engine.sync_enabled = k == li - 1
+                        out = trainer.iteration({"inputs": x, "labels": y, "ix": ix})
+                        (out["loss"] / li).backward()
+                        avg.accumulate(out["averages"])
+                        met.accumulate(out["metrics"])
+                        nsamp += len(y)
+                scale = engine.reduce()
+                trainer.optimizer.step(grad_scale=scale)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            dt = time.time() - t0
+            itd.append(dt / max(steps, 1))
+            tl.append([round(avg.average, 6)] + met.get((monitor if monitor != "loss" else "auc",)))
+            logs.setdefault(f"{tag}samples_per_sec", []).append(nsamp / dt if dt > 0 else 0.0)
+            stop = False
+            if epoch % val_every == 0:
+                if group is self.group:
+                    r = self.global_eval(trainer, va)
+                else:
+                    res = trainer.evaluate(va)
+                    r = {"loss": res["averages"].average, "scores": res["metrics"].scores(),
+                         "local_loss": res["averages"].average, "local_scores": res["metrics"].scores()}
+                score = r["loss"] if monitor.lower() == "loss" else metric_value(r["scores"], monitor)
+                vl.append([round(r["loss"], 6), round(score, 6)])
+                lvl.append([round(r["local_loss"], 6),
+                            round(r["local_loss"] if monitor.lower() == "loss"
+                                  else metric_value(r["local_scores"], monitor), 6)])
+                if improved(score, best["score"], direction):
+                    best.update(score=score, epoch=epoch, wait=0)
+                    trainer.save_checkpoint(os.path.join(fold_dir, f"{tag}checkpoint_best.pt"),
+                                            epoch=epoch, best_val_epoch=epoch, best_val_score=score)
+                else:
+                    best["wait"] += 1
+                    if best["wait"] >= patience:
+                        stop = True
+                self.log(f"{tag}epoch {epoch} train_loss {avg.average:.4f} val_loss {r['loss']:.4f} "
+                         f"val_{monitor} {score:.4f} best@{best['epoch']}")
+                if cfg.get("checkpoint_every_validation", True):
+                    trainer.save_checkpoint(os.path.join(fold_dir, f"{tag}checkpoint_last.pt"),
+                                            epoch=epoch, best=dict(best), logs=None)
+                if cfg.get("check_replicas") and group.distributed and engine.name != "dSGD-local":
+                    ok = self._replica_checksum(trainer)
+                    logs.setdefault("replica_check", []).append(bool(ok))
+            comp.append(time.time() - t0)
+            cum.append(time.time() - t_run)
+            if stop:
+                logs[f"{tag}stopped_epoch"] = epoch
+                break
+        if best["score"] is None:  # no validation happened: keep the last model as "best"
+            trainer.save_checkpoint(os.path.join(fold_dir, f"{tag}checkpoint_best.pt"),
+                                    epoch=epochs, best_val_epoch=epochs, best_val_score=None)
+            best["epoch"] = epochs
+        logs[f"{tag}best_val_epoch"] = best["epoch"]
+        logs[f"{tag}best_val_score"] = best["score"]
+        return best
+
+    def _pretrain(self, trainer: NNTrainer, data, fold_dir: str, seed: int, logs: Dict[str, Any]):
+        sizes = self.group.all_gather_object(int(data["train"][0].shape[0]))
+        src = max(range(len(sizes)), key=lambda r: (sizes[r], -r))
+        logs["pretrain_site"] = f"local{src}"
+        pa = dict(self.cfg.get("pretrain_args") or {})
+        if self.group.rank == src and int(pa.get("epochs", 0)) > 0:
+            pcfg = copy.deepcopy(self.cfg)
+            pcfg.update(pa)
+            from ..parallel import DSGDEngine
+            from ..parallel.group import SiteGroup as _SG
+            solo = _SG(device=self.device)
+            trainer.optimizer.lr = float(pa.get("learning_rate", trainer.optimizer.lr))
+            eng = DSGDEngine(trainer.modules(), trainer.flat, solo, pcfg, overlap=False)
+            eng.name = "dSGD-local"
+            self.log(f"pretraining alone on {sizes[src]} samples for {pa.get('epochs')} epochs")
+            b = self._train_epochs(trainer, eng, data, pcfg, solo, fold_dir, seed, logs, tag="pretrain_")
+            trainer.load_checkpoint(os.path.join(fold_dir, "pretrain_checkpoint_best.pt"))
+            logs["pretrain_best_val_epoch"] = b["epoch"]
+        self._broadcast_model(trainer, src)
+        # fresh optimizer state for the federated phase
+        trainer._init_optimizer()
+
+    # ---- folds ------------------------------------------------------------------------------
+    def run_fold(self, fold: int, split: Dict[str, List[Any]]) -> Dict[str, Any]:
+        cfg = self.cfg
+        t_fold = time.time()
+        fdir = L.fold_dir(self.out_dir, self.site, self.task_id, fold)
+        seed = site_seed(cfg, self.group.rank) + 7919 * fold
+        data = self._datasets(split)
+        logs: Dict[str, Any] = {
+            "task_id": self.task_id, "agg_engine": cfg.get("agg_engine"), "fold": fold,
+            "site": self.site, "rank": self.group.rank, "num_sites": self.group.world,
+            "log_header": cfg.get("log_header"), "mode": cfg.get("mode"),
+            "split_sizes": {k: int(v[1].shape[0]) for k, v in data.items()},
+            "device": str(self.device),
+        }
+        trainer = self.Trainer(cache=cfg, state=self.state, device=self.device)
+        trainer.init_nn(seed=int(cfg.get("seed", 0) or 0) + fold)  # same init on every site
+        self._broadcast_model(trainer, 0)
+        start_epoch, best = 1, None
+        last = os.path.join(fdir, "checkpoint_last.pt")
+        if cfg.get("mode") == "test":
+            path = cfg.get("pretrained_path") or os.path.join(fdir, "checkpoint_best.pt")
+            trainer.load_checkpoint(path)
+            best = {"epoch": 0, "score": None}
+        else:
+            if cfg.get("resume") and os.path.exists(last):
+                st = trainer.load_checkpoint(last, load_optimizer=True)
+                start_epoch = int(st.get("epoch", 0)) + 1
+                best = st.get("best")
+                self.log(f"resuming fold {fold} at epoch {start_epoch}")
+            elif cfg.get("pretrain"):
+                self._pretrain(trainer, data, fdir, seed, logs)
+            engine = make_engine(str(cfg.get("agg_engine", "dSGD")), trainer.modules(), trainer.flat,
+                                 self.group, cfg)
+            best = self._train_epochs(trainer, engine, data, cfg, self.group, fdir, seed, logs,
+                                      start_epoch=start_epoch, best=best)
+            if hasattr(engine, "close"):
+                engine.close()
+            trainer.load_checkpoint(os.path.join(fdir, "checkpoint_best.pt"))
+        te = self._loader(*data["test"], "test", int(cfg.get("batch_size", 16)), seed)
+        r = self.global_eval(trainer, te)
+        logs["test_metrics"] = L.test_row(r["loss"], r["scores"])
+        logs["local_test_metrics"] = L.test_row(r["local_loss"], r["local_scores"])
+        logs["test_scores"] = r["scores"]
+        logs["test_header"] = L.TEST_HEADER
+        logs["fold_duration"] = time.time() - t_fold
+        L.write_logs(fdir, logs)
+        L.write_test_metrics(fdir, [logs["local_test_metrics"]])
+        if self.group.is_master:
+            rdir = L.fold_dir(self.out_dir, "remote", self.task_id, fold)
+            rlogs = {k: v for k, v in logs.items() if not k.startswith("local_")}
+            rlogs["remote_iter_duration"] = logs.get("local_iter_duration", [])  # NB.ipynb:860
+            rlogs["site"] = "remote"
+            rlogs["sites"] = [f"local{i}" for i in range(self.group.world)]
+            L.write_logs(rdir, rlogs)
+            L.write_test_metrics(rdir, [logs["test_metrics"]])
+            L.zip_results(rdir, os.path.join(rdir, f"{self.task_id}_fold_{fold}_results.zip"))
+        self.log(f"fold {fold} test: loss {r['loss']:.4f} " +
+                 " ".join(f"{k} {v:.4f}" for k, v in r["scores"].items()))
+        return logs
+
+    def run(self) -> List[Dict[str, Any]]:
+        set_seed(site_seed(self.cfg, self.group.rank))
+        handle = self.DataHandle(cache=self.cfg, state=self.state)
+        files = handle.list_files()
+        splits = make_splits(files, self.cfg, site_seed(self.cfg, self.group.rank),
+                             base=self.state.get("baseDirectory", "."))
+        nfolds = self._global_max(len(splits))
+        if nfolds != len(splits):
+            raise RuntimeError("all sites must run the same number of folds")
+        return [self.run_fold(k, s) for k, s in enumerate(splits)]

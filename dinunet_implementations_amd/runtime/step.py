@@ -93,6 +93,8 @@ class TrainStep:
                 return loss
             self._capture(x, y)
         sx, sy, out, loss, pred = self.static
+        if sx.shape != x.shape or sy.shape != y.shape:  # e.g. a ragged last batch
+            return self._eager(x, y)
         if sx.data_ptr() != x.data_ptr():
             sx.copy_(x, non_blocking=True)
             sy.copy_(y, non_blocking=True)

@@ -1,0 +1,150 @@
+"""Trainer base — the ``COINNTrainer`` role.
+
+A task plugin subclasses :class:`NNTrainer` exactly like the reference's
+``FreeSurferTrainer(COINNTrainer)`` (``comps/fs/__init__.py:42-63``): it registers modules in
+``self.nn`` from ``_init_nn_model`` and implements ``iteration(batch)`` returning
+``{'out', 'loss', 'averages', 'metrics', ...}``.  The base owns device placement, the flat
+fp32 parameter buffer + fused Adam (``learning_rate``), evaluation, checkpoints with the
+reference ``state_dict`` key names, and the fast training step.
+
+Fast path: a plugin that implements ``forward_loss(x, y) -> (out, loss, pred)`` and
+``score(out, pred)`` gets the HIP-graph-captured :class:`runtime.step.TrainStep`; any other
+plugin trains through ``iteration`` eagerly (still on the fused kernels).
+"""
+from __future__ import annotations
+
+import os
+import random
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ..ops import FlatParams, FusedAdam
+from ..utils.metrics import Averages, Metrics
+
+
+def set_seed(seed: int):
+    random.seed(seed)
+    np.random.seed(seed % (2 ** 32))
+    torch.manual_seed(seed)
+
+
+class NNTrainer:
+    def __init__(self, cache: Optional[Dict[str, Any]] = None, state: Optional[Dict[str, Any]] = None,
+                 device=None, **kw):
+        self.cache = cache if cache is not None else {}
+        self.state = state if state is not None else {}
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.device = {"gpu": dev}
+        self.nn: Dict[str, nn.Module] = {}
+        self.flat: Optional[FlatParams] = None
+        self.optimizer: Optional[FusedAdam] = None
+
+    # ---- plugin hooks ------------------------------------------------------------------------
+    def _init_nn_model(self):
+        raise NotImplementedError
+
+    def iteration(self, batch) -> Dict[str, Any]:
+        """Default iteration for plugins that implement ``forward_loss``."""
+        x = batch["inputs"].to(self.device["gpu"], non_blocking=True)
+        y = batch["labels"].to(self.device["gpu"], non_blocking=True).long()
+        out, loss, pred = self.forward_loss(x, y)
+        m = self.new_metrics()
+        m.add(self.score(out, pred), y)
+        a = self.new_averages()
+        a.add(loss.detach(), len(x))
+        return {"out": out, "loss": loss, "averages": a, "metrics": m, "prediction": pred,
+                "indices": batch.get("ix")}
+
+    def forward_loss(self, x, y):  # pragma: no cover - optional fast path
+        raise NotImplementedError
+
+    def score(self, out, pred):
+        return pred
+
+    @property
+    def has_fast_path(self) -> bool:
+        return type(self).forward_loss is not NNTrainer.forward_loss
+
+    # ---- framework -----------------------------------------------------------------------------
+    def new_metrics(self) -> Metrics:
+        return Metrics(int(self.cache.get("num_class", 2)))
+
+    def new_averages(self) -> Averages:
+        return Averages()
+
+    def init_nn(self, init_model: bool = True, init_optimizer: bool = True, seed: Optional[int] = None):
+        if seed is not None:
+            set_seed(seed)
+        if init_model:
+            self.nn = {}
+            self._init_nn_model()
+            for k in self.nn:
+                self.nn[k] = self.nn[k].to(self.device["gpu"])
+        if init_optimizer:
+            self._init_optimizer()
+
+    def parameters(self):
+        for k in sorted(self.nn):
+            yield from self.nn[k].parameters()
+
+    def _init_optimizer(self, lr: Optional[float] = None):
+        self.flat = FlatParams(self.parameters(), device=self.device["gpu"])
+        lr = float(lr if lr is not None else self.cache.get("learning_rate", 1e-3))
+        self.optimizer = FusedAdam(self.flat, lr=lr, weight_decay=float(self.cache.get("weight_decay", 0.0)))
+
+    def modules(self) -> nn.Module:
+        """All registered modules as one container (engines walk ``.modules()``)."""
+        return nn.ModuleDict({k: v for k, v in self.nn.items()})
+
+    def train(self):
+        for m in self.nn.values():
+            m.train()
+
+    def eval(self):
+        for m in self.nn.values():
+            m.eval()
+
+    @torch.no_grad()
+    def evaluate(self, loader) -> Dict[str, Any]:
+        """Run ``iteration`` over a loader; returns merged averages/metrics and predictions."""
+        self.eval()
+        avg, met = self.new_averages(), self.new_metrics()
+        outs = []
+        for x, y, ix in loader:
+            it = self.iteration({"inputs": x, "labels": y, "ix": ix})
+            avg.accumulate(it["averages"])
+            met.accumulate(it["metrics"])
+            outs.append(it["out"].detach())
+        self.train()
+        return {"averages": avg, "metrics": met, "out": torch.cat(outs) if outs else None}
+
+    # ---- checkpoints (reference state_dict key names) -------------------------
+    def checkpoint_state(self, **extra) -> Dict[str, Any]:
+        st = {"models": {k: {n: t.detach().cpu() for n, t in v.state_dict().items()}
+                         for k, v in self.nn.items()}}
+        if self.optimizer is not None:
+            st["optimizer"] = self.optimizer.state_dict()
+        st.update(extra)
+        return st
+
+    def save_checkpoint(self, path: str, **extra):
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        tmp = path + ".tmp"
+        torch.save(self.checkpoint_state(**extra), tmp)
+        os.replace(tmp, path)
+
+    def load_checkpoint(self, path: str, load_optimizer: bool = False) -> Dict[str, Any]:
+        st = torch.load(path, map_location="cpu", weights_only=True)
+        self.load_state(st, load_optimizer)
+        return st
+
+    def load_state(self, st: Dict[str, Any], load_optimizer: bool = False):
+        models = st.get("models", st)
+        for k, sd in models.items():
+            if k in self.nn:
+                self.nn[k].load_state_dict(sd)
+        if load_optimizer and self.optimizer is not None and "optimizer" in st:
+            self.optimizer.load_state_dict(st["optimizer"])

@@ -1,0 +1,107 @@
+"""FS-Classification plugin (reference ``comps/fs/__init__.py``).
+
+Same classes and hooks as the reference — ``FreeSurferDataset`` (``load_index`` /
+``__getitem__``), ``FreeSurferTrainer`` (``_init_nn_model`` / ``iteration``), ``FSVDataHandle``
+(``list_files``) — with two MI355X-first changes: every subject's stats file is parsed and
+max-normalised ONCE into an fp32 tensor held in HBM (the reference re-parses the CSV per sample
+per epoch, ``comps/fs/__init__.py:33-39``), and the loss/metric path never syncs the host
+(``loss.item()`` at ``comps/fs/__init__.py:61`` becomes a device-side running sum).
+"""
+from __future__ import annotations
+
+import csv
+import os
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+
+from .. import ops
+from ..data.base import SiteDataHandle, SiteDataset
+from ..models import MSANNet
+from ..runtime.trainer import NNTrainer
+
+
+def read_stats_file(path: str) -> Tuple[List[str], List[float]]:
+    """FreeSurfer aseg stats: header ``Measure:volume\\t<subject>`` then ``<region>\\t<value>``."""
+    names, vals = [], []
+    with open(path) as f:
+        next(f, None)
+        for line in f:
+            line = line.strip()
+            if not line:
+                continue
+            parts = line.split("\t") if "\t" in line else line.split()
+            names.append(parts[0])
+            vals.append(float(parts[-1]))
+    return names, vals
+
+
+def _parse_label(v) -> int:
+    if isinstance(v, str):
+        s = v.strip().lower()
+        if s in ("true", "false"):
+            return int(s == "true")
+        return int(float(s))
+    return int(v)
+
+
+class FreeSurferDataset(SiteDataset):
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.labels: Optional[Dict[str, Any]] = None
+
+    def _read_labels(self):
+        path = os.path.join(self.state.get("baseDirectory", "."), self.cache["labels_file"])
+        with open(path, newline="") as f:
+            rows = list(csv.DictReader(f))
+        key = self.cache.get("data_column")
+        if not rows or key not in rows[0]:
+            key = list(rows[0].keys())[0] if rows else None
+        self.labels = {r[key]: r for r in rows}
+
+    def load_index(self, file):
+        if self.labels is None:
+            self._read_labels()
+        y = _parse_label(self.labels[file][self.cache["labels_column"]])
+        self.indices.append([file, int(y)])
+
+    def __getitem__(self, ix):
+        file, y = self.indices[ix]
+        _, vals = read_stats_file(os.path.join(self.path(), file))
+        x = torch.tensor(vals, dtype=torch.float64)
+        x = x / x.max()  # per-subject max normalisation (quirk A8: MaskVol)
+        return {"inputs": x, "labels": torch.tensor(y), "ix": torch.tensor(ix)}
+
+    def materialize(self, device=None):
+        X = torch.stack([self[i]["inputs"].float() for i in range(len(self))]) if self.indices \
+            else torch.zeros(0, int(self.cache.get("input_size", 66)))
+        y = torch.tensor([int(v[1]) for v in self.indices], dtype=torch.long)
+        return (X.to(device), y.to(device)) if device is not None else (X, y)
+
+
+class FreeSurferTrainer(NNTrainer):
+    def _init_nn_model(self):
+        self.nn["fs_net"] = MSANNet(in_size=self.cache["input_size"],
+                                    hidden_sizes=self.cache["hidden_sizes"],
+                                    out_size=self.cache["num_class"],
+                                    dropout_in=self.cache.get("dropout_in", []))
+
+    def forward_loss(self, x, y):
+        logits = self.nn["fs_net"](x.float())
+        return ops.log_softmax_nll(logits, y)
+
+    def score(self, out, pred):
+        return pred  # metrics on hard argmax labels (comps/fs/__init__.py:57-59, quirk A10)
+
+
+class FSVDataHandle(SiteDataHandle):
+    def list_files(self):
+        path = os.path.join(self.state.get("baseDirectory", "."), self.cache["labels_file"])
+        with open(path, newline="") as f:
+            rows = list(csv.DictReader(f))
+        key = self.cache.get("data_column")
+        if not rows:
+            return []
+        if key not in rows[0]:
+            key = list(rows[0].keys())[0]
+        return [r[key] for r in rows]

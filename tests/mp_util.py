@@ -1,0 +1,54 @@
+"""Spawn a gloo process group on CPU (127.0.0.1) and collect per-rank results."""
+import os
+import pickle
+import socket
+import tempfile
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _entry(rank, world, port, fn, args, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    os.environ.setdefault("OMP_NUM_THREADS", "2")
+    import torch
+    torch.set_num_threads(2)
+    from dinunet_implementations_amd.parallel import init_sites, shutdown
+    res = None
+    try:
+        grp = init_sites(backend="gloo", device="cpu")
+        res = ("ok", fn(grp, *args))
+        shutdown()
+    except Exception:  # pragma: no cover - surfaced by the parent
+        res = ("err", traceback.format_exc())
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)
+
+
+def run_world(fn, world, *args):
+    outdir = tempfile.mkdtemp()
+    # spawn (not fork): the pytest parent has live OpenMP/autograd threads; workers must be
+    # module-level functions of an importable test module
+    mp.start_processes(_entry, args=(world, free_port(), fn, args, outdir), nprocs=world,
+                       join=True, start_method="spawn")
+    out, errs = [], []
+    for r in range(world):
+        with open(os.path.join(outdir, f"r{r}.pkl"), "rb") as f:
+            status, val = pickle.load(f)
+        if status != "ok":
+            errs.append(f"rank {r} failed:\n{val}")
+        out.append(val)
+    if errs:
+        # the root cause is usually the one that is NOT a gloo "connection closed" echo
+        errs.sort(key=lambda e: "Connection closed" in e)
+        raise AssertionError("\n".join(errs))
+    return out

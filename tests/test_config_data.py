@@ -1,0 +1,133 @@
+"""Config precedence/flattening, FS/ICA data semantics, splits, loader (CPU)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from dinunet_implementations_amd.config import (build_config, compspec_defaults, generate_compspec,
+                                                load_inputspec, unwrap_values)
+from dinunet_implementations_amd.data.loader import DeviceLoader
+from dinunet_implementations_amd.data.splits import kfold_splits, make_splits, ratio_split
+from dinunet_implementations_amd.ops.reference import ica_windows
+from dinunet_implementations_amd.tasks import (FreeSurferDataset, FSVDataHandle, ICADataHandle,
+                                               ICADataset, read_stats_file)
+
+
+def test_precedence_and_flatten():
+    # kwargs (local.py-style defaults) < site input; task args flattened (compspec.json:225-250)
+    c = build_config(site_input={"epochs": {"value": 7}}, epochs=21, batch_size=16)
+    assert c["epochs"] == 7 and c["batch_size"] == 16
+    assert c["input_size"] == 66 and c["hidden_sizes"] == [256, 128, 64, 32]
+    assert c["labels_column"] == "isControl"
+    assert "FS-Classification_args" not in c
+
+
+def test_ica_names_and_aliases():
+    c = build_config(site_input={"task_id": "ICA-Classification", "hidden_size": 348})
+    assert c["hidden_size"] == 348 and c["num_components"] == 100 and c["temporal_size"] == 980
+    c2 = build_config(site_input={"task_id": "ICA-Classification",
+                                  "ICA-Classification_args": {"full_comp_size": 53}})
+    assert c2["num_components"] == 53
+
+
+def test_validation_errors():
+    with pytest.raises(ValueError):
+        build_config(site_input={"agg_engine": "fedavg"})
+    with pytest.raises(ValueError):
+        build_config(site_input={"split_ratio": [0.5, 0.2]})
+
+
+def test_compspec_roundtrip_has_reference_keys():
+    spec = generate_compspec()
+    keys = set(spec["computation"]["input"])
+    for k in ["task_id", "mode", "agg_engine", "num_reducers", "batch_size", "local_iterations",
+              "learning_rate", "epochs", "pretrain", "pretrain_args", "validation_epochs",
+              "precision_bits", "pin_memory", "num_workers", "patience", "split_ratio",
+              "num_folds", "FS-Classification_args", "ICA-Classification_args"]:
+        assert k in keys, k
+    d = compspec_defaults(spec)
+    assert d["agg_engine"] == "dSGD" and d["precision_bits"] == "32"
+
+
+def test_reference_inputspec(fs_data_root):
+    specs = load_inputspec(os.path.join(fs_data_root, "inputspec.json"))
+    assert len(specs) == 5
+    assert specs[0]["labels_column"] == "isControl"
+    assert unwrap_values({"a": {"value": 3}, "b": 4}) == {"a": 3, "b": 4}
+
+
+def test_fs_dataset_semantics(fs_data_root):
+    cfg = build_config(site_input=load_inputspec(os.path.join(fs_data_root, "inputspec.json"))[0])
+    state = {"baseDirectory": os.path.join(fs_data_root, "input", "local0", "simulatorRun")}
+    files = FSVDataHandle(cache=cfg, state=state).list_files()
+    ds = FreeSurferDataset(cache=cfg, state=state)
+    ds.add(files[:10])
+    it = ds[0]
+    assert it["inputs"].shape == (66,) and it["inputs"].dtype == torch.float64
+    assert float(it["inputs"].max()) == 1.0  # per-subject max normalisation (A8)
+    assert int(it["labels"]) in (0, 1)
+    names, vals = read_stats_file(os.path.join(state["baseDirectory"], files[0]))
+    assert len(names) == 66 and names[int(np.argmax(vals))] == "MaskVol"  # MaskVol is the max
+    X, y = ds.materialize()
+    assert X.shape == (10, 66) and X.dtype == torch.float32 and y.shape == (10,)
+
+
+def test_ica_windows_quirk():
+    d = torch.arange(2 * 3 * 40, dtype=torch.float32).view(2, 3, 40)
+    w = ica_windows(d, window_size=10, window_stride=5, temporal_size=40)
+    # S from the window SIZE (4), offsets from the STRIDE (0,5,10,15): A9
+    assert w.shape == (2, 4, 3, 10)
+    assert torch.equal(w[1, 2], d[1, :, 10:20])
+
+
+def test_ica_dataset_npy_and_npz(tmp_path):
+    x = np.random.randn(6, 4, 50).astype(np.float32)
+    np.save(tmp_path / "d.npy", x)
+    np.savez(tmp_path / "d.npz", data=x)
+    with open(tmp_path / "lab.csv", "w") as f:
+        f.write("idx,label\n" + "\n".join(f"{i},{i % 2}" for i in range(6)))
+    for fn in ("d.npy", "d.npz"):
+        cfg = {"window_size": 10, "window_stride": 10, "temporal_size": 50, "num_components": 4,
+               "data_file": fn, "labels_file": "lab.csv"}
+        st = {"baseDirectory": str(tmp_path)}
+        files = ICADataHandle(cache=cfg, state=st).list_files()
+        assert files[3] == [3, 1]
+        ds = ICADataset(cache=cfg, state=st)
+        ds.add(files)
+        X, y = ds.materialize()
+        assert X.shape == (6, 5, 4, 10) and torch.equal(y, torch.tensor([0, 1, 0, 1, 0, 1]))
+        assert np.allclose(X[2, 1].numpy(), x[2, :, 10:20])
+
+
+def test_splits_deterministic():
+    items = list(range(100))
+    a = ratio_split(items, [0.7, 0.15, 0.15], seed=3)
+    b = ratio_split(items, [0.7, 0.15, 0.15], seed=3)
+    assert a == b and len(a["train"]) == 70 and len(a["validation"]) == 15 and len(a["test"]) == 15
+    assert sorted(a["train"] + a["validation"] + a["test"]) == items
+    folds = kfold_splits(items, 5, seed=1)
+    assert len(folds) == 5
+    tests = sorted(x for f in folds for x in f["test"])
+    assert tests == items  # every sample tested exactly once
+    for f in folds:
+        assert not set(f["train"]) & set(f["test"]) and not set(f["validation"]) & set(f["test"])
+
+
+def test_split_files(tmp_path):
+    p = tmp_path / "s.json"
+    p.write_text(json.dumps({"train": [1, 2], "validation": [3], "test": [4]}))
+    s = make_splits([1, 2, 3, 4], {"split_files": [str(p)]}, 0)
+    assert s == [{"train": [1, 2], "validation": [3], "test": [4]}]
+
+
+def test_device_loader():
+    X = torch.arange(10).float().view(10, 1)
+    y = torch.arange(10)
+    dl = DeviceLoader(X, y, 4, shuffle=True, drop_last=True, seed=0)
+    assert len(dl) == 2
+    seen = [int(v) for _, yy, _ in dl for v in yy]
+    assert len(seen) == 8 and len(set(seen)) == 8
+    dl2 = DeviceLoader(X, y, 4, shuffle=False, drop_last=False)
+    assert [len(b[1]) for b in dl2] == [4, 4, 2]
