@@ -26,6 +26,17 @@
 // dW_ih = dpre^T x, dW_hh = dpre^T h_{t-1} that run after it on the full chip.
 #include "common.h"
 
+#ifdef DN_STAMPS
+// diagnostic build only (tools/lstm_stamps.py): per-wave phase cycle sums
+__device__ unsigned long long* dn_stamp_buf;
+DN_API int dn_set_stamp_buf(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(dn_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+#define STAMP(v) do { __builtin_amdgcn_sched_barrier(0); \
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) :: "memory"); \
+  __builtin_amdgcn_sched_barrier(0); } while (0)
+#endif
+
 namespace {
 
 template <typename XT> struct Gate4Raw;
@@ -120,7 +131,13 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
     for (int mt = 0; mt < 4; ++mt) xn[mt] = *reinterpret_cast<const f32x4*>(xrow + (long)tau0 * rowX + 16 * mt);
   }
   int cur = 0;
+#ifdef DN_STAMPS
+  unsigned long long st_a = 0, st_b = 0, st_c = 0, ts0, ts1, ts2, ts3;
+#endif
   for (int t = 0; t < S; ++t) {
+#ifdef DN_STAMPS
+    STAMP(ts0);
+#endif
     const int tau = dir == 0 ? t : S - 1 - t;
     const int t1 = t + 1 < S ? t + 1 : t;
     const int tau1 = dir == 0 ? t1 : S - 1 - t1;
@@ -140,6 +157,10 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
     }
     // gates + cell update: lane-local (unit u = 16w + 4mt + q, row b), 4 gates in acc regs
     const int nxt = cur ^ 1;
+#ifdef DN_STAMPS
+    { float z = acc[0][0] + acc[1][0] + acc[2][0] + acc[3][0]; asm volatile("" :: "v"(z)); }
+    STAMP(ts1);
+#endif
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int u = 16 * w + 4 * mt + q;
@@ -162,9 +183,22 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
       hl[mt] = h;
       hbuf[nxt][bl][u] = (bf16)h;
     }
+#ifdef DN_STAMPS
+    STAMP(ts2);
+#endif
     __syncthreads();
+#ifdef DN_STAMPS
+    STAMP(ts3);
+    st_a += ts1 - ts0; st_b += ts2 - ts1; st_c += ts3 - ts2;
+#endif
     cur = nxt;
   }
+#ifdef DN_STAMPS
+  if (lane == 0 && blockIdx.x == 0) {
+    unsigned long long* o = dn_stamp_buf + (blockIdx.y * 64 + w) * 4;
+    o[0] = st_a; o[1] = st_b; o[2] = st_c; o[3] = S;
+  }
+#endif
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
     const int u = 16 * w + 4 * mt + q;
@@ -251,7 +285,13 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   __syncthreads();
 
   int cur = 0;
+#ifdef DN_STAMPS
+  unsigned long long st_a = 0, st_b = 0, st_c = 0, ts0, ts1, ts2, ts3;
+#endif
   for (int t = S - 1; t >= 0; --t) {
+#ifdef DN_STAMPS
+    STAMP(ts0);
+#endif
     const int tau = dir == 0 ? t : S - 1 - t;
     f32x4 pc[4];
 #pragma unroll
@@ -290,6 +330,10 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
       acc = mfma16(ks < NRK ? af[ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db, acc);
     }
     const int nxt = cur ^ 1;
+#ifdef DN_STAMPS
+    { float z = acc[0] + acc[1] + acc[2] + acc[3]; asm volatile("" :: "v"(z)); }
+    STAMP(ts1);
+#endif
     bf16x8 lo, hi;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -316,9 +360,22 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     *reinterpret_cast<bf16x8*>(&dbuf[nxt][bl][4 * u0 + 8]) = hi;
     *reinterpret_cast<bf16x8*>(drow + (long)tau * rowX) = lo;
     *reinterpret_cast<bf16x8*>(drow + (long)tau * rowX + 8) = hi;
+#ifdef DN_STAMPS
+    STAMP(ts2);
+#endif
     __syncthreads();
+#ifdef DN_STAMPS
+    STAMP(ts3);
+    st_a += ts1 - ts0; st_b += ts2 - ts1; st_c += ts3 - ts2;
+#endif
     cur = nxt;
   }
+#ifdef DN_STAMPS
+  if (lane == 0 && blockIdx.x == 0) {
+    unsigned long long* o = dn_stamp_buf + (256 + blockIdx.y * 64 + w) * 4;
+    o[0] = st_a; o[1] = st_b; o[2] = st_c; o[3] = S;
+  }
+#endif
 }
 
 // deterministic column sums of a bf16 [N][C] matrix into slab partials [slabs][C] (fp32)
