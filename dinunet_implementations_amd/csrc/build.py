@@ -32,7 +32,7 @@ HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", shutil.which("g++") or "c++")
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
-             "-munsafe-fp-atomics", "-Wno-unused-result"]
+             "-munsafe-fp-atomics", "-fno-slp-vectorize", "-Wno-unused-result"]
 
 
 def _sources(kind: str):

@@ -15,12 +15,20 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // Error codes returned by every launcher (0 = launched).
 enum DnStatus { DN_OK = 0, DN_BAD_SHAPE = 1, DN_LAUNCH_FAILED = 2, DN_UNSUPPORTED = 3 };
 
-__device__ __forceinline__ float dn_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+// Transcendentals on the hardware units: v_exp_f32 (2^x) and v_rcp_f32 (1 ulp).  A plain
+// `1.f / y` compiles to the ~10-instruction IEEE division sequence (v_div_scale/fmas/fixup),
+// which made the LSTM gate phase VALU-bound at 2x the necessary instruction count.
+__device__ __forceinline__ float dn_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float dn_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
-// tanh via one exp + one rcp; saturates cleanly to +-1 for large |x|.
+constexpr float DN_LOG2E = 1.4426950408889634f;
+
+// sigmoid(x) = 1 / (1 + 2^(-x log2 e)); saturates to 0 / 1 (rcp(inf) = 0)
+__device__ __forceinline__ float dn_sigmoid(float x) { return dn_rcp(1.f + dn_exp2(-DN_LOG2E * x)); }
+
+// tanh(x) = 1 - 2 / (2^(2x log2 e) + 1); saturates cleanly to +-1 for large |x|
 __device__ __forceinline__ float dn_tanh(float x) {
-  float e = __expf(2.f * x);
-  return 1.f - 2.f / (e + 1.f);
+  return 1.f - 2.f * dn_rcp(dn_exp2((2.f * DN_LOG2E) * x) + 1.f);
 }
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {

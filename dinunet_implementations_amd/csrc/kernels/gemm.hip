@@ -5,9 +5,11 @@
 // * op(A): A stored [M][lda] (k contiguous) or, with TA, [K][lda] (m contiguous); same for B
 //   (TB: [N][ldb] k contiguous, else [K][ldb] n contiguous).  Operands may be fp32 or bf16: fp32
 //   is rounded to bf16 while staging, so an fp32 activation never needs a separate cast kernel.
-// * Tiles are staged global -> VGPR -> LDS (k-contiguous, +16 B row pad: the 16-lane groups of
-//   ds_read_b128 hit distinct bank quads), double-buffered with the next tile's global loads in
-//   flight during the current tile's MFMAs (16x16x32 bf16, fp32 accumulators).
+// * Tiles are staged global -> VGPR (16 B vectors along the contiguous axis) -> LDS in the
+//   operand's own layout, double-buffered with the next tile's global loads in flight during the
+//   current tile's MFMAs (16x16x32 bf16, fp32 accumulators).  k-major operands are turned into
+//   MFMA fragments by the CDNA4 LDS transpose read (ds_read_b64_tr_b16), so no layout costs a
+//   register shuffle.
 // * Small/skinny problems (the ICA shapes: M = B*S = 3136, N <= 1536) use 64x64 tiles to put
 //   >= 200 workgroups on the 256 CUs; long-K weight-gradient GEMMs (K = B*S) split K across
 //   workgroups into fp32 slabs reduced by a second, deterministic kernel (no float atomics, so
@@ -20,99 +22,105 @@ namespace {
 
 template <typename T> __device__ __forceinline__ bf16 to_bf(T v) { return (bf16)v; }
 
-template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe>
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// LDS images, by the operand's memory layout:
+//  k-contiguous (A with !TA, B with TB): [rows][64 + 8] bf16; a fragment = one ds_read_b128.
+//  k-major      (A with TA,  B with !TB): [64 k][cols + 16] bf16, filled with 16 B vectors
+//    along cols; a fragment = two ds_read_b64_tr_b16 (4 k each, hardware transpose).  The row
+//    stride is 8 * odd banks and k-rows are stored with bit 2 flipped in odd 8-row groups, so
+//    each 32-lane half touches 8 distinct rows mod 8 -> conflict-free transposed reads.
+template <int ROWS, bool KCONTIG> struct Img {
+  static constexpr int R = KCONTIG ? ROWS : 64;          // image rows
+  static constexpr int C = KCONTIG ? 64 + 8 : ROWS + 16; // image row length (elements)
+  static constexpr int ELEMS = R * C;
+};
+
+template <int BM, int BN, bool TA, bool TB>
 struct GemmTile {
-  static constexpr int BK = 32;
-  static constexpr int LDK = BK + 8;
+  static constexpr int BK = 64;
   static constexpr int NT = 256;
   static constexpr int WM = BM / 2, WN = BN / 2;   // 2x2 waves
   static constexpr int FM = WM / 16, FN = WN / 16;  // 16x16 frags per wave
   static constexpr int A_ELEMS = BM * BK / NT;      // elements each thread stages per tile
   static constexpr int B_ELEMS = BN * BK / NT;
+  typedef Img<BM, !TA> IA;
+  typedef Img<BN, TB> IB;
 };
 
-// Stage one operand tile (rows x BK, logical [row][k]) into registers as bf16.
-// KCONTIG: element (r,k) at base[r*ld + k] (vector along k); else at base[k*ld + r] (along r).
+// Stage one operand tile (ROWS x 64 logical [row][k]) into registers as bf16, 8 elements per
+// 16 B vector (fp32 sources are rounded while staging).
+//  KCONTIG: element (r,k) at base[r*ld + k]; chunk -> (row, 8 consecutive k)
+//  else   : element (r,k) at base[k*ld + r]; chunk -> (k, 8 consecutive rows)
 template <int ROWS, bool KCONTIG, typename TE>
 __device__ __forceinline__ void stage_load(const TE* __restrict__ base, long ld, int row0, int k0,
-                                           int nrows, int K, int tid, bf16 (&reg)[ROWS * 32 / 256]) {
-  constexpr int PER = ROWS * 32 / 256;  // 8 or 16
-  if constexpr (KCONTIG) {
-    // thread -> (row, 8-wide k chunk); PER/8 chunks per thread
+                                           int nrows, int K, int tid, bf16 (&reg)[ROWS * 64 / 256]) {
+  constexpr int PER = ROWS * 64 / 256;  // 16 or 32
+  constexpr int CPR = KCONTIG ? 8 : ROWS / 8;  // chunks per image row
 #pragma unroll
-    for (int c = 0; c < PER / 8; ++c) {
-      const int idx = tid + c * 256;
-      const int r = idx >> 2, kk = (idx & 3) * 8;
-      const int gr = row0 + r, gk = k0 + kk;
-      const TE* p = base + (long)gr * ld + gk;
-      if (gr < nrows && gk + 8 <= K && ((((uintptr_t)p) & (sizeof(TE) * 8 - 1)) == 0)) {
-        if constexpr (sizeof(TE) == 2) {
-          bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+  for (int c = 0; c < PER / 8; ++c) {
+    const int idx = tid + c * 256;
+    const int ir = idx / CPR, ic = (idx % CPR) * 8;
+    const int gr = KCONTIG ? row0 + ir : row0 + ic;  // logical row of the chunk's first element
+    const int gk = KCONTIG ? k0 + ic : k0 + ir;
+    const TE* p = KCONTIG ? base + (long)gr * ld + gk : base + (long)gk * ld + gr;
+    const bool full = KCONTIG ? (gr < nrows && gk + 8 <= K) : (gk < K && gr + 8 <= nrows);
+    if (full && ((((uintptr_t)p) & (sizeof(TE) * 8 - 1)) == 0)) {
+      if constexpr (sizeof(TE) == 2) {
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) reg[c * 8 + e] = v[e];
-        } else {
-          f32x4 v0 = *reinterpret_cast<const f32x4*>(p);
-          f32x4 v1 = *reinterpret_cast<const f32x4*>(p + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { reg[c * 8 + e] = (bf16)v0[e]; reg[c * 8 + 4 + e] = (bf16)v1[e]; }
-        }
+        for (int e = 0; e < 8; ++e) reg[c * 8 + e] = v[e];
       } else {
+        f32x4 v0 = *reinterpret_cast<const f32x4*>(p);
+        f32x4 v1 = *reinterpret_cast<const f32x4*>(p + 4);
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          reg[c * 8 + e] = (gr < nrows && gk + e < K) ? to_bf(p[e]) : (bf16)0.f;
+        for (int e = 0; e < 4; ++e) { reg[c * 8 + e] = (bf16)v0[e]; reg[c * 8 + 4 + e] = (bf16)v1[e]; }
       }
-    }
-  } else {
-    // thread -> (k, 8-wide row chunk)
-    constexpr int RCH = ROWS / 8;  // row chunks per k
+    } else {
 #pragma unroll
-    for (int c = 0; c < PER / 8; ++c) {
-      const int idx = tid + c * 256;
-      const int kk = idx / RCH, r = (idx % RCH) * 8;
-      const int gk = k0 + kk, gr = row0 + r;
-      const TE* p = base + (long)gk * ld + gr;
-      if (gk < K && gr + 8 <= nrows && ((((uintptr_t)p) & (sizeof(TE) * 8 - 1)) == 0)) {
-        if constexpr (sizeof(TE) == 2) {
-          bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) reg[c * 8 + e] = v[e];
-        } else {
-          f32x4 v0 = *reinterpret_cast<const f32x4*>(p);
-          f32x4 v1 = *reinterpret_cast<const f32x4*>(p + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { reg[c * 8 + e] = (bf16)v0[e]; reg[c * 8 + 4 + e] = (bf16)v1[e]; }
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          reg[c * 8 + e] = (gk < K && gr + e < nrows) ? to_bf(p[e]) : (bf16)0.f;
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = KCONTIG ? (gr < nrows && gk + e < K) : (gk < K && gr + e < nrows);
+        reg[c * 8 + e] = ok ? to_bf(p[e]) : (bf16)0.f;
       }
     }
   }
 }
 
 template <int ROWS, bool KCONTIG>
-__device__ __forceinline__ void stage_store(bf16 (*lds)[40], int tid, const bf16 (&reg)[ROWS * 32 / 256]) {
-  constexpr int PER = ROWS * 32 / 256;
+__device__ __forceinline__ void stage_store(bf16* __restrict__ img, int tid, const bf16 (&reg)[ROWS * 64 / 256]) {
+  constexpr int PER = ROWS * 64 / 256;
+  constexpr int CPR = KCONTIG ? 8 : ROWS / 8;
+  constexpr int C = Img<ROWS, KCONTIG>::C;
+#pragma unroll
+  for (int c = 0; c < PER / 8; ++c) {
+    const int idx = tid + c * 256;
+    const int ir = idx / CPR, ic = (idx % CPR) * 8;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = reg[c * 8 + e];
+    // k-major images store k-row k at row k ^ 4*((k>>3)&1): the two 16-lane groups of each
+    // 32-lane half then read rows 8 apart mod 8 -> distinct banks (row stride = 8*odd banks)
+    const int r = KCONTIG ? ir : (ir ^ ((ir >> 1) & 4));
+    *reinterpret_cast<bf16x8*>(img + r * C + ic) = v;
+  }
+}
+
+// 16x32 MFMA operand fragment (16 rows starting at r0, k = 32*ks .. +31) from an image
+template <int ROWS, bool KCONTIG>
+__device__ __forceinline__ bf16x8 frag(const bf16* __restrict__ img, int r0, int ks, int lane) {
+  constexpr int C = Img<ROWS, KCONTIG>::C;
   if constexpr (KCONTIG) {
-#pragma unroll
-    for (int c = 0; c < PER / 8; ++c) {
-      const int idx = tid + c * 256;
-      const int r = idx >> 2, kk = (idx & 3) * 8;
-      bf16x8 v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = reg[c * 8 + e];
-      *reinterpret_cast<bf16x8*>(&lds[r][kk]) = v;
-    }
+    return *reinterpret_cast<const bf16x8*>(img + (r0 + (lane & 15)) * C + 32 * ks + 8 * (lane >> 4));
   } else {
-    constexpr int RCH = ROWS / 8;
-#pragma unroll
-    for (int c = 0; c < PER / 8; ++c) {
-      const int idx = tid + c * 256;
-      const int kk = idx / RCH, r = (idx % RCH) * 8;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) lds[r + e][kk] = reg[c * 8 + e];
-    }
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int kb = 32 * ks + 8 * g + q;
+    const int h0 = (g & 1) ? 4 : 0;  // image row of k is k ^ 4*((k>>3)&1), see stage_store
+    const bf16* a0 = img + (kb + h0) * C + r0 + 4 * p;
+    const bf16* a1 = img + (kb + (4 - h0)) * C + r0 + 4 * p;
+    s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+    s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
   }
 }
 
@@ -129,9 +137,11 @@ __global__ void __launch_bounds__(256)
 gemm_kernel(const TAe* __restrict__ A, long lda, const TBe* __restrict__ B, long ldb,
             void* __restrict__ C, long ldc, int M, int N, int K, int kchunk,
             float* __restrict__ slab, Epi epi) {
-  typedef GemmTile<BM, BN, TA, TB, TAe, TBe> T;
-  __shared__ __attribute__((aligned(16))) bf16 As[2][BM][T::LDK];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN][T::LDK];
+  typedef GemmTile<BM, BN, TA, TB> T;
+  // one LDS array (A images then B images, double-buffered)
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (T::IA::ELEMS + T::IB::ELEMS)];
+#define As(b) (smem + (b) * T::IA::ELEMS)
+#define Bs(b) (smem + 2 * T::IA::ELEMS + (b) * T::IB::ELEMS)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -152,8 +162,8 @@ gemm_kernel(const TAe* __restrict__ A, long lda, const TBe* __restrict__ B, long
   if (nk > 0) {
     stage_load<BM, !TA, TAe>(A, lda, row0, kbeg, M, kend, tid, ra);
     stage_load<BN, TB, TBe>(B, ldb, col0, kbeg, N, kend, tid, rb);
-    stage_store<BM, !TA>(As[0], tid, ra);
-    stage_store<BN, TB>(Bs[0], tid, rb);
+    stage_store<BM, !TA>(As(0), tid, ra);
+    stage_store<BN, TB>(Bs(0), tid, rb);
   }
   __syncthreads();
   for (int it = 0; it < nk; ++it) {
@@ -164,24 +174,27 @@ gemm_kernel(const TAe* __restrict__ A, long lda, const TBe* __restrict__ B, long
       stage_load<BM, !TA, TAe>(A, lda, row0, k0, M, kend, tid, ra);
       stage_load<BN, TB, TBe>(B, ldb, col0, k0, N, kend, tid, rb);
     }
-    bf16x8 af[T::FM], bfr[T::FN];
 #pragma unroll
-    for (int i = 0; i < T::FM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(&As[cur][wm * T::WM + 16 * i + (lane & 15)][8 * (lane >> 4)]);
+    for (int ks = 0; ks < T::BK / 32; ++ks) {
+      bf16x8 af[T::FM], bfr[T::FN];
 #pragma unroll
-    for (int j = 0; j < T::FN; ++j)
-      bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][wn * T::WN + 16 * j + (lane & 15)][8 * (lane >> 4)]);
+      for (int i = 0; i < T::FM; ++i) af[i] = frag<BM, !TA>(As(cur), wm * T::WM + 16 * i, ks, lane);
 #pragma unroll
-    for (int i = 0; i < T::FM; ++i)
+      for (int j = 0; j < T::FN; ++j) bfr[j] = frag<BN, TB>(Bs(cur), wn * T::WN + 16 * j, ks, lane);
 #pragma unroll
-      for (int j = 0; j < T::FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
     if (more) {
-      stage_store<BM, !TA>(As[cur ^ 1], tid, ra);
-      stage_store<BN, TB>(Bs[cur ^ 1], tid, rb);
+      stage_store<BM, !TA>(As(cur ^ 1), tid, ra);
+      stage_store<BN, TB>(Bs(cur ^ 1), tid, rb);
     }
     __syncthreads();
   }
 
+#undef As
+#undef Bs
   // epilogue
   const bool split = slab != nullptr;
 #pragma unroll
@@ -250,7 +263,7 @@ int launch(const void* A, long lda, const void* B, long ldb, void* C, long ldc, 
   int kchunk = K;
   if (splits > 1) {
     kchunk = (K + splits - 1) / splits;
-    kchunk = (kchunk + 31) / 32 * 32;
+    kchunk = (kchunk + 63) / 64 * 64;
     splits = (K + kchunk - 1) / kchunk;
   }
   dim3 grid(tiles, 1, splits);

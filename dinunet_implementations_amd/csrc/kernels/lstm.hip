@@ -25,6 +25,7 @@
 // pre-activations, and writes dpre (bf16, original time order) for the weight-gradient GEMMs
 // dW_ih = dpre^T x, dW_hh = dpre^T h_{t-1} that run after it on the full chip.
 #include "common.h"
+#include <stdlib.h>
 
 #ifdef DN_STAMPS
 // diagnostic build only (tools/lstm_stamps.py): per-wave phase cycle sums
@@ -66,11 +67,17 @@ __device__ __forceinline__ void load_gate4(const float* p, bool ok, float (&v)[4
 template <int HD> struct LdsSplit { static constexpr int FWD_MT = 0, BWD_KS = 0; };
 template <> struct LdsSplit<192> { static constexpr int FWD_MT = 1, BWD_KS = 9; };
 
-// All per-step global traffic is UNCONDITIONAL (internal buffers are padded to Bp = 16*chunks
-// rows and HD units; loads of padded batch rows are clamped to row B-1): no divergent branches
-// around memory ops, so hipcc emits counted s_waitcnt vmcnt(N) and a step never waits for the
-// previous step's stores.  The x-projection of step t+1 is issued before step t's MFMAs.
-template <int HD, bool SEQ>
+// BR = batch rows per workgroup (4, 8 or 16).  The recurrent MFMA always computes 16 columns;
+// columns >= BR are zero.  For the gate phase the BR valid columns are redistributed over all
+// 64 lanes (ds_bpermute), so each lane owns BR/4 (unit, row) slots instead of 4: the VALU-bound
+// gate work per CU shrinks by 16/BR while batch rows stay independent (no cross-CU traffic).
+// Lane map: q = lane>>4, n = lane&15, r = n / BR (lane group), b = n % BR (row in chunk);
+// slot s holds m-tile mt = r + s*(16/BR) -> unit u = 16w + 4*mt + q.
+//
+// All per-step global traffic is UNCONDITIONAL (internal buffers padded to Bp rows and HD
+// units; loads of padded rows clamp to row B-1): no divergent branches around memory ops, so
+// hipcc emits counted s_waitcnt vmcnt(N) and a step never waits for the previous step's stores.
+template <int HD, int BR, bool SEQ>
 __global__ void __launch_bounds__(HD / 16 * 64)
 lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted cols, no bias
                 const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
@@ -86,16 +93,18 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
   constexpr int LDH = HD + 8;  // +16 B per row: the 16 rows land on distinct bank quads
   constexpr int NLM = LdsSplit<HD>::FWD_MT, NRM = 4 - NLM;
   constexpr int NW = HD / 16;
+  constexpr int G16 = 16 / BR, NSL = BR / 4;
+  constexpr int EPT = BR * HD / NT;  // h_{t-1} copy: elements per thread (1, 2 or 4)
   __shared__ __attribute__((aligned(16))) bf16 hbuf[2][16][LDH];
   __shared__ __attribute__((aligned(16))) float bias_s[4 * HD];
   // lane-linear fragment image: one 1 KiB row per (wave, m-tile, k-step) -> conflict-free b128
   __shared__ __attribute__((aligned(16))) bf16x8 wlds[NW][NLM > 0 ? NLM : 1][KS][64];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int q = lane >> 4, bl = lane & 15;
+  const int q = lane >> 4, n = lane & 15, r = n / BR, bl = n % BR;
   const int dir = blockIdx.y;
-  const int Bp = gridDim.x * 16;
-  const int b = blockIdx.x * 16 + bl;          // padded row (always < Bp)
+  const int Bp = gridDim.x * BR;
+  const int b = blockIdx.x * BR + bl;           // padded row (always < Bp)
   const int bc = b < B ? b : B - 1;             // clamped row for loads
   const long rowX = (long)ndir * 4 * HD;
 
@@ -106,7 +115,7 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const int row = 16 * (4 * w + mt) + bl;
+        const int row = 16 * (4 * w + mt) + n;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(wd + (long)row * HD + 32 * ks + 8 * q);
         if (mt < NRM) wf[mt < NRM ? mt : 0][ks] = v;
         else wlds[w][mt - NRM][ks][lane] = v;
@@ -116,19 +125,23 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
   for (int i = tid; i < 2 * 16 * LDH; i += NT) (&hbuf[0][0][0])[i] = (bf16)0.f;
   __syncthreads();
 
-  const float* xrow = xp + (long)bc * S * rowX + (long)dir * 4 * HD + 4 * (16 * w + q);
-  const long hplane = (long)dir * Bp * S * HD;
-  // cooperative h_{t-1} copy: thread -> 4 consecutive bf16 of the [16][HD] tile
-  const int cp_r = (tid * 4) / HD, cp_c = (tid * 4) % HD;
-  bf16* hcp = hprev + hplane + ((long)(blockIdx.x * 16 + cp_r) * S) * HD + cp_c;
-  float* csv = c_save + hplane + (long)b * S * HD + 16 * w + q;
-
-  float c[4] = {0.f, 0.f, 0.f, 0.f}, hs[4] = {0.f, 0.f, 0.f, 0.f}, hl[4] = {0.f, 0.f, 0.f, 0.f};
-  f32x4 xn[4];
-  {
-    const int tau0 = dir == 0 ? 0 : S - 1;
+  int uu[NSL];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) xn[mt] = *reinterpret_cast<const f32x4*>(xrow + (long)tau0 * rowX + 16 * mt);
+  for (int s = 0; s < NSL; ++s) uu[s] = 16 * w + 4 * (r + s * G16) + q;
+  const float* xrow = xp + (long)bc * S * rowX + (long)dir * 4 * HD;
+  const long hplane = (long)dir * Bp * S * HD;
+  const int cp_r = (tid * EPT) / HD, cp_c = (tid * EPT) % HD;
+  bf16* hcp = hprev + hplane + ((long)(blockIdx.x * BR + cp_r) * S) * HD + cp_c;
+  float* csv = c_save + hplane + (long)b * S * HD;
+  const int src = 16 * q + bl;  // lane holding this lane's column in the MFMA output
+
+  float c[NSL], hs[NSL], hl[NSL];
+  f32x4 xn[NSL];
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) {
+    c[s] = hs[s] = hl[s] = 0.f;
+    const int tau0 = dir == 0 ? 0 : S - 1;
+    xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau0 * rowX + 4 * uu[s]);
   }
   int cur = 0;
 #ifdef DN_STAMPS
@@ -142,45 +155,66 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
     const int t1 = t + 1 < S ? t + 1 : t;
     const int tau1 = dir == 0 ? t1 : S - 1 - t1;
     // h_{t-1} (the tile every wave reads below) -> global for the weight-gradient GEMMs
-    *reinterpret_cast<bf16x4*>(hcp + (long)tau * HD) = *reinterpret_cast<const bf16x4*>(&hbuf[cur][cp_r][cp_c]);
+    if constexpr (EPT == 4) {
+      *reinterpret_cast<bf16x4*>(hcp + (long)tau * HD) = *reinterpret_cast<const bf16x4*>(&hbuf[cur][cp_r][cp_c]);
+    } else if constexpr (EPT == 2) {
+      *reinterpret_cast<unsigned*>(hcp + (long)tau * HD) = *reinterpret_cast<const unsigned*>(&hbuf[cur][cp_r][cp_c]);
+    } else {
+      hcp[(long)tau * HD] = hbuf[cur][cp_r][cp_c];
+    }
     // recurrent GEMM  pre^T[m][b] = sum_k W[m][k] h[b][k]  (W resident)
     f32x4 acc[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][bl][32 * ks + 8 * q]);
+      // columns >= BR are zero: skip their LDS reads (exec-masked lanes cost no LDS cycles)
+      bf16x8 hb = {};
+      if (BR == 16 || n < BR) hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n][32 * ks + 8 * q]);
 #pragma unroll
       for (int mt = 0; mt < NRM; ++mt) acc[mt] = mfma16(wf[mt][ks], hb, acc[mt]);
 #pragma unroll
       for (int mt = NRM; mt < 4; ++mt) acc[mt] = mfma16(wlds[w][mt - NRM][ks][lane], hb, acc[mt]);
     }
-    // gates + cell update: lane-local (unit u = 16w + 4mt + q, row b), 4 gates in acc regs
-    const int nxt = cur ^ 1;
+    // redistribute the BR valid columns over all lanes (identity when BR == 16)
+    f32x4 pa[NSL];
+    if constexpr (BR == 16) {
+#pragma unroll
+      for (int s = 0; s < NSL; ++s) pa[s] = acc[s];
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = __shfl(acc[mt][j], src, 64);
+        if (mt % G16 == r) pa[mt / G16] = v;
+      }
+    }
 #ifdef DN_STAMPS
-    { float z = acc[0][0] + acc[1][0] + acc[2][0] + acc[3][0]; asm volatile("" :: "v"(z)); }
+    { float z = pa[0][0]; asm volatile("" :: "v"(z)); }
     STAMP(ts1);
 #endif
+    const int nxt = cur ^ 1;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int u = 16 * w + 4 * mt + q;
+    for (int s = 0; s < NSL; ++s) {
+      const int u = uu[s];
       const f32x4 bb = *reinterpret_cast<const f32x4*>(&bias_s[4 * u]);
-      const float p0 = acc[mt][0] + xn[mt][0] + bb[0];
-      const float p1 = acc[mt][1] + xn[mt][1] + bb[1];
-      const float p2 = acc[mt][2] + xn[mt][2] + bb[2];
-      const float p3 = acc[mt][3] + xn[mt][3] + bb[3];
-      // this m-tile's projection is consumed: issue step t+1's (hidden by its MFMA phase)
-      xn[mt] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 16 * mt);
+      const float p0 = pa[s][0] + xn[s][0] + bb[0];
+      const float p1 = pa[s][1] + xn[s][1] + bb[1];
+      const float p2 = pa[s][2] + xn[s][2] + bb[2];
+      const float p3 = pa[s][3] + xn[s][3] + bb[3];
+      // consumed: issue step t+1's projection (hidden by its MFMA phase)
+      xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 4 * u);
       const float gi = dn_sigmoid(dn_sigmoid(p0));
       const float gf = dn_sigmoid(dn_sigmoid(p1));
       const float go = dn_sigmoid(dn_sigmoid(p2));
       const float gg = dn_tanh(p3);
-      c[mt] = gf * c[mt] + gi * gg;
-      const float h = go * dn_tanh(c[mt]);
-      csv[(long)tau * HD + 4 * mt] = c[mt];
+      c[s] = gf * c[s] + gi * gg;
+      const float h = go * dn_tanh(c[s]);
+      csv[(long)tau * HD + u] = c[s];
       if constexpr (SEQ) hseq[((long)b * S + t) * ndir * HD + dir * HD + u] = h;
-      hs[mt] += h;
-      hl[mt] = h;
+      hs[s] += h;
+      hl[s] = h;
       hbuf[nxt][bl][u] = (bf16)h;
     }
 #ifdef DN_STAMPS
@@ -200,13 +234,13 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
   }
 #endif
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int u = 16 * w + 4 * mt + q;
+  for (int s = 0; s < NSL; ++s) {
+    const int u = uu[s];
     if (b < B && u < Hd) {
       const long o = (long)b * ndir * Hd + dir * Hd + u;
-      if (hmean) hmean[o] = hs[mt] * mean_scale;
-      if (hT) hT[o] = hl[mt];
-      if (cT) cT[o] = c[mt];
+      if (hmean) hmean[o] = hs[s] * mean_scale;
+      if (hT) hT[o] = hl[s];
+      if (cT) cT[o] = c[s];
     }
   }
 }
@@ -216,7 +250,9 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
 // ---------------------------------------------------------------------------------------------
 // pre: the gate pre-activations, recomputed time-parallel after the forward by one GEMM
 // (pre = x W_ih^T + h_{t-1} W_hh^T + b) instead of being stored per step by the forward kernel.
-template <int HD, bool DSEQ>
+// MFMA output: lane (q, n) holds dh for units u0 + j (u0 = 16w + 4q, j = 0..3) of column n; as in
+// the forward, the BR valid columns are redistributed: lane (q, r, b) owns units u0 + r + s*(16/BR).
+template <int HD, int BR, bool DSEQ>
 __global__ void __launch_bounds__(HD / 16 * 64)
 lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time order
                 const float* __restrict__ c_save,  // [ndir][Bp][S][HD]
@@ -230,17 +266,19 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   constexpr int NLK = LdsSplit<HD>::BWD_KS, NRK = KS - NLK;
   constexpr int NW = HD / 16;
   constexpr int NT = NW * 64;
+  constexpr int G16 = 16 / BR, NSL = BR / 4;
   __shared__ __attribute__((aligned(16))) bf16 dbuf[2][16][LDD];
   __shared__ __attribute__((aligned(16))) bf16x8 wlds[NW][NLK > 0 ? NLK : 1][64];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int q = lane >> 4, bl = lane & 15;
+  const int q = lane >> 4, n = lane & 15, r = n / BR, bl = n % BR;
   const int dir = blockIdx.y;
-  const int Bp = gridDim.x * 16;
-  const int b = blockIdx.x * 16 + bl;
+  const int Bp = gridDim.x * BR;
+  const int b = blockIdx.x * BR + bl;
   const bool vb = b < B;
   const int bc = vb ? b : B - 1;
   const long rowX = (long)ndir * 4 * HD;
+  const int src = 16 * q + bl;
 
   bf16x8 af[NRK];
   {
@@ -248,39 +286,39 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const bf16x8 v =
-          *reinterpret_cast<const bf16x8*>(wt + (long)(16 * w + bl) * 4 * HD + 32 * ks + 8 * q);
+          *reinterpret_cast<const bf16x8*>(wt + (long)(16 * w + n) * 4 * HD + 32 * ks + 8 * q);
       if (ks < NRK) af[ks < NRK ? ks : 0] = v;
       else wlds[w][ks - NRK][lane] = v;
     }
   }
   for (int i = tid; i < 2 * 16 * LDD; i += NT) (&dbuf[0][0][0])[i] = (bf16)0.f;
 
-  const int u0 = 16 * w + 4 * q;  // this lane's 4 consecutive units u0..u0+3
-  const float* prow = pre + (long)bc * S * rowX + (long)dir * 4 * HD + 4 * u0;
-  const float* crow = c_save + (long)dir * Bp * S * HD + (long)b * S * HD + u0;
-  bf16* drow = dpre + (long)b * S * rowX + (long)dir * 4 * HD + 4 * u0;
-  // external grads: lanes of padded rows / units read a clamped address and are zeroed
-  float msk[4], dhx[4], dcc[4];
+  const int u0 = 16 * w + 4 * q;
+  int uu[NSL];
+  float msk[NSL], dhx[NSL], dcc[NSL];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int u = u0 + j;
-    msk[j] = (vb && u < Hd) ? 1.f : 0.f;
-    const long eo = (long)bc * dh_sb + dir * Hd + (u < Hd ? u : Hd - 1);
-    dhx[j] = DSEQ ? 0.f : dh_ext[eo] * dh_scale * msk[j];
-    const long fo = (long)bc * ndir * Hd + dir * Hd + (u < Hd ? u : Hd - 1);
-    dcc[j] = dcT ? dcT[fo] * msk[j] : 0.f;
+  for (int s = 0; s < NSL; ++s) {
+    const int u = u0 + r + s * G16;
+    uu[s] = u;
+    msk[s] = (vb && u < Hd) ? 1.f : 0.f;
+    const int uc = u < Hd ? u : Hd - 1;
+    dhx[s] = DSEQ ? 0.f : dh_ext[(long)bc * dh_sb + dir * Hd + uc] * dh_scale * msk[s];
+    dcc[s] = dcT ? dcT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s] : 0.f;
   }
+  const float* prow = pre + (long)bc * S * rowX + (long)dir * 4 * HD;
+  const float* crow = c_save + (long)dir * Bp * S * HD + (long)b * S * HD;
+  bf16* drow = dpre + (long)b * S * rowX + (long)dir * 4 * HD;
   const float* dhrow = dh_ext + (long)bc * dh_sb + dir * Hd;
-  // state of step t (processing order) and prefetch of step t-1
   const int tauL = dir == 0 ? S - 1 : 0;
-  f32x4 cc = *reinterpret_cast<const f32x4*>(crow + (long)tauL * HD);
-  f32x4 pn[4], cpn;
+  const int tp0 = S >= 2 ? S - 2 : 0;
+  const int tauP = dir == 0 ? tp0 : S - 1 - tp0;
+  float cc[NSL], cpn[NSL];
+  f32x4 pn[NSL];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) pn[j] = *reinterpret_cast<const f32x4*>(prow + (long)tauL * rowX + 4 * j);
-  {
-    const int tp = S >= 2 ? S - 2 : 0;
-    const int taup = dir == 0 ? tp : S - 1 - tp;
-    cpn = *reinterpret_cast<const f32x4*>(crow + (long)taup * HD);
+  for (int s = 0; s < NSL; ++s) {
+    cc[s] = crow[(long)tauL * HD + uu[s]];
+    cpn[s] = crow[(long)tauP * HD + uu[s]];
+    pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tauL * rowX + 4 * uu[s]);
   }
   __syncthreads();
 
@@ -293,73 +331,75 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     STAMP(ts0);
 #endif
     const int tau = dir == 0 ? t : S - 1 - t;
-    f32x4 pc[4];
+    float dx[NSL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pc[j] = pn[j];
-    f32x4 cp = t > 0 ? cpn : f32x4{0.f, 0.f, 0.f, 0.f};
-    {  // prefetch step t-1 (pre) and t-2 (c_{t-2} = c_prev of step t-1), clamped at 0
-      const int t1 = t > 0 ? t - 1 : 0;
-      const int tau1 = dir == 0 ? t1 : S - 1 - t1;
-      const int t2 = t > 1 ? t - 2 : 0;
-      const int tau2 = dir == 0 ? t2 : S - 1 - t2;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pn[j] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * j);
-      cpn = *reinterpret_cast<const f32x4*>(crow + (long)tau2 * HD);
-    }
-    float dx[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dx[j] = dhx[j];
-    if constexpr (DSEQ) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int u = u0 + j < Hd ? u0 + j : Hd - 1;
-        dx[j] = dhrow[(long)t * dh_st + u] * dh_scale * msk[j];
+    for (int s = 0; s < NSL; ++s) {
+      dx[s] = dhx[s];
+      if constexpr (DSEQ) {
+        const int uc = uu[s] < Hd ? uu[s] : Hd - 1;
+        dx[s] = dhrow[(long)t * dh_st + uc] * dh_scale * msk[s];
       }
     }
     if (t == S - 1 && dhT) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int u = u0 + j;
-        dx[j] += dhT[(long)bc * ndir * Hd + dir * Hd + (u < Hd ? u : Hd - 1)] * msk[j];
+      for (int s = 0; s < NSL; ++s) {
+        const int uc = uu[s] < Hd ? uu[s] : Hd - 1;
+        dx[s] += dhT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s];
       }
     }
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][bl][32 * ks + 8 * q]);
+      bf16x8 db = {};
+      if (BR == 16 || n < BR) db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n][32 * ks + 8 * q]);
       acc = mfma16(ks < NRK ? af[ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db, acc);
     }
-    const int nxt = cur ^ 1;
+    float dhr[NSL];
+    if constexpr (BR == 16) {
+#pragma unroll
+      for (int s = 0; s < NSL; ++s) dhr[s] = acc[s];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = __shfl(acc[j], src, 64);
+        if (j % G16 == r) dhr[j / G16] = v;
+      }
+    }
 #ifdef DN_STAMPS
-    { float z = acc[0] + acc[1] + acc[2] + acc[3]; asm volatile("" :: "v"(z)); }
+    { float z = dhr[0]; asm volatile("" :: "v"(z)); }
     STAMP(ts1);
 #endif
-    bf16x8 lo, hi;
+    const int nxt = cur ^ 1;
+    const int t1 = t > 0 ? t - 1 : 0;
+    const int tau1 = dir == 0 ? t1 : S - 1 - t1;
+    const int t2 = t > 1 ? t - 2 : 0;
+    const int tau2 = dir == 0 ? t2 : S - 1 - t2;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float si = dn_sigmoid(pc[j][0]), sf = dn_sigmoid(pc[j][1]), so = dn_sigmoid(pc[j][2]);
+    for (int s = 0; s < NSL; ++s) {
+      const f32x4 pc = pn[s];
+      const float cp = t > 0 ? cpn[s] : 0.f;
+      // consumed: issue step t-1's pre and c_{t-2} (hidden by the next MFMA phase)
+      pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
+      cpn[s] = crow[(long)tau2 * HD + uu[s]];
+      const float si = dn_sigmoid(pc[0]), sf = dn_sigmoid(pc[1]), so = dn_sigmoid(pc[2]);
       const float gi = dn_sigmoid(si), gf = dn_sigmoid(sf), go = dn_sigmoid(so);
-      const float gg = dn_tanh(pc[j][3]);
-      const float tc = dn_tanh(cc[j]);
-      const float dh = acc[j] + dx[j];
-      const float dc = dcc[j] + dh * go * (1.f - tc * tc);
+      const float gg = dn_tanh(pc[3]);
+      const float tc = dn_tanh(cc[s]);
+      const float dh = dhr[s] + dx[s];
+      const float dc = dcc[s] + dh * go * (1.f - tc * tc);
       const float d_o = dh * tc;
-      const float d_i = dc * gg, d_g = dc * gi, d_f = dc * cp[j];
-      dcc[j] = dc * gf * msk[j];
-      const float m = msk[j];
-      const bf16 e0 = (bf16)(m * d_i * gi * (1.f - gi) * si * (1.f - si));
-      const bf16 e1 = (bf16)(m * d_f * gf * (1.f - gf) * sf * (1.f - sf));
-      const bf16 e2 = (bf16)(m * d_o * go * (1.f - go) * so * (1.f - so));
-      const bf16 e3 = (bf16)(m * d_g * (1.f - gg * gg));
-      if (j < 2) { lo[4 * j] = e0; lo[4 * j + 1] = e1; lo[4 * j + 2] = e2; lo[4 * j + 3] = e3; }
-      else { hi[4 * j - 8] = e0; hi[4 * j - 7] = e1; hi[4 * j - 6] = e2; hi[4 * j - 5] = e3; }
+      const float d_i = dc * gg, d_g = dc * gi, d_f = dc * cp;
+      const float m = msk[s];
+      dcc[s] = dc * gf * m;
+      cc[s] = cp;
+      bf16x4 e;
+      e[0] = (bf16)(m * d_i * gi * (1.f - gi) * si * (1.f - si));
+      e[1] = (bf16)(m * d_f * gf * (1.f - gf) * sf * (1.f - sf));
+      e[2] = (bf16)(m * d_o * go * (1.f - go) * so * (1.f - so));
+      e[3] = (bf16)(m * d_g * (1.f - gg * gg));
+      *reinterpret_cast<bf16x4*>(&dbuf[nxt][bl][4 * uu[s]]) = e;
+      *reinterpret_cast<bf16x4*>(drow + (long)tau * rowX + 4 * uu[s]) = e;
     }
-    cc = cp;
-    // gate cols of this lane's 4 units are contiguous: 4*u0 .. 4*u0+15
-    *reinterpret_cast<bf16x8*>(&dbuf[nxt][bl][4 * u0]) = lo;
-    *reinterpret_cast<bf16x8*>(&dbuf[nxt][bl][4 * u0 + 8]) = hi;
-    *reinterpret_cast<bf16x8*>(drow + (long)tau * rowX) = lo;
-    *reinterpret_cast<bf16x8*>(drow + (long)tau * rowX + 8) = hi;
 #ifdef DN_STAMPS
     STAMP(ts2);
 #endif
@@ -465,38 +505,73 @@ __global__ void lstm_bias_grad_kernel(const float* __restrict__ part, int slabs,
   if (idx >= ndir * G) return;
   const int d = idx / G, r = idx % G, g = r / Hd, u = r % Hd;
   const int col = d * 4 * HD + 4 * u + g;
-  float s = 0.f;
-  for (int k = 0; k < slabs; ++k) s += part[(long)k * ndir * 4 * HD + col];
+  const long C = (long)ndir * 4 * HD;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // independent chains: loads in flight
+  int k = 0;
+  for (; k + 8 <= slabs; k += 8)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += part[(long)(k + e) * C + col];
+  for (; k < slabs; ++k) acc[0] += part[(long)k * C + col];
+  const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   if (out.bih[d]) const_cast<float*>(out.bih[d])[r] += s;
   if (out.bhh[d]) const_cast<float*>(out.bhh[d])[r] += s;
 }
 
-template <int HD>
-int launch_fwd(const float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
-               float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
-               float* cT, hipStream_t st) {
-  dim3 grid((B + 15) / 16, ndir), block(HD / 16 * 64);
+// rows per workgroup: spread small batches over more CUs (the gate phase is VALU-bound per CU)
+static inline int pick_br(int B) {
+  if (const char* e = getenv("DN_LSTM_BR")) {
+    const int v = atoi(e);
+    if (v == 4 || v == 8 || v == 16) return v;
+  }
+  if (B <= 128) return 4;
+  if (B <= 512) return 8;
+  return 16;
+}
+
+template <int HD, int BR>
+int launch_fwd_br(const float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
+                  float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
+                  float* cT, hipStream_t st) {
+  dim3 grid((B + BR - 1) / BR, ndir), block(HD / 16 * 64);
   if (hseq)
-    hipLaunchKernelGGL((lstm_fwd_kernel<HD, true>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
+    hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, true>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
                        ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT);
   else
-    hipLaunchKernelGGL((lstm_fwd_kernel<HD, false>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
+    hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
                        ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT);
   return dn_launch_status();
 }
 
 template <int HD>
-int launch_bwd(const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
-               long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
-               int Hd, int ndir, bf16* dpre, hipStream_t st) {
-  dim3 grid((B + 15) / 16, ndir), block(HD / 16 * 64);
+int launch_fwd(int BR, const float* xp, const float* bias, const bf16* whh, int B, int S, int Hd,
+               int ndir, float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale,
+               float* hT, float* cT, hipStream_t st) {
+  if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, st);
+  if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, st);
+  return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, st);
+}
+
+template <int HD, int BR>
+int launch_bwd_br(const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
+                  long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
+                  int Hd, int ndir, bf16* dpre, hipStream_t st) {
+  dim3 grid((B + BR - 1) / BR, ndir), block(HD / 16 * 64);
   if (st_ != 0)
-    hipLaunchKernelGGL((lstm_bwd_kernel<HD, true>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
+    hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, true>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
                        sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
   else
-    hipLaunchKernelGGL((lstm_bwd_kernel<HD, false>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
+    hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, false>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
                        sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
   return dn_launch_status();
+}
+
+template <int HD>
+int launch_bwd(int BR, const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
+               long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
+               int Hd, int ndir, bf16* dpre, hipStream_t st) {
+  if (BR == 4) return launch_bwd_br<HD, 4>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
+  if (BR == 8) return launch_bwd_br<HD, 8>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
+  return launch_bwd_br<HD, 16>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
 }
 
 }  // namespace
@@ -524,15 +599,19 @@ DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0,
   return dn_launch_status();
 }
 
+// rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
+DN_API int dn_lstm_rows_per_wg(int B) { return pick_br(B); }
+
 DN_API int dn_lstm_fwd(const float* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
                        int ndir, float* c_save, void* hprev, float* hseq, float* hmean,
                        float mean_scale, float* hT, float* cT, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
+  const int BR = pick_br(B);
   switch (HD) {
-    case 64: return launch_fwd<64>(xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
-    case 128: return launch_fwd<128>(xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
-    case 192: return launch_fwd<192>(xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
+    case 64: return launch_fwd<64>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
+    case 128: return launch_fwd<128>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
+    case 192: return launch_fwd<192>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
   }
   return DN_UNSUPPORTED;
 }
@@ -543,10 +622,11 @@ DN_API int dn_lstm_bwd(const float* pre, const float* c_save, const void* whhT_p
                        void* dpre, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
+  const int BR = pick_br(B);
   switch (HD) {
-    case 64: return launch_bwd<64>(pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
-    case 128: return launch_bwd<128>(pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
-    case 192: return launch_bwd<192>(pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 64: return launch_bwd<64>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 128: return launch_bwd<128>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 192: return launch_bwd<192>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
   }
   return DN_UNSUPPORTED;
 }

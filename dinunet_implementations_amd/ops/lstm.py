@@ -41,6 +41,7 @@ _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.
                               _lib.c_long, _lib.c_long, _lib.c_float, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
                               _lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_lstm_rows_per_wg", [_lib.c_int])
 _lib.register("dn_lstm_bias_grad", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
                                     _lib.c_void_p] + [_lib.c_void_p] * 4 + [_lib.c_void_p])
 
@@ -81,8 +82,8 @@ class _BiLSTMFn(torch.autograd.Function):
         Hd = params[2].shape[1]
         HD = padded_hidden(Hd)
         GP = 4 * HD
-        nch = (B + 15) // 16
-        Bp = nch * 16
+        BR = int(_lib.lib().dn_lstm_rows_per_wg(B))  # rows per workgroup the kernels use
+        Bp = (B + BR - 1) // BR * BR
         dev = enc.device
         st = _lib.stream()
         wih_p = torch.empty(ndir * GP, I, dtype=torch.bfloat16, device=dev)

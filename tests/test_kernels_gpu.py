@@ -167,3 +167,27 @@ def test_ica_model_gpu_matches_cpu_oracle():
     out, _ = m(x.to(DEV))
     ref, _ = mc(x)
     assert rel(out.cpu(), ref) < 3e-2
+
+
+@pytest.mark.parametrize("br", ["4", "8", "16"])
+def test_lstm_rows_per_workgroup_variants(br, monkeypatch):
+    """Every rows-per-workgroup instantiation (column redistribution) matches the oracle."""
+    monkeypatch.setenv("DN_LSTM_BR", br)
+    from dinunet_implementations_amd.ops import reference as ref
+    from dinunet_implementations_amd.ops.lstm import bilstm
+    B, S, I, Hd = 37, 13, 64, 174
+    ps = _lstm_params(I, Hd, 2)
+    x = torch.randn(B, S, I, device=DEV).requires_grad_()
+    out, _ = bilstm(x, ps, reduce="mean")
+    ps_r = [tuple(bf(t.detach()).requires_grad_() for t in p) for p in ps]
+    xr = bf(x.detach()).requires_grad_()
+    hs, _ = ref.bilstm(xr, ps_r)
+    ro = hs.mean(1)
+    assert rel(out, ro) < 2e-2
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    (ro * g).sum().backward()
+    assert rel(x.grad, xr.grad) < 5e-2
+    for p, pr in zip(ps, ps_r):
+        for t, tr in zip(p, pr):
+            assert rel(t.grad, tr.grad) < 5e-2

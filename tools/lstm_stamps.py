@@ -22,7 +22,7 @@ OUT = os.path.join(ROOT, "tools", "_stamps", "libdn_lstm_stamps.so")
 
 def build():
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
                            "-DDN_STAMPS", "-I", os.path.dirname(SRC), SRC, "-o", OUT])
 
 
@@ -43,7 +43,7 @@ def main():
     HD = padded_hidden(Hd)
     ndir = 2
     GP = 4 * HD
-    Bp = (B + 15) // 16 * 16
+    BR = int(_lib.lib().dn_lstm_rows_per_wg(B)); Bp = (B + BR - 1) // BR * BR
     torch.manual_seed(0)
     ps = []
     for _ in range(ndir):
