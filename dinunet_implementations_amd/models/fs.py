@@ -6,13 +6,13 @@ The BatchNorm never tracks running statistics, so evaluation also uses batch sta
 (SURVEY.md A5).  ``state_dict`` keys are identical to the reference:
 ``layers.{i}.0.weight``, ``layers.{i}.1.{weight,bias}``, ``fc_out.{weight,bias}``.
 
-On a GPU the whole forward+backward of the default 66->256->128->64->32->2 network runs as one
-fused HIP kernel per direction (``ops.fs_mlp``); the module tree below is kept for parameter
-ownership, checkpoint compatibility and the CPU oracle path.
+On a GPU ``forward_loss`` runs the whole network + log-softmax/NLL as one fused HIP launch
+forward and one backward (``ops.head``); the module tree is kept for parameter ownership,
+checkpoint compatibility, the CPU oracle path and ``forward`` (logits).
 """
 from __future__ import annotations
 
-from typing import Sequence
+from typing import Optional, Sequence
 
 import torch
 import torch.nn as nn
@@ -39,18 +39,22 @@ class MSANNet(nn.Module):
             d = h
         self.fc_out = nn.Linear(d, self.out_size)
         self.use_fused = True
+        self._head: Optional[ops.HeadSpec] = None
 
-    def fused_ok(self, x: torch.Tensor) -> bool:
-        return (self.use_fused and x.is_cuda and not self.dropout_in
-                and ops.fs_mlp_supported(self.in_size, self.hidden_sizes, self.out_size, x.shape[0]))
+    def head_spec(self) -> "ops.HeadSpec":
+        if self._head is None:
+            mods = [m for blk in self.layers for m in blk] + [self.fc_out]
+            self._head = ops.HeadSpec(mods)
+        return self._head
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.fused_ok(x):
-            ws = [blk[0].weight for blk in self.layers]
-            gs = [blk[1].weight for blk in self.layers]
-            bs = [blk[1].bias for blk in self.layers]
-            return ops.fs_mlp(x, ws, gs, bs, self.fc_out.weight, self.fc_out.bias,
-                              eps=self.layers[0][1].eps)
         for layer in self.layers:
             x = layer(x)
         return self.fc_out(x)
+
+    def forward_loss(self, x: torch.Tensor, y: torch.Tensor):
+        """``(log_probs, nll_loss, argmax)`` (reference ``comps/fs/__init__.py:54-57``)."""
+        if self.use_fused and x.is_cuda:
+            return ops.head_loss(x, self.head_spec(), y, log_out=True)
+        logits = self.forward(x)
+        return ops.log_softmax_nll(logits, y)

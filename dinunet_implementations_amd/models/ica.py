@@ -10,7 +10,8 @@ Execution is MI355X-first: on a GPU the encoder runs as one ``[B*S, C*W] x [C*W,
 GEMM with a fused bias+ReLU epilogue (no per-sample Python loop, reference ``models.py:107``),
 the input projection of both directions is one GEMM hoisted out of the recurrence, and the
 recurrence of both directions runs in one persistent HIP kernel whose recurrent weights stay
-resident in VGPRs for all time steps (``ops.lstm``).  On CPU the module runs the reference math
+resident in VGPRs for all time steps (``ops.lstm``); classifier + softmax-CE are one fused
+launch per direction (``ops.head``).  On CPU the module runs the reference math
 (``ops.reference``), which is also the test oracle.
 """
 from __future__ import annotations
@@ -114,6 +115,12 @@ class ICALstm(nn.Module):
             nn.Linear(64, num_cls),
         )
         self.use_fused = True
+        self._head: Optional[ops.HeadSpec] = None
+
+    def head_spec(self) -> "ops.HeadSpec":
+        if self._head is None:
+            self._head = ops.HeadSpec(list(self.classifier))
+        return self._head
 
     def encode(self, x: torch.Tensor) -> torch.Tensor:
         """``[B, S, C, W] -> [B, S, I]``: one batched GEMM instead of the per-sample loop."""
@@ -130,3 +137,14 @@ class ICALstm(nn.Module):
         enc = self.encode(x)
         o, h = self.lstm(enc, reduce="mean")
         return self.classifier(o.flatten(1).to(self.classifier[1].weight.dtype)), h
+
+    def forward_loss(self, x: torch.Tensor, y: torch.Tensor):
+        """``(probs, ce_loss, argmax)`` (reference ``comps/icalstm/__init__.py:59-63``); on a GPU
+        the classifier, softmax and cross-entropy are one fused launch each way."""
+        enc = self.encode(x)
+        o, _ = self.lstm(enc, reduce="mean")
+        o = o.flatten(1).to(self.classifier[1].weight.dtype)
+        if self.use_fused and x.is_cuda:
+            return ops.head_loss(o, self.head_spec(), y, log_out=False)
+        logits = self.classifier(o)
+        return ops.softmax_ce(logits, y)

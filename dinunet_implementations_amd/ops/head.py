@@ -1,0 +1,254 @@
+"""Fused MLP head + loss (``csrc/kernels/mlp_head.hip``).
+
+Covers the two classifier heads of the reference:
+
+* ICA  (``comps/icalstm/models.py:95-103`` + ``comps/icalstm/__init__.py:59-63``):
+  ``Dropout(0.25) -> Linear -> BatchNorm1d(running stats) -> ReLU -> Linear -> ReLU -> Linear``
+  then softmax cross-entropy; ``out`` = probabilities.
+* FS   (``comps/fs/models.py:4-31`` + ``comps/fs/__init__.py:54-57``): the whole MSANNet,
+  ``[Linear(no bias) -> BatchNorm1d(batch stats) -> ReLU (-> Dropout)] x L -> fc_out`` then
+  log-softmax + NLL; ``out`` = log-probabilities.
+
+A :class:`HeadSpec` is parsed from the module sequence itself, so the fused path always matches
+what the modules would compute (parameters, BN eps/momentum/mode, dropout placement); anything the
+kernel does not cover (batch > 64, > 16 classes, unknown modules) runs the modules + the loss op.
+
+The forward is one launch: loss, outputs, argmax, BatchNorm running-stat update and the dropout
+masks (counter-based hash; the seed is a device counter the kernel bumps, so HIP-graph replays
+draw fresh masks).  The backward is one launch that scales by ``dloss`` on the device and
+accumulates every head parameter gradient straight into its ``.grad`` (flat-buffer view) and
+returns ``d input``.  Dropout masks are not bit-identical to ``torch.nn.Dropout``'s generator
+stream (same distribution, independent draws); everything else matches the module math with
+bf16 MFMA operands and fp32 accumulation / statistics.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from . import _grad
+from . import _lib
+from . import capture as _cap
+from . import reference as ref
+
+Tensor = torch.Tensor
+_MAXL = 6
+
+_P = _lib.c_void_p
+_lib.register("dn_head_layout", [_P, _P, _P, _lib.c_int, _P])
+_lib.register("dn_head_fwd", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int, _P, _P,
+                              _P, _P, _P, _P, _lib.c_int, _lib.c_int, _P])
+_lib.register("dn_head_bwd", [_lib.c_int, _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _P, _lib.c_long,
+                              _P])
+
+
+class _Layer:
+    __slots__ = ("linear", "bn", "relu", "drop")
+
+    def __init__(self, linear: nn.Linear, drop: float):
+        self.linear = linear
+        self.bn: Optional[nn.BatchNorm1d] = None
+        self.relu = False
+        self.drop = drop
+
+
+class HeadSpec:
+    """A fusable description of ``modules`` (run in order) followed by a loss."""
+
+    def __init__(self, modules: Sequence[nn.Module]):
+        self.modules = list(modules)
+        self.layers: List[_Layer] = []
+        self.ok = True
+        pending = 0.0
+        for m in self.modules:
+            if isinstance(m, nn.Dropout):
+                if pending:
+                    self.ok = False
+                pending = float(m.p)
+            elif isinstance(m, nn.Linear):
+                self.layers.append(_Layer(m, pending))
+                pending = 0.0
+            elif isinstance(m, nn.BatchNorm1d):
+                L = self.layers[-1] if self.layers else None
+                if (L is None or L.bn is not None or L.relu or not m.affine
+                        or (m.track_running_stats and m.momentum is None)):
+                    self.ok = False
+                else:
+                    L.bn = m
+            elif isinstance(m, nn.ReLU):
+                if not self.layers or self.layers[-1].relu:
+                    self.ok = False
+                else:
+                    self.layers[-1].relu = True
+            else:
+                self.ok = False
+        if pending or not self.layers or len(self.layers) > _MAXL:
+            self.ok = False
+        if self.ok:
+            self.dims = [self.layers[0].linear.in_features] + [L.linear.out_features for L in self.layers]
+            for L, d in zip(self.layers, self.dims[:-1]):
+                if L.linear.in_features != d:
+                    self.ok = False
+        if not self.ok:
+            return
+        n = len(self.layers)
+        self.nl = n
+        self._dims = (ctypes.c_int * (n + 1))(*self.dims)
+        self._flags = (ctypes.c_int * n)(*[self._bn_mode(L) | (int(L.relu) << 2) for L in self.layers])
+        self._drops = (ctypes.c_float * n)(*[L.drop for L in self.layers])
+        bnp = []
+        for L in self.layers:
+            bnp += [L.bn.eps, L.bn.momentum or 0.0] if L.bn is not None else [1e-5, 0.1]
+        self._bnp = (ctypes.c_float * (2 * n))(*bnp)
+        self._layout = {}
+        self._rng: Optional[Tensor] = None
+
+    @staticmethod
+    def _bn_mode(L: _Layer) -> int:
+        if L.bn is None:
+            return 0
+        return 2 if L.bn.track_running_stats and L.bn.running_mean is not None else 1
+
+    # ---- parameters / pointers --------------------------------------------------------------
+    def params(self) -> List[nn.Parameter]:
+        ps = []
+        for L in self.layers:
+            ps.append(L.linear.weight)
+            if L.linear.bias is not None:
+                ps.append(L.linear.bias)
+            if L.bn is not None:
+                ps += [L.bn.weight, L.bn.bias]
+        return ps
+
+    @property
+    def training(self) -> bool:
+        return any(m.training for m in self.modules)
+
+    def layout(self, B: int):
+        lay = self._layout.get(B)
+        if lay is None:
+            buf = (ctypes.c_long * (1 + 4 * self.nl))()
+            rc = _lib.lib().dn_head_layout(self.nl, self._dims, self._flags, B, buf)
+            lay = list(buf) if rc == 0 else None
+            self._layout[B] = lay
+        return lay
+
+    def supported(self, x: Tensor) -> bool:
+        if not (self.ok and x.is_cuda and x.dim() == 2 and x.shape[1] == self.dims[0]):
+            return False
+        if not _lib.native_available():
+            if _lib.require_native():
+                raise RuntimeError("fused head on GPU needs the gfx950 kernel library")
+            return False
+        B = x.shape[0]
+        if B < 2 and any(self._bn_mode(L) == 1 or (L.bn is not None and self.training)
+                         for L in self.layers):
+            return False  # BatchNorm on one sample: let the modules raise like torch does
+        if any(p.dtype != torch.float32 or not p.is_contiguous() for p in self.params()):
+            return False
+        return self.layout(B) is not None
+
+    def rng(self, device) -> Tensor:
+        if self._rng is None or self._rng.device != device:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            self._rng = torch.tensor([seed], dtype=torch.int64, device=device)
+        return self._rng
+
+    def ptrs(self, with_grads: bool):
+        arr = (ctypes.c_void_p * (11 * self.nl))()
+        grads = []
+        for l, L in enumerate(self.layers):
+            lin, bn = L.linear, L.bn
+            v = [lin.weight, lin.bias]
+            if bn is not None:
+                v += [bn.weight, bn.bias]
+                if self._bn_mode(L) == 2:
+                    v += [bn.running_mean, bn.running_var, bn.num_batches_tracked]
+                else:
+                    v += [None, None, None]
+            else:
+                v += [None] * 5
+            g = [None] * 4
+            if with_grads:
+                g = [_grad.grad_buffer(lin.weight),
+                     _grad.grad_buffer(lin.bias) if lin.bias is not None else None,
+                     _grad.grad_buffer(bn.weight) if bn is not None else None,
+                     _grad.grad_buffer(bn.bias) if bn is not None else None]
+                grads += [t for t in g if t is not None]
+            for j, t in enumerate(v + g):
+                arr[11 * l + j] = None if t is None else t.data_ptr()
+        return arr
+
+    # ---- unfused path -----------------------------------------------------------------------
+    def run_modules(self, x: Tensor) -> Tensor:
+        for m in self.modules:
+            x = m(x)
+        return x
+
+
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, spec: HeadSpec, log_out: bool, *params):
+        x = x.float().contiguous()
+        y = y.long().contiguous()
+        B = x.shape[0]
+        C = spec.dims[-1]
+        train = spec.training
+        lay = spec.layout(B)
+        ws = torch.empty(lay[0], dtype=torch.uint8, device=x.device)
+        out = torch.empty(B, C, dtype=torch.float32, device=x.device)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        pred = torch.empty(B, dtype=torch.long, device=x.device)
+        rng = spec.rng(x.device)
+        _lib.call("dn_head_fwd", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
+                  spec.ptrs(False), x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(),
+                  loss.data_ptr(), pred.data_ptr(), rng.data_ptr(), ws.data_ptr(), int(train),
+                  int(log_out), _lib.stream())
+        ctx.spec, ctx.B, ctx.D0, ctx.train = spec, B, x.shape[1], train
+        ctx.ws = ws if train else None
+        ctx.mark_non_differentiable(out, pred)
+        return out, loss, pred
+
+    @staticmethod
+    def backward(ctx, dout, dloss, dpred):
+        n_in = 4 + len(ctx.spec.params())
+        if dloss is None:
+            return (None,) * n_in
+        if not ctx.train:
+            raise RuntimeError("fused head: backward needs a training-mode forward")
+        spec, B = ctx.spec, ctx.B
+        dloss = dloss.float().contiguous()
+        dx = torch.empty(B, ctx.D0, dtype=torch.float32, device=dloss.device) \
+            if ctx.needs_input_grad[0] else None
+        _lib.call("dn_head_bwd", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
+                  spec.ptrs(True), B, ctx.ws.data_ptr(), dloss.data_ptr(), _lib.ptr(dx),
+                  ctx.D0, _lib.stream())
+        params = spec.params()
+        _grad.notify(params)
+        if _cap.active() is not None:
+            lay = spec.layout(B)
+            for l, L in enumerate(spec.layers):
+                a_off, s_a, dz_off, s_z = lay[1 + 4 * l: 5 + 4 * l]
+                A = _ws_image(ctx.ws, a_off, B, s_a)[:, :L.linear.in_features]
+                D = _ws_image(ctx.ws, dz_off, B, s_z)[:, :L.linear.out_features]
+                _cap.record(L.linear, A.float(), D.float())
+        ctx.ws = None
+        return (dx,) + (None,) * (n_in - 1)
+
+
+def _ws_image(ws: Tensor, off: int, rows: int, stride: int) -> Tensor:
+    return ws[off: off + 2 * rows * stride].view(torch.bfloat16).view(rows, stride)
+
+
+def head_loss(x: Tensor, spec: HeadSpec, y: Tensor, log_out: bool):
+    """``(out, loss, pred)`` of ``loss(modules(x), y)``; fused on a GPU when supported."""
+    if spec.supported(x):
+        return _HeadFn.apply(x, y, spec, bool(log_out), *spec.params())
+    logits = spec.run_modules(x)
+    if logits.is_cuda:
+        from .heads import log_softmax_nll, softmax_ce
+        return (log_softmax_nll if log_out else softmax_ce)(logits, y)
+    return (ref.log_softmax_nll if log_out else ref.softmax_ce)(logits, y)

@@ -1,4 +1,4 @@
-"""Loss heads and the fused FreeSurfer MLP.
+"""Standalone loss heads (used when the classifier itself is not fused, see ``ops.head``).
 
 ``softmax_ce``  : ICA head, reference ``comps/icalstm/__init__.py:59-63``
 ``log_softmax_nll``: FS head, reference ``comps/fs/__init__.py:54-57``
@@ -6,8 +6,6 @@ Both return ``(out, loss, pred)`` where ``out`` is the probability (ICA) or log-
 tensor, exactly what the reference trainers hand to their metrics.
 """
 from __future__ import annotations
-
-from typing import List, Sequence
 
 import torch
 
@@ -53,14 +51,3 @@ def log_softmax_nll(logits: torch.Tensor, labels: torch.Tensor):
     if logits.is_cuda:
         return _SoftmaxXent.apply(logits, labels, True)
     return ref.log_softmax_nll(logits, labels)
-
-
-# ---- fused FS MLP (implemented in csrc/kernels/fs_mlp.hip when available) -----------------------
-def fs_mlp_supported(in_size: int, hidden: Sequence[int], out_size: int, batch: int) -> bool:
-    from . import fs_mlp as _f
-    return _f.supported(in_size, hidden, out_size, batch)
-
-
-def fs_mlp(x, ws: List[torch.Tensor], gammas, betas, w_out, b_out, eps: float = 1e-5):
-    from . import fs_mlp as _f
-    return _f.fs_mlp(x, ws, gammas, betas, w_out, b_out, eps)

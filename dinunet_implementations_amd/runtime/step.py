@@ -17,13 +17,11 @@ from .. import ops
 
 
 def ica_forward_loss(model, x, y):
-    logits, _ = model(x)
-    return ops.softmax_ce(logits, y)
+    return model.forward_loss(x, y)
 
 
 def fs_forward_loss(model, x, y):
-    logits = model(x)
-    return ops.log_softmax_nll(logits, y)
+    return model.forward_loss(x, y)
 
 
 HEADS = {"ica": ica_forward_loss, "fs": fs_forward_loss}

@@ -87,8 +87,7 @@ class FreeSurferTrainer(NNTrainer):
                                     dropout_in=self.cache.get("dropout_in", []))
 
     def forward_loss(self, x, y):
-        logits = self.nn["fs_net"](x.float())
-        return ops.log_softmax_nll(logits, y)
+        return self.nn["fs_net"].forward_loss(x.float(), y)
 
     def score(self, out, pred):
         return pred  # metrics on hard argmax labels (comps/fs/__init__.py:57-59, quirk A10)

@@ -87,8 +87,7 @@ class ICATrainer(NNTrainer):
                                  bidirectional=c.setdefault("bidirectional", True))
 
     def forward_loss(self, x, y):
-        logits, _ = self.nn["net"](x.float())
-        return ops.softmax_ce(logits, y)
+        return self.nn["net"].forward_loss(x.float(), y)
 
     def score(self, out, pred):
         return out[:, 1]  # AUC on prob[:, 1] (comps/icalstm/__init__.py:64-65)

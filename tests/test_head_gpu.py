@@ -1,0 +1,200 @@
+"""Fused MLP head + loss (csrc/kernels/mlp_head.hip) against the plain module path in fp32."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-12)
+
+
+def _ica_head(p=0.25, hidden=384, ncls=2):
+    return nn.Sequential(nn.Dropout(p), nn.Linear(hidden, 256), nn.BatchNorm1d(256), nn.ReLU(),
+                         nn.Linear(256, 64), nn.ReLU(), nn.Linear(64, ncls))
+
+
+def _fs_head(in_size=66, hidden=(256, 128, 64, 32), ncls=2, dropout_in=()):
+    from dinunet_implementations_amd.models import MSANNet
+    return MSANNet(in_size, list(hidden), ncls, dropout_in=list(dropout_in))
+
+
+class _RoundFwd(torch.autograd.Function):
+    """bf16 rounding of a forward value (an MFMA operand); gradient passes through."""
+    @staticmethod
+    def forward(ctx, t):
+        return t.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, d):
+        return d
+
+
+class _RoundBwd(torch.autograd.Function):
+    """Identity forward; rounds the incoming gradient to bf16 (the kernel's dZ operand)."""
+    @staticmethod
+    def forward(ctx, t):
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, d):
+        return d.to(torch.bfloat16).float()
+
+
+def _emulated(mods, x):
+    """The module chain with the fused kernel's rounding points (bf16 MFMA operands, fp32
+    bias / BatchNorm / accumulation), no dropout."""
+    from dinunet_implementations_amd.ops.head import HeadSpec
+    spec = HeadSpec(mods)
+    a = x
+    for L in spec.layers:
+        lin = L.linear
+        z = _RoundBwd.apply(_RoundFwd.apply(a) @ _RoundFwd.apply(lin.weight).t())
+        if lin.bias is not None:
+            z = z + lin.bias
+        if L.bn is not None:
+            z = L.bn(z)
+        if L.relu:
+            z = torch.relu(z)
+        a = z
+    return a
+
+
+def _compare(mods_fused, mods_ref, fused_fn, x, y, log_out, train=True, emulate=True):
+    from dinunet_implementations_amd.ops import reference as ref
+    from dinunet_implementations_amd.ops.head import HeadSpec, head_loss
+    spec = HeadSpec(mods_fused)
+    assert spec.ok and spec.supported(x)
+    xf = x.clone().requires_grad_()
+    xr = x.clone().requires_grad_()
+    out, loss, pred = head_loss(xf, spec, y, log_out=log_out)
+    if emulate:
+        z = _emulated(mods_ref, xr)
+    else:
+        z = xr
+        for m in mods_ref:
+            z = m(z)
+    ro, rl, rp = (ref.log_softmax_nll if log_out else ref.softmax_ce)(z, y)
+    assert abs(loss.item() - rl.item()) < 2e-2 * max(1.0, abs(rl.item()))
+    assert rel(out, ro) < 2e-2
+    agree = (pred == rp).float().mean().item()
+    assert agree > 0.9
+    if train:
+        loss.backward()
+        rl.backward()
+        assert rel(xf.grad, xr.grad) < 2e-2
+    return xf, xr
+
+
+@pytest.mark.parametrize("B", [32, 7, 50])
+def test_ica_head_train_matches_modules(B):
+    torch.manual_seed(0)
+    head = _ica_head(p=0.0).to(DEV).train()
+    ref_head = copy.deepcopy(head)
+    x = torch.randn(B, 384, device=DEV)
+    y = torch.randint(0, 2, (B,), device=DEV)
+    _compare(list(head), list(ref_head), None, x, y, log_out=False)
+    for (n, p), (_, q) in zip(head.named_parameters(), ref_head.named_parameters()):
+        if n == "1.bias":  # feeds a batch-statistics BatchNorm: true gradient is ~0
+            assert p.grad.abs().max() < 1e-5
+            continue
+        assert rel(p.grad, q.grad) < 2e-2, n
+    bn, rbn = head[2], ref_head[2]
+    assert torch.allclose(bn.running_mean, rbn.running_mean, atol=2e-3, rtol=2e-2)
+    assert torch.allclose(bn.running_var, rbn.running_var, atol=2e-3, rtol=2e-2)
+    assert int(bn.num_batches_tracked) == int(rbn.num_batches_tracked) == 1
+
+
+def test_ica_head_eval_uses_running_stats():
+    torch.manual_seed(1)
+    head = _ica_head().to(DEV)
+    head[2].running_mean.uniform_(-0.5, 0.5)
+    head[2].running_var.uniform_(0.5, 2.0)
+    head.eval()
+    ref_head = copy.deepcopy(head)
+    x = torch.randn(20, 384, device=DEV)
+    y = torch.randint(0, 2, (20,), device=DEV)
+    with torch.no_grad():
+        _compare(list(head), list(ref_head), None, x, y, log_out=False, train=False, emulate=False)
+
+
+def test_ica_head_dropout_statistics_and_fresh_masks():
+    from dinunet_implementations_amd.ops.head import HeadSpec, head_loss
+    torch.manual_seed(2)
+    head = _ica_head(p=0.25).to(DEV).train()
+    spec = HeadSpec(list(head))
+    x = torch.randn(32, 384, device=DEV).abs() + 0.1
+    y = torch.randint(0, 2, (32,), device=DEV)
+    masks = []
+    for _ in range(2):
+        xf = x.clone().requires_grad_()
+        _, loss, _ = head_loss(xf, spec, y, log_out=False)
+        loss.backward()
+        masks.append(xf.grad != 0)
+    for m in masks:
+        frac = 1.0 - m.float().mean().item()
+        assert 0.2 < frac < 0.3, frac
+    assert not torch.equal(masks[0], masks[1])
+
+
+@pytest.mark.parametrize("B,dropout_in", [(16, ()), (45, ()), (16, (1,))])
+def test_fs_network_fused_matches_modules(B, dropout_in):
+    torch.manual_seed(3)
+    net = _fs_head(dropout_in=dropout_in).to(DEV).train()
+    ref_net = copy.deepcopy(net)
+    x = torch.rand(B, 66, device=DEV)
+    y = torch.randint(0, 2, (B,), device=DEV)
+    out, loss, pred = net.forward_loss(x, y)
+    from dinunet_implementations_amd.ops import reference as ref
+    ro, rl, rp = ref.log_softmax_nll(_emulated([m for blk in ref_net.layers for m in blk]
+                                               + [ref_net.fc_out], x), y)
+    if dropout_in:
+        assert torch.isfinite(loss) and out.shape == ro.shape
+        loss.backward()
+        assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
+        return
+    assert abs(loss.item() - rl.item()) < 2e-2 * max(1.0, abs(rl.item()))
+    assert rel(out, ro) < 2e-2
+    loss.backward()
+    rl.backward()
+    for (n, p), (_, q) in zip(net.named_parameters(), ref_net.named_parameters()):
+        assert rel(p.grad, q.grad) < 2e-2, n
+
+
+def test_head_grads_accumulate_and_scale():
+    """Gradients add into existing .grad and scale with d loss (loss * 3)."""
+    from dinunet_implementations_amd.ops.head import HeadSpec, head_loss
+    torch.manual_seed(4)
+    head = _ica_head(p=0.0).to(DEV).train()
+    spec = HeadSpec(list(head))
+    x = torch.randn(32, 384, device=DEV)
+    y = torch.randint(0, 2, (32,), device=DEV)
+    _, loss, _ = head_loss(x, spec, y, log_out=False)
+    loss.backward()
+    g1 = [p.grad.clone() for p in head.parameters()]
+    _, loss, _ = head_loss(x, spec, y, log_out=False)
+    (3.0 * loss).backward()
+    for (n, p), g in zip(head.named_parameters(), g1):
+        if n != "1.bias":
+            assert rel(p.grad, 4.0 * g) < 1e-3, n
+
+
+def test_ica_model_forward_loss_fused_vs_cpu():
+    from dinunet_implementations_amd.models import ICALstm
+    torch.manual_seed(5)
+    m = ICALstm(input_size=64, hidden_size=96, num_comps=20, window_size=5, num_cls=2)
+    mc = copy.deepcopy(m)
+    m = m.to(DEV).eval()
+    mc.eval()
+    x = torch.randn(24, 11, 20, 5)
+    y = torch.randint(0, 2, (24,))
+    with torch.no_grad():
+        out, loss, pred = m.forward_loss(x.to(DEV), y.to(DEV))
+        ro, rl, rp = mc.forward_loss(x, y)
+    assert rel(out.cpu(), ro) < 3e-2
+    assert abs(loss.item() - rl.item()) < 3e-2
