@@ -1,31 +1,35 @@
 // Fused MLP head + loss for gfx950: the ICA classifier (reference comps/icalstm/models.py:95-103
 // + comps/icalstm/__init__.py:59-63) and the FreeSurfer MSANNet (comps/fs/models.py:4-31 +
-// comps/fs/__init__.py:54-57) as ONE forward launch and ONE backward launch.
+// comps/fs/__init__.py:54-57) in two launches forward and two backward (instead of ~40 kernels).
 //
 // A head is a chain of at most HMAXL layers, each
 //     [dropout on the input] -> Linear (+bias) -> [BatchNorm1d] -> [ReLU]
 // ending in softmax cross-entropy (probabilities out) or log-softmax + NLL (log-probs out).
-// At these sizes (batch <= 64, widths <= ~1k) the head is pure latency: the unfused graph is ~40
-// tiny kernels.  Here one 16-wave workgroup keeps every activation in LDS:
-//  * forward: wave w owns output-column tiles n = 16w.. for ALL batch rows, so BatchNorm column
-//    statistics are an in-register reduction (lanes l, l^16, l^32, l^48 hold one column); the
-//    layer GEMM is 16x16x32 bf16 MFMA, A = activation rows from LDS (ds_read_b128), B = the fp32
-//    master weight rows read straight from global memory and rounded while loading.
-//  * backward: dW = dZ^T A is an MFMA over the batch whose operands are built with the CDNA4 LDS
-//    transpose read (ds_read_b64_tr_b16) from the same row-major activation images; dA = dZ W
-//    again gives each wave whole columns, so ReLU/dropout masks and the BatchNorm backward
-//    (two column sums) happen in the epilogue.  Parameter gradients are accumulated into the
-//    caller's fp32 .grad buffers (flat gradient buffer views), so no autograd adds run.
-//  * dropout masks come from a counter-based hash of (seed, layer, row, col); the seed lives in
-//    device memory and is bumped by the kernel, so a captured HIP graph draws fresh masks on
-//    every replay.  The backward regenerates the mask from the seed saved in the workspace.
+// Batch <= 64: everything is latency / per-CU-bandwidth bound (one CU streams only ~50 GB/s),
+// so the launches are split by where the bytes are:
+//  fwd0  (grid = layer-0 column tiles): the widest layer.  Each workgroup builds the bf16 input
+//        image in LDS, its four waves split K, and wave 0 owns 16 output columns for ALL batch
+//        rows, so BatchNorm column statistics are an in-register reduction (lanes l, l^16, l^32,
+//        l^48 hold one column).  Output activations go to the workspace.
+//  fwd1  (one workgroup): the remaining (narrow) layers from LDS, softmax/CE, argmax, loss.
+//  bwd1  (one workgroup): the output-gradient chain dZ_l -> dA = dZ W -> dropout / ReLU /
+//        BatchNorm backward in the epilogue (wave-owned columns again) down to dZ_0, plus the
+//        bias / BatchNorm parameter gradients (column sums).
+//  bwd0  (grid = every layer's 16-row dW slices + the 16-column slices of dX): dW = dZ^T A as
+//        MFMA over the batch with operands from the CDNA4 LDS transpose read
+//        (ds_read_b64_tr_b16), accumulated into the caller's fp32 .grad buffers; dX = dZ_0 W_0.
+// GEMMs are 16x16x32 bf16 MFMA with fp32 accumulation; the fp32 master weights are read straight
+// from global memory and rounded while loading.  Kernel boundaries are the only inter-workgroup
+// synchronisation.  Dropout masks come from a counter-based hash of (seed, layer, row, col); the
+// seed is a device word bumped by fwd1, so a captured HIP graph draws fresh masks on every replay,
+// and the backward regenerates the mask from the seed saved in the workspace.
 #include "common.h"
 
 namespace {
 
 constexpr int HMAXL = 6;
-// 16 waves for batches <= 32 (MT = 2); 8 waves (256-VGPR budget, no spills) for batches <= 64
-template <int MT> struct HCfg { static constexpr int NT = MT == 2 ? 1024 : 512, NW = NT / 64; };
+constexpr int HW_NT = 256;  // fwd0 / bwd0 workgroups (4 waves)
+constexpr int HS_NT = 512;  // fwd1 / bwd1 single workgroup (8 waves, 256-VGPR budget)
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -56,10 +60,18 @@ struct HLayer {
 struct HArgs {
   HLayer L[HMAXL];
   int nl, B;
-  int buf_a, buf_z;  // LDS image sizes (elements) for the activation / gradient buffers
+  int buf_a1;        // LDS elements of the largest activation image of layers >= 1
+  int buf_z;         // LDS elements of the largest output-gradient image
+  int buf_aall;      // LDS elements of the largest activation image of any layer
   long dzl_off;      // fp32 [Mp][16] d loss / d logits (unscaled)
+  long logit_off;    // fp32 [Mp][16] logits of a one-layer head (fwd0 -> fwd1)
+  int dw_jobs[HMAXL + 1];  // bwd0: prefix sums of 16-row dW slices per layer
   int train, log_out;
 };
+
+// Optional phase timestamps (s_memrealtime, 100 MHz) written by thread 0 when a stamp buffer is
+// installed with dn_head_set_stamps (diagnostics: tools/bench_head.py --stamps).
+#define HSTAMP(i) do { if (stamps && threadIdx.x == 0) stamps[(i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 __host__ __device__ constexpr int rup32(int v) { return (v + 31) & ~31; }
 
@@ -82,17 +94,28 @@ __device__ __forceinline__ float colsum4(float v) {
   return v;
 }
 
-// B fragment from weight ROWS: lane -> n = n (row), k .. k+7 (contiguous)
+// B fragment from weight ROWS: lane -> row n, k .. k+7 (contiguous).  Branchless (clamped
+// address + select) so a batch of these issues all its loads before the first use.
+template <bool VEC>
 __device__ __forceinline__ bf16x8 wfrag_rows(const float* __restrict__ W, int N, int K, int n, int k) {
   bf16x8 f;
-  if (n < N && k + 8 <= K && (K & 3) == 0) {
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(W + (long)n * K + k);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(W + (long)n * K + k + 4);
+  if constexpr (VEC) {  // K % 8 == 0: the 8 elements are all in or all out
+    const bool ok = n < N && k < K;
+    const float* p = W + (ok ? (long)n * K + k : 0);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(p);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + 4);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { f[e] = (bf16)v0[e]; f[4 + e] = (bf16)v1[e]; }
+    for (int e = 0; e < 4; ++e) {
+      f[e] = (bf16)(ok ? v0[e] : 0.f);
+      f[4 + e] = (bf16)(ok ? v1[e] : 0.f);
+    }
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = (n < N && k + e < K) ? (bf16)W[(long)n * K + k + e] : (bf16)0.f;
+    for (int e = 0; e < 8; ++e) {
+      const bool ok = n < N && k + e < K;
+      const float v = W[ok ? (long)n * K + k + e : 0];
+      f[e] = (bf16)(ok ? v : 0.f);
+    }
   }
   return f;
 }
@@ -101,7 +124,11 @@ __device__ __forceinline__ bf16x8 wfrag_rows(const float* __restrict__ W, int N,
 __device__ __forceinline__ bf16x8 wfrag_cols(const float* __restrict__ W, int N, int K, int n, int kk) {
   bf16x8 f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = (n + j < N && kk < K) ? (bf16)W[(long)(n + j) * K + kk] : (bf16)0.f;
+  for (int j = 0; j < 8; ++j) {
+    const bool ok = n + j < N && kk < K;
+    const float v = W[ok ? (long)(n + j) * K + kk : 0];
+    f[j] = (bf16)(ok ? v : 0.f);
+  }
   return f;
 }
 
@@ -115,141 +142,279 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int S, int c0, int k0
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+
+// bias -> BatchNorm -> ReLU -> (next layer's dropout) epilogue of one 16-column tile of layer l,
+// held as MFMA accumulators for every batch row by one wave.  Activations go to the LDS image
+// `nxt` (if given) and to the workspace image; logits of the last layer to `logit`.
 template <int MT>
-__global__ void __launch_bounds__(HCfg<MT>::NT)
-head_fwd_kernel(HArgs a, const float* __restrict__ x, long ldx, const long long* __restrict__ y,
-                float* __restrict__ out, float* __restrict__ loss, long long* __restrict__ pred,
-                unsigned long long* __restrict__ rng, char* __restrict__ ws) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int Mp = 16 * MT;
-  constexpr int HNT = HCfg<MT>::NT, HNW = HCfg<MT>::NW;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int B = a.B;
+__device__ __forceinline__ void fwd_epilogue(const HArgs& a, int l, const f32x4 (&acc)[MT], int n,
+                                             int lane, uint64_t seed, char* __restrict__ ws,
+                                             bf16* nxt, float* logit) {
+  const HLayer& L = a.L[l];
+  const int N = L.out, B = a.B;
   const bool train = a.train != 0;
-  bf16* cur = reinterpret_cast<bf16*>(smem);
-  bf16* nxt = cur + a.buf_a;
-  float* logit = reinterpret_cast<float*>(nxt + a.buf_a);  // [Mp][16]
-  const uint64_t seed = rng ? *rng : 0ull;
-
-  // ---- input image (dropout of layer 0 applied), also saved for the backward
-  {
-    const HLayer& L0 = a.L[0];
-    const int K = L0.in, Kp = rup32(K), S = L0.S_a;
-    const float inv = L0.drop > 0.f ? 1.f / (1.f - L0.drop) : 1.f;
-    bf16* wimg = reinterpret_cast<bf16*>(ws + L0.a_off);
-    for (int idx = tid; idx < Mp * Kp; idx += HNT) {
-      const int m = idx / Kp, k = idx - m * Kp;
-      float v = 0.f;
-      if (m < B && k < K) {
-        v = x[(long)m * ldx + k];
-        if (train && L0.drop > 0.f) v = hkeep(seed, 0, m, k, K, L0.drop) ? v * inv : 0.f;
-      }
-      const bf16 bv = (bf16)v;
-      cur[m * S + k] = bv;
-      if (train) wimg[m * S + k] = bv;
-    }
-  }
-  __syncthreads();
-
-  for (int l = 0; l < a.nl; ++l) {
-    const HLayer& L = a.L[l];
-    const int K = L.in, N = L.out, Kp = rup32(K), S = L.S_a;
-    const bool last = l == a.nl - 1;
-    const int ntiles = last ? 1 : L.Np / 16;  // cover rup32(out): the next image's pad is zeroed
-    const HLayer& Ln = a.L[last ? l : l + 1];
-    const int Sn = Ln.S_a;
-    const float pn = last ? 0.f : Ln.drop;
-    const float invn = pn > 0.f ? 1.f / (1.f - pn) : 1.f;
-    bf16* wnext = reinterpret_cast<bf16*>(ws + Ln.a_off);
-    float* xhat_ws = reinterpret_cast<float*>(ws + L.xhat_off);
-    float* rstd_ws = reinterpret_cast<float*>(ws + L.rstd_off);
-    for (int t = wid; t < ntiles; t += HNW) {
-      const int n = 16 * t + (lane & 15);
-      f32x4 acc[MT];
+  const bool last = l == a.nl - 1;
+  const bool cv = n < N;
+  const float bias = (L.b && cv) ? L.b[n] : 0.f;
+  float z[MT][4];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int k0 = 0; k0 < Kp; k0 += 32) {
-        const bf16x8 bfr = wfrag_rows(L.W, N, K, n, k0 + 8 * (lane >> 4));
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(cur + (16 * mt + (lane & 15)) * S + k0 + 8 * (lane >> 4));
-          acc[mt] = mfma16(af, bfr, acc[mt]);
-        }
-      }
-      const bool cv = n < N;
-      const float bias = (L.b && cv) ? L.b[n] : 0.f;
-      float z[MT][4];
+    for (int r = 0; r < 4; ++r) z[mt][r] = acc[mt][r] + bias;
+  if (L.bn) {
+    float mean, rstd;
+    if (train || L.bn == 1) {
+      float s = 0.f;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) z[mt][r] = acc[mt][r] + bias;
-      if (L.bn) {
-        float mean, rstd;
-        if (train || L.bn == 1) {
-          float s = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s += (16 * mt + 4 * (lane >> 4) + r < B) ? z[mt][r] : 0.f;
-          mean = colsum4(s) / (float)B;
-          float v = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float d = z[mt][r] - mean;
-              v += (16 * mt + 4 * (lane >> 4) + r < B) ? d * d : 0.f;
-            }
-          v = colsum4(v) / (float)B;
-          rstd = rsqrtf(v + L.eps);
-          if (train && L.bn == 2 && lane < 16 && cv) {
-            const float mo = L.momentum;
-            L.rmean[n] = (1.f - mo) * L.rmean[n] + mo * mean;
-            L.rvar[n] = (1.f - mo) * L.rvar[n] + mo * v * ((float)B / (float)(B > 1 ? B - 1 : 1));
-          }
-        } else {
-          mean = cv ? L.rmean[n] : 0.f;
-          rstd = cv ? rsqrtf(L.rvar[n] + L.eps) : 0.f;
-        }
-        const float ga = cv ? L.gamma[n] : 0.f, be = cv ? L.beta[n] : 0.f;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = 16 * mt + 4 * (lane >> 4) + r;
-            const float xh = (z[mt][r] - mean) * rstd;
-            if (train) xhat_ws[row * L.Np + n] = (row < B && cv) ? xh : 0.f;
-            z[mt][r] = ga * xh + be;
-          }
-        if (train && lane < 16) rstd_ws[n] = cv ? rstd : 0.f;
-      }
+        for (int r = 0; r < 4; ++r) s += (16 * mt + 4 * (lane >> 4) + r < B) ? z[mt][r] : 0.f;
+      mean = colsum4(s) / (float)B;
+      float v = 0.f;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = 16 * mt + 4 * (lane >> 4) + r;
-          float v = z[mt][r];
-          if (L.relu) v = fmaxf(v, 0.f);
-          if (last) {
-            logit[row * 16 + (lane & 15)] = v;
-          } else {
-            v = (row < B && cv) ? v : 0.f;
-            if (train && pn > 0.f && v != 0.f) v = hkeep(seed, l + 1, row, n, N, pn) ? v * invn : 0.f;
-            const bf16 bv = (bf16)v;
-            nxt[row * Sn + n] = bv;
-            if (train) wnext[row * Sn + n] = bv;
+          const float d = z[mt][r] - mean;
+          v += (16 * mt + 4 * (lane >> 4) + r < B) ? d * d : 0.f;
+        }
+      v = colsum4(v) / (float)B;
+      rstd = rsqrtf(v + L.eps);
+      if (train && L.bn == 2 && lane < 16 && cv) {
+        const float mo = L.momentum;
+        L.rmean[n] = (1.f - mo) * L.rmean[n] + mo * mean;
+        L.rvar[n] = (1.f - mo) * L.rvar[n] + mo * v * ((float)B / (float)(B > 1 ? B - 1 : 1));
+      }
+    } else {
+      mean = cv ? L.rmean[n] : 0.f;
+      rstd = cv ? rsqrtf(L.rvar[n] + L.eps) : 0.f;
+    }
+    const float ga = cv ? L.gamma[n] : 0.f, be = cv ? L.beta[n] : 0.f;
+    float* xhat_ws = reinterpret_cast<float*>(ws + L.xhat_off);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * mt + 4 * (lane >> 4) + r;
+        const float xh = (z[mt][r] - mean) * rstd;
+        if (train) xhat_ws[row * L.Np + n] = (row < B && cv) ? xh : 0.f;
+        z[mt][r] = ga * xh + be;
+      }
+    if (train && lane < 16) reinterpret_cast<float*>(ws + L.rstd_off)[n] = cv ? rstd : 0.f;
+  }
+  const HLayer& Ln = a.L[last ? l : l + 1];
+  const int Sn = Ln.S_a;
+  const float pn = (last || !train) ? 0.f : Ln.drop;
+  const float invn = pn > 0.f ? 1.f / (1.f - pn) : 1.f;
+  bf16* wnext = reinterpret_cast<bf16*>(ws + Ln.a_off);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * mt + 4 * (lane >> 4) + r;
+      float v = z[mt][r];
+      if (L.relu) v = fmaxf(v, 0.f);
+      if (last) {
+        logit[row * 16 + (lane & 15)] = v;
+      } else {
+        v = (row < B && cv) ? v : 0.f;
+        if (pn > 0.f && v != 0.f) v = hkeep(seed, l + 1, row, n, N, pn) ? v * invn : 0.f;
+        const bf16 bv = (bf16)v;
+        if (nxt) nxt[row * Sn + n] = bv;
+        wnext[row * Sn + n] = bv;
+      }
+    }
+}
+
+// Copy a bf16 workspace image (rows x S elements, S % 8 == 0) into LDS, loads batched.
+template <int NT>
+__device__ __forceinline__ void ws_to_lds(bf16* __restrict__ dst_, const char* __restrict__ src_,
+                                          int elems, int tid) {
+  const bf16x8* src = reinterpret_cast<const bf16x8*>(src_);
+  bf16x8* dst = reinterpret_cast<bf16x8*>(dst_);
+  const int nv = elems / 8;
+  for (int base = tid; base < nv; base += 4 * NT) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src[base + u * NT < nv ? base + u * NT : 0];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * NT < nv) dst[base + u * NT] = v[u];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// fwd0: layer 0, one 16-column tile per workgroup; the four waves split K.
+template <int MT>
+__global__ void __launch_bounds__(HW_NT)
+head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
+                 const unsigned long long* __restrict__ rng, char* __restrict__ ws,
+                 unsigned long long* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int Mp = 16 * MT, NT = HW_NT, NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int B = a.B;
+  const bool train = a.train != 0;
+  const HLayer& L0 = a.L[0];
+  const int K = L0.in, N = L0.out, Kp = rup32(K), S = L0.S_a;
+  bf16* img = reinterpret_cast<bf16*>(smem);
+  float* red = reinterpret_cast<float*>(smem + ((2 * Mp * S + 15) & ~15));  // [NW][MT*4][64]
+  const uint64_t seed = rng ? *rng : 0ull;
+  if (blockIdx.x == 0) HSTAMP(0);
+
+  {  // input image (layer-0 dropout applied); workgroup 0 saves it for the backward
+    const float inv = L0.drop > 0.f ? 1.f / (1.f - L0.drop) : 1.f;
+    const bool save = train && blockIdx.x == 0;
+    bf16* wimg = reinterpret_cast<bf16*>(ws + L0.a_off);
+    const int nch = Mp * Kp / 4;  // 4-element chunks (Kp % 32 == 0: chunks never straddle rows)
+    const bool vec = (K % 4) == 0 && (ldx % 4) == 0 && (((uintptr_t)x) & 15) == 0;
+    for (int base = tid; base < nch; base += 4 * NT) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // all loads of the round first
+        const int c = base + u * NT;
+        const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
+        const bool ok = c < nch && m < B && k < K;
+        if (vec) {
+          v[u] = *reinterpret_cast<const f32x4*>(x + (ok ? (long)m * ldx + k : 0));
+          if (!ok) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool oe = ok && k + e < K;
+            const float t = x[oe ? (long)m * ldx + k + e : 0];
+            v[u][e] = oe ? t : 0.f;
           }
         }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = base + u * NT;
+        if (c >= nch) break;
+        const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = v[u][e];
+          if (train && L0.drop > 0.f && t != 0.f) t = hkeep(seed, 0, m, k + e, K, L0.drop) ? t * inv : 0.f;
+          o[e] = (bf16)t;
+        }
+        *reinterpret_cast<bf16x4*>(img + m * S + k) = o;
+        if (save) *reinterpret_cast<bf16x4*>(wimg + m * S + k) = o;
+      }
     }
-    if (train && L.bn == 2 && tid == 0 && L.nbt) *L.nbt += 1;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) HSTAMP(1);
+
+  const int n = 16 * blockIdx.x + (lane & 15);
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nks = Kp / 32;
+  const bool vecw = (K % 8) == 0;
+  for (int kb = wid; kb < nks; kb += 4 * NW) {  // this wave's k-steps, four loads in flight
+    bf16x8 bq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k0 = 32 * (kb + u * NW) + 8 * (lane >> 4);
+      bq[u] = vecw ? wfrag_rows<true>(L0.W, N, K, n, k0) : wfrag_rows<false>(L0.W, N, K, n, k0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ks = kb + u * NW;
+      if (ks >= nks) break;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + (16 * mt + (lane & 15)) * S + 32 * ks + 8 * (lane >> 4));
+        acc[mt] = mfma16(af, bq[u], acc[mt]);
+      }
+    }
+  }
+  if (wid > 0) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((wid - 1) * MT * 4 + mt * 4 + r) * 64 + lane] = acc[mt][r];
+  }
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int w = 0; w < NW - 1; ++w)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mt][r] += red[(w * MT * 4 + mt * 4 + r) * 64 + lane];
+    fwd_epilogue<MT>(a, 0, acc, n, lane, seed, ws, nullptr,
+                     reinterpret_cast<float*>(ws + a.logit_off));
+    if (blockIdx.x == 0) HSTAMP(2);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// fwd1: layers 1.. and the loss in one workgroup.
+template <int MT>
+__global__ void __launch_bounds__(HS_NT)
+head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ out,
+                 float* __restrict__ loss, long long* __restrict__ pred,
+                 unsigned long long* __restrict__ rng, char* __restrict__ ws,
+                 unsigned long long* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int Mp = 16 * MT, NT = HS_NT, NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int B = a.B;
+  const bool train = a.train != 0;
+  bf16* cur = reinterpret_cast<bf16*>(smem);
+  bf16* nxt = cur + a.buf_a1;
+  float* logit = reinterpret_cast<float*>(nxt + a.buf_a1);  // [Mp][16]
+  const uint64_t seed = rng ? *rng : 0ull;
+  HSTAMP(3);
+  if (a.nl >= 2) {
+    ws_to_lds<NT>(cur, ws + a.L[1].a_off, Mp * a.L[1].S_a, tid);
+  } else {
+    const float* src = reinterpret_cast<const float*>(ws + a.logit_off);
+    for (int i = tid; i < Mp * 16; i += NT) logit[i] = src[i];
+  }
+  __syncthreads();
+  HSTAMP(4);
+  for (int l = 1; l < a.nl; ++l) {
+    const HLayer& L = a.L[l];
+    const int K = L.in, N = L.out, Kp = rup32(K), S = L.S_a;
+    const bool last = l == a.nl - 1;
+    const int ntiles = last ? 1 : L.Np / 16;  // cover rup32(out): the next image's pad is zeroed
+    const bool vecw = (K % 8) == 0;
+    for (int t = wid; t < ntiles; t += NW) {
+      const int n = 16 * t + (lane & 15);
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kb = 0; kb < Kp; kb += 8 * 32) {  // 8 k-steps of weight loads in flight
+        bf16x8 bq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          bq[u] = vecw ? wfrag_rows<true>(L.W, N, K, n, kb + 32 * u + 8 * (lane >> 4))
+                       : wfrag_rows<false>(L.W, N, K, n, kb + 32 * u + 8 * (lane >> 4));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k0 = kb + 32 * u;
+          if (k0 >= Kp) break;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(cur + (16 * mt + (lane & 15)) * S + k0 + 8 * (lane >> 4));
+            acc[mt] = mfma16(af, bq[u], acc[mt]);
+          }
+        }
+      }
+      fwd_epilogue<MT>(a, l, acc, n, lane, seed, ws, nxt, logit);
+    }
     __syncthreads();
+    HSTAMP(4 + l);
     bf16* t = cur;
     cur = nxt;
     nxt = t;
   }
 
-  // ---- softmax / log-softmax + CE / NLL, argmax; wave 0, lane = batch row
+  // softmax / log-softmax + CE / NLL, argmax; wave 0, lane = batch row
   if (wid == 0) {
     const int C = a.L[a.nl - 1].out;
     const int m = lane;
@@ -280,20 +445,26 @@ head_fwd_kernel(HArgs a, const float* __restrict__ x, long ldx, const long long*
     for (int off = 32; off >= 1; off >>= 1) ls += __shfl_xor(ls, off);
     if (lane == 0) {
       *loss = ls / (float)B;
-      if (train) *reinterpret_cast<unsigned long long*>(ws) = seed;
-      if (train && rng) *rng = seed + 1ull;
+      if (train) {
+        *reinterpret_cast<unsigned long long*>(ws) = seed;
+        if (rng) *rng = seed + 1ull;
+        for (int l = 0; l < a.nl; ++l)
+          if (a.L[l].bn == 2 && a.L[l].nbt) *a.L[l].nbt += 1;
+      }
     }
+    HSTAMP(12);
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// bwd1: output-gradient chain down to dZ_0 (+ bias / BatchNorm parameter gradients).
 template <int MT>
-__global__ void __launch_bounds__(HCfg<MT>::NT)
-head_bwd_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss,
-                float* __restrict__ dx, long lddx) {
+__global__ void __launch_bounds__(HS_NT)
+head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss,
+                 unsigned long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int Mp = 16 * MT;
-  constexpr int HNT = HCfg<MT>::NT, HNW = HCfg<MT>::NW;
-  constexpr int G = 4;  // dW tiles per wave batch (global read-modify-write in flight together)
+  constexpr int Mp = 16 * MT, NT = HS_NT, NW = NT / 64;
+  constexpr int CB = MT == 2 ? 4 : 2;  // weight-column k-steps per load batch
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int B = a.B;
   bf16* dz = reinterpret_cast<bf16*>(smem);
@@ -302,12 +473,12 @@ head_bwd_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss,
   const float gs = *dloss;
   const uint64_t seed = *reinterpret_cast<const unsigned long long*>(ws);
   const float* dzl = reinterpret_cast<const float*>(ws + a.dzl_off);
-
+  HSTAMP(16);
   {  // gradient of the logits
     const HLayer& L = a.L[a.nl - 1];
     const int C = L.out, Cp = rup32(C), S = L.S_z;
     bf16* wdz = reinterpret_cast<bf16*>(ws + L.dz_off);
-    for (int idx = tid; idx < Mp * Cp; idx += HNT) {
+    for (int idx = tid; idx < Mp * Cp; idx += NT) {
       const int m = idx / Cp, c = idx - m * Cp;
       const float v = (m < B && c < C) ? gs * dzl[m * 16 + c] : 0.f;
       dz[m * S + c] = (bf16)v;
@@ -319,168 +490,233 @@ head_bwd_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss,
       L.gb[tid] += gs * s;
     }
   }
-
-  for (int l = a.nl - 1; l >= 0; --l) {
+  for (int l = a.nl - 1; l >= 1; --l) {
     const HLayer& L = a.L[l];
+    const HLayer& P = a.L[l - 1];
     const int K = L.in, N = L.out, Kp = rup32(K), Np = L.Np, Sa = L.S_a, Sz = L.S_z;
-    {  // this layer's input activations (post-dropout, bf16) into LDS
-      const bf16x8* src = reinterpret_cast<const bf16x8*>(ws + L.a_off);
-      bf16x8* dst = reinterpret_cast<bf16x8*>(abuf);
-      for (int i = tid; i < Mp * Sa / 8; i += HNT) dst[i] = src[i];
-    }
+    ws_to_lds<NT>(abuf, ws + L.a_off, Mp * Sa, tid);  // relu mask of the layer below
     __syncthreads();
-
-    // (i) dW[n][k] += sum_m dz[m][n] a[m][k]
-    {
-      const int tn = (N + 15) / 16, tk = (K + 15) / 16, T = tn * tk;
-      for (int t0 = wid * G; t0 < T; t0 += HNW * G) {
-        f32x4 acc[G];
+    const float inv = L.drop > 0.f ? 1.f / (1.f - L.drop) : 1.f;
+    const float* xhat_ws = reinterpret_cast<const float*>(ws + P.xhat_off);
+    const float* rstd_ws = reinterpret_cast<const float*>(ws + P.rstd_off);
+    bf16* wdz = reinterpret_cast<bf16*>(ws + P.dz_off);
+    for (int t = wid; t < Kp / 16; t += NW) {
+      const int kk = 16 * t + (lane & 15);
+      f32x4 acc[MT];
 #pragma unroll
-        for (int gi = 0; gi < G; ++gi) {
-          acc[gi] = f32x4{0.f, 0.f, 0.f, 0.f};
-          const int t = t0 + gi;
-          if (t < T) {
-            const int n0 = 16 * (t / tk), k0 = 16 * (t % tk);
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nb = 0; nb < Np; nb += CB * 32) {  // CB k-steps of column loads in flight
+        bf16x8 bq[CB];
 #pragma unroll
-            for (int ms = 0; ms < Mp; ms += 32)
-              acc[gi] = mfma16(tr_frag(dz, Sz, n0, ms, lane), tr_frag(abuf, Sa, k0, ms, lane), acc[gi]);
-          }
-        }
-        float old[G][4];
+        for (int u = 0; u < CB; ++u) bq[u] = wfrag_cols(L.W, N, K, nb + 32 * u + 8 * (lane >> 4), kk);
 #pragma unroll
-        for (int gi = 0; gi < G; ++gi) {
-          const int t = t0 + gi;
-          const int n0 = 16 * (t / tk), k = 16 * (t % tk) + (lane & 15);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = n0 + 4 * (lane >> 4) + r;
-            old[gi][r] = (t < T && n < N && k < K) ? L.gW[(long)n * K + k] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int gi = 0; gi < G; ++gi) {
-          const int t = t0 + gi;
-          const int n0 = 16 * (t / tk), k = 16 * (t % tk) + (lane & 15);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = n0 + 4 * (lane >> 4) + r;
-            if (t < T && n < N && k < K) L.gW[(long)n * K + k] = old[gi][r] + acc[gi][r];
-          }
-        }
-      }
-    }
-
-    // (ii) dA = dz W, then (dropout, ReLU, BatchNorm, bias) backward of the layer below
-    if (l > 0 || dx) {
-      const HLayer& P = a.L[l > 0 ? l - 1 : 0];
-      const float inv = L.drop > 0.f ? 1.f / (1.f - L.drop) : 1.f;
-      const float* xhat_ws = reinterpret_cast<const float*>(ws + P.xhat_off);
-      const float* rstd_ws = reinterpret_cast<const float*>(ws + P.rstd_off);
-      bf16* wdz = reinterpret_cast<bf16*>(ws + P.dz_off);
-      for (int t = wid; t < Kp / 16; t += HNW) {
-        const int kk = 16 * t + (lane & 15);
-        f32x4 acc[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-        for (int ns = 0; ns < Np; ns += 32) {
-          const bf16x8 bfr = wfrag_cols(L.W, N, K, ns + 8 * (lane >> 4), kk);
+        for (int u = 0; u < CB; ++u) {
+          const int ns = nb + 32 * u;
+          if (ns >= Np) break;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const bf16x8 af = *reinterpret_cast<const bf16x8*>(dz + (16 * mt + (lane & 15)) * Sz + ns + 8 * (lane >> 4));
-            acc[mt] = mfma16(af, bfr, acc[mt]);
+            acc[mt] = mfma16(af, bq[u], acc[mt]);
           }
         }
-        const bool kv = kk < K;
-        float d[MT][4];
+      }
+      const bool kv = kk < K;
+      float d[MT][4];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * mt + 4 * (lane >> 4) + r;
+          float v = (row < B && kv) ? acc[mt][r] : 0.f;
+          if (L.drop > 0.f && v != 0.f) v = hkeep(seed, l, row, kk, K, L.drop) ? v * inv : 0.f;
+          if (P.relu && !((float)abuf[row * Sa + kk] > 0.f)) v = 0.f;
+          d[mt][r] = v;
+        }
+      if (P.bn) {
+        float xh[MT][4];
+        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * mt + 4 * (lane >> 4) + r;
-            float v = (row < B && kv) ? acc[mt][r] : 0.f;
-            if (a.train && L.drop > 0.f && v != 0.f) v = hkeep(seed, l, row, kk, K, L.drop) ? v * inv : 0.f;
-            d[mt][r] = v;
+            xh[mt][r] = xhat_ws[row * P.Np + kk];
+            s1 += d[mt][r];
+            s2 += d[mt][r] * xh[mt][r];
           }
-        if (l == 0) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = 16 * mt + 4 * (lane >> 4) + r;
-              if (row < B && kv) dx[(long)row * lddx + kk] = d[mt][r];
-            }
-          continue;
+        s1 = colsum4(s1);
+        s2 = colsum4(s2);
+        if (lane < 16 && kv) {
+          P.ggamma[kk] += s2;
+          P.gbeta[kk] += s1;
         }
-        if (P.relu) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = 16 * mt + 4 * (lane >> 4) + r;
-              if (!((float)abuf[row * Sa + kk] > 0.f)) d[mt][r] = 0.f;
-            }
-        }
-        if (P.bn) {
-          float xh[MT][4];
-          float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = 16 * mt + 4 * (lane >> 4) + r;
-              xh[mt][r] = xhat_ws[row * P.Np + kk];
-              s1 += d[mt][r];
-              s2 += d[mt][r] * xh[mt][r];
-            }
-          s1 = colsum4(s1);
-          s2 = colsum4(s2);
-          if (lane < 16 && kv) {
-            P.ggamma[kk] += s2;
-            P.gbeta[kk] += s1;
-          }
-          const float ga = kv ? P.gamma[kk] : 0.f, rs = rstd_ws[kk];
-          const float m1 = s1 / (float)B, m2 = s2 / (float)B;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = 16 * mt + 4 * (lane >> 4) + r;
-              d[mt][r] = (row < B && kv) ? ga * rs * (d[mt][r] - m1 - xh[mt][r] * m2) : 0.f;
-            }
-        }
-        if (P.gb) {
-          float sb = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sb += d[mt][r];
-          sb = colsum4(sb);
-          if (lane < 16 && kv) P.gb[kk] += sb;
-        }
+        const float ga = kv ? P.gamma[kk] : 0.f, rs = rstd_ws[kk];
+        const float m1 = s1 / (float)B, m2 = s2 / (float)B;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * mt + 4 * (lane >> 4) + r;
-            const bf16 bv = (bf16)d[mt][r];
-            dzn[row * P.S_z + kk] = bv;
-            wdz[row * P.S_z + kk] = bv;
+            d[mt][r] = (row < B && kv) ? ga * rs * (d[mt][r] - m1 - xh[mt][r] * m2) : 0.f;
           }
       }
+      if (P.gb) {
+        float sb = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sb += d[mt][r];
+        sb = colsum4(sb);
+        if (lane < 16 && kv) P.gb[kk] += sb;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * mt + 4 * (lane >> 4) + r;
+          const bf16 bv = (bf16)d[mt][r];
+          dzn[row * P.S_z + kk] = bv;
+          wdz[row * P.S_z + kk] = bv;
+        }
     }
     __syncthreads();
+    HSTAMP(17 + (a.nl - 1 - l));
     bf16* t = dz;
     dz = dzn;
     dzn = t;
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// bwd0: blocks [0, dw_jobs[nl]) -> 16-row slices of every layer's dW (read-modify-write into the
+// fp32 gradient); blocks after that -> 16-column slices of dX = dZ_0 W_0 (+ layer-0 dropout).
+template <int MT>
+__global__ void __launch_bounds__(HW_NT)
+head_bwd0_kernel(HArgs a, const char* __restrict__ ws, float* __restrict__ dx, long lddx,
+                 unsigned long long* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int Mp = 16 * MT, NT = HW_NT, NW = NT / 64;
+  constexpr int G = 6;  // dW tiles per wave batch (global read-modify-write in flight together)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int B = a.B;
+  const int job = blockIdx.x;
+  if (job == 0) HSTAMP(24);
+  if (job < a.dw_jobs[a.nl]) {
+    int l = 0;
+    while (job >= a.dw_jobs[l + 1]) ++l;
+    const HLayer& L = a.L[l];
+    const int K = L.in, N = L.out, Sa = L.S_a, Sz = L.S_z;
+    const int n0 = 16 * (job - a.dw_jobs[l]);
+    constexpr int SD = 24;  // LDS row stride of the 16-column dZ slice
+    bf16* abuf = reinterpret_cast<bf16*>(smem);
+    bf16* dzs = abuf + a.buf_aall;
+    {
+      const bf16* src = reinterpret_cast<const bf16*>(ws + L.dz_off);
+      for (int i = tid; i < Mp * 2; i += NT) {  // two 16-B vectors per row
+        const int m = i >> 1, h = i & 1;
+        *reinterpret_cast<bf16x8*>(dzs + m * SD + 8 * h) =
+            *reinterpret_cast<const bf16x8*>(src + m * Sz + n0 + 8 * h);
+      }
+    }
+    ws_to_lds<NT>(abuf, ws + L.a_off, Mp * Sa, tid);
+    __syncthreads();
+    const int tk = (K + 15) / 16;
+    for (int t0 = wid * G; t0 < tk; t0 += NW * G) {
+      float old[G][4];
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {  // gradient reads first
+        const int k = 16 * (t0 + gi) + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + 4 * (lane >> 4) + r;
+          const bool ok = t0 + gi < tk && n < N && k < K;
+          const float v = L.gW[ok ? (long)n * K + k : 0];
+          old[gi][r] = ok ? v : 0.f;
+        }
+      }
+      f32x4 acc[G];
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        acc[gi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (t0 + gi < tk) {
+#pragma unroll
+          for (int ms = 0; ms < Mp; ms += 32)
+            acc[gi] = mfma16(tr_frag(dzs, SD, 0, ms, lane), tr_frag(abuf, Sa, 16 * (t0 + gi), ms, lane), acc[gi]);
+        }
+      }
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        const int k = 16 * (t0 + gi) + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + 4 * (lane >> 4) + r;
+          if (t0 + gi < tk && n < N && k < K) L.gW[(long)n * K + k] = old[gi][r] + acc[gi][r];
+        }
+      }
+    }
+    return;
+  }
+  // dX slice: dx[:, kk] = sum_n dZ_0[:, n] W_0[n, kk]; the four waves split n
+  const HLayer& L = a.L[0];
+  const int K = L.in, N = L.out, Np = L.Np, Sz = L.S_z;
+  const int kk = 16 * (job - a.dw_jobs[a.nl]) + (lane & 15);
+  const bf16* dz0 = reinterpret_cast<const bf16*>(ws + L.dz_off);
+  float* red = reinterpret_cast<float*>(smem);
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nks = Np / 32;
+  for (int kb = wid; kb < nks; kb += 4 * NW) {
+    bf16x8 bq[4];
+    bf16x8 aq[4][MT];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ks = kb + u * NW < nks ? kb + u * NW : 0;
+      bq[u] = wfrag_cols(L.W, N, K, 32 * ks + 8 * (lane >> 4), kk);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        aq[u][mt] = *reinterpret_cast<const bf16x8*>(dz0 + (16 * mt + (lane & 15)) * Sz + 32 * ks + 8 * (lane >> 4));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (kb + u * NW >= nks) break;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(aq[u][mt], bq[u], acc[mt]);
+    }
+  }
+  if (wid > 0) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((wid - 1) * MT * 4 + mt * 4 + r) * 64 + lane] = acc[mt][r];
+  }
+  __syncthreads();
+  if (wid != 0) return;
+#pragma unroll
+  for (int w = 0; w < NW - 1; ++w)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mt][r] += red[(w * MT * 4 + mt * 4 + r) * 64 + lane];
+  const uint64_t seed = *reinterpret_cast<const unsigned long long*>(ws);
+  const float inv = L.drop > 0.f ? 1.f / (1.f - L.drop) : 1.f;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * mt + 4 * (lane >> 4) + r;
+      float v = acc[mt][r];
+      if (L.drop > 0.f && v != 0.f) v = hkeep(seed, 0, row, kk, K, L.drop) ? v * inv : 0.f;
+      if (row < B && kk < K) dx[(long)row * lddx + kk] = v;
+    }
+}
+
 struct Plan {
   HArgs a;
   long ws_bytes;
   int Mp;
-  long lds_fwd, lds_bwd;
+  int grid_fwd0, grid_bwd0_dw, grid_bwd0_dx;
+  long lds_fwd0, lds_fwd1, lds_bwd1, lds_bwd0;
 };
 
 static long al256(long v) { return (v + 255) & ~255L; }
@@ -497,7 +733,8 @@ static bool make_plan(int nl, const int* dims, const int* flags, const float* dr
   a.nl = nl;
   a.B = B;
   long off = 256;  // header: dropout seed
-  int buf_a = 0, buf_z = 0;
+  int buf_a1 = 8, buf_z = 8, buf_aall = 8;
+  a.dw_jobs[0] = 0;
   for (int l = 0; l < nl; ++l) {
     HLayer& L = a.L[l];
     L.in = dims[l];
@@ -538,18 +775,30 @@ static bool make_plan(int nl, const int* dims, const int* flags, const float* dr
     if (L.bn) off = al256(off + 4L * L.Np);
     L.dz_off = off;
     off = al256(off + 2L * Mp * L.S_z);
-    buf_a = buf_a > Mp * L.S_a ? buf_a : Mp * L.S_a;
+    if (l >= 1) buf_a1 = buf_a1 > Mp * L.S_a ? buf_a1 : Mp * L.S_a;
+    buf_aall = buf_aall > Mp * L.S_a ? buf_aall : Mp * L.S_a;
     buf_z = buf_z > Mp * L.S_z ? buf_z : Mp * L.S_z;
-    if (l + 1 < nl && L.Np != rup32(dims[l + 1])) return false;
+    a.dw_jobs[l + 1] = a.dw_jobs[l] + (L.out + 15) / 16;
   }
   a.dzl_off = off;
   off = al256(off + 4L * Mp * 16);
-  a.buf_a = (buf_a + 7) & ~7;
+  a.logit_off = off;
+  off = al256(off + 4L * Mp * 16);
+  a.buf_a1 = (buf_a1 + 7) & ~7;
   a.buf_z = (buf_z + 7) & ~7;
+  a.buf_aall = (buf_aall + 7) & ~7;
   p.ws_bytes = off;
-  p.lds_fwd = 2L * 2 * a.buf_a + 4L * Mp * 16;
-  p.lds_bwd = 2L * (2 * a.buf_z + a.buf_a);
-  return p.lds_fwd <= 160 * 1024 && p.lds_bwd <= 160 * 1024;
+  p.grid_fwd0 = nl == 1 ? 1 : a.L[0].Np / 16;
+  p.grid_bwd0_dw = a.dw_jobs[nl];
+  p.grid_bwd0_dx = (a.L[0].in + 15) / 16;
+  const long red = 4L * (HW_NT / 64) * (Mp / 16) * 4 * 64;
+  p.lds_fwd0 = ((2L * Mp * a.L[0].S_a + 15) & ~15L) + red;
+  p.lds_fwd1 = 2L * 2 * a.buf_a1 + 4L * Mp * 16;
+  p.lds_bwd1 = 2L * (2 * a.buf_z + a.buf_a1);
+  const long dwl = 2L * (a.buf_aall + Mp * 24);
+  p.lds_bwd0 = dwl > red ? dwl : red;
+  const long lim = 160 * 1024;
+  return p.lds_fwd0 <= lim && p.lds_fwd1 <= lim && p.lds_bwd1 <= lim && p.lds_bwd0 <= lim;
 }
 
 template <typename K>
@@ -559,16 +808,37 @@ static void allow_lds(K kern) {
 }
 
 static bool g_head_init = false;
+static unsigned long long* g_head_stamps = nullptr;
 static void head_init() {
   if (g_head_init) return;
-  allow_lds(head_fwd_kernel<2>);
-  allow_lds(head_fwd_kernel<4>);
-  allow_lds(head_bwd_kernel<2>);
-  allow_lds(head_bwd_kernel<4>);
+  allow_lds(head_fwd0_kernel<2>);
+  allow_lds(head_fwd0_kernel<4>);
+  allow_lds(head_fwd1_kernel<2>);
+  allow_lds(head_fwd1_kernel<4>);
+  allow_lds(head_bwd1_kernel<2>);
+  allow_lds(head_bwd1_kernel<4>);
+  allow_lds(head_bwd0_kernel<2>);
+  allow_lds(head_bwd0_kernel<4>);
   g_head_init = true;
 }
 
+template <int MT>
+static void launch_fwd(const Plan& p, const float* x, long ldx, const long long* y, float* out,
+                       float* loss, long long* pred, unsigned long long* rng, void* ws,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(head_fwd0_kernel<MT>, dim3(p.grid_fwd0), dim3(HW_NT), p.lds_fwd0, st, p.a,
+                     x, ldx, rng, (char*)ws, g_head_stamps);
+  hipLaunchKernelGGL(head_fwd1_kernel<MT>, dim3(1), dim3(HS_NT), p.lds_fwd1, st, p.a, y, out,
+                     loss, pred, rng, (char*)ws, g_head_stamps);
+}
+
 }  // namespace
+
+// Install (or clear with null) a device buffer of >= 64 u64 phase timestamps for the next launches.
+DN_API int dn_head_set_stamps(void* p) {
+  g_head_stamps = (unsigned long long*)p;
+  return DN_OK;
+}
 
 // Workspace layout of the fused head for batch B: out[0] = workspace bytes, then per layer
 // {input image byte offset, its row stride, output-gradient image byte offset, its row stride}
@@ -600,15 +870,14 @@ DN_API int dn_head_fwd(int nl, const int* dims, const int* flags, const float* d
   p.a.train = train;
   p.a.log_out = log_out;
   if (p.Mp == 32)
-    hipLaunchKernelGGL(head_fwd_kernel<2>, dim3(1), dim3(HCfg<2>::NT), p.lds_fwd, st, p.a, x, ldx, y, out,
-                       loss, pred, rng, (char*)ws);
+    launch_fwd<2>(p, x, ldx, y, out, loss, pred, rng, ws, st);
   else
-    hipLaunchKernelGGL(head_fwd_kernel<4>, dim3(1), dim3(HCfg<4>::NT), p.lds_fwd, st, p.a, x, ldx, y, out,
-                       loss, pred, rng, (char*)ws);
+    launch_fwd<4>(p, x, ldx, y, out, loss, pred, rng, ws, st);
   return dn_launch_status();
 }
 
-// Backward of a training-mode dn_head_fwd on the same workspace; dloss: device scalar d out/d loss.
+// Backward of a training-mode dn_head_fwd on the same workspace; dloss: device scalar d out/d loss;
+// dx (may be null): d loss / d x, row stride lddx.
 DN_API int dn_head_bwd(int nl, const int* dims, const int* flags, const float* drops,
                        const float* bnp, void* const* ptrs, int B, void* ws, const float* dloss,
                        float* dx, long lddx, hipStream_t st) {
@@ -621,11 +890,17 @@ DN_API int dn_head_bwd(int nl, const int* dims, const int* flags, const float* d
   head_init();
   p.a.train = 1;
   p.a.log_out = 0;
-  if (p.Mp == 32)
-    hipLaunchKernelGGL(head_bwd_kernel<2>, dim3(1), dim3(HCfg<2>::NT), p.lds_bwd, st, p.a, (char*)ws,
-                       dloss, dx, lddx);
-  else
-    hipLaunchKernelGGL(head_bwd_kernel<4>, dim3(1), dim3(HCfg<4>::NT), p.lds_bwd, st, p.a, (char*)ws,
-                       dloss, dx, lddx);
+  const int grid0 = p.grid_bwd0_dw + (dx ? p.grid_bwd0_dx : 0);
+  if (p.Mp == 32) {
+    hipLaunchKernelGGL(head_bwd1_kernel<2>, dim3(1), dim3(HS_NT), p.lds_bwd1, st, p.a, (char*)ws,
+                       dloss, g_head_stamps);
+    hipLaunchKernelGGL(head_bwd0_kernel<2>, dim3(grid0), dim3(HW_NT), p.lds_bwd0, st, p.a,
+                       (const char*)ws, dx, lddx, g_head_stamps);
+  } else {
+    hipLaunchKernelGGL(head_bwd1_kernel<4>, dim3(1), dim3(HS_NT), p.lds_bwd1, st, p.a, (char*)ws,
+                       dloss, g_head_stamps);
+    hipLaunchKernelGGL(head_bwd0_kernel<4>, dim3(grid0), dim3(HW_NT), p.lds_bwd0, st, p.a,
+                       (const char*)ws, dx, lddx, g_head_stamps);
+  }
   return dn_launch_status();
 }

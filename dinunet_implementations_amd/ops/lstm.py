@@ -11,11 +11,15 @@ forward
 backward
   4. gate pre-activations for every step at once, in place on the projection buffer:
      ``pre = xp + h_{t-1} W_hh^T + b`` (one GEMM per direction, full chip, time-parallel).
+     When a backward will follow, these GEMMs are issued at the end of the FORWARD on a side
+     stream, so they run beside the (latency-bound, few-CU) classifier head.
   5. ``dn_lstm_bwd``: reverse-time recurrence -> gate grads ``dpre`` (bf16, original time order).
   6. parameter grads ACCUMULATED straight into ``.grad`` (flat buffer) by GEMM epilogues with a
      row map back to the reference ``[i|f|o|g]`` layout: ``dW_ih += dpre^T x``,
      ``dW_hh += dpre^T h_{t-1}``; bias grads from a deterministic column sum of ``dpre``.
-  7. ``dx = dpre W_ih`` only when the input needs a gradient.
+  7. ``dx = dpre W_ih`` only when the input needs a gradient.  The weight-gradient GEMMs of (6)
+     run on the side stream beside (7) and the encoder backward that follows; the side stream
+     is joined (and the engines notified) when the autograd pass ends.
 
 Reference math: ``comps/icalstm/models.py:5-66`` (oracle: ``ops.reference.bilstm``).
 """
@@ -27,6 +31,7 @@ import torch
 
 from . import _grad
 from . import _lib
+from . import _streams
 from . import capture as _cap
 from .gemm import mm
 
@@ -114,6 +119,14 @@ class _BiLSTMFn(torch.autograd.Function):
             out = hmean
         else:
             out = hseq.view(Bp, S, ndir, HD)[:B, :, :, :Hd].reshape(B, S, ndir * Hd)
+        ctx.pre_ev = None
+        if any(ctx.needs_input_grad) and _cap.active() is None:
+            side = _streams.fork(dev)
+            with torch.cuda.stream(side):
+                _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir)
+                ctx.pre_ev = torch.cuda.Event()
+                ctx.pre_ev.record(side)
+            _streams.keep_alive(side, (xp, hprev, whh_p, bias_p))
         ctx.save_for_backward(x2d, wih_p, whh_p, whhT_p, bias_p, xp, c_save, hprev)
         ctx.params = params
         ctx.meta = (B, S, I, Hd, HD, ndir, mode, enc.dtype)
@@ -131,9 +144,11 @@ class _BiLSTMFn(torch.autograd.Function):
         dev = x2d.device
         st = _lib.stream()
         # (4) time-parallel pre-activations, in place on the projection buffer
-        for d in range(ndir):
-            mm(hprev[d].view(Bp * S, HD)[:N], whh_p[d], trans_b=True, out=xp[:, d * GP:(d + 1) * GP],
-               beta=1.0, bias=bias_p[d * GP:(d + 1) * GP])
+        if ctx.pre_ev is not None:
+            torch.cuda.current_stream(dev).wait_event(ctx.pre_ev)
+            ctx.pre_ev = None
+        else:
+            _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir)
         # (5) reverse-time recurrence
         if dout is None:
             dout = torch.zeros((B, ndir * Hd) if mode == "mean" else (B, S, ndir * Hd),
@@ -150,35 +165,70 @@ class _BiLSTMFn(torch.autograd.Function):
                   dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir,
                   dpre.data_ptr(), st)
         dpre_v = dpre[:N]
-        # (6) parameter grads accumulated into .grad (reference layout via row map)
-        rmap = _row_map(Hd, HD, dev)
-        ws = torch.empty(64 * ndir * GP, dtype=torch.float32, device=dev)
-        gb = [None] * 8
-        for d in range(ndir):
-            w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
-            gb[4 * d + 1] = _grad.grad_buffer(b_ih) if b_ih is not None else None
-            gb[4 * d + 3] = _grad.grad_buffer(b_hh) if b_hh is not None else None
-        _lib.call("dn_lstm_bias_grad", dpre_v.data_ptr(), N, Hd, ndir, ws.data_ptr(),
-                  _lib.ptr(gb[1]), _lib.ptr(gb[3]), _lib.ptr(gb[5]), _lib.ptr(gb[7]), st)
-        for d in range(ndir):
-            w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
-            dsl = dpre_v[:, d * GP:(d + 1) * GP]
-            mm(dsl, x2d, trans_a=True, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap)
-            mm(dsl, hprev[d].view(Bp * S, HD)[:N, :Hd], trans_a=True, out=_grad.grad_buffer(w_hh),
-               beta=1.0, row_map=rmap)
-        _grad.notify([p for p in params if p is not None])
+        capturing = _cap.active() is not None and ctx.modules is not None
+        # (6) parameter grads accumulated into .grad (reference layout via row map), on the side
+        # stream unless rank-dAD is capturing activations
+        overlap = not capturing
+        if overlap:
+            side = _streams.fork(dev)
+            with torch.cuda.stream(side):
+                _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
+                done = torch.cuda.Event()
+                done.record(side)
+            _streams.keep_alive(side, (dpre, x2d, hprev))
+            live = [p for p in params if p is not None]
+
+            def _join():
+                torch.cuda.current_stream(dev).wait_event(done)
+                _grad.notify(live)
+            torch.autograd.Variable._execution_engine.queue_callback(_join)
+        else:
+            _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
+            _grad.notify([p for p in params if p is not None])
         # (7) input grad
         dx = None
         if ctx.needs_input_grad[0]:
             dx = mm(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
             if enc_dtype != torch.bfloat16:
                 dx = dx.to(enc_dtype)
-        if _cap.active() is not None and ctx.modules is not None:
+        if capturing:
             dref = dpre_v.view(N, ndir, HD, 4)[:, :, :Hd, :].transpose(2, 3).reshape(N, ndir, 4 * Hd)
             for d, cell in enumerate(ctx.modules):
                 _cap.record(cell.i2h, x2d, dref[:, d])
                 _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
         return (dx, None, None) + (None,) * len(params)
+
+
+def _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir):
+    """``xp[:, d] += h_{t-1} W_hh^T + b`` for every step (in place): the gate pre-activations."""
+    GP = 4 * HD
+    N = B * S
+    Bp = hprev.shape[1]
+    for d in range(ndir):
+        mm(hprev[d].view(Bp * S, HD)[:N], whh_p[d], trans_b=True, out=xp[:, d * GP:(d + 1) * GP],
+           beta=1.0, bias=bias_p[d * GP:(d + 1) * GP])
+
+
+def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
+    """Accumulate dW_ih, dW_hh, b_ih, b_hh gradients of every direction into ``.grad``."""
+    GP = 4 * HD
+    N = B * S
+    Bp = hprev.shape[1]
+    rmap = _row_map(Hd, HD, dev)
+    ws = torch.empty(64 * ndir * GP, dtype=torch.float32, device=dev)
+    gb = [None] * 8
+    for d in range(ndir):
+        w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
+        gb[4 * d + 1] = _grad.grad_buffer(b_ih) if b_ih is not None else None
+        gb[4 * d + 3] = _grad.grad_buffer(b_hh) if b_hh is not None else None
+    _lib.call("dn_lstm_bias_grad", dpre_v.data_ptr(), N, Hd, ndir, ws.data_ptr(),
+              _lib.ptr(gb[1]), _lib.ptr(gb[3]), _lib.ptr(gb[5]), _lib.ptr(gb[7]), _lib.stream())
+    for d in range(ndir):
+        w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
+        dsl = dpre_v[:, d * GP:(d + 1) * GP]
+        mm(dsl, x2d, trans_a=True, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap)
+        mm(dsl, hprev[d].view(Bp * S, HD)[:N, :Hd], trans_a=True, out=_grad.grad_buffer(w_hh),
+           beta=1.0, row_map=rmap)
 
 
 def bilstm(x: Tensor, params: Sequence[Tuple[Tensor, Tensor, Tensor, Tensor]],
