@@ -132,24 +132,70 @@ struct Epi {
   int out_bf16;
 };
 
+constexpr int GMAX = 8;  // problems per grouped launch
+
+// One GEMM problem of a (possibly grouped) launch.
+struct GemmProb {
+  const void* A;
+  const void* B;
+  void* C;
+  float* slab;  // split-K partials [splits][M][N] (null: no split)
+  long lda, ldb, ldc;
+  int M, N, K, kchunk;
+  Epi epi;
+};
+
+// A launch: problems sharing layouts / element types / tile shape.  blockIdx.x enumerates the
+// output tiles of problem 0, then problem 1, ...; blockIdx.z is the K split.
+struct GemmGroup {
+  GemmProb p[GMAX];
+  int tile_start[GMAX + 1];
+  long elem_start[GMAX + 1];  // split-K reduce: prefix of M*N
+  int n, splits;
+};
+
+__device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int row, int col, float v) {
+  v *= epi.alpha;
+  if (epi.bias) v += epi.bias[col];
+  if (epi.relu) v = fmaxf(v, 0.f);
+  const long orow = epi.row_map ? epi.row_map[row] : row;
+  if (orow < 0) return;  // dropped row (e.g. zero-padded LSTM units)
+  if (epi.out_bf16) {
+    bf16* cp = reinterpret_cast<bf16*>(C) + orow * ldc + col;
+    if (epi.beta != 0.f) v += epi.beta * (float)*cp;
+    *cp = (bf16)v;
+  } else {
+    float* cp = reinterpret_cast<float*>(C) + orow * ldc + col;
+    if (epi.beta != 0.f) v += epi.beta * *cp;
+    *cp = v;
+  }
+}
+
 template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe>
 __global__ void __launch_bounds__(256)
-gemm_kernel(const TAe* __restrict__ A, long lda, const TBe* __restrict__ B, long ldb,
-            void* __restrict__ C, long ldc, int M, int N, int K, int kchunk,
-            float* __restrict__ slab, Epi epi) {
+gemm_kernel(GemmGroup g) {
   typedef GemmTile<BM, BN, TA, TB> T;
   // one LDS array (A images then B images, double-buffered)
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (T::IA::ELEMS + T::IB::ELEMS)];
 #define As(b) (smem + (b) * T::IA::ELEMS)
 #define Bs(b) (smem + 2 * T::IA::ELEMS + (b) * T::IB::ELEMS)
 
+  int pi = 0;
+  while (pi + 1 < g.n && (int)blockIdx.x >= g.tile_start[pi + 1]) ++pi;
+  const GemmProb& P = g.p[pi];
+  const TAe* __restrict__ A = reinterpret_cast<const TAe*>(P.A);
+  const TBe* __restrict__ B = reinterpret_cast<const TBe*>(P.B);
+  const long lda = P.lda, ldb = P.ldb;
+  const int M = P.M, N = P.N, K = P.K;
+  const int tile = blockIdx.x - g.tile_start[pi];
+
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (N + BN - 1) / BN;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int row0 = tm * BM, col0 = tn * BN;
-  const int kbeg = blockIdx.z * kchunk;
-  const int kend = min(K, kbeg + kchunk);
+  const int kbeg = blockIdx.z * P.kchunk;
+  const int kend = min(K, kbeg + P.kchunk);
 
   bf16 ra[T::A_ELEMS], rb[T::B_ELEMS];
   f32x4 acc[T::FM][T::FN];
@@ -158,7 +204,7 @@ gemm_kernel(const TAe* __restrict__ A, long lda, const TBe* __restrict__ B, long
 #pragma unroll
     for (int j = 0; j < T::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (kend - kbeg + T::BK - 1) / T::BK;
+  const int nk = kend > kbeg ? (kend - kbeg + T::BK - 1) / T::BK : 0;
   if (nk > 0) {
     stage_load<BM, !TA, TAe>(A, lda, row0, kbeg, M, kend, tid, ra);
     stage_load<BN, TB, TBe>(B, ldb, col0, kbeg, N, kend, tid, rb);
@@ -196,7 +242,7 @@ gemm_kernel(const TAe* __restrict__ A, long lda, const TBe* __restrict__ B, long
 #undef As
 #undef Bs
   // epilogue
-  const bool split = slab != nullptr;
+  float* slab = P.slab;
 #pragma unroll
   for (int i = 0; i < T::FM; ++i)
 #pragma unroll
@@ -207,95 +253,86 @@ gemm_kernel(const TAe* __restrict__ A, long lda, const TBe* __restrict__ B, long
       for (int r = 0; r < 4; ++r) {
         const int row = row0 + wm * T::WM + 16 * i + 4 * (lane >> 4) + r;
         if (row >= M) continue;
-        float v = acc[i][j][r];
-        if (split) {
-          slab[((long)blockIdx.z * M + row) * N + col] = v;
-          continue;
-        }
-        v *= epi.alpha;
-        if (epi.bias) v += epi.bias[col];
-        if (epi.relu) v = fmaxf(v, 0.f);
-        const long orow = epi.row_map ? epi.row_map[row] : row;
-        if (orow < 0) continue;  // dropped row (e.g. zero-padded LSTM units)
-        if (epi.out_bf16) {
-          bf16* cp = reinterpret_cast<bf16*>(C) + orow * ldc + col;
-          if (epi.beta != 0.f) v += epi.beta * (float)*cp;
-          *cp = (bf16)v;
-        } else {
-          float* cp = reinterpret_cast<float*>(C) + orow * ldc + col;
-          if (epi.beta != 0.f) v += epi.beta * *cp;
-          *cp = v;
-        }
+        if (slab) slab[((long)blockIdx.z * M + row) * N + col] = acc[i][j][r];
+        else epi_store(P.epi, P.C, P.ldc, row, col, acc[i][j][r]);
       }
     }
 }
 
-// deterministic split-K combine + epilogue
-__global__ void gemm_splitk_reduce(const float* __restrict__ slab, int splits, int M, int N,
-                                   void* __restrict__ C, long ldc, Epi epi) {
-  const long total = (long)M * N;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += slab[(long)s * total + idx];
-    const int row = (int)(idx / N), col = (int)(idx % N);
-    v *= epi.alpha;
-    if (epi.bias) v += epi.bias[col];
-    if (epi.relu) v = fmaxf(v, 0.f);
-    const long orow = epi.row_map ? epi.row_map[row] : row;
-    if (orow < 0) continue;
-    if (epi.out_bf16) {
-      bf16* cp = reinterpret_cast<bf16*>(C) + orow * ldc + col;
-      if (epi.beta != 0.f) v += epi.beta * (float)*cp;
-      *cp = (bf16)v;
-    } else {
-      float* cp = reinterpret_cast<float*>(C) + orow * ldc + col;
-      if (epi.beta != 0.f) v += epi.beta * *cp;
-      *cp = v;
+// deterministic split-K combine + epilogue over every problem of a group; each thread handles
+// 4 consecutive columns of one row
+__global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
+  const long total = g.elem_start[g.n];
+  for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; 4 * i4 < total;
+       i4 += (long)gridDim.x * blockDim.x) {
+    const long idx0 = 4 * i4;
+    int pi = 0;
+    while (pi + 1 < g.n && idx0 >= g.elem_start[pi + 1]) ++pi;
+    const GemmProb& P = g.p[pi];
+    const long base = g.elem_start[pi];
+    const long mn = (long)P.M * P.N;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long idx = idx0 + e - base;
+      if (idx >= mn) break;  // (problems are padded to multiples of 4 elements in elem_start)
+      float v = 0.f;
+      for (int s = 0; s < g.splits; ++s) v += P.slab[(long)s * mn + idx];
+      const int row = (int)(idx / P.N), col = (int)(idx - (long)row * P.N);
+      epi_store(P.epi, P.C, P.ldc, row, col, v);
     }
   }
 }
 
-template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe>
-int launch(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
-           int K, int splits, float* slab, Epi epi, hipStream_t st) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+static int kchunk_for(int K, int& splits) {
   int kchunk = K;
   if (splits > 1) {
     kchunk = (K + splits - 1) / splits;
     kchunk = (kchunk + 63) / 64 * 64;
-    splits = (K + kchunk - 1) / kchunk;
   }
-  dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe>), grid, dim3(256), 0, st,
-                     (const TAe*)A, lda, (const TBe*)B, ldb, C, ldc, M, N, K, kchunk,
-                     splits > 1 ? slab : nullptr, epi);
-  if (splits > 1) {
-    const long total = (long)M * N;
-    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, C,
-                       ldc, epi);
+  return kchunk;
+}
+
+template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe>
+int launch(GemmGroup& g, hipStream_t st) {
+  int tiles = 0;
+  long elems = 0;
+  for (int i = 0; i < g.n; ++i) {
+    g.tile_start[i] = tiles;
+    g.elem_start[i] = elems;
+    tiles += ((g.p[i].M + BM - 1) / BM) * ((g.p[i].N + BN - 1) / BN);
+    elems += ((long)g.p[i].M * g.p[i].N + 3) / 4 * 4;
+  }
+  g.tile_start[g.n] = tiles;
+  g.elem_start[g.n] = elems;
+  dim3 grid(tiles, 1, g.splits);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe>), grid, dim3(256), 0, st, g);
+  if (g.splits > 1) {
+    const long t4 = elems / 4;
+    const int blocks = (int)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g);
   }
   return dn_launch_status();
 }
 
 template <int BM, int BN, typename TAe, typename TBe>
-int dispatch_t(int ta, int tb, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-               int M, int N, int K, int splits, float* slab, Epi epi, hipStream_t st) {
-  if (!ta && !tb) return launch<BM, BN, false, false, TAe, TBe>(A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
-  if (!ta && tb) return launch<BM, BN, false, true, TAe, TBe>(A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
-  if (ta && !tb) return launch<BM, BN, true, false, TAe, TBe>(A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
-  return launch<BM, BN, true, true, TAe, TBe>(A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
+int dispatch_t(int ta, int tb, GemmGroup& g, hipStream_t st) {
+  if (!ta && !tb) return launch<BM, BN, false, false, TAe, TBe>(g, st);
+  if (!ta && tb) return launch<BM, BN, false, true, TAe, TBe>(g, st);
+  if (ta && !tb) return launch<BM, BN, true, false, TAe, TBe>(g, st);
+  return launch<BM, BN, true, true, TAe, TBe>(g, st);
 }
 
 template <int BM, int BN>
-int dispatch_tile(int a_bf16, int b_bf16, int ta, int tb, const void* A, long lda, const void* B,
-                  long ldb, void* C, long ldc, int M, int N, int K, int splits, float* slab, Epi epi,
-                  hipStream_t st) {
-  if (a_bf16 && b_bf16) return dispatch_t<BM, BN, bf16, bf16>(ta, tb, A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
-  if (a_bf16 && !b_bf16) return dispatch_t<BM, BN, bf16, float>(ta, tb, A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
-  if (!a_bf16 && b_bf16) return dispatch_t<BM, BN, float, bf16>(ta, tb, A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
-  return dispatch_t<BM, BN, float, float>(ta, tb, A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
+int dispatch_tile(int a_bf16, int b_bf16, int ta, int tb, GemmGroup& g, hipStream_t st) {
+  if (a_bf16 && b_bf16) return dispatch_t<BM, BN, bf16, bf16>(ta, tb, g, st);
+  if (a_bf16 && !b_bf16) return dispatch_t<BM, BN, bf16, float>(ta, tb, g, st);
+  if (!a_bf16 && b_bf16) return dispatch_t<BM, BN, float, bf16>(ta, tb, g, st);
+  return dispatch_t<BM, BN, float, float>(ta, tb, g, st);
+}
+
+static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int tile, hipStream_t st) {
+  if (tile == 1) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
+  return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, g, st);
 }
 
 }  // namespace
@@ -312,8 +349,46 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
                    int splits, float* slab, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
-  Epi epi{bias, row_map, alpha, beta, relu, c_bf16};
-  if (tile == 1)
-    return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
-  return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, A, lda, B, ldb, C, ldc, M, N, K, splits, slab, epi, st);
+  GemmGroup g;
+  g.n = 1;
+  g.splits = splits > 1 ? splits : 1;
+  GemmProb& P = g.p[0];
+  P.A = A; P.B = B; P.C = C;
+  P.lda = lda; P.ldb = ldb; P.ldc = ldc;
+  P.M = M; P.N = N; P.K = K;
+  P.kchunk = kchunk_for(K, g.splits);
+  if (g.splits > 1) g.splits = (K + P.kchunk - 1) / P.kchunk;
+  P.slab = g.splits > 1 ? slab : nullptr;
+  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16};
+  return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
+}
+
+// Grouped GEMM: n <= 8 independent problems with the same operand layouts / element types /
+// output type in ONE launch (+ one split-K reduce).  Per-problem arrays; `slab` holds
+// splits * sum(M_i * N_i) fp32 when splits > 1.  Every problem uses the same K split count.
+DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const void* const* B,
+                           const long* ldb, void* const* C, const long* ldc, const int* M,
+                           const int* N, const int* K, const float* alpha, const float* beta,
+                           const void* const* bias, const void* const* row_map, int relu,
+                           int a_bf16, int b_bf16, int ta, int tb, int c_bf16, int tile,
+                           int splits, float* slab, hipStream_t st) {
+  if (n < 1 || n > GMAX) return DN_BAD_SHAPE;
+  if (splits > 1 && !slab) return DN_BAD_SHAPE;
+  GemmGroup g;
+  g.n = n;
+  g.splits = splits > 1 ? splits : 1;
+  long soff = 0;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] <= 0 || N[i] <= 0 || K[i] <= 0) return DN_BAD_SHAPE;
+    GemmProb& P = g.p[i];
+    P.A = A[i]; P.B = B[i]; P.C = C[i];
+    P.lda = lda[i]; P.ldb = ldb[i]; P.ldc = ldc[i];
+    P.M = M[i]; P.N = N[i]; P.K = K[i];
+    int sp = g.splits;
+    P.kchunk = kchunk_for(K[i], sp);
+    P.slab = g.splits > 1 ? slab + soff : nullptr;
+    soff += (long)g.splits * M[i] * N[i];
+    P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16};
+  }
+  return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }

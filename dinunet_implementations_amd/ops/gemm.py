@@ -24,6 +24,9 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
                           _lib.c_int, _lib.c_void_p, _lib.c_void_p])
 
+_lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 13 + [_lib.c_int] * 8
+              + [_lib.c_void_p, _lib.c_void_p])
+
 _NCU = 256
 
 
@@ -113,3 +116,85 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
               _lib.ptr(bias), int(relu), _lib.ptr(row_map), tile, sp, _lib.ptr(slab),
               _lib.stream())
     return out
+
+
+def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
+               splits: Optional[int] = None):
+    """Several independent ``out_i (+)= alpha_i * op(a_i) @ op(b_i)`` in ONE launch.
+
+    ``problems``: sequence of dicts with keys ``a``, ``b``, ``out`` (required, fp32 or bf16 like
+    every other ``out`` of the group) and optional ``alpha``, ``beta``, ``bias``, ``row_map``.
+    All ``a`` (and all ``b``) share dtype and memory layout.  On CPU runs :func:`mm` per problem.
+    """
+    import ctypes
+    probs = list(problems)
+    if not probs:
+        return
+    if len(probs) > 8:
+        for i in range(0, len(probs), 8):
+            mm_grouped(probs[i:i + 8], trans_a, trans_b, splits)
+        return
+    if not probs[0]["a"].is_cuda:
+        for q in probs:
+            mm(q["a"], q["b"], trans_a=trans_a, trans_b=trans_b, out=q["out"],
+               alpha=q.get("alpha", 1.0), beta=q.get("beta", 0.0), bias=q.get("bias"),
+               row_map=q.get("row_map"))
+        return
+    n = len(probs)
+    arrs = {k: [] for k in ("A", "lda", "B", "ldb", "C", "ldc", "M", "N", "K", "alpha", "beta",
+                            "bias", "rmap")}
+    keep = []
+    ta = tb = None
+    a_bf = b_bf = c_bf = None
+    maxk = 0
+    t64 = 0
+    for q in probs:
+        A = q["a"].t() if trans_a else q["a"]
+        B = q["b"].t() if trans_b else q["b"]
+        M, K = A.shape
+        _, N = B.shape
+        A, ta_i, lda = _layout(A, True)
+        B, tb_i, ldb = _layout(B, False)
+        if ta is None:
+            ta, tb = ta_i, tb_i
+            a_bf, b_bf = A.dtype == torch.bfloat16, B.dtype == torch.bfloat16
+            c_bf = q["out"].dtype == torch.bfloat16
+        elif (ta_i, tb_i, A.dtype == torch.bfloat16, B.dtype == torch.bfloat16,
+              q["out"].dtype == torch.bfloat16) != (ta, tb, a_bf, b_bf, c_bf):
+            raise ValueError("mm_grouped: problems must share layouts and dtypes")
+        out = q["out"]
+        if out.stride(1) != 1:
+            raise ValueError("mm_grouped output must be row-contiguous")
+        bias = q.get("bias")
+        bias = bias.float().contiguous() if bias is not None else None
+        rmap = q.get("row_map")
+        if rmap is not None:
+            rmap = rmap.to(device=out.device, dtype=torch.int32).contiguous()
+        keep += [A, B, bias, rmap]
+        for k, v in (("A", A.data_ptr()), ("lda", lda), ("B", B.data_ptr()), ("ldb", ldb),
+                     ("C", out.data_ptr()), ("ldc", out.stride(0)), ("M", M), ("N", N), ("K", K),
+                     ("alpha", float(q.get("alpha", 1.0))), ("beta", float(q.get("beta", 0.0))),
+                     ("bias", _lib.ptr(bias)), ("rmap", _lib.ptr(rmap))):
+            arrs[k].append(v)
+        maxk = max(maxk, K)
+        t64 += ((M + 63) // 64) * ((N + 63) // 64)
+    if splits is None:
+        splits = 1
+        if maxk >= 768 and t64 < 2 * _NCU:
+            splits = max(1, min(8, round(maxk / 384), (4 * _NCU) // max(t64, 1)))
+    sp = max(1, int(splits))
+    dev = probs[0]["out"].device
+    slab = None
+    if sp > 1:
+        slab = torch.empty(sp * sum(m * nn for m, nn in zip(arrs["M"], arrs["N"])),
+                           dtype=torch.float32, device=dev)
+    P = ctypes.c_void_p
+    L = ctypes.c_long
+    I = ctypes.c_int
+    F = ctypes.c_float
+    _lib.call("dn_gemm_grouped", n, (P * n)(*arrs["A"]), (L * n)(*arrs["lda"]),
+              (P * n)(*arrs["B"]), (L * n)(*arrs["ldb"]), (P * n)(*arrs["C"]),
+              (L * n)(*arrs["ldc"]), (I * n)(*arrs["M"]), (I * n)(*arrs["N"]),
+              (I * n)(*arrs["K"]), (F * n)(*arrs["alpha"]), (F * n)(*arrs["beta"]),
+              (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), 0, int(a_bf), int(b_bf), ta, tb,
+              int(c_bf), 0, sp, _lib.ptr(slab), _lib.stream())

@@ -33,7 +33,7 @@ from . import _grad
 from . import _lib
 from . import _streams
 from . import capture as _cap
-from .gemm import mm
+from .gemm import mm, mm_grouped
 
 Tensor = torch.Tensor
 
@@ -204,9 +204,9 @@ def _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir):
     GP = 4 * HD
     N = B * S
     Bp = hprev.shape[1]
-    for d in range(ndir):
-        mm(hprev[d].view(Bp * S, HD)[:N], whh_p[d], trans_b=True, out=xp[:, d * GP:(d + 1) * GP],
-           beta=1.0, bias=bias_p[d * GP:(d + 1) * GP])
+    mm_grouped([dict(a=hprev[d].view(Bp * S, HD)[:N], b=whh_p[d], out=xp[:, d * GP:(d + 1) * GP],
+                     beta=1.0, bias=bias_p[d * GP:(d + 1) * GP]) for d in range(ndir)],
+               trans_b=True)
 
 
 def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
@@ -223,12 +223,14 @@ def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
         gb[4 * d + 3] = _grad.grad_buffer(b_hh) if b_hh is not None else None
     _lib.call("dn_lstm_bias_grad", dpre_v.data_ptr(), N, Hd, ndir, ws.data_ptr(),
               _lib.ptr(gb[1]), _lib.ptr(gb[3]), _lib.ptr(gb[5]), _lib.ptr(gb[7]), _lib.stream())
+    probs = []
     for d in range(ndir):
         w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
         dsl = dpre_v[:, d * GP:(d + 1) * GP]
-        mm(dsl, x2d, trans_a=True, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap)
-        mm(dsl, hprev[d].view(Bp * S, HD)[:N, :Hd], trans_a=True, out=_grad.grad_buffer(w_hh),
-           beta=1.0, row_map=rmap)
+        probs.append(dict(a=dsl, b=x2d, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap))
+        probs.append(dict(a=dsl, b=hprev[d].view(Bp * S, HD)[:N, :Hd],
+                          out=_grad.grad_buffer(w_hh), beta=1.0, row_map=rmap))
+    mm_grouped(probs, trans_a=True)  # every direction's dW_ih and dW_hh in one launch
 
 
 def bilstm(x: Tensor, params: Sequence[Tuple[Tensor, Tensor, Tensor, Tensor]],

@@ -191,3 +191,24 @@ def test_lstm_rows_per_workgroup_variants(br, monkeypatch):
     for p, pr in zip(ps, ps_r):
         for t, tr in zip(p, pr):
             assert rel(t.grad, tr.grad) < 5e-2
+
+
+@pytest.mark.parametrize("splits", [1, 3, None])
+def test_gemm_grouped_matches_per_problem(splits):
+    from dinunet_implementations_amd.ops.gemm import mm_grouped
+    torch.manual_seed(7)
+    shapes = [(768, 256, 3136), (768, 192, 3136), (100, 70, 500), (64, 64, 64)]
+    probs, refs = [], []
+    for i, (M, N, K) in enumerate(shapes):
+        a = torch.randn(K, M, device=DEV).to(torch.bfloat16)  # trans_a: stored [K][M]
+        b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+        out = torch.randn(M + 5, N, device=DEV)
+        rmap = torch.randperm(M + 5, device=DEV)[:M].to(torch.int32)
+        bias = torch.randn(N, device=DEV)
+        ref = out.clone()
+        ref[rmap.long()] = 0.5 * (a.float().t() @ b.float()) + bias + ref[rmap.long()]
+        probs.append(dict(a=a, b=b, out=out, alpha=0.5, beta=1.0, row_map=rmap, bias=bias))
+        refs.append(ref)
+    mm_grouped(probs, trans_a=True, splits=splits)
+    for q, ref in zip(probs, refs):
+        assert rel(q["out"], ref) < 2e-3
