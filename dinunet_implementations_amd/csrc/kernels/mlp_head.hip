@@ -132,6 +132,59 @@ __device__ __forceinline__ bf16x8 wfrag_cols(const float* __restrict__ W, int N,
   return f;
 }
 
+// Raw fp32 weight-row fragment (lane -> row n, k .. k+7) held as two f32x4 so the loads can be
+// issued long before the MFMA that consumes them.  Out-of-range lanes load a clamped (valid)
+// address and are zeroed at conversion: zeroing the registers right after the load would make
+// the compiler wait for the load first (write-after-write on a pending VGPR).
+template <bool VEC>
+__device__ __forceinline__ void wraw_rows(const float* __restrict__ W, int N, int K, int n, int k,
+                                          f32x4 (&r)[2]) {
+  if constexpr (VEC) {
+    const int idx = (n < N && k < K) ? n * K + k : 0;  // weights < 2^31 elements
+    r[0] = *reinterpret_cast<const f32x4*>(W + idx);
+    r[1] = *reinterpret_cast<const f32x4*>(W + idx + 4);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = (n < N && k + e < K) ? n * K + k + e : 0;
+      r[e >> 2][e & 3] = W[idx];
+    }
+  }
+}
+
+// bf16 operand from a raw fragment; elements with k + e >= K (or a row n >= N) become 0
+__device__ __forceinline__ bf16x8 cvt_raw(const f32x4 (&r)[2], int N, int K, int n, int k) {
+  bf16x8 f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bool ok = n < N && k + e < K;
+    f[e] = (bf16)(ok ? r[e >> 2][e & 3] : 0.f);
+  }
+  return f;
+}
+
+// Per-column epilogue parameters of one layer, loaded early (their latency hides under the GEMM).
+struct ColP {
+  float bias, gamma, beta, rmean, rvar;
+};
+
+// Raw loads (clamped index, no use): the validity select happens in the epilogue, so nothing
+// waits on these loads (or on the loads issued before them) until the GEMM is done.
+__device__ __forceinline__ ColP load_colp(const HLayer& L, int n, bool train) {
+  ColP c{0.f, 1.f, 0.f, 0.f, 1.f};
+  const int i = n < L.out ? n : 0;
+  if (L.b) c.bias = L.b[i];
+  if (L.bn) {
+    c.gamma = L.gamma[i];
+    c.beta = L.beta[i];
+    if (L.bn == 2) {
+      c.rmean = L.rmean[i];
+      c.rvar = L.rvar[i];
+    }
+  }
+  return c;
+}
+
 // Fragment with lane i <- column c0 + (i & 15) and element j <- row k0 + 8 * (i >> 4) + j of a
 // row-major LDS image (row stride S elements): two hardware-transposed 4x16 reads.
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int S, int c0, int k0, int lane) {
@@ -149,13 +202,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int S, int c0, int k0
 template <int MT>
 __device__ __forceinline__ void fwd_epilogue(const HArgs& a, int l, const f32x4 (&acc)[MT], int n,
                                              int lane, uint64_t seed, char* __restrict__ ws,
-                                             bf16* nxt, float* logit) {
+                                             bf16* nxt, float* logit, const ColP& cp) {
   const HLayer& L = a.L[l];
   const int N = L.out, B = a.B;
   const bool train = a.train != 0;
   const bool last = l == a.nl - 1;
   const bool cv = n < N;
-  const float bias = (L.b && cv) ? L.b[n] : 0.f;
+  const float bias = cv ? cp.bias : 0.f;
   float z[MT][4];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -182,14 +235,14 @@ __device__ __forceinline__ void fwd_epilogue(const HArgs& a, int l, const f32x4 
       rstd = rsqrtf(v + L.eps);
       if (train && L.bn == 2 && lane < 16 && cv) {
         const float mo = L.momentum;
-        L.rmean[n] = (1.f - mo) * L.rmean[n] + mo * mean;
-        L.rvar[n] = (1.f - mo) * L.rvar[n] + mo * v * ((float)B / (float)(B > 1 ? B - 1 : 1));
+        L.rmean[n] = (1.f - mo) * cp.rmean + mo * mean;
+        L.rvar[n] = (1.f - mo) * cp.rvar + mo * v * ((float)B / (float)(B > 1 ? B - 1 : 1));
       }
     } else {
-      mean = cv ? L.rmean[n] : 0.f;
-      rstd = cv ? rsqrtf(L.rvar[n] + L.eps) : 0.f;
+      mean = cv ? cp.rmean : 0.f;
+      rstd = cv ? rsqrtf(cp.rvar + L.eps) : 0.f;
     }
-    const float ga = cv ? L.gamma[n] : 0.f, be = cv ? L.beta[n] : 0.f;
+    const float ga = cv ? cp.gamma : 0.f, be = cv ? cp.beta : 0.f;
     float* xhat_ws = reinterpret_cast<float*>(ws + L.xhat_off);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -245,7 +298,7 @@ __device__ __forceinline__ void ws_to_lds(bf16* __restrict__ dst_, const char* _
 
 // ---------------------------------------------------------------------------------------------
 // fwd0: layer 0, one 16-column tile per workgroup; the four waves split K.
-template <int MT>
+template <int MT, bool VECW>
 __global__ void __launch_bounds__(HW_NT)
 head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
                  const unsigned long long* __restrict__ rng, char* __restrict__ ws,
@@ -262,40 +315,58 @@ head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
   const uint64_t seed = rng ? *rng : 0ull;
   if (blockIdx.x == 0) HSTAMP(0);
 
+  // weights of this wave's first four k-steps and the epilogue parameters: issued before the
+  // input image so their latency overlaps it
+  const int n = 16 * blockIdx.x + (lane & 15);
+  const int nks = Kp / 32;
+  f32x4 wr[4][2];
+  auto load_w = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ks = kb + u * NW;
+      const int k0 = 32 * (ks < nks ? ks : 0) + 8 * (lane >> 4);
+      wraw_rows<VECW>(L0.W, N, K, n, k0, wr[u]);
+    }
+  };
+  const ColP cp = load_colp(L0, n, train);
+  load_w(wid);
+
   {  // input image (layer-0 dropout applied); workgroup 0 saves it for the backward
     const float inv = L0.drop > 0.f ? 1.f / (1.f - L0.drop) : 1.f;
     const bool save = train && blockIdx.x == 0;
     bf16* wimg = reinterpret_cast<bf16*>(ws + L0.a_off);
+    constexpr int R = 16;         // chunk loads per thread in flight
     const int nch = Mp * Kp / 4;  // 4-element chunks (Kp % 32 == 0: chunks never straddle rows)
     const bool vec = (K % 4) == 0 && (ldx % 4) == 0 && (((uintptr_t)x) & 15) == 0;
-    for (int base = tid; base < nch; base += 4 * NT) {
-      f32x4 v[4];
+    for (int base = tid; base < nch; base += R * NT) {
+      f32x4 v[R];
+      if (vec) {  // (uniform) all loads of the round first
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // all loads of the round first
-        const int c = base + u * NT;
-        const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
-        const bool ok = c < nch && m < B && k < K;
-        if (vec) {
-          v[u] = *reinterpret_cast<const f32x4*>(x + (ok ? (long)m * ldx + k : 0));
-          if (!ok) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-        } else {
+        for (int u = 0; u < R; ++u) {
+          const int c = base + u * NT;
+          const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
+          const int idx = (c < nch && m < B && k < K) ? m * (int)ldx + k : 0;
+          v[u] = *reinterpret_cast<const f32x4*>(x + idx);
+        }
+      } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool oe = ok && k + e < K;
-            const float t = x[oe ? (long)m * ldx + k + e : 0];
-            v[u][e] = oe ? t : 0.f;
-          }
+        for (int u = 0; u < R; ++u) {
+          const int c = base + u * NT;
+          const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[u][e] = x[(c < nch && m < B && k + e < K) ? m * (int)ldx + k + e : 0];
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < R; ++u) {
         const int c = base + u * NT;
         if (c >= nch) break;
         const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
         bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float t = v[u][e];
+          float t = (m < B && k + e < K) ? v[u][e] : 0.f;
           if (train && L0.drop > 0.f && t != 0.f) t = hkeep(seed, 0, m, k + e, K, L0.drop) ? t * inv : 0.f;
           o[e] = (bf16)t;
         }
@@ -307,27 +378,20 @@ head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
   __syncthreads();
   if (blockIdx.x == 0) HSTAMP(1);
 
-  const int n = 16 * blockIdx.x + (lane & 15);
   f32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nks = Kp / 32;
-  const bool vecw = (K % 8) == 0;
   for (int kb = wid; kb < nks; kb += 4 * NW) {  // this wave's k-steps, four loads in flight
-    bf16x8 bq[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k0 = 32 * (kb + u * NW) + 8 * (lane >> 4);
-      bq[u] = vecw ? wfrag_rows<true>(L0.W, N, K, n, k0) : wfrag_rows<false>(L0.W, N, K, n, k0);
-    }
+    if (kb != wid) load_w(kb);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int ks = kb + u * NW;
       if (ks >= nks) break;
+      const bf16x8 bq = cvt_raw(wr[u], N, K, n, 32 * ks + 8 * (lane >> 4));
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + (16 * mt + (lane & 15)) * S + 32 * ks + 8 * (lane >> 4));
-        acc[mt] = mfma16(af, bq[u], acc[mt]);
+        acc[mt] = mfma16(af, bq, acc[mt]);
       }
     }
   }
@@ -346,14 +410,14 @@ head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][r] += red[(w * MT * 4 + mt * 4 + r) * 64 + lane];
     fwd_epilogue<MT>(a, 0, acc, n, lane, seed, ws, nullptr,
-                     reinterpret_cast<float*>(ws + a.logit_off));
+                     reinterpret_cast<float*>(ws + a.logit_off), cp);
     if (blockIdx.x == 0) HSTAMP(2);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // fwd1: layers 1.. and the loss in one workgroup.
-template <int MT>
+template <int MT, bool VECW>
 __global__ void __launch_bounds__(HS_NT)
 head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ out,
                  float* __restrict__ loss, long long* __restrict__ pred,
@@ -369,6 +433,24 @@ head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ o
   float* logit = reinterpret_cast<float*>(nxt + a.buf_a1);  // [Mp][16]
   const uint64_t seed = rng ? *rng : 0ull;
   HSTAMP(3);
+  // this wave's first layer-1 tile: weights (first 8 k-steps) and epilogue parameters are
+  // requested before the activation image is copied in, so their latency overlaps it
+  f32x4 wr[8][2];
+  ColP cp1{0.f, 0.f, 0.f, 0.f, 1.f};
+  auto load_w = [&](const HLayer& L, int n, int kb) {
+    const int Kp = rup32(L.in);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k0 = kb + 32 * u;
+      const int kk = (k0 < Kp ? k0 : 0) + 8 * (lane >> 4);
+      wraw_rows<VECW>(L.W, L.out, L.in, n, kk, wr[u]);
+    }
+  };
+  const int tiles1 = a.nl >= 2 ? (a.nl == 2 ? 1 : a.L[1].Np / 16) : 0;
+  if (wid < tiles1) {
+    load_w(a.L[1], 16 * wid + (lane & 15), 0);
+    cp1 = load_colp(a.L[1], 16 * wid + (lane & 15), train);
+  }
   if (a.nl >= 2) {
     ws_to_lds<NT>(cur, ws + a.L[1].a_off, Mp * a.L[1].S_a, tid);
   } else {
@@ -379,33 +461,31 @@ head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ o
   HSTAMP(4);
   for (int l = 1; l < a.nl; ++l) {
     const HLayer& L = a.L[l];
-    const int K = L.in, N = L.out, Kp = rup32(K), S = L.S_a;
+    const int Kp = rup32(L.in), S = L.S_a;
     const bool last = l == a.nl - 1;
     const int ntiles = last ? 1 : L.Np / 16;  // cover rup32(out): the next image's pad is zeroed
-    const bool vecw = (K % 8) == 0;
     for (int t = wid; t < ntiles; t += NW) {
       const int n = 16 * t + (lane & 15);
+      const bool first = l == 1 && t == wid;  // prefetched above
+      const ColP cp = first ? cp1 : load_colp(L, n, train);
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int kb = 0; kb < Kp; kb += 8 * 32) {  // 8 k-steps of weight loads in flight
-        bf16x8 bq[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          bq[u] = vecw ? wfrag_rows<true>(L.W, N, K, n, kb + 32 * u + 8 * (lane >> 4))
-                       : wfrag_rows<false>(L.W, N, K, n, kb + 32 * u + 8 * (lane >> 4));
+        if (!(first && kb == 0)) load_w(L, n, kb);
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int k0 = kb + 32 * u;
           if (k0 >= Kp) break;
+          const bf16x8 bq = cvt_raw(wr[u], L.out, L.in, n, k0 + 8 * (lane >> 4));
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const bf16x8 af = *reinterpret_cast<const bf16x8*>(cur + (16 * mt + (lane & 15)) * S + k0 + 8 * (lane >> 4));
-            acc[mt] = mfma16(af, bq[u], acc[mt]);
+            acc[mt] = mfma16(af, bq, acc[mt]);
           }
         }
       }
-      fwd_epilogue<MT>(a, l, acc, n, lane, seed, ws, nxt, logit);
+      fwd_epilogue<MT>(a, l, acc, n, lane, seed, ws, nxt, logit, cp);
     }
     __syncthreads();
     HSTAMP(4 + l);
@@ -478,6 +558,12 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
     const HLayer& L = a.L[a.nl - 1];
     const int C = L.out, Cp = rup32(C), S = L.S_z;
     bf16* wdz = reinterpret_cast<bf16*>(ws + L.dz_off);
+    float gbold = 0.f, colv[Mp];
+    if (L.gb && tid < C) {  // bias-gradient loads first (old value + the column of dL/dz)
+      gbold = L.gb[tid];
+#pragma unroll
+      for (int m = 0; m < Mp; ++m) colv[m] = dzl[m * 16 + tid];
+    }
     for (int idx = tid; idx < Mp * Cp; idx += NT) {
       const int m = idx / Cp, c = idx - m * Cp;
       const float v = (m < B && c < C) ? gs * dzl[m * 16 + c] : 0.f;
@@ -486,41 +572,77 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
     }
     if (L.gb && tid < C) {
       float s = 0.f;
-      for (int m = 0; m < B; ++m) s += dzl[m * 16 + tid];
-      L.gb[tid] += gs * s;
+#pragma unroll
+      for (int m = 0; m < Mp; ++m) s += m < B ? colv[m] : 0.f;
+      L.gb[tid] = gbold + gs * s;
     }
   }
   for (int l = a.nl - 1; l >= 1; --l) {
     const HLayer& L = a.L[l];
     const HLayer& P = a.L[l - 1];
     const int K = L.in, N = L.out, Kp = rup32(K), Np = L.Np, Sa = L.S_a, Sz = L.S_z;
-    ws_to_lds<NT>(abuf, ws + L.a_off, Mp * Sa, tid);  // relu mask of the layer below
-    __syncthreads();
+    const int ntl = Kp / 16;
     const float inv = L.drop > 0.f ? 1.f / (1.f - L.drop) : 1.f;
     const float* xhat_ws = reinterpret_cast<const float*>(ws + P.xhat_off);
     const float* rstd_ws = reinterpret_cast<const float*>(ws + P.rstd_off);
     bf16* wdz = reinterpret_cast<bf16*>(ws + P.dz_off);
-    for (int t = wid; t < Kp / 16; t += NW) {
+
+    // Everything a tile needs from global memory, requested in one go (clamped addresses, no
+    // use until the MFMAs / epilogue): weight columns of the first CB k-steps, the saved
+    // BatchNorm xhat / rstd, gamma and the old values of the parameter gradients it updates.
+    float wc[CB][8], xhp[MT][4];
+    float rsp = 0.f, gap = 0.f, ggo = 0.f, gbeo = 0.f, gbo = 0.f;
+    auto load_wc = [&](int nb, int kk) {
+#pragma unroll
+      for (int u = 0; u < CB; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = nb + 32 * u + 8 * (lane >> 4) + j;
+          wc[u][j] = L.W[(n < N && kk < K) ? n * K + kk : 0];
+        }
+    };
+    auto prefetch = [&](int t) {
       const int kk = 16 * t + (lane & 15);
+      const int kc = kk < K ? kk : 0;
+      load_wc(0, kk);
+      if (P.bn) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xhp[mt][r] = xhat_ws[(16 * mt + 4 * (lane >> 4) + r) * P.Np + kk];
+        rsp = rstd_ws[kk];
+        gap = P.gamma[kc];
+        ggo = P.ggamma[kc];
+        gbeo = P.gbeta[kc];
+      }
+      if (P.gb) gbo = P.gb[kc];
+    };
+    if (wid < ntl) prefetch(wid);
+    ws_to_lds<NT>(abuf, ws + L.a_off, Mp * Sa, tid);  // relu mask of the layer below
+    __syncthreads();
+    for (int t = wid; t < ntl; t += NW) {
+      if (t != wid) prefetch(t);
+      const int kk = 16 * t + (lane & 15);
+      const bool kv = kk < K;
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int nb = 0; nb < Np; nb += CB * 32) {  // CB k-steps of column loads in flight
-        bf16x8 bq[CB];
-#pragma unroll
-        for (int u = 0; u < CB; ++u) bq[u] = wfrag_cols(L.W, N, K, nb + 32 * u + 8 * (lane >> 4), kk);
+        if (nb > 0) load_wc(nb, kk);
 #pragma unroll
         for (int u = 0; u < CB; ++u) {
           const int ns = nb + 32 * u;
           if (ns >= Np) break;
+          bf16x8 bq;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bq[j] = (bf16)((ns + 8 * (lane >> 4) + j < N && kv) ? wc[u][j] : 0.f);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const bf16x8 af = *reinterpret_cast<const bf16x8*>(dz + (16 * mt + (lane & 15)) * Sz + ns + 8 * (lane >> 4));
-            acc[mt] = mfma16(af, bq[u], acc[mt]);
+            acc[mt] = mfma16(af, bq, acc[mt]);
           }
         }
       }
-      const bool kv = kk < K;
       float d[MT][4];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -533,31 +655,28 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
           d[mt][r] = v;
         }
       if (P.bn) {
-        float xh[MT][4];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int row = 16 * mt + 4 * (lane >> 4) + r;
-            xh[mt][r] = xhat_ws[row * P.Np + kk];
             s1 += d[mt][r];
-            s2 += d[mt][r] * xh[mt][r];
+            s2 += d[mt][r] * xhp[mt][r];
           }
         s1 = colsum4(s1);
         s2 = colsum4(s2);
         if (lane < 16 && kv) {
-          P.ggamma[kk] += s2;
-          P.gbeta[kk] += s1;
+          P.ggamma[kk] = ggo + s2;
+          P.gbeta[kk] = gbeo + s1;
         }
-        const float ga = kv ? P.gamma[kk] : 0.f, rs = rstd_ws[kk];
+        const float ga = kv ? gap : 0.f;
         const float m1 = s1 / (float)B, m2 = s2 / (float)B;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * mt + 4 * (lane >> 4) + r;
-            d[mt][r] = (row < B && kv) ? ga * rs * (d[mt][r] - m1 - xh[mt][r] * m2) : 0.f;
+            d[mt][r] = (row < B && kv) ? ga * rsp * (d[mt][r] - m1 - xhp[mt][r] * m2) : 0.f;
           }
       }
       if (P.gb) {
@@ -567,7 +686,7 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
 #pragma unroll
           for (int r = 0; r < 4; ++r) sb += d[mt][r];
         sb = colsum4(sb);
-        if (lane < 16 && kv) P.gb[kk] += sb;
+        if (lane < 16 && kv) P.gb[kk] = gbo + sb;
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -811,10 +930,14 @@ static bool g_head_init = false;
 static unsigned long long* g_head_stamps = nullptr;
 static void head_init() {
   if (g_head_init) return;
-  allow_lds(head_fwd0_kernel<2>);
-  allow_lds(head_fwd0_kernel<4>);
-  allow_lds(head_fwd1_kernel<2>);
-  allow_lds(head_fwd1_kernel<4>);
+  allow_lds(head_fwd0_kernel<2, true>);
+  allow_lds(head_fwd0_kernel<2, false>);
+  allow_lds(head_fwd0_kernel<4, true>);
+  allow_lds(head_fwd0_kernel<4, false>);
+  allow_lds(head_fwd1_kernel<2, true>);
+  allow_lds(head_fwd1_kernel<2, false>);
+  allow_lds(head_fwd1_kernel<4, true>);
+  allow_lds(head_fwd1_kernel<4, false>);
   allow_lds(head_bwd1_kernel<2>);
   allow_lds(head_bwd1_kernel<4>);
   allow_lds(head_bwd0_kernel<2>);
@@ -822,14 +945,28 @@ static void head_init() {
   g_head_init = true;
 }
 
+template <int MT, bool V0, bool V1>
+static void launch_fwd_t(const Plan& p, const float* x, long ldx, const long long* y, float* out,
+                         float* loss, long long* pred, unsigned long long* rng, void* ws,
+                         hipStream_t st) {
+  hipLaunchKernelGGL((head_fwd0_kernel<MT, V0>), dim3(p.grid_fwd0), dim3(HW_NT), p.lds_fwd0, st,
+                     p.a, x, ldx, rng, (char*)ws, g_head_stamps);
+  hipLaunchKernelGGL((head_fwd1_kernel<MT, V1>), dim3(1), dim3(HS_NT), p.lds_fwd1, st, p.a, y,
+                     out, loss, pred, rng, (char*)ws, g_head_stamps);
+}
+
+// weight rows may be read as 16-B vectors when every K of the launch is a multiple of 8
 template <int MT>
 static void launch_fwd(const Plan& p, const float* x, long ldx, const long long* y, float* out,
                        float* loss, long long* pred, unsigned long long* rng, void* ws,
                        hipStream_t st) {
-  hipLaunchKernelGGL(head_fwd0_kernel<MT>, dim3(p.grid_fwd0), dim3(HW_NT), p.lds_fwd0, st, p.a,
-                     x, ldx, rng, (char*)ws, g_head_stamps);
-  hipLaunchKernelGGL(head_fwd1_kernel<MT>, dim3(1), dim3(HS_NT), p.lds_fwd1, st, p.a, y, out,
-                     loss, pred, rng, (char*)ws, g_head_stamps);
+  const bool v0 = p.a.L[0].in % 8 == 0;
+  bool v1 = true;
+  for (int l = 1; l < p.a.nl; ++l) v1 = v1 && p.a.L[l].in % 8 == 0;
+  if (v0 && v1) launch_fwd_t<MT, true, true>(p, x, ldx, y, out, loss, pred, rng, ws, st);
+  else if (v1) launch_fwd_t<MT, false, true>(p, x, ldx, y, out, loss, pred, rng, ws, st);
+  else if (v0) launch_fwd_t<MT, true, false>(p, x, ldx, y, out, loss, pred, rng, ws, st);
+  else launch_fwd_t<MT, false, false>(p, x, ldx, y, out, loss, pred, rng, ws, st);
 }
 
 }  // namespace

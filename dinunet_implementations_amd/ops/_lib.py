@@ -89,11 +89,22 @@ def require_native() -> bool:
     return os.environ.get("DINUNET_REQUIRE_NATIVE", "1") != "0"
 
 
+_SYNC_CHECK = os.environ.get("DINUNET_SYNC_CHECK", "0") == "1"
+
+
 def call(name: str, *args) -> None:
+    """Call a native launcher; raise on a non-zero status.  With ``DINUNET_SYNC_CHECK=1`` every
+    launch is followed by a device synchronize so an asynchronous fault is attributed to the
+    kernel that caused it (the HIP_LAUNCH_BLOCKING debug mode of SURVEY.md §5.2)."""
     fn = getattr(lib(), name)
     rc = fn(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with status {rc}")
+    if _SYNC_CHECK and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # pragma: no cover - GPU fault path
+            raise RuntimeError(f"{name}: device error after launch: {e}") from e
 
 
 def ptr(t: Optional[torch.Tensor]) -> Optional[int]:

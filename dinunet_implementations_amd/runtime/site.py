@@ -231,6 +231,8 @@ class FederatedSite:
             best["epoch"] = epochs
         logs[f"{tag}best_val_epoch"] = best["epoch"]
         logs[f"{tag}best_val_score"] = best["score"]
+        if step is not None and step.timers.summary():
+            logs[f"{tag}phase_ms"] = step.timers.summary()  # DINUNET_PHASE_TIMERS=1
         return best
 
     def _pretrain(self, trainer: NNTrainer, data, fold_dir: str, seed: int, logs: Dict[str, Any]):

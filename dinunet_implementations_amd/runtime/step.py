@@ -14,6 +14,7 @@ from typing import Callable, Optional
 import torch
 
 from .. import ops
+from .timers import NULL, PhaseTimer, enabled_by_env
 
 
 def ica_forward_loss(model, x, y):
@@ -29,7 +30,8 @@ HEADS = {"ica": ica_forward_loss, "fs": fs_forward_loss}
 
 class TrainStep:
     def __init__(self, model, flat, opt, engine, task: str = "ica", use_graph: bool = True,
-                 eager_warmup: int = 3, forward_loss: Optional[Callable] = None):
+                 eager_warmup: int = 3, forward_loss: Optional[Callable] = None,
+                 timers: Optional[PhaseTimer] = None):
         self.model = model
         self.flat = flat
         self.opt = opt
@@ -43,6 +45,7 @@ class TrainStep:
         self.last_loss = torch.zeros(())
         self.last_out = None
         self.last_pred = None
+        self.timers = timers if timers is not None else (PhaseTimer() if enabled_by_env() else NULL)
 
     def _fwd_bwd(self, x, y):
         with self.engine.step_context():
@@ -51,10 +54,14 @@ class TrainStep:
         return out, loss, pred
 
     def _eager(self, x, y):
-        self.flat.zero_grad()
-        out, loss, pred = self._fwd_bwd(x, y)
-        scale = self.engine.reduce()
-        self.opt.step(grad_scale=scale)
+        T = self.timers
+        with T.phase("fwd_bwd"):
+            self.flat.zero_grad()
+            out, loss, pred = self._fwd_bwd(x, y)
+        with T.phase("reduce"):
+            scale = self.engine.reduce()
+        with T.phase("optim"):
+            self.opt.step(grad_scale=scale)
         self.last_out, self.last_loss, self.last_pred = out.detach(), loss.detach(), pred
         return loss
 
@@ -96,10 +103,14 @@ class TrainStep:
         if sx.data_ptr() != x.data_ptr():
             sx.copy_(x, non_blocking=True)
             sy.copy_(y, non_blocking=True)
-        self.graph.replay()
+        T = self.timers
+        with T.phase("fwd_bwd"):
+            self.graph.replay()
         if hasattr(self.engine, "sync_enabled"):
             self.engine.sync_enabled = True
-        scale = self.engine.reduce()
-        self.opt.step(grad_scale=scale)
+        with T.phase("reduce"):
+            scale = self.engine.reduce()
+        with T.phase("optim"):
+            self.opt.step(grad_scale=scale)
         self.last_out, self.last_loss, self.last_pred = out, loss, pred
         return loss
