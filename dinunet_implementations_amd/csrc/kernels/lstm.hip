@@ -59,6 +59,30 @@ __device__ __forceinline__ void load_gate4(const float* p, bool ok, float (&v)[4
   v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
 }
 
+// Cross-lane redistribution of the MFMA output without LDS: lane n of a 16-lane row receives
+// register v[n / BR] of lane n % BR of the same row.  DPP row shifts (VALU, a few cycles) instead
+// of ds_bpermute (an LDS round trip each): BR=4 -> 3 moves, BR=8 -> 1, BR=16 -> none.
+template <int SHR, int BANK>
+__device__ __forceinline__ float dpp_row_shr(float old, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+      __builtin_bit_cast(int, old), __builtin_bit_cast(int, v), 0x110 + SHR, 0xF, BANK, false));
+}
+
+template <int BR>
+__device__ __forceinline__ float row_gather(const float (&v)[16 / BR]) {
+  if constexpr (BR == 4) {
+    float o = v[0];
+    o = dpp_row_shr<4, 0x2>(o, v[1]);
+    o = dpp_row_shr<8, 0x4>(o, v[2]);
+    o = dpp_row_shr<12, 0x8>(o, v[3]);
+    return o;
+  } else if constexpr (BR == 8) {
+    return dpp_row_shr<8, 0xC>(v[0], v[1]);
+  } else {
+    return v[0];
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
@@ -133,7 +157,6 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
   const int cp_r = (tid * EPT) / HD, cp_c = (tid * EPT) % HD;
   bf16* hcp = hprev + hplane + ((long)(blockIdx.x * BR + cp_r) * S) * HD + cp_c;
   float* csv = c_save + hplane + (long)b * S * HD;
-  const int src = 16 * q + bl;  // lane holding this lane's column in the MFMA output
 
   float c[NSL], hs[NSL], hl[NSL];
   f32x4 xn[NSL];
@@ -182,13 +205,16 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
 #pragma unroll
       for (int s = 0; s < NSL; ++s) pa[s] = acc[s];
     } else {
+      // slot s of lane (q, r, bl) = m-tile r + s*G16 of column bl (held by lane (q, bl))
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        f32x4 v;
+      for (int sl = 0; sl < NSL; ++sl)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = __shfl(acc[mt][j], src, 64);
-        if (mt % G16 == r) pa[mt / G16] = v;
-      }
+        for (int j = 0; j < 4; ++j) {
+          float v[G16];
+#pragma unroll
+          for (int g = 0; g < G16; ++g) v[g] = acc[g + sl * G16][j];
+          pa[sl][j] = row_gather<BR>(v);
+        }
     }
 #ifdef DN_STAMPS
     { float z = pa[0][0]; asm volatile("" :: "v"(z)); }
@@ -278,7 +304,6 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   const bool vb = b < B;
   const int bc = vb ? b : B - 1;
   const long rowX = (long)ndir * 4 * HD;
-  const int src = 16 * q + bl;
 
   bf16x8 af[NRK];
   {
@@ -360,9 +385,11 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
       for (int s = 0; s < NSL; ++s) dhr[s] = acc[s];
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = __shfl(acc[j], src, 64);
-        if (j % G16 == r) dhr[j / G16] = v;
+      for (int sl = 0; sl < NSL; ++sl) {
+        float v[G16];
+#pragma unroll
+        for (int g = 0; g < G16; ++g) v[g] = acc[g + sl * G16];
+        dhr[sl] = row_gather<BR>(v);
       }
     }
 #ifdef DN_STAMPS

@@ -72,13 +72,19 @@ class LSTM(nn.Module):
                 and ops.lstm_supported(x.shape[0], self.input_size, self.hidden_size,
                                        self.num_direction))
 
-    def forward(self, x: torch.Tensor, h=None, reduce: str = "none"):
+    def prepack(self, device):
+        """Start packing the recurrent weights on the side stream (overlaps the encoder)."""
+        from ..ops.lstm import pack_params
+        flat = [t for cell in self.lstms for t in cell.params()]
+        return pack_params(flat, self.input_size, device, side=True)
+
+    def forward(self, x: torch.Tensor, h=None, reduce: str = "none", packed=None):
         """``reduce='none'`` returns ``(hidden_seq [B,S,H*dirs], (h, c))`` like the reference;
         ``reduce='mean'`` returns the temporal mean ``[B, H*dirs]`` instead of the sequence
         (what ``ICALstm`` consumes) so the fused kernel never materialises the sequence."""
         if h is None and self.fused_ok(x):
             params = [cell.params() for cell in self.lstms]
-            return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms))
+            return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms), packed=packed)
         if h is not None:
             hs, (h_t, c_t) = self.lstms[0](x, h)
             if self.bidirectional:
@@ -141,8 +147,11 @@ class ICALstm(nn.Module):
     def forward_loss(self, x: torch.Tensor, y: torch.Tensor):
         """``(probs, ce_loss, argmax)`` (reference ``comps/icalstm/__init__.py:59-63``); on a GPU
         the classifier, softmax and cross-entropy are one fused launch each way."""
+        packed = None
+        if self.use_fused and x.is_cuda and self.lstm.fused_ok(x) and ops.capture.active() is None:
+            packed = self.lstm.prepack(x.device)
         enc = self.encode(x)
-        o, _ = self.lstm(enc, reduce="mean")
+        o, _ = self.lstm(enc, reduce="mean", packed=packed)
         o = o.flatten(1).to(self.classifier[1].weight.dtype)
         if self.use_fused and x.is_cuda:
             return ops.head_loss(o, self.head_spec(), y, log_out=False)

@@ -10,8 +10,8 @@ from .heads import softmax_ce, log_softmax_nll
 from .head import HeadSpec, head_loss
 
 
-def bilstm(x, params, reduce: str = "none", modules=None):
-    return _bilstm_fused(x, params, reduce=reduce, modules=modules)
+def bilstm(x, params, reduce: str = "none", modules=None, packed=None):
+    return _bilstm_fused(x, params, reduce=reduce, modules=modules, packed=packed)
 
 
 __all__ = [

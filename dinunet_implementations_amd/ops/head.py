@@ -13,11 +13,12 @@ A :class:`HeadSpec` is parsed from the module sequence itself, so the fused path
 what the modules would compute (parameters, BN eps/momentum/mode, dropout placement); anything the
 kernel does not cover (batch > 64, > 16 classes, unknown modules) runs the modules + the loss op.
 
-The forward is one launch: loss, outputs, argmax, BatchNorm running-stat update and the dropout
-masks (counter-based hash; the seed is a device counter the kernel bumps, so HIP-graph replays
-draw fresh masks).  The backward is one launch that scales by ``dloss`` on the device and
-accumulates every head parameter gradient straight into its ``.grad`` (flat-buffer view) and
-returns ``d input``.  Dropout masks are not bit-identical to ``torch.nn.Dropout``'s generator
+The forward is two launches (the wide first layer over many workgroups, then the narrow tail +
+loss in one): loss, outputs, argmax, BatchNorm running-stat update and the dropout masks
+(counter-based hash; the seed is a device counter the kernel bumps, so HIP-graph replays draw
+fresh masks).  The backward is two launches (the output-gradient chain, then every dW slice and
+dX over many workgroups); it scales by ``dloss`` on the device, accumulates every head parameter
+gradient straight into its ``.grad`` (flat-buffer view) and returns ``d input``.  Dropout masks are not bit-identical to ``torch.nn.Dropout``'s generator
 stream (same distribution, independent draws); everything else matches the module math with
 bf16 MFMA operands and fp32 accumulation / statistics.
 """
@@ -192,6 +193,7 @@ class HeadSpec:
 class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y, spec: HeadSpec, log_out: bool, *params):
+        ctx.set_materialize_grads(False)  # no zero-filled grads for out / pred
         x = x.float().contiguous()
         y = y.long().contiguous()
         B = x.shape[0]

@@ -80,7 +80,7 @@ def _row_map(Hd: int, HD: int, device) -> Tensor:
 
 class _BiLSTMFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, enc: Tensor, mode: str, modules, *params: Tensor):
+    def forward(ctx, enc: Tensor, mode: str, modules, packed, *params: Tensor):
         ctx.set_materialize_grads(False)  # unused hT / cT -> None (no zero tensors, no syncs)
         B, S, I = enc.shape
         ndir = len(params) // 4
@@ -91,13 +91,11 @@ class _BiLSTMFn(torch.autograd.Function):
         Bp = (B + BR - 1) // BR * BR
         dev = enc.device
         st = _lib.stream()
-        wih_p = torch.empty(ndir * GP, I, dtype=torch.bfloat16, device=dev)
-        bias_p = torch.empty(ndir * GP, dtype=torch.float32, device=dev)
-        whh_p = torch.empty(ndir, GP, HD, dtype=torch.bfloat16, device=dev)
-        whhT_p = torch.empty(ndir, HD, GP, dtype=torch.bfloat16, device=dev)
-        ps = [p.detach().contiguous() for p in params] + [None] * (8 - len(params))
-        _lib.call("dn_lstm_pack", *[_lib.ptr(p) for p in ps], I, Hd, ndir, wih_p.data_ptr(),
-                  bias_p.data_ptr(), whh_p.data_ptr(), whhT_p.data_ptr(), st)
+        if packed is None:
+            packed = pack_params(params, I, dev)
+        wih_p, bias_p, whh_p, whhT_p, ev = packed
+        if ev is not None:  # packed on the side stream while the encoder ran
+            torch.cuda.current_stream(dev).wait_event(ev)
         x2d = enc.reshape(B * S, I)
         if x2d.dtype != torch.bfloat16:
             x2d = x2d.to(torch.bfloat16)
@@ -196,7 +194,48 @@ class _BiLSTMFn(torch.autograd.Function):
             for d, cell in enumerate(ctx.modules):
                 _cap.record(cell.i2h, x2d, dref[:, d])
                 _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
-        return (dx, None, None) + (None,) * len(params)
+        return (dx, None, None, None) + (None,) * len(params)
+
+
+def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = False):
+    """``dn_lstm_pack``: fp32 reference-layout params -> bf16 kernel layouts + fused bias.
+
+    With ``side=True`` the pack runs on the side stream (it depends only on the parameters, so
+    it overlaps the encoder GEMM) and the returned event orders the consumer after it.
+    """
+    ndir = len(params) // 4
+    Hd = params[2].shape[1]
+    HD = padded_hidden(Hd)
+    GP = 4 * HD
+    I = int(input_size)
+    stream = _streams.fork(device) if side else None
+    ctx = torch.cuda.stream(stream) if side else _nullctx()
+    with ctx:
+        wih_p = torch.empty(ndir * GP, I, dtype=torch.bfloat16, device=device)
+        bias_p = torch.empty(ndir * GP, dtype=torch.float32, device=device)
+        whh_p = torch.empty(ndir, GP, HD, dtype=torch.bfloat16, device=device)
+        whhT_p = torch.empty(ndir, HD, GP, dtype=torch.bfloat16, device=device)
+        ps = [p.detach().contiguous() for p in params] + [None] * (8 - len(params))
+        _lib.call("dn_lstm_pack", *[_lib.ptr(p) for p in ps], I, Hd, ndir, wih_p.data_ptr(),
+                  bias_p.data_ptr(), whh_p.data_ptr(), whhT_p.data_ptr(), _lib.stream())
+        ev = None
+        if side:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+    if side:
+        # the packed tensors are consumed on the main stream: keep their blocks alive there
+        main = torch.cuda.current_stream(device)
+        for t in (wih_p, bias_p, whh_p, whhT_p):
+            t.record_stream(main)
+    return wih_p, bias_p, whh_p, whhT_p, ev
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir):
@@ -234,12 +273,12 @@ def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
 
 
 def bilstm(x: Tensor, params: Sequence[Tuple[Tensor, Tensor, Tensor, Tensor]],
-           reduce: str = "none", modules=None):
+           reduce: str = "none", modules=None, packed=None):
     """Fused bi-LSTM: returns ``(hmean [B, ndir*Hd] | hseq [B, S, ndir*Hd], (hT, cT))``."""
     if not _lib.native_available():
         raise RuntimeError("fused LSTM requested but the gfx950 kernel library is not built")
     flat: List[Tensor] = []
     for p in params:
         flat.extend(p)
-    out, hT, cT = _BiLSTMFn.apply(x, "mean" if reduce == "mean" else "seq", modules, *flat)
+    out, hT, cT = _BiLSTMFn.apply(x, "mean" if reduce == "mean" else "seq", modules, packed, *flat)
     return out, (hT, cT)
