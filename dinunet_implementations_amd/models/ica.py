@@ -147,13 +147,28 @@ class ICALstm(nn.Module):
     def forward_loss(self, x: torch.Tensor, y: torch.Tensor):
         """``(probs, ce_loss, argmax)`` (reference ``comps/icalstm/__init__.py:59-63``); on a GPU
         the classifier, softmax and cross-entropy are one fused launch each way."""
-        packed = None
+        return self.body_loss(self.stem(x), y)
+
+    def stem(self, x: torch.Tensor) -> torch.Tensor:
+        """First half of :meth:`forward_loss`: the encoder (``[B,S,C,W] -> [B,S,I]``).
+
+        Its parameter gradients are the LAST ones the backward produces, so a training step can
+        stop the backward at the stem output, start the all-reduce of every other gradient, and
+        only then run the stem's backward (``runtime.step.TrainStep`` split capture)."""
+        self._packed = None
         if self.use_fused and x.is_cuda and self.lstm.fused_ok(x) and ops.capture.active() is None:
-            packed = self.lstm.prepack(x.device)
-        enc = self.encode(x)
+            self._packed = self.lstm.prepack(x.device)  # side stream, beside the encoder GEMM
+        return self.encode(x)
+
+    def stem_parameters(self):
+        return self.encoder.parameters()
+
+    def body_loss(self, enc: torch.Tensor, y: torch.Tensor):
+        """Second half of :meth:`forward_loss`: bi-LSTM, classifier, softmax-CE on ``enc``."""
+        packed, self._packed = getattr(self, "_packed", None), None
         o, _ = self.lstm(enc, reduce="mean", packed=packed)
         o = o.flatten(1).to(self.classifier[1].weight.dtype)
-        if self.use_fused and x.is_cuda:
+        if self.use_fused and o.is_cuda:
             return ops.head_loss(o, self.head_spec(), y, log_out=False)
         logits = self.classifier(o)
         return ops.softmax_ce(logits, y)

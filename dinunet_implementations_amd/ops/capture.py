@@ -8,13 +8,14 @@ hold (the encoder output / ``h_{t-1}`` sequence and the gate gradients), so no e
 """
 from __future__ import annotations
 
-import threading
 from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
 
-_state = threading.local()
+# Process-global, NOT thread-local: autograd runs the backward of CUDA tensors on its own
+# device thread, and the fused ops record from their backward.
+_STACK: List["DADCapture"] = []
 
 
 class DADCapture:
@@ -43,10 +44,7 @@ class DADCapture:
         for m in self.modules:
             self._handles.append(m.register_forward_hook(self._fwd_hook))
             self._handles.append(m.register_full_backward_hook(self._bwd_hook))
-        stack = getattr(_state, "stack", None)
-        if stack is None:
-            stack = _state.stack = []
-        stack.append(self)
+        _STACK.append(self)
         return self
 
     def __exit__(self, *exc):
@@ -54,7 +52,7 @@ class DADCapture:
             h.remove()
         self._handles.clear()
         self._inputs.clear()
-        _state.stack.pop()
+        _STACK.remove(self)
         return False
 
     def clear(self):
@@ -63,8 +61,7 @@ class DADCapture:
 
 
 def active() -> Optional[DADCapture]:
-    stack = getattr(_state, "stack", None)
-    return stack[-1] if stack else None
+    return _STACK[-1] if _STACK else None
 
 
 def record(module: nn.Module, a: torch.Tensor, delta: torch.Tensor) -> None:

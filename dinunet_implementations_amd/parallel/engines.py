@@ -135,7 +135,40 @@ class DSGDEngine(Engine):
         self._pending = list(self._expected)
         self._handles.clear()
 
+    def split_buckets(self, stem_params) -> List[int]:
+        """Re-bucket for a step whose backward is replayed in two parts (``TrainStep`` split
+        capture): every gradient outside ``stem_params`` first (ready when the first part ends),
+        then the stem's.  Returns the bucket ids of the first group; the caller launches them
+        with :meth:`launch_bucket` between the two parts, ``reduce()`` launches the rest."""
+        ids = {id(p) for p in stem_params}
+        segs = list(self.flat.segments())
+        stem = [(o, o + ((n + 3) // 4) * 4) for p, o, n in segs if id(p) in ids]
+        if not stem:
+            raise ValueError("stem parameters are not in the flat buffer")
+        s0, s1 = min(a for a, _ in stem), max(b for _, b in stem)
+        if sum(b - a for a, b in stem) != s1 - s0 or any(s0 <= o < s1 and id(p) not in ids
+                                                        for p, o, _ in segs):
+            raise ValueError("stem parameters must occupy one contiguous flat range")
+        body = [r for r in ((s1, self.flat.numel), (0, s0)) if r[1] > r[0]]
+        self.buckets = body + [(s0, s1)]
+        self._param_bucket = {}
+        for p, o, _ in segs:
+            self._param_bucket[id(p)] = next(i for i, (a, b) in enumerate(self.buckets) if a <= o < b)
+        self._expected = [0] * len(self.buckets)
+        for p, _, _ in segs:
+            self._expected[self._param_bucket[id(p)]] += 1
+        self._half_bufs.clear()
+        self._reset()
+        return list(range(len(body)))
+
+    def launch_bucket(self, b: int):
+        """Start bucket ``b``'s all-reduce now (RCCL stream ordered after the current stream)."""
+        if self.group.distributed and b not in self._handles:
+            self._launch(b)
+
     def _launch(self, b: int):
+        if not self._handles:  # first bucket of this step
+            self.comm_bytes = 0
         s, e = self.buckets[b]
         view = self.flat.grad[s:e]
         if self.half:
@@ -164,7 +197,6 @@ class DSGDEngine(Engine):
         if not g.distributed:
             self._reset()
             return 1.0
-        self.comm_bytes = 0 if not self._handles else self.comm_bytes
         for b in range(len(self.buckets)):
             if b not in self._handles:
                 self._launch(b)

@@ -6,9 +6,16 @@ aggregation (RCCL collectives) and the single fused Adam launch run after the re
 optimizer's bias-correction scalars change every step and collective capture is not needed for a
 handful of bucketed all-reduces.  Engines whose reduction needs host-side logic (rank-dAD,
 PowerSGD) or that capture activations run eagerly.
+
+Split capture (dSGD across sites): the model's ``stem`` (ICA: the encoder) produces the LAST
+gradients of the backward, so the step is captured as TWO graphs cut at the stem output —
+A = zero-grad + forward + backward of everything after the stem (its input gradient included),
+B = the stem's backward.  Between the replays the all-reduce of every non-stem gradient starts on
+RCCL's stream and runs under graph B; only the small stem bucket's all-reduce is exposed.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 import torch
@@ -27,11 +34,17 @@ def fs_forward_loss(model, x, y):
 
 HEADS = {"ica": ica_forward_loss, "fs": fs_forward_loss}
 
+# Capture in thread-local mode: RCCL's process-group watchdog thread polls the events of
+# finished collectives (hipEventQuery) at any time, and under the default global mode such a
+# query from another thread while this thread captures invalidates the capture and kills the
+# watchdog (hipErrorStreamCaptureUnsupported -> abort).
+CAPTURE_MODE = "thread_local"
+
 
 class TrainStep:
     def __init__(self, model, flat, opt, engine, task: str = "ica", use_graph: bool = True,
                  eager_warmup: int = 3, forward_loss: Optional[Callable] = None,
-                 timers: Optional[PhaseTimer] = None):
+                 timers: Optional[PhaseTimer] = None, split: Optional[bool] = None):
         self.model = model
         self.flat = flat
         self.opt = opt
@@ -46,6 +59,15 @@ class TrainStep:
         self.last_out = None
         self.last_pred = None
         self.timers = timers if timers is not None else (PhaseTimer() if enabled_by_env() else NULL)
+        # split capture: needs a stem/body model, the default loss, and sites to overlap with
+        can_split = (self.use_graph and forward_loss is None and hasattr(model, "stem")
+                     and hasattr(model, "body_loss") and hasattr(model, "stem_parameters"))
+        if split is None:
+            env = os.environ.get("DINUNET_SPLIT_GRAPH", "")
+            split = can_split and (engine.group.distributed if env == "" else env == "1")
+        self.split = bool(split and can_split)
+        self._first_buckets = engine.split_buckets(list(model.stem_parameters())) if self.split else []
+        self.graph_b = None
 
     def _fwd_bwd(self, x, y):
         with self.engine.step_context():
@@ -75,7 +97,7 @@ class TrainStep:
         if prev is not None:
             self.engine.sync_enabled = False  # no collectives inside the captured region
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 self.flat.grad.zero_()
                 out, loss, pred = self._fwd_bwd(sx, sy)
         finally:
@@ -83,6 +105,30 @@ class TrainStep:
                 self.engine.sync_enabled = prev
         self.graph = g
         self.static = (sx, sy, out, loss, pred)
+
+    def _capture_split(self, x, y):
+        sx = torch.empty_like(x)
+        sy = torch.empty_like(y)
+        sx.copy_(x)
+        sy.copy_(y)
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        self.engine.sync_enabled = False
+        try:
+            with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
+                self.flat.grad.zero_()
+                with self.engine.step_context():
+                    h = self.model.stem(sx)
+                    hd = h.detach().requires_grad_(h.requires_grad)
+                    out, loss, pred = self.model.body_loss(hd, sy)
+                    loss.backward()
+            with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):
+                if h.requires_grad:
+                    torch.autograd.backward(h, hd.grad)
+        finally:
+            self.engine.sync_enabled = True
+        self.graph, self.graph_b = ga, gb
+        self.static = (sx, sy, out, loss, pred)
+        self._keep = (h, hd)  # the graphs replay into these buffers
 
     def __call__(self, x, y):
         self.calls += 1
@@ -96,7 +142,7 @@ class TrainStep:
                     loss = self._eager(x, y)
                 torch.cuda.current_stream().wait_stream(s)
                 return loss
-            self._capture(x, y)
+            (self._capture_split if self.split else self._capture)(x, y)
         sx, sy, out, loss, pred = self.static
         if sx.shape != x.shape or sy.shape != y.shape:  # e.g. a ragged last batch
             return self._eager(x, y)
@@ -106,6 +152,10 @@ class TrainStep:
         T = self.timers
         with T.phase("fwd_bwd"):
             self.graph.replay()
+            if self.graph_b is not None:
+                for b in self._first_buckets:  # all-reduce under the stem backward
+                    self.engine.launch_bucket(b)
+                self.graph_b.replay()
         if hasattr(self.engine, "sync_enabled"):
             self.engine.sync_enabled = True
         with T.phase("reduce"):

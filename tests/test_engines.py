@@ -158,3 +158,22 @@ def test_file_transport_matches_collectives():
             eng.apply(agg)
         assert torch.allclose(sites[0][1].grad, ref, atol=1e-5), cls.__name__
         assert torch.allclose(sites[1][1].grad, ref, atol=1e-5), cls.__name__
+
+
+def test_dsgd_split_buckets_partition_flat_buffer():
+    """Split capture: non-stem gradients form the first bucket(s), the stem the last one."""
+    from dinunet_implementations_amd.models import ICALstm
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    m = ICALstm(input_size=16, hidden_size=16, num_comps=4, window_size=3)
+    flat = FlatParams(m.parameters())
+    eng = make_engine("dSGD", m, flat, SiteGroup(), {})
+    first = eng.split_buckets(list(m.stem_parameters()))
+    covered = sorted(eng.buckets)
+    assert covered[0][0] == 0 and covered[-1][1] == flat.numel
+    assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+    stem_ids = {id(p) for p in m.stem_parameters()}
+    for p, o, n in flat.segments():
+        b = eng._param_bucket[id(p)]
+        assert (b not in first) == (id(p) in stem_ids)
