@@ -155,6 +155,8 @@ class ICALstm(nn.Module):
         Its parameter gradients are the LAST ones the backward produces, so a training step can
         stop the backward at the stem output, start the all-reduce of every other gradient, and
         only then run the stem's backward (``runtime.step.TrainStep`` split capture)."""
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()  # host datasets are float64 (reference comps/icalstm/__init__.py:29)
         self._packed = None
         if self.use_fused and x.is_cuda and self.lstm.fused_ok(x) and ops.capture.active() is None:
             self._packed = self.lstm.prepack(x.device)  # side stream, beside the encoder GEMM

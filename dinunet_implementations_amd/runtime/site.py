@@ -136,10 +136,16 @@ class FederatedSite:
             direction = "minimize"
         best = best or {"score": None, "epoch": 0, "wait": 0}
         use_fast = trainer.has_fast_path and li == 1
-        step = TrainStep(trainer.modules(), trainer.flat, trainer.optimizer, engine,
-                         use_graph=bool(cfg.get("use_graph", True)) and self.device.type == "cuda",
-                         forward_loss=lambda m, x, y: trainer.forward_loss(x, y)) \
-            if use_fast else None
+        step = None
+        if use_fast:
+            use_graph = bool(cfg.get("use_graph", True)) and self.device.type == "cuda"
+            sm = trainer.split_module()
+            if sm is not None:  # stem/body model: split capture overlaps the all-reduce
+                step = TrainStep(sm, trainer.flat, trainer.optimizer, engine, use_graph=use_graph)
+            else:
+                step = TrainStep(trainer.modules(), trainer.flat, trainer.optimizer, engine,
+                                 use_graph=use_graph,
+                                 forward_loss=lambda m, x, y: trainer.forward_loss(x, y))
         it = iter(tr)
         tl = logs.setdefault(f"{tag}train_log", [])
         vl = logs.setdefault(f"{tag}validation_log", [])

@@ -61,6 +61,12 @@ class NNTrainer:
     def forward_loss(self, x, y):  # pragma: no cover - optional fast path
         raise NotImplementedError
 
+    def split_module(self):
+        """A model with ``stem`` / ``body_loss`` / ``stem_parameters`` whose
+        ``body_loss(stem(x), y)`` equals :meth:`forward_loss` (enables the split-capture
+        training step), or None."""
+        return None
+
     def score(self, out, pred):
         return pred
 

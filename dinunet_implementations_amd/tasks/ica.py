@@ -89,6 +89,9 @@ class ICATrainer(NNTrainer):
     def forward_loss(self, x, y):
         return self.nn["net"].forward_loss(x.float(), y)
 
+    def split_module(self):
+        return self.nn["net"]  # loader batches are fp32 already: stem(x) == forward_loss's
+
     def score(self, out, pred):
         return out[:, 1]  # AUC on prob[:, 1] (comps/icalstm/__init__.py:64-65)
 
