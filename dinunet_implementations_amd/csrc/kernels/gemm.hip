@@ -87,6 +87,85 @@ __device__ __forceinline__ void stage_load(const TE* __restrict__ base, long ld,
   }
 }
 
+// Branch-free variant for the common aligned case (host-checked, GemmGroup::vec): the
+// contiguous axis (k when KCONTIG, rows otherwise) has extent and leading dimension divisible by
+// 8 and 16-B aligned bases, so a chunk is entirely in range or entirely out.  Out-of-range chunks
+// load a clamped in-range address and are zeroed by a select.  The RAW vectors stay in registers
+// until the LDS store after the MFMAs (rounding / zeroing happens there), so the next tile's
+// loads issue back to back and their latency hides under the current tile's MFMAs -- the
+// branchy variant makes the compiler drain vmcnt after every chunk.
+template <typename TE> struct Chunk;
+template <> struct Chunk<bf16> { bf16x8 v; };
+template <> struct Chunk<float> { f32x4 lo, hi; };
+
+template <int ROWS, bool KCONTIG, typename TE>
+struct VecStager {
+  static constexpr int CH = ROWS * 64 / 256 / 8;  // 16-B chunks per thread per tile
+  static constexpr int CPR = KCONTIG ? 8 : ROWS / 8;
+  Chunk<TE> c[CH];
+  bool ok[CH];
+  __device__ __forceinline__ void load(const TE* __restrict__ base, long ld, int row0, int k0,
+                                       int nrows, int K, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int idx = tid + i * 256;
+      const int ir = idx / CPR, ic = (idx % CPR) * 8;
+      const int gr = KCONTIG ? row0 + ir : row0 + ic;
+      const int gk = KCONTIG ? k0 + ic : k0 + ir;
+      ok[i] = gr < nrows && gk < K;
+      const int grc = min(gr, nrows - (KCONTIG ? 1 : 8));
+      const int gkc = min(gk, K - (KCONTIG ? 8 : 1));
+      const TE* p = KCONTIG ? base + (long)grc * ld + gkc : base + (long)gkc * ld + grc;
+      if constexpr (sizeof(TE) == 2) {
+        c[i].v = *reinterpret_cast<const bf16x8*>(p);
+      } else {
+        c[i].lo = *reinterpret_cast<const f32x4*>(p);
+        c[i].hi = *reinterpret_cast<const f32x4*>(p + 4);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(bf16* __restrict__ img, int tid) const {
+    constexpr int C = Img<ROWS, KCONTIG>::C;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int idx = tid + i * 256;
+      const int ir = idx / CPR, ic = (idx % CPR) * 8;
+      bf16x8 v;
+      if constexpr (sizeof(TE) == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ok[i] ? c[i].v[e] : (bf16)0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = (bf16)(ok[i] ? c[i].lo[e] : 0.f);
+          v[4 + e] = (bf16)(ok[i] ? c[i].hi[e] : 0.f);
+        }
+      }
+      const int r = KCONTIG ? ir : (ir ^ ((ir >> 1) & 4));  // see stage_store
+      *reinterpret_cast<bf16x8*>(img + r * C + ic) = v;
+    }
+  }
+};
+
+template <int ROWS, bool KCONTIG>
+__device__ __forceinline__ void stage_store(bf16* __restrict__ img, int tid, const bf16 (&reg)[ROWS * 64 / 256]);
+
+// the general (ragged / unaligned) stager: converts while loading
+template <int ROWS, bool KCONTIG, typename TE>
+struct GenStager {
+  bf16 reg[ROWS * 64 / 256];
+  __device__ __forceinline__ void load(const TE* __restrict__ base, long ld, int row0, int k0,
+                                       int nrows, int K, int tid) {
+    stage_load<ROWS, KCONTIG, TE>(base, ld, row0, k0, nrows, K, tid, reg);
+  }
+  __device__ __forceinline__ void store(bf16* __restrict__ img, int tid) const {
+    stage_store<ROWS, KCONTIG>(img, tid, reg);
+  }
+};
+
+template <bool VEC, int ROWS, bool KCONTIG, typename TE> struct StagerSel { typedef GenStager<ROWS, KCONTIG, TE> type; };
+template <int ROWS, bool KCONTIG, typename TE> struct StagerSel<true, ROWS, KCONTIG, TE> { typedef VecStager<ROWS, KCONTIG, TE> type; };
+
 template <int ROWS, bool KCONTIG>
 __device__ __forceinline__ void stage_store(bf16* __restrict__ img, int tid, const bf16 (&reg)[ROWS * 64 / 256]) {
   constexpr int PER = ROWS * 64 / 256;
@@ -152,6 +231,7 @@ struct GemmGroup {
   int tile_start[GMAX + 1];
   long elem_start[GMAX + 1];  // split-K reduce: prefix of M*N
   int n, splits;
+  int vec;  // every operand satisfies stage_load_vec's alignment contract
 };
 
 __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int row, int col, float v) {
@@ -171,7 +251,7 @@ __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int
   }
 }
 
-template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe>
+template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe, bool VEC>
 __global__ void __launch_bounds__(256)
 gemm_kernel(GemmGroup g) {
   typedef GemmTile<BM, BN, TA, TB> T;
@@ -180,14 +260,22 @@ gemm_kernel(GemmGroup g) {
 #define As(b) (smem + (b) * T::IA::ELEMS)
 #define Bs(b) (smem + 2 * T::IA::ELEMS + (b) * T::IB::ELEMS)
 
+  // XCD-aware tile order: the hardware deals workgroups round-robin over the 8 XCDs (blocks b
+  // and b+8 share one L2), so give every XCD a CONTIGUOUS run of row-major tiles -- the tiles
+  // of one row band (same A rows) then share that XCD's L2 instead of fetching A 8 times.
+  // gridDim.x is padded to a multiple of 8 by the launcher; surplus blocks exit.
+  const int ntiles = g.tile_start[g.n];
+  const int bid = (int)blockIdx.x;
+  const int gtile = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
+  if (gtile >= ntiles) return;
   int pi = 0;
-  while (pi + 1 < g.n && (int)blockIdx.x >= g.tile_start[pi + 1]) ++pi;
+  while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
   const GemmProb& P = g.p[pi];
   const TAe* __restrict__ A = reinterpret_cast<const TAe*>(P.A);
   const TBe* __restrict__ B = reinterpret_cast<const TBe*>(P.B);
   const long lda = P.lda, ldb = P.ldb;
   const int M = P.M, N = P.N, K = P.K;
-  const int tile = blockIdx.x - g.tile_start[pi];
+  const int tile = gtile - g.tile_start[pi];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -197,7 +285,8 @@ gemm_kernel(GemmGroup g) {
   const int kbeg = blockIdx.z * P.kchunk;
   const int kend = min(K, kbeg + P.kchunk);
 
-  bf16 ra[T::A_ELEMS], rb[T::B_ELEMS];
+  typename StagerSel<VEC, BM, !TA, TAe>::type sa;
+  typename StagerSel<VEC, BN, TB, TBe>::type sb;
   f32x4 acc[T::FM][T::FN];
 #pragma unroll
   for (int i = 0; i < T::FM; ++i)
@@ -206,10 +295,10 @@ gemm_kernel(GemmGroup g) {
 
   const int nk = kend > kbeg ? (kend - kbeg + T::BK - 1) / T::BK : 0;
   if (nk > 0) {
-    stage_load<BM, !TA, TAe>(A, lda, row0, kbeg, M, kend, tid, ra);
-    stage_load<BN, TB, TBe>(B, ldb, col0, kbeg, N, kend, tid, rb);
-    stage_store<BM, !TA>(As(0), tid, ra);
-    stage_store<BN, TB>(Bs(0), tid, rb);
+    sa.load(A, lda, row0, kbeg, M, kend, tid);
+    sb.load(B, ldb, col0, kbeg, N, kend, tid);
+    sa.store(As(0), tid);
+    sb.store(Bs(0), tid);
   }
   __syncthreads();
   for (int it = 0; it < nk; ++it) {
@@ -217,8 +306,8 @@ gemm_kernel(GemmGroup g) {
     const bool more = it + 1 < nk;
     if (more) {  // next tile's global loads fly under this tile's MFMAs
       const int k0 = kbeg + (it + 1) * T::BK;
-      stage_load<BM, !TA, TAe>(A, lda, row0, k0, M, kend, tid, ra);
-      stage_load<BN, TB, TBe>(B, ldb, col0, k0, N, kend, tid, rb);
+      sa.load(A, lda, row0, k0, M, kend, tid);
+      sb.load(B, ldb, col0, k0, N, kend, tid);
     }
 #pragma unroll
     for (int ks = 0; ks < T::BK / 32; ++ks) {
@@ -233,8 +322,8 @@ gemm_kernel(GemmGroup g) {
         for (int j = 0; j < T::FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
     if (more) {
-      stage_store<BM, !TA>(As(cur ^ 1), tid, ra);
-      stage_store<BN, TB>(Bs(cur ^ 1), tid, rb);
+      sa.store(As(cur ^ 1), tid);
+      sb.store(Bs(cur ^ 1), tid);
     }
     __syncthreads();
   }
@@ -304,8 +393,11 @@ int launch(GemmGroup& g, hipStream_t st) {
   }
   g.tile_start[g.n] = tiles;
   g.elem_start[g.n] = elems;
-  dim3 grid(tiles, 1, g.splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe>), grid, dim3(256), 0, st, g);
+  dim3 grid((tiles + 7) / 8 * 8, 1, g.splits);
+  if (g.vec)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, true>), grid, dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, false>), grid, dim3(256), 0, st, g);
   if (g.splits > 1) {
     const long t4 = elems / 4;
     const int blocks = (int)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
@@ -330,7 +422,20 @@ int dispatch_tile(int a_bf16, int b_bf16, int ta, int tb, GemmGroup& g, hipStrea
   return dispatch_t<BM, BN, float, float>(ta, tb, g, st);
 }
 
+// tile: 0 -> 64x64, 1 -> 128x128 (BM x BN)
+static bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+// stage_load_vec's contract for one operand: contiguous-axis extent and leading dim % 8 == 0
+static bool vec_ok(const void* base, int kcontig, int rows, int K, long ld) {
+  return aligned16(base) && ld % 8 == 0 && (kcontig ? K % 8 == 0 : rows % 8 == 0);
+}
+
 static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int tile, hipStream_t st) {
+  g.vec = 1;
+  for (int i = 0; i < g.n; ++i) {
+    const GemmProb& P = g.p[i];
+    if (!vec_ok(P.A, !ta, P.M, P.K, P.lda) || !vec_ok(P.B, tb, P.N, P.K, P.ldb)) g.vec = 0;
+  }
   if (tile == 1) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
   return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, g, st);
 }
@@ -342,7 +447,7 @@ DN_API long dn_gemm_workspace(int M, int N, int K, int splits) {
   return splits > 1 ? (long)splits * M * N : 0;
 }
 
-// tile: 0 -> 64x64, 1 -> 128x128
+// tile: see run_group
 DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, int b_bf16, int tb,
                    long ldb, void* C, int c_bf16, long ldc, int M, int N, int K, float alpha,
                    float beta, const float* bias, int relu, const int* row_map, int tile,

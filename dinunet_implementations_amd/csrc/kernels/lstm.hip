@@ -88,8 +88,18 @@ __device__ __forceinline__ float row_gather(const float (&v)[16 / BR]) {
 // ---------------------------------------------------------------------------------------------
 // m-tiles (of 4 per wave) whose W fragments live in LDS instead of VGPRs (fwd), and k-steps
 // (of 4*HD/32) of W^T kept in LDS (bwd): sized so HD=192 fits 168 VGPRs (3 waves/SIMD) spill-free.
-template <int HD> struct LdsSplit { static constexpr int FWD_MT = 0, BWD_KS = 0; };
-template <> struct LdsSplit<192> { static constexpr int FWD_MT = 1, BWD_KS = 9; };
+// At BR = 4 / 8 a lane owns 1-2 gate slots, which leaves room for all of W_hh in VGPRs in the
+// forward and all but 4 k-steps of W_hh^T in the backward (whose exchange-tile reads run ahead
+// of the MFMA chain and need the registers): spill-free at 168.
+template <int HD, int BR> struct LdsSplit { static constexpr int FWD_MT = 0, BWD_KS = 0; };
+template <> struct LdsSplit<192, 4> { static constexpr int FWD_MT = 0, BWD_KS = 4; };
+template <> struct LdsSplit<192, 8> { static constexpr int FWD_MT = 0, BWD_KS = 6; };
+template <> struct LdsSplit<192, 16> { static constexpr int FWD_MT = 1, BWD_KS = 9; };
+
+// Column of the all-zero 16 B slot (row BR of the h / dpre exchange tile) that MFMA lanes of
+// padded batch columns read: its banks (16 + 32 = 48..51 for every HD the kernels take) are not
+// touched by the valid lanes of the same ds_read_b128 lane group.
+constexpr int ZCOL = 64;
 
 // BR = batch rows per workgroup (4, 8 or 16).  The recurrent MFMA always computes 16 columns;
 // columns >= BR are zero.  For the gate phase the BR valid columns are redistributed over all
@@ -115,14 +125,14 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
   constexpr int NT = HD / 16 * 64;
   constexpr int KS = HD / 32;
   constexpr int LDH = HD + 8;  // +16 B per row: the 16 rows land on distinct bank quads
-  constexpr int NLM = LdsSplit<HD>::FWD_MT, NRM = 4 - NLM;
+  constexpr int NLM = LdsSplit<HD, BR>::FWD_MT, NRM = 4 - NLM;
   constexpr int NW = HD / 16;
   constexpr int G16 = 16 / BR, NSL = BR / 4;
   constexpr int EPT = BR * HD / NT;  // h_{t-1} copy: elements per thread (1, 2 or 4)
   __shared__ __attribute__((aligned(16))) bf16 hbuf[2][16][LDH];
   __shared__ __attribute__((aligned(16))) float bias_s[4 * HD];
   // lane-linear fragment image: one 1 KiB row per (wave, m-tile, k-step) -> conflict-free b128
-  __shared__ __attribute__((aligned(16))) bf16x8 wlds[NW][NLM > 0 ? NLM : 1][KS][64];
+  __shared__ __attribute__((aligned(16))) bf16x8 wlds[NLM > 0 ? NW : 1][NLM > 0 ? NLM : 1][NLM > 0 ? KS : 1][64];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane >> 4, n = lane & 15, r = n / BR, bl = n % BR;
@@ -191,9 +201,13 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
     for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      // columns >= BR are zero: skip their LDS reads (exec-masked lanes cost no LDS cycles)
-      bf16x8 hb = {};
-      if (BR == 16 || n < BR) hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n][32 * ks + 8 * q]);
+      // columns >= BR must be zero: those lanes read one all-zero 16 B slot (row BR is never
+      // written) instead of being exec-masked -- every lane group of ds_read_b128 holds valid
+      // lanes anyway, so masking saved no LDS cycle but made the compiler branch and drain
+      // lgkmcnt before every MFMA; unmasked, the reads of later k-steps issue ahead
+      const bool hv = BR == 16 || n < BR;
+      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(
+          &hbuf[cur][hv ? n : (BR & 15)][hv ? 32 * ks + 8 * q : ZCOL]);
 #pragma unroll
       for (int mt = 0; mt < NRM; ++mt) acc[mt] = mfma16(wf[mt][ks], hb, acc[mt]);
 #pragma unroll
@@ -289,12 +303,12 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
                 bf16* __restrict__ dpre) {          // [Bp*S][ndir][4*HD] permuted, original time
   constexpr int KS = 4 * HD / 32;
   constexpr int LDD = 4 * HD + 8;
-  constexpr int NLK = LdsSplit<HD>::BWD_KS, NRK = KS - NLK;
+  constexpr int NLK = LdsSplit<HD, BR>::BWD_KS, NRK = KS - NLK;
   constexpr int NW = HD / 16;
   constexpr int NT = NW * 64;
   constexpr int G16 = 16 / BR, NSL = BR / 4;
   __shared__ __attribute__((aligned(16))) bf16 dbuf[2][16][LDD];
-  __shared__ __attribute__((aligned(16))) bf16x8 wlds[NW][NLK > 0 ? NLK : 1][64];
+  __shared__ __attribute__((aligned(16))) bf16x8 wlds[NLK > 0 ? NW : 1][NLK > 0 ? NLK : 1][64];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane >> 4, n = lane & 15, r = n / BR, bl = n % BR;
@@ -375,8 +389,9 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 db = {};
-      if (BR == 16 || n < BR) db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n][32 * ks + 8 * q]);
+      const bool dv = BR == 16 || n < BR;  // see the forward: unmasked zero-slot reads
+      const bf16x8 db = *reinterpret_cast<const bf16x8*>(
+          &dbuf[cur][dv ? n : (BR & 15)][dv ? 32 * ks + 8 * q : ZCOL]);
       acc = mfma16(ks < NRK ? af[ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db, acc);
     }
     float dhr[NSL];

@@ -66,7 +66,8 @@ def choose_tiling(M: int, N: int, K: int):
 def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
        out_dtype: torch.dtype = torch.float32, out: Optional[Tensor] = None,
        bias: Optional[Tensor] = None, relu: bool = False, alpha: float = 1.0, beta: float = 0.0,
-       row_map: Optional[Tensor] = None, splits: Optional[int] = None) -> Tensor:
+       row_map: Optional[Tensor] = None, splits: Optional[int] = None,
+       tile: Optional[int] = None) -> Tensor:
     A = a.t() if trans_a else a
     B = b.t() if trans_b else b
     M, K = A.shape
@@ -101,7 +102,8 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
             raise ValueError("beta != 0 needs an existing `out`")
     if out.stride(1) != 1:
         raise ValueError("mm output must be row-contiguous")
-    tile, auto_splits = choose_tiling(M, N, K)
+    auto_tile, auto_splits = choose_tiling(M, N, K)
+    tile = auto_tile if tile is None else int(tile)
     sp = auto_splits if splits is None else max(1, int(splits))
     slab = None
     if sp > 1:
@@ -119,7 +121,7 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
 
 
 def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
-               splits: Optional[int] = None):
+               splits: Optional[int] = None, tile: Optional[int] = None):
     """Several independent ``out_i (+)= alpha_i * op(a_i) @ op(b_i)`` in ONE launch.
 
     ``problems``: sequence of dicts with keys ``a``, ``b``, ``out`` (required, fp32 or bf16 like
@@ -132,7 +134,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         return
     if len(probs) > 8:
         for i in range(0, len(probs), 8):
-            mm_grouped(probs[i:i + 8], trans_a, trans_b, splits)
+            mm_grouped(probs[i:i + 8], trans_a, trans_b, splits, tile)
         return
     if not probs[0]["a"].is_cuda:
         for q in probs:
@@ -197,4 +199,4 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               (L * n)(*arrs["ldc"]), (I * n)(*arrs["M"]), (I * n)(*arrs["N"]),
               (I * n)(*arrs["K"]), (F * n)(*arrs["alpha"]), (F * n)(*arrs["beta"]),
               (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), 0, int(a_bf), int(b_bf), ta, tb,
-              int(c_bf), 0, sp, _lib.ptr(slab), _lib.stream())
+              int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.stream())

@@ -39,6 +39,21 @@ def test_gemm_layouts(M, N, K, ta, tb):
     assert rel(out, ref) < 2e-3
 
 
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(333, 197, 420), (328, 200, 416)])
+def test_gemm_tile_shapes(tile, splits, ta, tb, M, N, K):
+    """Both tile shapes x split-K, ragged shapes (branchy staging) and 8-aligned ones (the
+    branch-free vector staging with clamped loads at the tile edges)."""
+    from dinunet_implementations_amd.ops import mm
+    a = torch.randn(K, M, device=DEV) if ta else torch.randn(M, K, device=DEV)
+    b = torch.randn(N, K, device=DEV) if tb else torch.randn(K, N, device=DEV)
+    ref = bf(a.t() if ta else a) @ bf(b.t() if tb else b)
+    out = mm(a, b, trans_a=ta, trans_b=tb, tile=tile, splits=splits)
+    assert rel(out, ref) < 2e-3
+
+
 def test_gemm_epilogue_bias_relu_bf16_out_and_beta():
     from dinunet_implementations_amd.ops import mm
     M, N, K = 300, 200, 128
