@@ -113,7 +113,8 @@ constexpr int ZCOL = 64;
 // hipcc emits counted s_waitcnt vmcnt(N) and a step never waits for the previous step's stores.
 template <int HD, int BR, bool SEQ>
 __global__ void __launch_bounds__(HD / 16 * 64)
-lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted cols, no bias
+lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted cols, no bias;
+                                                 // store_pre: overwritten by the gate pre-activations
                 const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
                 const bf16* __restrict__ whh,    // [ndir][4*HD][HD] permuted rows, zero padded
                 int B, int S, int Hd, int ndir,
@@ -121,7 +122,8 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
                 bf16* __restrict__ hprev,        // [ndir][Bp][S][HD]   h_{t-1} at original time idx
                 float* __restrict__ hseq,        // SEQ: [Bp][S][ndir*HD] (processing order)
                 float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
-                float* __restrict__ hT, float* __restrict__ cT) {  // [B][ndir*Hd]
+                float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
+                int store_pre) {
   constexpr int NT = HD / 16 * 64;
   constexpr int KS = HD / 32;
   constexpr int LDH = HD + 8;  // +16 B per row: the 16 rows land on distinct bank quads
@@ -162,7 +164,8 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
   int uu[NSL];
 #pragma unroll
   for (int s = 0; s < NSL; ++s) uu[s] = 16 * w + 4 * (r + s * G16) + q;
-  const float* xrow = xp + (long)bc * S * rowX + (long)dir * 4 * HD;
+  float* xrow = xp + (long)bc * S * rowX + (long)dir * 4 * HD;
+  const bool wpre = store_pre && b < B;  // padded rows alias row B-1: never store them
   const long hplane = (long)dir * Bp * S * HD;
   const int cp_r = (tid * EPT) / HD, cp_c = (tid * EPT) % HD;
   bf16* hcp = hprev + hplane + ((long)(blockIdx.x * BR + cp_r) * S) * HD + cp_c;
@@ -243,6 +246,9 @@ lstm_fwd_kernel(const float* __restrict__ xp,    // [B*S][ndir][4*HD] permuted c
       const float p1 = pa[s][1] + xn[s][1] + bb[1];
       const float p2 = pa[s][2] + xn[s][2] + bb[2];
       const float p3 = pa[s][3] + xn[s][3] + bb[3];
+      // the gate pre-activations x W_ih^T + h W_hh^T + b, in place of the projection they were
+      // built from: the backward reads them instead of re-running a time-parallel GEMM
+      if (wpre) *reinterpret_cast<f32x4*>(xrow + (long)tau * rowX + 4 * u) = f32x4{p0, p1, p2, p3};
       // consumed: issue step t+1's projection (hidden by its MFMA phase)
       xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 4 * u);
       const float gi = dn_sigmoid(dn_sigmoid(p0));
@@ -571,26 +577,26 @@ static inline int pick_br(int B) {
 }
 
 template <int HD, int BR>
-int launch_fwd_br(const float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
+int launch_fwd_br(float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
-                  float* cT, hipStream_t st) {
+                  float* cT, int store_pre, hipStream_t st) {
   dim3 grid((B + BR - 1) / BR, ndir), block(HD / 16 * 64);
   if (hseq)
     hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, true>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
-                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT);
+                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
   else
     hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
-                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT);
+                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
   return dn_launch_status();
 }
 
 template <int HD>
-int launch_fwd(int BR, const float* xp, const float* bias, const bf16* whh, int B, int S, int Hd,
+int launch_fwd(int BR, float* xp, const float* bias, const bf16* whh, int B, int S, int Hd,
                int ndir, float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale,
-               float* hT, float* cT, hipStream_t st) {
-  if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, st);
-  if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, st);
-  return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, st);
+               float* hT, float* cT, int store_pre, hipStream_t st) {
+  if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+  if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+  return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
 }
 
 template <int HD, int BR>
@@ -644,16 +650,18 @@ DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0,
 // rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
 DN_API int dn_lstm_rows_per_wg(int B) { return pick_br(B); }
 
-DN_API int dn_lstm_fwd(const float* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
+// store_pre != 0: xp is overwritten in place by the gate pre-activations (+ bias) the
+// backward consumes
+DN_API int dn_lstm_fwd(float* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
                        int ndir, float* c_save, void* hprev, float* hseq, float* hmean,
-                       float mean_scale, float* hT, float* cT, hipStream_t st) {
+                       float mean_scale, float* hT, float* cT, int store_pre, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
   const int BR = pick_br(B);
   switch (HD) {
-    case 64: return launch_fwd<64>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
-    case 128: return launch_fwd<128>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
-    case 192: return launch_fwd<192>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, st);
+    case 64: return launch_fwd<64>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+    case 128: return launch_fwd<128>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+    case 192: return launch_fwd<192>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
   }
   return DN_UNSUPPORTED;
 }

@@ -50,16 +50,17 @@ def _layout(t: Tensor, rows_first: bool):
 
 
 def choose_tiling(M: int, N: int, K: int):
-    """(tile, split-K).  These GEMMs are latency-bound (few tiles, serial K loop): long K is cut
-    into ~384-deep chunks on separate workgroups (measured on MI355X: dx 3136x256x1536
-    73 -> 38 us at 4 splits; dW 768x256x3136 120 -> 35 us at 8)."""
+    """(tile, split-K).  Few-tile long-K GEMMs (the weight gradients, 64 tiles of K = 3136) cut K
+    into ~384-deep chunks on separate workgroups; from ~128 tiles on, the deterministic slab
+    reduce costs more than it saves (tools/bench_gemm_sweep.py on MI355X: encoder 3136x256x1000
+    18.1 us unsplit vs 21.2 at 2 splits; dx 3136x256x1536 19.6 vs 21.8)."""
     t128 = ((M + 127) // 128) * ((N + 127) // 128)
     t64 = ((M + 63) // 64) * ((N + 63) // 64)
     if t128 >= 2 * _NCU:
         return 1, 1
     splits = 1
-    if K >= 768 and t64 < 2 * _NCU:
-        splits = max(1, min(8, round(K / 384)))
+    if K >= 768 and t64 < _NCU // 2:  # measured: at ~200 tiles the slab reduce costs more
+        splits = max(1, min(8, round(K / 384), (4 * _NCU) // max(t64, 1)))
     return 0, splits
 
 
@@ -182,7 +183,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
     if splits is None:
         splits = 1
-        if maxk >= 768 and t64 < 2 * _NCU:
+        if maxk >= 768 and t64 < _NCU // 2:
             splits = max(1, min(8, round(maxk / 384), (4 * _NCU) // max(t64, 1)))
     sp = max(1, int(splits))
     dev = probs[0]["out"].device

@@ -6,13 +6,12 @@ forward
   1. ``dn_lstm_pack``: fp32 reference-layout params -> bf16 kernel layouts (gate rows permuted to
      ``m = 4u + g``, units zero-padded to HD in {64,128,192}), fused bias ``b_ih + b_hh``.
   2. input projection of both directions as ONE GEMM ``[B*S, I] x [I, ndir*4*HD]`` (fp32 out).
-  3. ``dn_lstm_fwd``: persistent recurrence (grid = 16-row batch chunks x directions), stores
-     only ``c_t`` and ``h_{t-1}`` per step.
+  3. ``dn_lstm_fwd``: persistent recurrence (grid = batch-row chunks x directions), stores
+     ``c_t`` and ``h_{t-1}`` per step and, when a backward will follow, the gate
+     pre-activations ``x W_ih^T + h_{t-1} W_hh^T + b`` in place of the projection it read
+     (one 16-B store per lane and step, no extra GEMM).
 backward
-  4. gate pre-activations for every step at once, in place on the projection buffer:
-     ``pre = xp + h_{t-1} W_hh^T + b`` (one GEMM per direction, full chip, time-parallel).
-     When a backward will follow, these GEMMs are issued at the end of the FORWARD on a side
-     stream, so they run beside the (latency-bound, few-CU) classifier head.
+  4. (nothing to recompute: the projection buffer holds the pre-activations).
   5. ``dn_lstm_bwd``: reverse-time recurrence -> gate grads ``dpre`` (bf16, original time order).
   6. parameter grads ACCUMULATED straight into ``.grad`` (flat buffer) by GEMM epilogues with a
      row map back to the reference ``[i|f|o|g]`` layout: ``dW_ih += dpre^T x``,
@@ -41,7 +40,7 @@ _lib.register("dn_lstm_pack", [_lib.c_void_p] * 8 + [_lib.c_int] * 3 + [_lib.c_v
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
-                              _lib.c_void_p])
+                              _lib.c_int, _lib.c_void_p])
 _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_long, _lib.c_long, _lib.c_float, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
@@ -110,21 +109,14 @@ class _BiLSTMFn(torch.autograd.Function):
             hmean = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
         else:
             hseq = torch.empty(Bp, S, ndir * HD, dtype=torch.float32, device=dev)
+        need_bwd = any(ctx.needs_input_grad)
         _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
                   ndir, c_save.data_ptr(), hprev.data_ptr(), _lib.ptr(hseq), _lib.ptr(hmean),
-                  1.0 / S, hT.data_ptr(), cT.data_ptr(), st)
+                  1.0 / S, hT.data_ptr(), cT.data_ptr(), int(need_bwd), st)
         if mode == "mean":
             out = hmean
         else:
             out = hseq.view(Bp, S, ndir, HD)[:B, :, :, :Hd].reshape(B, S, ndir * Hd)
-        ctx.pre_ev = None
-        if any(ctx.needs_input_grad) and _cap.active() is None:
-            side = _streams.fork(dev)
-            with torch.cuda.stream(side):
-                _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir)
-                ctx.pre_ev = torch.cuda.Event()
-                ctx.pre_ev.record(side)
-            _streams.keep_alive(side, (xp, hprev, whh_p, bias_p))
         ctx.save_for_backward(x2d, wih_p, whh_p, whhT_p, bias_p, xp, c_save, hprev)
         ctx.params = params
         ctx.meta = (B, S, I, Hd, HD, ndir, mode, enc.dtype)
@@ -141,12 +133,7 @@ class _BiLSTMFn(torch.autograd.Function):
         Bp = c_save.shape[1]
         dev = x2d.device
         st = _lib.stream()
-        # (4) time-parallel pre-activations, in place on the projection buffer
-        if ctx.pre_ev is not None:
-            torch.cuda.current_stream(dev).wait_event(ctx.pre_ev)
-            ctx.pre_ev = None
-        else:
-            _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir)
+        # (4) xp already holds the gate pre-activations (stored in place by the forward kernel)
         # (5) reverse-time recurrence
         if dout is None:
             dout = torch.zeros((B, ndir * Hd) if mode == "mean" else (B, S, ndir * Hd),
@@ -236,16 +223,6 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
-
-
-def _pre_activations(xp, hprev, whh_p, bias_p, B, S, HD, ndir):
-    """``xp[:, d] += h_{t-1} W_hh^T + b`` for every step (in place): the gate pre-activations."""
-    GP = 4 * HD
-    N = B * S
-    Bp = hprev.shape[1]
-    mm_grouped([dict(a=hprev[d].view(Bp * S, HD)[:N], b=whh_p[d], out=xp[:, d * GP:(d + 1) * GP],
-                     beta=1.0, bias=bias_p[d * GP:(d + 1) * GP]) for d in range(ndir)],
-               trans_b=True)
 
 
 def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
