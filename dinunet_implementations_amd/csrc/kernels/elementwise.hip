@@ -67,7 +67,46 @@ __global__ void colsum_slabs_kernel(const float* __restrict__ part, int slabs, i
   out[c] = accumulate ? out[c] + v : v;
 }
 
+// Training-step prologue in ONE launch (it replaces three: two copies into the HIP graph's static
+// inputs and the gradient zeroing): x fp32 -> bf16 static input (the GEMMs round their operands
+// to bf16 while staging anyway, so this is bit-identical and halves their reads), the int64
+// labels, and zeros into the flat gradient buffer.  Grid-stride over 8-element x units, 4-element
+// gradient units and single labels; n_x % 8 == 0 and n_g % 4 == 0 (host-checked).
+__global__ void __launch_bounds__(256)
+step_prologue_kernel(const float* __restrict__ x, long ux, bf16* __restrict__ xb,
+                     const long long* __restrict__ y, long ny, long long* __restrict__ yd,
+                     float* __restrict__ g, long ug) {
+  const long total = ux + ug + ny;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    if (i < ux) {
+      const f32x4 a = reinterpret_cast<const f32x4*>(x)[2 * i];
+      const f32x4 b = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { o[e] = (bf16)a[e]; o[4 + e] = (bf16)b[e]; }
+      reinterpret_cast<bf16x8*>(xb)[i] = o;
+    } else if (i < ux + ug) {
+      reinterpret_cast<f32x4*>(g)[i - ux] = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      yd[i - ux - ug] = y[i - ux - ug];
+    }
+  }
+}
+
 }  // namespace
+
+DN_API int dn_step_prologue(const float* x, long nx, void* xb, const long long* y, long ny,
+                            long long* yd, float* g, long ng, hipStream_t st) {
+  if (nx % 8 || ng % 4 || (((uintptr_t)x | (uintptr_t)xb | (uintptr_t)g) & 15)) return DN_BAD_SHAPE;
+  const long total = nx / 8 + ng / 4 + ny;
+  if (total <= 0) return DN_OK;
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, nx / 8,
+                     (bf16*)xb, y, ny, yd, g, ng / 4);
+  return dn_launch_status();
+}
 
 DN_API long dn_relu_bwd_colsum_workspace(int N, int O) { return (long)RB_SLABS * O; }
 

@@ -75,12 +75,19 @@ struct HArgs {
 
 __host__ __device__ constexpr int rup32(int v) { return (v + 31) & ~31; }
 
+// 32-bit counter hash (Wellons' lowbias32 finaliser over idx ^ key(seed, layer)): two 32-bit
+// multiplies per element.  The former 64-bit splitmix finaliser (six 64-bit multiplies, each a
+// chain of quarter-rate 32-bit ones) made the layer-0 dropout the longest phase of the forward.
 __device__ __forceinline__ uint32_t hmix(uint64_t seed, uint32_t layer, uint32_t idx) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ull + ((((uint64_t)layer) << 32) | idx) + 0x632BE59BD9B4E019ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 40);
+  const uint32_t key = (uint32_t)seed * 0x9E3779B9u ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu ^
+                       (layer + 1u) * 0xC2B2AE35u;
+  uint32_t x = idx ^ key;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x >> 8;  // 24 uniform bits
 }
 
 __device__ __forceinline__ bool hkeep(uint64_t seed, int layer, int m, int k, int K, float p) {

@@ -11,7 +11,14 @@ namespace {
 __global__ void __launch_bounds__(256)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
-            float bc1, float inv_sqrt_bc2, float grad_scale) {
+            float bc1, float inv_sqrt_bc2, float grad_scale, const int* __restrict__ tdev,
+            double b1d, double b2d) {
+  if (tdev) {  // graph-replayable form: the step number lives on the device (adam_bump_kernel);
+               // double math as on the host, so both forms round to the same fp32 corrections
+    const double t = (double)(*tdev + 1);
+    bc1 = (float)(1.0 - pow(b1d, t));
+    inv_sqrt_bc2 = (float)(1.0 / sqrt(1.0 - pow(b2d, t)));
+  }
   const long n4 = n >> 2;
   const float step = lr / bc1;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
@@ -39,6 +46,8 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
     p[t] -= step * m[t] / (sqrtf(v[t]) * inv_sqrt_bc2 + eps);
   }
 }
+
+__global__ void adam_bump_kernel(int* __restrict__ tdev) { *tdev += 1; }
 
 // plain SGD with momentum (torch.optim.SGD semantics, dampening 0, no nesterov)
 __global__ void __launch_bounds__(256)
@@ -81,7 +90,19 @@ DN_API int dn_adam(float* p, const float* g, float* m, float* v, long n, float l
   if (n <= 0) return DN_OK;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, n, lr,
-                     b1, b2, eps, wd, bc1, inv_sqrt_bc2, grad_scale);
+                     b1, b2, eps, wd, bc1, inv_sqrt_bc2, grad_scale, (const int*)nullptr, 0.0, 0.0);
+  return dn_launch_status();
+}
+
+// Adam whose step number t is read from (and then advanced in) device memory: capturable in a
+// HIP graph and replayed every step with the right bias corrections.  *tdev = completed steps.
+DN_API int dn_adam_dev(float* p, const float* g, float* m, float* v, long n, float lr, double b1,
+                       double b2, float eps, float wd, float grad_scale, int* tdev, hipStream_t st) {
+  if (n <= 0) return DN_OK;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, n, lr,
+                     (float)b1, (float)b2, eps, wd, 0.f, 0.f, grad_scale, (const int*)tdev, b1, b2);
+  hipLaunchKernelGGL(adam_bump_kernel, dim3(1), dim3(1), 0, st, tdev);
   return dn_launch_status();
 }
 

@@ -100,6 +100,9 @@ class LSTM(nn.Module):
 
 
 class ICALstm(nn.Module):
+    # the encoder GEMM rounds its input to bf16 while staging: a bf16 batch is bit-identical
+    accepts_bf16_input = True
+
     def __init__(self, input_size: int = 256, hidden_size: int = 256, bidirectional: bool = True,
                  num_cls: int = 2, num_comps: int = 53, window_size: int = 20,
                  num_layers: int = 1):

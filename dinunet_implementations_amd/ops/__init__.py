@@ -5,7 +5,7 @@ from ._lib import native_available
 from .gemm import mm
 from .linear import linear_bias_relu
 from .lstm import bilstm as _bilstm_fused, lstm_supported, padded_hidden
-from .optim import FlatParams, FusedAdam, cast_bf16_to_f32, cast_f32_to_bf16
+from .optim import FlatParams, FusedAdam, cast_bf16_to_f32, cast_f32_to_bf16, step_prologue
 from .heads import softmax_ce, log_softmax_nll
 from .head import HeadSpec, head_loss
 
@@ -16,6 +16,6 @@ def bilstm(x, params, reduce: str = "none", modules=None, packed=None):
 
 __all__ = [
     "mm", "linear_bias_relu", "bilstm", "lstm_supported", "padded_hidden", "FlatParams",
-    "FusedAdam", "cast_bf16_to_f32", "cast_f32_to_bf16", "HeadSpec", "head_loss",
+    "FusedAdam", "cast_bf16_to_f32", "cast_f32_to_bf16", "step_prologue", "HeadSpec", "head_loss",
     "softmax_ce", "log_softmax_nll", "native_available", "capture", "reference",
 ]

@@ -24,6 +24,7 @@ _lock = threading.Lock()
 _load_error: Optional[str] = None
 
 c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
+c_double = ctypes.c_double
 
 # name -> argtypes (restype is always int status)
 _SIGS = {

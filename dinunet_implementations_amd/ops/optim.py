@@ -21,6 +21,13 @@ from . import _lib
 
 _lib.register("dn_adam", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                           _lib.c_long] + [_lib.c_float] * 8 + [_lib.c_void_p])
+_lib.register("dn_adam_dev", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                              _lib.c_long, _lib.c_float, _lib.c_double, _lib.c_double,
+                              _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_void_p,
+                              _lib.c_void_p])
+_lib.register("dn_step_prologue", [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p,
+                                   _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                                   _lib.c_void_p])
 _lib.register("dn_sgd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                          _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_int,
                          _lib.c_void_p])
@@ -85,6 +92,7 @@ class FusedAdam:
         self.exp_avg = torch.zeros_like(flat.data)
         self.exp_avg_sq = torch.zeros_like(flat.data)
         self.step_count = 0
+        self._tdev: Optional[torch.Tensor] = None  # device step counter (graph-captured steps)
 
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
@@ -108,6 +116,25 @@ class FusedAdam:
         denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(self.eps)
         d.addcdiv_(self.exp_avg, denom, value=-self.lr / bc1)
 
+    # HIP-graph form --------------------------------------------------------------------------
+    def sync_device_step(self):
+        """Copy the host step count to the device counter :meth:`step_graphable` reads."""
+        if self._tdev is None:
+            self._tdev = torch.zeros(1, dtype=torch.int32, device=self.flat.data.device)
+        self._tdev.fill_(self.step_count)
+
+    def step_graphable(self, grad_scale: float = 1.0):
+        """One Adam step whose bias corrections come from the device step counter (advanced by
+        the same launch), so it can be captured once and replayed every step.  The caller keeps
+        ``step_count`` in sync (one increment per replay)."""
+        d = self.flat.data
+        if self._tdev is None:
+            self.sync_device_step()
+        b1, b2 = self.betas
+        _lib.call("dn_adam_dev", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
+                  self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
+                  self.weight_decay, grad_scale, self._tdev.data_ptr(), _lib.stream())
+
     def state_dict(self) -> Dict:
         return {"lr": self.lr, "betas": self.betas, "eps": self.eps,
                 "weight_decay": self.weight_decay, "step": self.step_count,
@@ -122,6 +149,18 @@ class FusedAdam:
         if "exp_avg" in sd:
             self.exp_avg.copy_(sd["exp_avg"].to(self.exp_avg.device))
             self.exp_avg_sq.copy_(sd["exp_avg_sq"].to(self.exp_avg_sq.device))
+
+
+def step_prologue(x: torch.Tensor, xb: Optional[torch.Tensor], y: torch.Tensor,
+                  yd: torch.Tensor, grad: torch.Tensor):
+    """ONE launch before a graph replay: ``xb <- bf16(x)`` (skipped when ``xb`` is None),
+    ``yd <- y`` (int64) and ``grad <- 0``."""
+    nx = x.numel() if xb is not None else 0
+    if nx % 8 or grad.numel() % 4 or y.dtype != torch.int64 or yd.dtype != torch.int64:
+        raise ValueError("step_prologue: x numel % 8, grad numel % 4 and int64 labels required")
+    _lib.call("dn_step_prologue", x.data_ptr() if nx else None, nx,
+              xb.data_ptr() if nx else None, y.data_ptr(), y.numel(), yd.data_ptr(),
+              grad.data_ptr(), grad.numel(), _lib.stream())
 
 
 def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):

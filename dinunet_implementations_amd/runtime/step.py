@@ -7,6 +7,10 @@ optimizer's bias-correction scalars change every step and collective capture is 
 handful of bucketed all-reduces.  Engines whose reduction needs host-side logic (rank-dAD,
 PowerSGD) or that capture activations run eagerly.
 
+Before each replay ONE prologue launch converts the batch into the graph's static (bf16) input,
+copies the labels and zeroes the flat gradient.  With a single site the fused Adam update is
+captured too (its step number lives on the device), so a step is prologue + one replay.
+
 Split capture (dSGD across sites): the model's ``stem`` (ICA: the encoder) produces the LAST
 gradients of the backward, so the step is captured as TWO graphs cut at the stem output —
 A = zero-grad + forward + backward of everything after the stem (its input gradient included),
@@ -68,11 +72,23 @@ class TrainStep:
         self.split = bool(split and can_split)
         self._first_buckets = engine.split_buckets(list(model.stem_parameters())) if self.split else []
         self.graph_b = None
+        self._one = None
+        self.graph_opt = False
+        self._cap_lr = None
+        self._bf16_in = False
+
+    def _backward(self, loss):
+        # a persistent d(loss)/d(loss) = 1: loss.backward() would launch a fill kernel for it
+        # inside every replay
+        one = self._one
+        if one is None or one.device != loss.device or one.dtype != loss.dtype:
+            one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+        torch.autograd.backward(loss, one)
 
     def _fwd_bwd(self, x, y):
         with self.engine.step_context():
             out, loss, pred = self.forward_loss(self.model, x, y)
-            loss.backward()
+            self._backward(loss)
         return out, loss, pred
 
     def _eager(self, x, y):
@@ -87,19 +103,51 @@ class TrainStep:
         self.last_out, self.last_loss, self.last_pred = out.detach(), loss.detach(), pred
         return loss
 
-    def _capture(self, x, y):
-        sx = torch.empty_like(x)
+    def _static_inputs(self, x, y):
+        # bf16 static input when the model takes it: the step prologue converts while copying
+        # (bit-identical: the GEMMs round their operands to bf16 while staging anyway)
+        bf = (x.dtype == torch.float32 and getattr(self.model, "accepts_bf16_input", False)
+              and x.numel() % 8 == 0 and y.dtype == torch.int64 and self.flat.grad.numel() % 4 == 0)
+        sx = torch.empty_like(x, dtype=torch.bfloat16 if bf else x.dtype)
         sy = torch.empty_like(y)
-        sx.copy_(x)
-        sy.copy_(y)
+        self._bf16_in = bf
+        return sx, sy
+
+    def _feed(self, x, y, sx, sy):
+        """Before a replay, in ONE launch when possible: inputs into the static buffers and the
+        gradient buffer zeroed (the graphs no longer contain the zeroing)."""
+        if self._bf16_in:
+            ops.step_prologue(x, sx, y, sy, self.flat.grad)
+            return
+        if sx.data_ptr() != x.data_ptr():
+            sx.copy_(x, non_blocking=True)
+        if y.dtype == torch.int64 and self.flat.grad.numel() % 4 == 0:
+            ops.step_prologue(x, None, y, sy, self.flat.grad)
+        else:
+            if sy.data_ptr() != y.data_ptr():
+                sy.copy_(y, non_blocking=True)
+            self.flat.grad.zero_()
+
+    def _graph_opt_ok(self) -> bool:
+        # the optimizer joins the graph when no collective sits between backward and update
+        return (not self.engine.group.distributed and isinstance(self.opt, ops.FusedAdam)
+                and self.flat.data.is_cuda)
+
+    def _capture(self, x, y):
+        sx, sy = self._static_inputs(x, y)
         g = torch.cuda.CUDAGraph()
         prev = getattr(self.engine, "sync_enabled", None)
         if prev is not None:
             self.engine.sync_enabled = False  # no collectives inside the captured region
+        self.graph_opt = self._graph_opt_ok()
+        if self.graph_opt:
+            self.opt.sync_device_step()
+            self._cap_lr = self.opt.lr
         try:
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-                self.flat.grad.zero_()
                 out, loss, pred = self._fwd_bwd(sx, sy)
+                if self.graph_opt:
+                    self.opt.step_graphable(grad_scale=self.engine.reduce())
         finally:
             if prev is not None:
                 self.engine.sync_enabled = prev
@@ -107,20 +155,17 @@ class TrainStep:
         self.static = (sx, sy, out, loss, pred)
 
     def _capture_split(self, x, y):
-        sx = torch.empty_like(x)
-        sy = torch.empty_like(y)
-        sx.copy_(x)
-        sy.copy_(y)
+        sx, sy = self._static_inputs(x, y)
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         self.engine.sync_enabled = False
+        self.graph_opt = False
         try:
             with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
-                self.flat.grad.zero_()
                 with self.engine.step_context():
                     h = self.model.stem(sx)
                     hd = h.detach().requires_grad_(h.requires_grad)
                     out, loss, pred = self.model.body_loss(hd, sy)
-                    loss.backward()
+                    self._backward(loss)
             with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):
                 if h.requires_grad:
                     torch.autograd.backward(h, hd.grad)
@@ -134,6 +179,8 @@ class TrainStep:
         self.calls += 1
         if not self.use_graph:
             return self._eager(x, y)
+        if self.graph is not None and self.graph_opt and self.opt.lr != self._cap_lr:
+            self.graph = None  # the learning rate is baked into the captured update
         if self.graph is None:
             if self.calls <= self.eager_warmup:
                 s = torch.cuda.Stream()
@@ -146,11 +193,9 @@ class TrainStep:
         sx, sy, out, loss, pred = self.static
         if sx.shape != x.shape or sy.shape != y.shape:  # e.g. a ragged last batch
             return self._eager(x, y)
-        if sx.data_ptr() != x.data_ptr():
-            sx.copy_(x, non_blocking=True)
-            sy.copy_(y, non_blocking=True)
         T = self.timers
         with T.phase("fwd_bwd"):
+            self._feed(x, y, sx, sy)
             self.graph.replay()
             if self.graph_b is not None:
                 for b in self._first_buckets:  # all-reduce under the stem backward
@@ -158,9 +203,12 @@ class TrainStep:
                 self.graph_b.replay()
         if hasattr(self.engine, "sync_enabled"):
             self.engine.sync_enabled = True
-        with T.phase("reduce"):
-            scale = self.engine.reduce()
-        with T.phase("optim"):
-            self.opt.step(grad_scale=scale)
+        if self.graph_opt:
+            self.opt.step_count += 1  # the replay ran the update
+        else:
+            with T.phase("reduce"):
+                scale = self.engine.reduce()
+            with T.phase("optim"):
+                self.opt.step(grad_scale=scale)
         self.last_out, self.last_loss, self.last_pred = out, loss, pred
         return loss

@@ -142,3 +142,21 @@ def test_lowrank_engines_train_on_gpu(engine):
     losses = _run(step, xs, ys)
     assert all(l == l for l in losses)
     assert not torch.equal(before, flat.data)
+
+
+def test_in_graph_adam_tracks_host_step_count_and_lr_change():
+    """Single site: the fused Adam is captured in the graph with a device step counter; the
+    host count stays in sync and a learning-rate change forces a re-capture."""
+    xs, ys = _batches()
+    _, fe, se = _trainer(0, use_graph=False)
+    _, fg, sg = _trainer(0, use_graph=True)
+    _run(se, xs, ys)
+    _run(sg, xs, ys)
+    assert sg.graph_opt and sg.opt.step_count == se.opt.step_count == xs.shape[0]
+    assert int(sg.opt._tdev.item()) == sg.opt.step_count
+    assert torch.allclose(fe.data, fg.data, rtol=1e-5, atol=1e-6)
+    se.opt.lr = sg.opt.lr = 5e-4
+    _run(se, xs, ys)
+    _run(sg, xs, ys)
+    assert sg._cap_lr == 5e-4
+    assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5)
