@@ -511,18 +511,19 @@ __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
                                  float* __restrict__ bias_p,  // [ndir*4HD]
                                  bf16* __restrict__ whh_p,    // [ndir][4HD][HD]
                                  bf16* __restrict__ whhT_p) { // [ndir][HD][4HD]
-  const long GP = 4L * HD;
-  const long n_wih = ndir * GP * I, n_b = ndir * GP, n_whh = ndir * GP * HD;
-  const long total = n_wih + n_b + 2 * n_whh;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
+  // 32-bit index math throughout (every extent < 2^31): 64-bit div/mod per element made this
+  // ~1M-element repack a 6 us kernel at the head of every step
+  const int GP = 4 * HD;
+  const int n_wih = ndir * GP * I, n_b = ndir * GP, n_whh = ndir * GP * HD;
+  const int total = n_wih + n_b + 2 * n_whh;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     if (idx < n_wih) {
-      const long k = idx % I, r = idx / I;
-      const int d = (int)(r / GP), m = (int)(r % GP), u = m >> 2, g = m & 3;
-      wih_p[idx] = (bf16)(u < Hd ? p.wih[d][((long)g * Hd + u) * I + k] : 0.f);
+      const int r = idx / I, k = idx - r * I;
+      const int d = r / GP, m = r - d * GP, u = m >> 2, g = m & 3;
+      wih_p[idx] = (bf16)(u < Hd ? p.wih[d][(g * Hd + u) * I + k] : 0.f);
     } else if (idx < n_wih + n_b) {
-      const long r = idx - n_wih;
-      const int d = (int)(r / GP), m = (int)(r % GP), u = m >> 2, g = m & 3;
+      const int r = idx - n_wih;
+      const int d = r / GP, m = r - d * GP, u = m >> 2, g = m & 3;
       float v = 0.f;
       if (u < Hd) {
         if (p.bih[d]) v += p.bih[d][g * Hd + u];
@@ -530,17 +531,15 @@ __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
       }
       bias_p[r] = v;
     } else if (idx < n_wih + n_b + n_whh) {
-      const long r = idx - n_wih - n_b;  // [d][m][k]
-      const int k = (int)(r % HD);
-      const long dm = r / HD;
-      const int d = (int)(dm / GP), m = (int)(dm % GP), u = m >> 2, g = m & 3;
-      whh_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][((long)g * Hd + u) * Hd + k] : 0.f);
+      const int r = idx - n_wih - n_b;  // [d][m][k]
+      const int dm = r / HD, k = r - dm * HD;
+      const int d = dm / GP, m = dm - d * GP, u = m >> 2, g = m & 3;
+      whh_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][(g * Hd + u) * Hd + k] : 0.f);
     } else {
-      const long r = idx - n_wih - n_b - n_whh;  // [d][k][m]
-      const int m = (int)(r % GP);
-      const long dk = r / GP;
-      const int d = (int)(dk / HD), k = (int)(dk % HD), u = m >> 2, g = m & 3;
-      whhT_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][((long)g * Hd + u) * Hd + k] : 0.f);
+      const int r = idx - n_wih - n_b - n_whh;  // [d][k][m]
+      const int dk = r / GP, m = r - dk * GP;
+      const int d = dk / HD, k = dk - d * HD, u = m >> 2, g = m & 3;
+      whhT_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][(g * Hd + u) * Hd + k] : 0.f);
     }
   }
 }

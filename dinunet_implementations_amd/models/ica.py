@@ -72,11 +72,12 @@ class LSTM(nn.Module):
                 and ops.lstm_supported(x.shape[0], self.input_size, self.hidden_size,
                                        self.num_direction))
 
-    def prepack(self, device):
-        """Start packing the recurrent weights on the side stream (overlaps the encoder)."""
+    def prepack(self, device, side: bool = True):
+        """Pack the LSTM weights into the kernel layouts ahead of the forward (on the side
+        stream when ``side``)."""
         from ..ops.lstm import pack_params
         flat = [t for cell in self.lstms for t in cell.params()]
-        return pack_params(flat, self.input_size, device, side=True)
+        return pack_params(flat, self.input_size, device, side=side)
 
     def forward(self, x: torch.Tensor, h=None, reduce: str = "none", packed=None):
         """``reduce='none'`` returns ``(hidden_seq [B,S,H*dirs], (h, c))`` like the reference;
@@ -162,7 +163,9 @@ class ICALstm(nn.Module):
             x = x.float()  # host datasets are float64 (reference comps/icalstm/__init__.py:29)
         self._packed = None
         if self.use_fused and x.is_cuda and self.lstm.fused_ok(x) and ops.capture.active() is None:
-            self._packed = self.lstm.prepack(x.device)  # side stream, beside the encoder GEMM
+            # in-stream: as a side-stream branch of the step graph the pack saved nothing (it
+            # fills the chip anyway) and added a cross-queue wait before the input projection
+            self._packed = self.lstm.prepack(x.device, side=False)
         return self.encode(x)
 
     def stem_parameters(self):
