@@ -368,7 +368,7 @@ head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
 #pragma unroll
       for (int u = 0; u < R; ++u) {
         const int c = base + u * NT;
-        if (c >= nch) break;
+        if (c >= nch) continue;  // (not break: keeps the loop unrolled and v[] in VGPRs)
         const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
         bf16x4 o;
 #pragma unroll
