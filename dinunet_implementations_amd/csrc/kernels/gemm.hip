@@ -285,8 +285,15 @@ gemm_kernel(GemmGroup g) {
   const int kbeg = blockIdx.z * P.kchunk;
   const int kend = min(K, kbeg + P.kchunk);
 
-  typename StagerSel<VEC, BM, !TA, TAe>::type sa;
-  typename StagerSel<VEC, BN, TB, TBe>::type sb;
+  // Two register stages + two LDS buffers: tile it+2's global loads are issued at the top of
+  // iteration it and land during two tiles' MFMAs (not one); the barriers are raw s_barrier +
+  // lgkmcnt(0) (a __syncthreads would drain vmcnt and kill the loads in flight).  The loop is
+  // unrolled by two so every stage index is a compile-time constant (no register-array
+  // indexing -> no scratch).
+  typedef typename StagerSel<VEC, BM, !TA, TAe>::type SA;
+  typedef typename StagerSel<VEC, BN, TB, TBe>::type SB;
+  SA sa0, sa1;
+  SB sb0, sb1;
   f32x4 acc[T::FM][T::FN];
 #pragma unroll
   for (int i = 0; i < T::FM; ++i)
@@ -294,38 +301,53 @@ gemm_kernel(GemmGroup g) {
     for (int j = 0; j < T::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = kend > kbeg ? (kend - kbeg + T::BK - 1) / T::BK : 0;
+  sa0.load(A, lda, row0, kbeg, M, kend, tid);
+  sb0.load(B, ldb, col0, kbeg, N, kend, tid);
+  sa1.load(A, lda, row0, kbeg + T::BK, M, kend, tid);
+  sb1.load(B, ldb, col0, kbeg + T::BK, N, kend, tid);
   if (nk > 0) {
-    sa.load(A, lda, row0, kbeg, M, kend, tid);
-    sb.load(B, ldb, col0, kbeg, N, kend, tid);
-    sa.store(As(0), tid);
-    sb.store(Bs(0), tid);
+    sa0.store(As(0), tid);
+    sb0.store(Bs(0), tid);
   }
-  __syncthreads();
-  for (int it = 0; it < nk; ++it) {
-    const int cur = it & 1;
-    const bool more = it + 1 < nk;
-    if (more) {  // next tile's global loads fly under this tile's MFMAs
-      const int k0 = kbeg + (it + 1) * T::BK;
-      sa.load(A, lda, row0, k0, M, kend, tid);
-      sb.load(B, ldb, col0, k0, N, kend, tid);
-    }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  auto mfma_tile = [&](const bf16* as, const bf16* bs) {
 #pragma unroll
     for (int ks = 0; ks < T::BK / 32; ++ks) {
       bf16x8 af[T::FM], bfr[T::FN];
 #pragma unroll
-      for (int i = 0; i < T::FM; ++i) af[i] = frag<BM, !TA>(As(cur), wm * T::WM + 16 * i, ks, lane);
+      for (int i = 0; i < T::FM; ++i) af[i] = frag<BM, !TA>(as, wm * T::WM + 16 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < T::FN; ++j) bfr[j] = frag<BN, TB>(Bs(cur), wn * T::WN + 16 * j, ks, lane);
+      for (int j = 0; j < T::FN; ++j) bfr[j] = frag<BN, TB>(bs, wn * T::WN + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < T::FM; ++i)
 #pragma unroll
         for (int j = 0; j < T::FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (more) {
-      sa.store(As(cur ^ 1), tid);
-      sb.store(Bs(cur ^ 1), tid);
+  };
+  // The refill loads are UNCONDITIONAL (past kend they read clamped addresses and are zeroed
+  // / never stored): conditional loads make the compiler's wait counting merge paths and emit
+  // vmcnt(0), which would wait for the tile just issued.
+  for (int it = 0; it < nk; it += 2) {
+    // even tile it: LDS buffer 0, its registers (stage 0) refill with tile it+2
+    sa0.load(A, lda, row0, kbeg + (it + 2) * T::BK, M, kend, tid);
+    sb0.load(B, ldb, col0, kbeg + (it + 2) * T::BK, N, kend, tid);
+    mfma_tile(As(0), Bs(0));
+    if (it + 1 < nk) {
+      sa1.store(As(1), tid);
+      sb1.store(Bs(1), tid);
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (it + 1 >= nk) break;
+    // odd tile it+1: LDS buffer 1, stage 1 refills with tile it+3
+    sa1.load(A, lda, row0, kbeg + (it + 3) * T::BK, M, kend, tid);
+    sb1.load(B, ldb, col0, kbeg + (it + 3) * T::BK, N, kend, tid);
+    mfma_tile(As(1), Bs(1));
+    if (it + 2 < nk) {
+      sa0.store(As(0), tid);
+      sb0.store(Bs(0), tid);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
 #undef As
