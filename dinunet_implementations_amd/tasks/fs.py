@@ -16,6 +16,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import torch
 
 from .. import ops
+from ..data import native
 from ..data.base import SiteDataHandle, SiteDataset
 from ..models import MSANNet
 from ..runtime.trainer import NNTrainer
@@ -73,8 +74,17 @@ class FreeSurferDataset(SiteDataset):
         return {"inputs": x, "labels": torch.tensor(y), "ix": torch.tensor(ix)}
 
     def materialize(self, device=None):
-        X = torch.stack([self[i]["inputs"].float() for i in range(len(self))]) if self.indices \
-            else torch.zeros(0, int(self.cache.get("input_size", 66)))
+        nfeat = int(self.cache.get("input_size", 66))
+        X = None
+        if self.indices:
+            # C++ host runtime: every file parsed + max-normalised in parallel (data/native.py)
+            arr = native.fs_load([os.path.join(self.path(), f) for f, _ in self.indices], nfeat)
+            if arr is not None:
+                X = torch.from_numpy(arr)
+            else:
+                X = torch.stack([self[i]["inputs"].float() for i in range(len(self))])
+        else:
+            X = torch.zeros(0, nfeat)
         y = torch.tensor([int(v[1]) for v in self.indices], dtype=torch.long)
         return (X.to(device), y.to(device)) if device is not None else (X, y)
 

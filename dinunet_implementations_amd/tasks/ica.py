@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..data import native
 from ..data.base import SiteDataHandle, SiteDataset
 from ..models import ICALstm
 from ..ops.reference import ica_windows
@@ -55,13 +56,21 @@ class ICADataset(SiteDataset):
             if shared is not None:
                 self.data = shared
             else:
-                raw = torch.from_numpy(np.ascontiguousarray(load_array(self.path(cache_key="data_file")),
-                                                            dtype=np.float32))
+                raw = load_array(self.path(cache_key="data_file"))
                 comps = self.cache.get("components_file")
                 if comps and os.path.exists(os.path.join(self.state.get("baseDirectory", "."), comps)):
                     sel = read_lines(os.path.join(self.state.get("baseDirectory", "."), comps))
-                    raw = raw[:, torch.as_tensor(sel, dtype=torch.long)]
-                self.data = ica_windows(raw, self.window_size, self.window_stride, self.temporal_size)
+                    raw = raw[:, np.asarray(sel, dtype=np.int64)]
+                # C++ host runtime windows straight from fp32 / fp64 (data/native.py); the torch
+                # reference (ops.reference.ica_windows) is the fallback and the test oracle
+                win = native.ica_windows(raw, self.window_size, self.window_stride,
+                                         self.temporal_size)
+                if win is not None:
+                    self.data = torch.from_numpy(win)
+                else:
+                    raw = torch.from_numpy(np.ascontiguousarray(raw, dtype=np.float32))
+                    self.data = ica_windows(raw, self.window_size, self.window_stride,
+                                            self.temporal_size)
                 self.cache["_ica_windows_cache"] = self.data
         self.indices += [[int(a), int(b)] for a, b in files]
 

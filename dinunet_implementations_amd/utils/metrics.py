@@ -73,7 +73,15 @@ class Averages:
 
 
 def roc_auc(scores: np.ndarray, labels: np.ndarray) -> float:
-    """Exact ROC-AUC (Mann-Whitney U with average ranks for ties).  0.5 if one class is absent."""
+    """Exact ROC-AUC (Mann-Whitney U with average ranks for ties).  0.5 if one class is absent.
+    Runs in the C++ host library when built (``data/native.py``); this Python body is the
+    fallback and the test oracle (:func:`roc_auc_py`)."""
+    from ..data import native
+    v = native.roc_auc(scores, labels)
+    return v if v is not None else roc_auc_py(scores, labels)
+
+
+def roc_auc_py(scores: np.ndarray, labels: np.ndarray) -> float:
     scores = np.asarray(scores, dtype=np.float64).ravel()
     labels = np.asarray(labels).ravel().astype(np.int64)
     pos = labels == 1
