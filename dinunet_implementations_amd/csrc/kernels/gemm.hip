@@ -256,9 +256,11 @@ __global__ void __launch_bounds__(256)
 gemm_kernel(GemmGroup g) {
   typedef GemmTile<BM, BN, TA, TB> T;
   // one LDS array (A images then B images, double-buffered)
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (T::IA::ELEMS + T::IB::ELEMS)];
-#define As(b) (smem + (b) * T::IA::ELEMS)
-#define Bs(b) (smem + 2 * T::IA::ELEMS + (b) * T::IB::ELEMS)
+  // ONE LDS tile (the next tiles wait in registers): 18 KB per 64x64 workgroup, so ~7
+  // workgroups share a CU and hide each other's load / store latency
+  __shared__ __attribute__((aligned(16))) bf16 smem[T::IA::ELEMS + T::IB::ELEMS];
+#define As (smem)
+#define Bs (smem + T::IA::ELEMS)
 
   // XCD-aware tile order: the hardware deals workgroups round-robin over the 8 XCDs (blocks b
   // and b+8 share one L2), so give every XCD a CONTIGUOUS run of row-major tiles -- the tiles
@@ -306,47 +308,45 @@ gemm_kernel(GemmGroup g) {
   sa1.load(A, lda, row0, kbeg + T::BK, M, kend, tid);
   sb1.load(B, ldb, col0, kbeg + T::BK, N, kend, tid);
   if (nk > 0) {
-    sa0.store(As(0), tid);
-    sb0.store(Bs(0), tid);
+    sa0.store(As, tid);
+    sb0.store(Bs, tid);
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
-  auto mfma_tile = [&](const bf16* as, const bf16* bs) {
+  auto mfma_tile = [&]() {
 #pragma unroll
     for (int ks = 0; ks < T::BK / 32; ++ks) {
       bf16x8 af[T::FM], bfr[T::FN];
 #pragma unroll
-      for (int i = 0; i < T::FM; ++i) af[i] = frag<BM, !TA>(as, wm * T::WM + 16 * i, ks, lane);
+      for (int i = 0; i < T::FM; ++i) af[i] = frag<BM, !TA>(As, wm * T::WM + 16 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < T::FN; ++j) bfr[j] = frag<BN, TB>(bs, wn * T::WN + 16 * j, ks, lane);
+      for (int j = 0; j < T::FN; ++j) bfr[j] = frag<BN, TB>(Bs, wn * T::WN + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < T::FM; ++i)
 #pragma unroll
         for (int j = 0; j < T::FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
   };
-  // The refill loads are UNCONDITIONAL (past kend they read clamped addresses and are zeroed
-  // / never stored): conditional loads make the compiler's wait counting merge paths and emit
-  // vmcnt(0), which would wait for the tile just issued.
+  // Per tile: refill loads (tile it+2) -> MFMAs on the LDS tile -> barrier -> tile it+1 from
+  // registers into LDS -> barrier.  The refill loads are UNCONDITIONAL (past kend they read
+  // clamped addresses and are zeroed / never stored): conditional loads make the compiler's
+  // wait counting merge paths and emit vmcnt(0), which would wait for the tile just issued.
   for (int it = 0; it < nk; it += 2) {
-    // even tile it: LDS buffer 0, its registers (stage 0) refill with tile it+2
     sa0.load(A, lda, row0, kbeg + (it + 2) * T::BK, M, kend, tid);
     sb0.load(B, ldb, col0, kbeg + (it + 2) * T::BK, N, kend, tid);
-    mfma_tile(As(0), Bs(0));
-    if (it + 1 < nk) {
-      sa1.store(As(1), tid);
-      sb1.store(Bs(1), tid);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    mfma_tile();
     if (it + 1 >= nk) break;
-    // odd tile it+1: LDS buffer 1, stage 1 refills with tile it+3
+    asm volatile("s_barrier" ::: "memory");
+    sa1.store(As, tid);
+    sb1.store(Bs, tid);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     sa1.load(A, lda, row0, kbeg + (it + 3) * T::BK, M, kend, tid);
     sb1.load(B, ldb, col0, kbeg + (it + 3) * T::BK, N, kend, tid);
-    mfma_tile(As(1), Bs(1));
-    if (it + 2 < nk) {
-      sa0.store(As(0), tid);
-      sb0.store(Bs(0), tid);
-    }
+    mfma_tile();
+    if (it + 2 >= nk) break;
+    asm volatile("s_barrier" ::: "memory");
+    sa0.store(As, tid);
+    sb0.store(Bs, tid);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 

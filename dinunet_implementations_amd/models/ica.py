@@ -16,6 +16,7 @@ launch per direction (``ops.head``).  On CPU the module runs the reference math
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -23,6 +24,8 @@ import torch.nn as nn
 
 from .. import ops
 from ..ops import reference as ref
+
+_FUSED_ENCPROJ = os.environ.get("DINUNET_FUSED_ENCPROJ", "0") == "1"
 
 
 class LSTMCell(nn.Module):
@@ -79,13 +82,14 @@ class LSTM(nn.Module):
         flat = [t for cell in self.lstms for t in cell.params()]
         return pack_params(flat, self.input_size, device, side=side)
 
-    def forward(self, x: torch.Tensor, h=None, reduce: str = "none", packed=None):
+    def forward(self, x: torch.Tensor, h=None, reduce: str = "none", packed=None, xp=None):
         """``reduce='none'`` returns ``(hidden_seq [B,S,H*dirs], (h, c))`` like the reference;
         ``reduce='mean'`` returns the temporal mean ``[B, H*dirs]`` instead of the sequence
         (what ``ICALstm`` consumes) so the fused kernel never materialises the sequence."""
         if h is None and self.fused_ok(x):
             params = [cell.params() for cell in self.lstms]
-            return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms), packed=packed)
+            return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms), packed=packed,
+                              xp=xp)
         if h is not None:
             hs, (h_t, c_t) = self.lstms[0](x, h)
             if self.bidirectional:
@@ -162,10 +166,22 @@ class ICALstm(nn.Module):
         if x.dtype not in (torch.float32, torch.bfloat16):
             x = x.float()  # host datasets are float64 (reference comps/icalstm/__init__.py:29)
         self._packed = None
+        self._xp = None
         if self.use_fused and x.is_cuda and self.lstm.fused_ok(x) and ops.capture.active() is None:
             # in-stream: as a side-stream branch of the step graph the pack saved nothing (it
             # fills the chip anyway) and added a cross-queue wait before the input projection
             self._packed = self.lstm.prepack(x.device, side=False)
+            B, S = x.shape[:2]
+            flat = x.reshape(B * S, -1)
+            lin = self.encoder[0]
+            wih_p = self._packed[0]
+            if _FUSED_ENCPROJ and ops.enc_proj_supported(flat, lin.weight, lin.bias, wih_p):
+                # encoder + LSTM input projection in ONE launch (csrc/kernels/encproj.hip);
+                # opt-in: measured 63 us vs 38 us for the two GEMM launches at B=32 (49
+                # row-chunk workgroups each stream all weights: per-CU bandwidth bound)
+                enc, self._xp = ops.encoder_projection(flat, lin.weight, lin.bias, wih_p,
+                                                       module=lin)
+                return enc.view(B, S, -1)
         return self.encode(x)
 
     def stem_parameters(self):
@@ -174,7 +190,8 @@ class ICALstm(nn.Module):
     def body_loss(self, enc: torch.Tensor, y: torch.Tensor):
         """Second half of :meth:`forward_loss`: bi-LSTM, classifier, softmax-CE on ``enc``."""
         packed, self._packed = getattr(self, "_packed", None), None
-        o, _ = self.lstm(enc, reduce="mean", packed=packed)
+        xp, self._xp = getattr(self, "_xp", None), None
+        o, _ = self.lstm(enc, reduce="mean", packed=packed, xp=xp)
         o = o.flatten(1).to(self.classifier[1].weight.dtype)
         if self.use_fused and o.is_cuda:
             return ops.head_loss(o, self.head_spec(), y, log_out=False)

@@ -79,7 +79,7 @@ def _row_map(Hd: int, HD: int, device) -> Tensor:
 
 class _BiLSTMFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, enc: Tensor, mode: str, modules, packed, *params: Tensor):
+    def forward(ctx, enc: Tensor, mode: str, modules, packed, xp_pre, *params: Tensor):
         ctx.set_materialize_grads(False)  # unused hT / cT -> None (no zero tensors, no syncs)
         B, S, I = enc.shape
         ndir = len(params) // 4
@@ -99,7 +99,12 @@ class _BiLSTMFn(torch.autograd.Function):
         if x2d.dtype != torch.bfloat16:
             x2d = x2d.to(torch.bfloat16)
         x2d = x2d.contiguous()
-        xp = mm(x2d, wih_p, trans_b=True, out_dtype=torch.float32)       # [B*S, ndir*GP]
+        if xp_pre is not None:  # projected together with the encoder (ops.encoder_projection)
+            if xp_pre.shape != (B * S, ndir * GP) or xp_pre.dtype != torch.float32:
+                raise ValueError("precomputed LSTM input projection has the wrong shape/dtype")
+            xp = xp_pre
+        else:
+            xp = mm(x2d, wih_p, trans_b=True, out_dtype=torch.float32)   # [B*S, ndir*GP]
         c_save = torch.empty(ndir, Bp, S, HD, dtype=torch.float32, device=dev)
         hprev = torch.empty(ndir, Bp, S, HD, dtype=torch.bfloat16, device=dev)
         hT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
@@ -181,7 +186,7 @@ class _BiLSTMFn(torch.autograd.Function):
             for d, cell in enumerate(ctx.modules):
                 _cap.record(cell.i2h, x2d, dref[:, d])
                 _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
-        return (dx, None, None, None) + (None,) * len(params)
+        return (dx, None, None, None, None) + (None,) * len(params)
 
 
 def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = False):
@@ -250,12 +255,13 @@ def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
 
 
 def bilstm(x: Tensor, params: Sequence[Tuple[Tensor, Tensor, Tensor, Tensor]],
-           reduce: str = "none", modules=None, packed=None):
+           reduce: str = "none", modules=None, packed=None, xp: Optional[Tensor] = None):
     """Fused bi-LSTM: returns ``(hmean [B, ndir*Hd] | hseq [B, S, ndir*Hd], (hT, cT))``."""
     if not _lib.native_available():
         raise RuntimeError("fused LSTM requested but the gfx950 kernel library is not built")
     flat: List[Tensor] = []
     for p in params:
         flat.extend(p)
-    out, hT, cT = _BiLSTMFn.apply(x, "mean" if reduce == "mean" else "seq", modules, packed, *flat)
+    out, hT, cT = _BiLSTMFn.apply(x, "mean" if reduce == "mean" else "seq", modules, packed, xp,
+                                  *flat)
     return out, (hT, cT)

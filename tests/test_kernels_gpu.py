@@ -227,3 +227,53 @@ def test_gemm_grouped_matches_per_problem(splits):
     mm_grouped(probs, trans_a=True, splits=splits)
     for q, ref in zip(probs, refs):
         assert rel(q["out"], ref) < 2e-3
+
+
+@pytest.mark.parametrize("N,KX,N2", [(3136, 1000, 1536), (200, 64, 512), (70, 1000, 1024)])
+def test_encoder_projection_fused_matches_two_gemms(N, KX, N2):
+    """csrc/kernels/encproj.hip: enc = relu(X We^T + be), xp = enc Wp^T in one launch, against
+    the fp32 reference of the same bf16-rounded operands (ragged row tails included)."""
+    from dinunet_implementations_amd.ops import encoder_projection
+    x = torch.randn(N, KX, device=DEV).to(torch.bfloat16)
+    w = torch.randn(256, KX, device=DEV) / KX ** 0.5
+    b = torch.randn(256, device=DEV) * 0.1
+    wp = (torch.randn(N2, 256, device=DEV) / 16).to(torch.bfloat16)
+    enc, xp = encoder_projection(x, w, b, wp)
+    ref_enc = torch.relu(x.float() @ bf(w).t() + b)
+    assert rel(enc, ref_enc) < 1e-2
+    ref_xp = enc.float() @ wp.float().t()  # phase 2 consumes the bf16 enc tile
+    assert rel(xp, ref_xp) < 2e-3
+
+
+def test_ica_step_with_fused_encoder_projection_matches_unfused():
+    """ICALstm at input_size 256 with a bf16 batch takes the fused encoder+projection launch;
+    loss and every gradient match the two-GEMM path (same bf16 operand rounding)."""
+    from dinunet_implementations_amd.models import ICALstm
+    from dinunet_implementations_amd.models import ica as ica_mod
+    from dinunet_implementations_amd.ops import linear as lin_mod
+    ica_mod._FUSED_ENCPROJ = True  # opt-in path (see models/ica.py)
+    torch.manual_seed(0)
+    m = ICALstm(input_size=256, hidden_size=128, num_comps=20, window_size=10).to(DEV).train()
+    m.classifier[0].p = 0.0
+    x = torch.randn(8, 12, 20, 10, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 2, (8,), device=DEV)
+    grads = []
+    for fused in (True, False):
+        for p in m.parameters():
+            p.grad = None
+        orig = lin_mod.enc_proj_supported
+        if not fused:
+            import dinunet_implementations_amd.ops as ops_pkg
+            ops_pkg.enc_proj_supported = lambda *a, **k: False
+        try:
+            _, loss, _ = m.forward_loss(x, y)
+            loss.backward()
+        finally:
+            import dinunet_implementations_amd.ops as ops_pkg
+            ops_pkg.enc_proj_supported = orig
+        grads.append((float(loss), [p.grad.clone() for p in m.parameters()]))
+    ica_mod._FUSED_ENCPROJ = False
+    (l1, g1), (l2, g2) = grads
+    assert abs(l1 - l2) < 1e-3
+    for a, b in zip(g1, g2):
+        assert rel(a, b) < 2e-2
