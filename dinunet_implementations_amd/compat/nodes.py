@@ -84,8 +84,10 @@ class LocalNode:
         self.data = self._datasets(self.splits[fold])
         self.trainer = self.Trainer(cache=self.cfg, state=self.state, device=self.device)
         self.trainer.init_nn(seed=seed)
+        # the file transport ships rank-dAD's structured (A, Delta) factors: keep that path
         self.engine = ENGINES[str(cfg.get("agg_engine", "dSGD"))](
-            self.trainer.modules(), self.trainer.flat, SiteGroup(device=self.device), cfg)
+            self.trainer.modules(), self.trainer.flat, SiteGroup(device=self.device),
+            dict(cfg, dad_gradient_space=False))
         bs = int(cfg.get("batch_size", 16))
         dl = (cfg.get("dataloader_args") or {}).get("train", {})
         Xtr = self.data["train"][0]

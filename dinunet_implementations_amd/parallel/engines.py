@@ -29,10 +29,12 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import _grad as _gradreg
+from ..ops import _lib
 from ..ops import capture as _cap
 from ..ops.optim import FlatParams, cast_bf16_to_f32, cast_f32_to_bf16
 from .group import SiteGroup
-from .lowrank import dad_factors, orthonormalize_
+from .lowrank import EPS as EPS_MGS
+from .lowrank import _mgs_torch_, dad_factors, orthonormalize_
 
 Tensor = torch.Tensor
 
@@ -248,8 +250,139 @@ class RankDADEngine(Engine):
         self.dense_segs = [(o, n) for p, o, n in flat.segments() if id(p) not in self._weight_ids]
         self._cap: Optional[_cap.DADCapture] = None
         self._gen = None
+        # GPU: factorise in GRADIENT space.  The fused kernels already produce each site's
+        # G_s = Delta_s^T A_s in the flat grad buffer, and the structured iteration
+        # P <- orth(Delta^T (A Q)), Q <- A^T (Delta P) is exactly the power iteration on G_s:
+        # running it on G_s ([out, in], a few hundred KB) instead of the [B*S, .] activation /
+        # delta factors gives the same factors without capturing them, with no host sync (the
+        # dad_tol early stop is a device-side mask), so it is captured in the step's HIP graph.
+        self.fast = bool(flat.data.is_cuda and self.cfg.get("dad_gradient_space", True))
+        if self.fast:
+            self._init_fast()
+
+    # ---- gradient-space path ---------------------------------------------------------------
+    def _init_fast(self):
+        """Device tables for the batched power-iteration kernels (csrc/kernels/lowrank.hip)."""
+        import ctypes
+        segs = {id(p): o for p, o, _ in self.flat.segments()}
+        dev = self.flat.data.device
+        gen = torch.Generator(device="cpu").manual_seed(int(self.cfg.get("seed", 0)) + 777)
+        r = max(1, min(self.rank, 16))
+        self.fast_layers = []  # (module, flat offset, out, in, r, send offset of P, of Q)
+        off = 0
+        for m in self.linears:
+            out_f, in_f = m.weight.shape
+            if self.rank >= min(out_f, in_f):
+                continue  # exact mode: the dense mean of G (== sum_s Delta_s^T A_s / W)
+            self.fast_layers.append((m, segs[id(m.weight)], out_f, in_f, r, off, off + out_f * r))
+            off += (out_f + in_f) * r
+        low = {id(l[0].weight) for l in self.fast_layers}
+        self.fast_dense = [(o, n) for p, o, n in self.flat.segments() if id(p) not in low]
+        self._send = torch.zeros(max(off, 1), dtype=torch.float32, device=dev)
+        n = len(self.fast_layers)
+        if not n:
+            return
+        W = self.group.world
+        self._gathered = (torch.zeros(W * self._send.numel(), dtype=torch.float32, device=dev)
+                          if self.group.distributed else self._send)
+        self._pc, self._qc, self._q = [], [], []
+        lib = _lib.lib()
+        self._splits = int(lib.dn_pi_splits())  # row-split partials of G^T P per layer
+        for _, _, out_f, in_f, rr, _, _ in self.fast_layers:
+            q = torch.randn(in_f, rr, generator=gen)  # identical on every site (same seed)
+            _mgs_torch_(q)
+            self._q.append(q.to(dev))
+            self._pc.append(torch.empty(out_f, rr, dtype=torch.float32, device=dev))
+            self._qc.append(torch.empty(self._splits, in_f, rr, dtype=torch.float32, device=dev))
+        self._active = torch.ones(n, dtype=torch.int32, device=dev)
+
+        class PiLayer(ctypes.Structure):
+            _fields_ = [(k, ctypes.c_void_p) for k in ("G", "Pc", "Q", "Qc", "Psend", "Qsend",
+                                                     "active")] + \
+                       [(k, ctypes.c_int) for k in ("out", "inn", "r", "row0", "col0")]
+
+        class PiRecon(ctypes.Structure):
+            _fields_ = [("G", ctypes.c_void_p), ("P", ctypes.c_void_p), ("Q", ctypes.c_void_p),
+                        ("out", ctypes.c_int), ("inn", ctypes.c_int), ("r", ctypes.c_int),
+                        ("start", ctypes.c_long)]
+        L = _lib.lib()
+        L.dn_pi_layer_size.restype = ctypes.c_long
+        L.dn_pi_recon_size.restype = ctypes.c_long
+        if ctypes.sizeof(PiLayer) != L.dn_pi_layer_size() or \
+                ctypes.sizeof(PiRecon) != L.dn_pi_recon_size():
+            raise RuntimeError("power-iteration table layout mismatch with the kernel library")
+        tab = (PiLayer * n)()
+        rec = (PiRecon * n)()
+        rows, cols, start = 0, 0, 0
+        row_starts, col_starts = [], []
+        G0 = self.flat.grad.data_ptr()
+        send0, gat0 = self._send.data_ptr(), self._gathered.data_ptr()
+        for i, (_, o, out_f, in_f, rr, po, qo) in enumerate(self.fast_layers):
+            t = tab[i]
+            t.G = G0 + 4 * o
+            t.Pc, t.Q, t.Qc = self._pc[i].data_ptr(), self._q[i].data_ptr(), self._qc[i].data_ptr()
+            t.Psend, t.Qsend = send0 + 4 * po, send0 + 4 * qo
+            t.active = self._active.data_ptr() + 4 * i
+            t.out, t.inn, t.r, t.row0, t.col0 = out_f, in_f, rr, rows, cols
+            row_starts.append(rows)
+            col_starts.append(cols)
+            rows += out_f
+            cols += (in_f + 63) // 64
+            c = rec[i]
+            c.G, c.P, c.Q = G0 + 4 * o, gat0 + 4 * po, gat0 + 4 * qo
+            c.out, c.inn, c.r, c.start = out_f, in_f, rr, start
+            start += out_f * in_f
+        self._rows, self._cols, self._recon_total = rows, cols, start
+
+        def dev_bytes(obj):
+            raw = bytes(obj)
+            return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+        self._tab = dev_bytes(tab)
+        self._rec = dev_bytes(rec)
+        self._row_starts = torch.tensor(row_starts, dtype=torch.int32).to(dev)
+        self._col_starts = torch.tensor(col_starts, dtype=torch.int32).to(dev)
+        self._mgs_ptrs = torch.tensor([t.data_ptr() for t in self._pc], dtype=torch.int64).to(dev)
+        self._mgs_dims = torch.tensor([[t.shape[0], t.shape[1], t.stride(0)] for t in self._pc],
+                                      dtype=torch.int32).to(dev)
+        self._act_ptrs = torch.tensor([self._active.data_ptr() + 4 * i for i in range(n)],
+                                      dtype=torch.int64).to(dev)
+
+    def pre_reduce(self):
+        """Local rank-r factors of every large Linear's gradient into the send buffer: one
+        ``dn_pi_iterate`` (4 launches, all layers) per power iteration, no host sync
+        (HIP-graph capturable)."""
+        if not self.fast or not self.fast_layers:
+            return
+        for it in range(max(1, self.iters)):
+            _lib.call("dn_pi_iterate", self._tab.data_ptr(), self._row_starts.data_ptr(),
+                      self._col_starts.data_ptr(), len(self.fast_layers), self._rows, self._cols,
+                      self._mgs_ptrs.data_ptr(), self._mgs_dims.data_ptr(),
+                      self._act_ptrs.data_ptr(), float(self.tol), int(it == 0), _lib.stream())
+
+    def _fast_reduce(self) -> float:
+        g = self.group
+        W = g.world
+        self.comm_bytes = 0
+        if g.distributed and self.fast_dense:
+            dense = torch.cat([self.flat.grad[o:o + n] for o, n in self.fast_dense])
+            self._allreduce_mean_(dense)
+            off = 0
+            for o, n in self.fast_dense:
+                self.flat.grad[o:o + n].copy_(dense[off:off + n])
+                off += n
+        if not self.fast_layers:
+            return 1.0
+        if g.distributed:
+            g.all_gather_into(self._gathered, self._send)
+            self.comm_bytes += self._send.numel() * 4
+        # every layer's G = [P_1..P_W][Q_1..Q_W]^T / W in one launch
+        _lib.call("dn_pi_reconstruct", self._rec.data_ptr(), len(self.fast_layers),
+                  self._recon_total, self._send.numel(), W if g.distributed else 1, _lib.stream())
+        return 1.0
 
     def step_context(self):
+        if self.fast:
+            return contextlib.nullcontext()
         self._cap = _cap.DADCapture(modules=self.linears)
         return self._cap
 
@@ -293,7 +426,12 @@ class RankDADEngine(Engine):
                 res.append((m, "lowrank", P, Q))
         return res
 
-    def reduce(self) -> float:
+    def reduce(self, factorized: bool = False) -> float:
+        """``factorized``: :meth:`pre_reduce` already ran (inside the captured step)."""
+        if self.fast:
+            if not factorized:
+                self.pre_reduce()
+            return self._fast_reduce()
         g = self.group
         self.comm_bytes = 0
         dense = self._dense_pack()

@@ -54,7 +54,11 @@ class TrainStep:
         self.opt = opt
         self.engine = engine
         self.forward_loss = forward_loss or HEADS[task]
-        self.use_graph = (use_graph and flat.data.is_cuda and engine.name == "dSGD")
+        # graph-capturable engines: dSGD, and rank-dAD in gradient space (its local
+        # factorisation joins the captured region via pre_reduce)
+        self.use_graph = (use_graph and flat.data.is_cuda
+                          and (engine.name == "dSGD" or getattr(engine, "fast", False)))
+        self._pre_reduce = getattr(engine, "pre_reduce", None) if engine.name != "dSGD" else None
         self.eager_warmup = eager_warmup
         self.calls = 0
         self.graph = None
@@ -65,7 +69,8 @@ class TrainStep:
         self.timers = timers if timers is not None else (PhaseTimer() if enabled_by_env() else NULL)
         # split capture: needs a stem/body model, the default loss, and sites to overlap with
         can_split = (self.use_graph and forward_loss is None and hasattr(model, "stem")
-                     and hasattr(model, "body_loss") and hasattr(model, "stem_parameters"))
+                     and hasattr(model, "body_loss") and hasattr(model, "stem_parameters")
+                     and hasattr(engine, "split_buckets"))
         if split is None:
             env = os.environ.get("DINUNET_SPLIT_GRAPH", "")
             split = can_split and (engine.group.distributed if env == "" else env == "1")
@@ -133,6 +138,11 @@ class TrainStep:
         return (not self.engine.group.distributed and isinstance(self.opt, ops.FusedAdam)
                 and self.flat.data.is_cuda)
 
+    def _reduce_after_replay(self):
+        if self._pre_reduce is not None:
+            return self.engine.reduce(factorized=True)
+        return self.engine.reduce()
+
     def _capture(self, x, y):
         sx, sy = self._static_inputs(x, y)
         g = torch.cuda.CUDAGraph()
@@ -146,8 +156,12 @@ class TrainStep:
         try:
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 out, loss, pred = self._fwd_bwd(sx, sy)
+                if self._pre_reduce is not None:
+                    self._pre_reduce()
                 if self.graph_opt:
-                    self.opt.step_graphable(grad_scale=self.engine.reduce())
+                    scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
+                             else self.engine.reduce())
+                    self.opt.step_graphable(grad_scale=scale)
         finally:
             if prev is not None:
                 self.engine.sync_enabled = prev
@@ -207,7 +221,7 @@ class TrainStep:
             self.opt.step_count += 1  # the replay ran the update
         else:
             with T.phase("reduce"):
-                scale = self.engine.reduce()
+                scale = self._reduce_after_replay()
             with T.phase("optim"):
                 self.opt.step(grad_scale=scale)
         self.last_out, self.last_loss, self.last_pred = out, loss, pred

@@ -160,3 +160,46 @@ def test_in_graph_adam_tracks_host_step_count_and_lr_change():
     _run(sg, xs, ys)
     assert sg._cap_lr == 5e-4
     assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5)
+
+
+def test_rankdad_gradient_space_factorisation():
+    """GPU rank-dAD factorises G = Delta^T A (already in .grad) by the same power iteration:
+    at world 1 every large Linear's gradient becomes a rank-r approximation close to the
+    optimal truncated SVD; layers with min(in, out) <= r stay exact; the step graph captures it."""
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    m = _model(0)
+    flat = FlatParams(m.parameters())
+    eng = make_engine("rankDAD", m, flat, SiteGroup(device=torch.device("cuda")),
+                      {"dad_reduction_rank": 4, "dad_num_pow_iters": 8, "dad_tol": 1e-4})
+    assert eng.fast and eng.fast_layers
+    xs, ys = _batches(1)
+    flat.zero_grad()
+    _, loss, _ = m.forward_loss(xs[0], ys[0])
+    loss.backward()
+    torch.cuda.synchronize()
+    before = flat.grad.clone()
+    eng.reduce()
+    torch.cuda.synchronize()
+    low = {id(l[0].weight) for l in eng.fast_layers}
+    for p, o, n in flat.segments():
+        g0, g1 = before[o:o + n], flat.grad[o:o + n]
+        if id(p) not in low:
+            assert torch.equal(g0, g1)
+            continue
+        G = g0.view_as(p).double()
+        s = torch.linalg.svdvals(G)
+        best = s[4:].norm() / s.norm()
+        err = (g1.view_as(p).double() - G).norm() / G.norm()
+        assert err <= best * 1.15 + 1e-6, (err.item(), best.item())
+
+
+def test_rankdad_step_graph_matches_eager():
+    xs, ys = _batches()
+    _, fe, se = _trainer(0, engine="rankDAD", use_graph=False)
+    _, fg, sg = _trainer(0, engine="rankDAD", use_graph=True)
+    _run(se, xs, ys)
+    _run(sg, xs, ys)
+    assert sg.graph is not None
+    assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5)
