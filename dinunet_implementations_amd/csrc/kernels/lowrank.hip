@@ -130,6 +130,7 @@ pi_gq_kernel(const PiLayer* __restrict__ L, const int* __restrict__ row_starts, 
 #pragma unroll
   for (int c = 0; c < PI_MAXR; ++c) acc[c] = 0.f;
   const float* g = P.G + (long)row * P.in;
+#pragma unroll 4
   for (int k = lane; k < P.in; k += 64) {
     const float gv = g[k];
     const float* q = P.Q + (long)k * r;
@@ -149,10 +150,10 @@ pi_gq_kernel(const PiLayer* __restrict__ L, const int* __restrict__ row_starts, 
 // waves split the rows, the P rows come from LDS, partial sums meet in LDS
 constexpr int GTP_LDS = 12288;  // floats of P staged (out * r <= this; larger layers read L2)
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 pi_gtp_kernel(const PiLayer* __restrict__ L, const int* __restrict__ col_starts, int n) {
   __shared__ float ps[GTP_LDS];
-  __shared__ float part[3][64 * PI_MAXR];
+  __shared__ float part[15][64 * PI_MAXR];
   const int l = find_layer(col_starts, n, blockIdx.x);
   const PiLayer& P = L[l];
   if (!*P.active) return;  // converged (dad_tol): this layer's iteration is a no-op
@@ -165,7 +166,7 @@ pi_gtp_kernel(const PiLayer* __restrict__ L, const int* __restrict__ col_starts,
   const int kc = kv ? k : 0;
   const bool lds = (re - rb) * r <= GTP_LDS;
   if (lds) {
-    for (int i = rb * r + threadIdx.x; i < re * r; i += 256) ps[i - rb * r] = P.Pc[i];
+    for (int i = rb * r + threadIdx.x; i < re * r; i += 1024) ps[i - rb * r] = P.Pc[i];
     __syncthreads();
   }
   // (index LDS relative to rb explicitly: a pointer below ps, even one never dereferenced,
@@ -173,8 +174,8 @@ pi_gtp_kernel(const PiLayer* __restrict__ L, const int* __restrict__ col_starts,
   float acc[PI_MAXR];
 #pragma unroll
   for (int c = 0; c < PI_MAXR; ++c) acc[c] = 0.f;
-#pragma unroll 4
-  for (int row = rb + w; row < re; row += 4) {
+#pragma unroll 8
+  for (int row = rb + w; row < re; row += 16) {
     const float gv = P.G[(long)row * P.in + kc];
     if (lds) {
       const float* p = ps + (row - rb) * r;
@@ -196,9 +197,12 @@ pi_gtp_kernel(const PiLayer* __restrict__ L, const int* __restrict__ col_starts,
   if (w == 0 && kv) {
     float* qp = P.Qc + (long)sp * P.in * r;
 #pragma unroll
-    for (int c = 0; c < PI_MAXR; ++c)
-      if (c < r) qp[(long)k * r + c] = acc[c] + part[0][c * 64 + lane] + part[1][c * 64 + lane] +
-                                       part[2][c * 64 + lane];
+    for (int c = 0; c < PI_MAXR; ++c) {
+      if (c >= r) break;
+      float v = acc[c];
+      for (int t = 0; t < 15; ++t) v += part[t][c * 64 + lane];  // fixed order
+      qp[(long)k * r + c] = v;
+    }
   }
 }
 
@@ -211,6 +215,7 @@ pi_commit_kernel(const PiLayer* __restrict__ L, float tol, int nsplit) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nq = P.in * P.r, np = P.out * P.r;
   float dd = 0.f, qq = 0.f;
+#pragma unroll 8
   for (int i = tid; i < nq; i += 256) {
     float a = P.Qc[i];  // row-split partials of G^T Pc, summed in a fixed order
     for (int s = 1; s < nsplit; ++s) a += P.Qc[(long)s * nq + i];
@@ -225,7 +230,9 @@ pi_commit_kernel(const PiLayer* __restrict__ L, float tol, int nsplit) {
   __syncthreads();
   const float D = red[0][0] + red[0][1] + red[0][2] + red[0][3];
   const float Qn = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+#pragma unroll 8
   for (int i = tid; i < np; i += 256) P.Psend[i] = P.Pc[i];
+#pragma unroll 8
   for (int i = tid; i < nq; i += 256) {
     const float v = P.Qc[i];
     P.Q[i] = v;
@@ -261,7 +268,63 @@ pi_reconstruct_kernel(const PiRecon* __restrict__ R, int n, long total, long str
   }
 }
 
-constexpr int PI_SPLITS = 8;  // row splits of G^T P (Qc holds PI_SPLITS partials)
+constexpr int PI_SPLITS = 1;  // row splits of G^T P (Qc holds PI_SPLITS partials)
+
+// Modified Gram-Schmidt of a [n, r] matrix by ONE wave with the matrix in registers (lane l holds
+// rows l, l+64, ...): every dot product is a wave reduction (DPP / shuffles, no barriers).  The
+// same column order and arithmetic as mgs_batched_kernel up to the reduction order.
+constexpr int MGSW_RPL = 12;  // rows per lane: n <= 768
+
+__global__ void __launch_bounds__(64)
+mgs_wave_kernel(float* const* __restrict__ mats, const int* __restrict__ dims, float eps,
+                const PiLayerFlag* __restrict__ skip) {
+  if (skip && !*skip[blockIdx.x].active) return;
+  float* g = mats[blockIdx.x];
+  const int n = dims[3 * blockIdx.x], r = dims[3 * blockIdx.x + 1], ld = dims[3 * blockIdx.x + 2];
+  const int lane = threadIdx.x;
+  float m[MGSW_RPL][PI_MAXR];
+#pragma unroll
+  for (int i = 0; i < MGSW_RPL; ++i) {
+    const int row = lane + 64 * i;
+    const int rc = row < n ? row : n - 1;  // clamped, unconditional loads (no per-load branch)
+#pragma unroll
+    for (int c = 0; c < PI_MAXR; ++c) {
+      const float v = g[(long)rc * ld + (c < r ? c : r - 1)];
+      m[i][c] = (row < n && c < r) ? v : 0.f;
+    }
+  }
+  // fully unrolled with compile-time indices (a `break` on the runtime r would leave m[][]
+  // dynamically indexed -> scratch); columns >= r are zero and skipped by predicate
+#pragma unroll
+  for (int j = 0; j < PI_MAXR; ++j) {
+    if (j < r) {
+#pragma unroll
+      for (int i = 0; i < j; ++i) {
+        float d = 0.f;
+#pragma unroll
+        for (int t = 0; t < MGSW_RPL; ++t) d += m[t][i] * m[t][j];
+        d = wave_sum(d);
+#pragma unroll
+        for (int t = 0; t < MGSW_RPL; ++t) m[t][j] -= d * m[t][i];
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int t = 0; t < MGSW_RPL; ++t) s += m[t][j] * m[t][j];
+      const float inv = 1.f / (sqrtf(wave_sum(s)) + eps);
+#pragma unroll
+      for (int t = 0; t < MGSW_RPL; ++t) m[t][j] *= inv;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MGSW_RPL; ++i) {
+    const int row = lane + 64 * i;
+    if (row < n) {
+#pragma unroll
+      for (int c = 0; c < PI_MAXR; ++c)
+        if (c < r) g[(long)row * ld + c] = m[i][c];
+    }
+  }
+}
 
 __global__ void pi_reset_kernel(const PiLayer* __restrict__ L, int n) {
   if ((int)threadIdx.x < n) *L[threadIdx.x].active = 1;
@@ -280,17 +343,21 @@ DN_API int dn_pi_splits() { return PI_SPLITS; }
 // Layers whose power iteration has converged (dad_tol) skip their work inside every launch.
 DN_API int dn_pi_iterate(const void* layers, const int* row_starts, const int* col_starts, int n,
                          int total_rows, int total_colblocks, float* const* pc_ptrs,
-                         const int* pc_dims, const void* active_ptrs, float tol, int first,
-                         hipStream_t st) {
+                         const int* pc_dims, const void* active_ptrs, int max_rows, float tol,
+                         int first, hipStream_t st) {
   if (n <= 0) return DN_OK;
   if (n > 256) return DN_BAD_SHAPE;
   const PiLayer* L = (const PiLayer*)layers;
   if (first) hipLaunchKernelGGL(pi_reset_kernel, dim3(1), dim3(256), 0, st, L, n);
   hipLaunchKernelGGL(pi_gq_kernel, dim3((total_rows + 3) / 4), dim3(256), 0, st, L, row_starts, n,
                      total_rows);
-  hipLaunchKernelGGL(mgs_batched_kernel, dim3(n), dim3(256), 0, st, pc_ptrs, pc_dims, 1e-8f,
-                     (const PiLayerFlag*)active_ptrs);
-  hipLaunchKernelGGL(pi_gtp_kernel, dim3(total_colblocks, PI_SPLITS), dim3(256), 0, st, L,
+  if (max_rows <= 64 * MGSW_RPL)
+    hipLaunchKernelGGL(mgs_wave_kernel, dim3(n), dim3(64), 0, st, pc_ptrs, pc_dims, 1e-8f,
+                       (const PiLayerFlag*)active_ptrs);
+  else
+    hipLaunchKernelGGL(mgs_batched_kernel, dim3(n), dim3(256), 0, st, pc_ptrs, pc_dims, 1e-8f,
+                       (const PiLayerFlag*)active_ptrs);
+  hipLaunchKernelGGL(pi_gtp_kernel, dim3(total_colblocks, PI_SPLITS), dim3(1024), 0, st, L,
                      col_starts, n);
   hipLaunchKernelGGL(pi_commit_kernel, dim3(n), dim3(256), 0, st, L, tol, PI_SPLITS);
   return dn_launch_status();

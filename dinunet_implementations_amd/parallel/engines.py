@@ -357,7 +357,8 @@ class RankDADEngine(Engine):
             _lib.call("dn_pi_iterate", self._tab.data_ptr(), self._row_starts.data_ptr(),
                       self._col_starts.data_ptr(), len(self.fast_layers), self._rows, self._cols,
                       self._mgs_ptrs.data_ptr(), self._mgs_dims.data_ptr(),
-                      self._act_ptrs.data_ptr(), float(self.tol), int(it == 0), _lib.stream())
+                      self._act_ptrs.data_ptr(), max(l[2] for l in self.fast_layers),
+                      float(self.tol), int(it == 0), _lib.stream())
 
     def _fast_reduce(self) -> float:
         g = self.group

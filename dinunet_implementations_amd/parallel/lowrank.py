@@ -21,7 +21,8 @@ _lib.register("dn_mgs_batched", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _l
                                   _lib.c_int, _lib.c_float, _lib.c_void_p])
 _lib.register("dn_pi_iterate", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
                                  _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_float, _lib.c_int, _lib.c_void_p])
+                                 _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_int,
+                                 _lib.c_void_p])
 _lib.register("dn_pi_reconstruct", [_lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_long,
                                      _lib.c_int, _lib.c_void_p])
 
