@@ -111,8 +111,12 @@ constexpr int ZCOL = 64;
 // All per-step global traffic is UNCONDITIONAL (internal buffers padded to Bp rows and HD
 // units; loads of padded rows clamp to row B-1): no divergent branches around memory ops, so
 // hipcc emits counted s_waitcnt vmcnt(N) and a step never waits for the previous step's stores.
-template <int HD, int BR, bool SEQ>
-__global__ void __launch_bounds__(HD / 16 * 64)
+// UG = unit groups (16 units = 4 m-tiles each) per wave: UG = 1 is 3 waves per SIMD at HD=192;
+// UG = 3 is ONE wave per SIMD owning 12 m-tiles -- the 72 MFMAs of a SIMD come from 12
+// independent accumulator chains of one wave (no issue arbitration between waves) and the h
+// tile is read once per k-step for 12 MFMAs instead of 4.
+template <int HD, int BR, bool SEQ, int UG>
+__global__ void __launch_bounds__(HD / (16 * UG) * 64)
 lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted cols, no bias;
                                                  // store_pre: overwritten by the gate pre-activations
                 const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
@@ -124,13 +128,14 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
                 float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
                 float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
                 int store_pre) {
-  constexpr int NT = HD / 16 * 64;
+  constexpr int NW = HD / (16 * UG);
+  constexpr int NT = NW * 64;
+  constexpr int MT = 4 * UG;   // m-tiles per wave
   constexpr int KS = HD / 32;
   constexpr int LDH = HD + 8;  // +16 B per row: the 16 rows land on distinct bank quads
-  constexpr int NLM = LdsSplit<HD, BR>::FWD_MT, NRM = 4 - NLM;
-  constexpr int NW = HD / 16;
-  constexpr int G16 = 16 / BR, NSL = BR / 4;
-  constexpr int EPT = BR * HD / NT;  // h_{t-1} copy: elements per thread (1, 2 or 4)
+  constexpr int NLM = UG == 1 ? LdsSplit<HD, BR>::FWD_MT : 0, NRM = MT - NLM;
+  constexpr int G16 = 16 / BR, NSL1 = BR / 4, NSL = UG * NSL1;
+  constexpr int EPT = BR * HD / NT;  // h_{t-1} copy: elements per thread
   __shared__ __attribute__((aligned(16))) bf16 hbuf[2][16][LDH];
   __shared__ __attribute__((aligned(16))) float bias_s[4 * HD];
   // lane-linear fragment image: one 1 KiB row per (wave, m-tile, k-step) -> conflict-free b128
@@ -148,10 +153,10 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   {
     const bf16* wd = whh + (long)dir * 4 * HD * HD;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const int row = 16 * (4 * w + mt) + n;
+        const int row = 16 * (MT * w + mt) + n;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(wd + (long)row * HD + 32 * ks + 8 * q);
         if (mt < NRM) wf[mt < NRM ? mt : 0][ks] = v;
         else wlds[w][mt - NRM][ks][lane] = v;
@@ -161,9 +166,10 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   for (int i = tid; i < 2 * 16 * LDH; i += NT) (&hbuf[0][0][0])[i] = (bf16)0.f;
   __syncthreads();
 
-  int uu[NSL];
+  int uu[NSL];  // slot (group gu, s1) -> unit of m-tile 4*gu + r + s1*G16 of this wave
 #pragma unroll
-  for (int s = 0; s < NSL; ++s) uu[s] = 16 * w + 4 * (r + s * G16) + q;
+  for (int s = 0; s < NSL; ++s)
+    uu[s] = 16 * (UG * w + s / NSL1) + 4 * (r + (s % NSL1) * G16) + q;
   float* xrow = xp + (long)bc * S * rowX + (long)dir * 4 * HD;
   const bool wpre = store_pre && b < B;  // padded rows alias row B-1: never store them
   const long hplane = (long)dir * Bp * S * HD;
@@ -196,12 +202,13 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
     } else if constexpr (EPT == 2) {
       *reinterpret_cast<unsigned*>(hcp + (long)tau * HD) = *reinterpret_cast<const unsigned*>(&hbuf[cur][cp_r][cp_c]);
     } else {
-      hcp[(long)tau * HD] = hbuf[cur][cp_r][cp_c];
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) hcp[(long)tau * HD + e] = hbuf[cur][cp_r][cp_c + e];
     }
     // recurrent GEMM  pre^T[m][b] = sum_k W[m][k] h[b][k]  (W resident)
-    f32x4 acc[4];
+    f32x4 acc[MT];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       // columns >= BR must be zero: those lanes read one all-zero 16 B slot (row BR is never
@@ -214,7 +221,7 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
 #pragma unroll
       for (int mt = 0; mt < NRM; ++mt) acc[mt] = mfma16(wf[mt][ks], hb, acc[mt]);
 #pragma unroll
-      for (int mt = NRM; mt < 4; ++mt) acc[mt] = mfma16(wlds[w][mt - NRM][ks][lane], hb, acc[mt]);
+      for (int mt = NRM; mt < MT; ++mt) acc[mt] = mfma16(wlds[w][mt - NRM][ks][lane], hb, acc[mt]);
     }
     // redistribute the BR valid columns over all lanes (identity when BR == 16)
     f32x4 pa[NSL];
@@ -222,14 +229,15 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
 #pragma unroll
       for (int s = 0; s < NSL; ++s) pa[s] = acc[s];
     } else {
-      // slot s of lane (q, r, bl) = m-tile r + s*G16 of column bl (held by lane (q, bl))
+      // slot (gu, s1) of lane (q, r, bl) = m-tile 4*gu + r + s1*G16 of column bl (held by
+      // lane (q, bl))
 #pragma unroll
       for (int sl = 0; sl < NSL; ++sl)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float v[G16];
 #pragma unroll
-          for (int g = 0; g < G16; ++g) v[g] = acc[g + sl * G16][j];
+          for (int g = 0; g < G16; ++g) v[g] = acc[4 * (sl / NSL1) + g + (sl % NSL1) * G16][j];
           pa[sl][j] = row_gather<BR>(v);
         }
     }
@@ -298,8 +306,8 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
 // (pre = x W_ih^T + h_{t-1} W_hh^T + b) instead of being stored per step by the forward kernel.
 // MFMA output: lane (q, n) holds dh for units u0 + j (u0 = 16w + 4q, j = 0..3) of column n; as in
 // the forward, the BR valid columns are redistributed: lane (q, r, b) owns units u0 + r + s*(16/BR).
-template <int HD, int BR, bool DSEQ>
-__global__ void __launch_bounds__(HD / 16 * 64)
+template <int HD, int BR, bool DSEQ, int UG>
+__global__ void __launch_bounds__(HD / (16 * UG) * 64)
 lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time order
                 const float* __restrict__ c_save,  // [ndir][Bp][S][HD]
                 const bf16* __restrict__ whhT,     // [ndir][HD][4*HD]
@@ -309,10 +317,10 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
                 bf16* __restrict__ dpre) {          // [Bp*S][ndir][4*HD] permuted, original time
   constexpr int KS = 4 * HD / 32;
   constexpr int LDD = 4 * HD + 8;
-  constexpr int NLK = LdsSplit<HD, BR>::BWD_KS, NRK = KS - NLK;
-  constexpr int NW = HD / 16;
+  constexpr int NLK = UG == 1 ? LdsSplit<HD, BR>::BWD_KS : 0, NRK = KS - NLK;
+  constexpr int NW = HD / (16 * UG);
   constexpr int NT = NW * 64;
-  constexpr int G16 = 16 / BR, NSL = BR / 4;
+  constexpr int G16 = 16 / BR, NSL1 = BR / 4, NSL = UG * NSL1;
   __shared__ __attribute__((aligned(16))) bf16 dbuf[2][16][LDD];
   __shared__ __attribute__((aligned(16))) bf16x8 wlds[NLK > 0 ? NW : 1][NLK > 0 ? NLK : 1][64];
 
@@ -325,25 +333,27 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   const int bc = vb ? b : B - 1;
   const long rowX = (long)ndir * 4 * HD;
 
-  bf16x8 af[NRK];
+  bf16x8 af[UG][NRK];
   {
     const bf16* wt = whhT + (long)dir * HD * 4 * HD;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 v =
-          *reinterpret_cast<const bf16x8*>(wt + (long)(16 * w + n) * 4 * HD + 32 * ks + 8 * q);
-      if (ks < NRK) af[ks < NRK ? ks : 0] = v;
-      else wlds[w][ks - NRK][lane] = v;
-    }
+    for (int g = 0; g < UG; ++g)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+            wt + (long)(16 * (UG * w + g) + n) * 4 * HD + 32 * ks + 8 * q);
+        if (ks < NRK) af[g][ks < NRK ? ks : 0] = v;
+        else wlds[w][ks - NRK][lane] = v;
+      }
   }
   for (int i = tid; i < 2 * 16 * LDD; i += NT) (&dbuf[0][0][0])[i] = (bf16)0.f;
 
-  const int u0 = 16 * w + 4 * q;
   int uu[NSL];
   float msk[NSL], dhx[NSL], dcc[NSL];
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
-    const int u = u0 + r + s * G16;
+    // slot (group s / NSL1, s1 = s % NSL1): unit offset r + s1*G16 of the group's lane quad
+    const int u = 16 * (UG * w + s / NSL1) + 4 * q + r + (s % NSL1) * G16;
     uu[s] = u;
     msk[s] = (vb && u < Hd) ? 1.f : 0.f;
     const int uc = u < Hd ? u : Hd - 1;
@@ -392,24 +402,29 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
         dx[s] += dhT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s];
       }
     }
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[UG];
+#pragma unroll
+    for (int g = 0; g < UG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const bool dv = BR == 16 || n < BR;  // see the forward: unmasked zero-slot reads
       const bf16x8 db = *reinterpret_cast<const bf16x8*>(
           &dbuf[cur][dv ? n : (BR & 15)][dv ? 32 * ks + 8 * q : ZCOL]);
-      acc = mfma16(ks < NRK ? af[ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db, acc);
+#pragma unroll
+      for (int g = 0; g < UG; ++g)
+        acc[g] = mfma16(ks < NRK ? af[g][ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane],
+                        db, acc[g]);
     }
     float dhr[NSL];
     if constexpr (BR == 16) {
 #pragma unroll
-      for (int s = 0; s < NSL; ++s) dhr[s] = acc[s];
+      for (int s = 0; s < NSL; ++s) dhr[s] = acc[s / 4][s % 4];
     } else {
 #pragma unroll
       for (int sl = 0; sl < NSL; ++sl) {
         float v[G16];
 #pragma unroll
-        for (int g = 0; g < G16; ++g) v[g] = acc[g + sl * G16];
+        for (int g = 0; g < G16; ++g) v[g] = acc[sl / NSL1][g + (sl % NSL1) * G16];
         dhr[sl] = row_gather<BR>(v);
       }
     }
@@ -575,18 +590,45 @@ static inline int pick_br(int B) {
   return 16;
 }
 
+// unit groups per wave for (HD, BR) = (192, 4): 1 (12 waves, 3 per SIMD) unless
+// DINUNET_LSTM_UG=3 asks for one wave per SIMD.  Measured on MI355X (tools/lstm_stamps.py): the
+// one-wave layout runs 2.06 us/step fwd and bwd vs 1.19 / 1.46 -- a lone wave issues its 72
+// MFMAs at ~2700 cycles (not 1152) and its 3 gate slots serialise (1400 cycles): the 3-wave
+// layout's inter-wave overlap of MFMA, LDS and VALU work is worth more than the 3x fewer
+// exchange-tile reads.
+static int lstm_ug() {
+  static const int ug = [] {
+    const char* e = getenv("DINUNET_LSTM_UG");
+    return (e && e[0] == '3') ? 3 : 1;
+  }();
+  return ug;
+}
+
+template <int HD, int BR, int UG>
+int launch_fwd_ug(float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
+                  float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
+                  float* cT, int store_pre, hipStream_t st) {
+  dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
+  if (hseq)
+    hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, true, UG>), grid, block, 0, st, xp, bias, whh, B, S,
+                       Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
+  else
+    hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false, UG>), grid, block, 0, st, xp, bias, whh, B,
+                       S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
+  return dn_launch_status();
+}
+
 template <int HD, int BR>
 int launch_fwd_br(float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
                   float* cT, int store_pre, hipStream_t st) {
-  dim3 grid((B + BR - 1) / BR, ndir), block(HD / 16 * 64);
-  if (hseq)
-    hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, true>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
-                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
-  else
-    hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false>), grid, block, 0, st, xp, bias, whh, B, S, Hd,
-                       ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
-  return dn_launch_status();
+  if constexpr (HD == 192 && BR == 4) {
+    if (lstm_ug() == 3)
+      return launch_fwd_ug<HD, BR, 3>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
+                                      mean_scale, hT, cT, store_pre, st);
+  }
+  return launch_fwd_ug<HD, BR, 1>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
+                                  mean_scale, hT, cT, store_pre, st);
 }
 
 template <int HD>
@@ -598,18 +640,31 @@ int launch_fwd(int BR, float* xp, const float* bias, const bf16* whh, int B, int
   return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
 }
 
+template <int HD, int BR, int UG>
+int launch_bwd_ug(const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
+                  long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
+                  int Hd, int ndir, bf16* dpre, hipStream_t st) {
+  dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
+  if (st_ != 0)
+    hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, true, UG>), grid, block, 0, st, pre, c_save, whhT,
+                       dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
+  else
+    hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, false, UG>), grid, block, 0, st, pre, c_save, whhT,
+                       dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
+  return dn_launch_status();
+}
+
 template <int HD, int BR>
 int launch_bwd_br(const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
                   long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
                   int Hd, int ndir, bf16* dpre, hipStream_t st) {
-  dim3 grid((B + BR - 1) / BR, ndir), block(HD / 16 * 64);
-  if (st_ != 0)
-    hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, true>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
-                       sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
-  else
-    hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, false>), grid, block, 0, st, pre, c_save, whhT, dh_ext,
-                       sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
-  return dn_launch_status();
+  if constexpr (HD == 192 && BR == 4) {
+    if (lstm_ug() == 3)
+      return launch_bwd_ug<HD, BR, 3>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S,
+                                      Hd, ndir, dpre, st);
+  }
+  return launch_bwd_ug<HD, BR, 1>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd,
+                                  ndir, dpre, st);
 }
 
 template <int HD>
