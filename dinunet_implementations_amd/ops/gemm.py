@@ -201,3 +201,25 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               (I * n)(*arrs["K"]), (F * n)(*arrs["alpha"]), (F * n)(*arrs["beta"]),
               (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), 0, int(a_bf), int(b_bf), ta, tb,
               int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.stream())
+
+
+# Plain GEMMs (no fused epilogue: bf16 operands, fp32 or bf16 output, no bias / beta / row map)
+# may go to the vendor library (hipBLASLt through torch), which at these skinny shapes measures
+# ~2x faster than the hand-written tile loop (tools/bench_gemm.py / rocprof: 3136x1536x256
+# 9.2 vs 18 us).  Every GEMM with a fused epilogue stays on csrc/kernels/gemm.hip.
+import os as _os
+
+PLAIN_BLAS = _os.environ.get("DINUNET_PLAIN_BLAS", "1") == "1"
+
+
+def mm_plain(a: Tensor, b: Tensor, trans_b: bool = False, out_dtype: torch.dtype = torch.float32,
+             trans_a: bool = False) -> Tensor:
+    """``op(a) @ op(b)`` for bf16 operands: hipBLASLt when enabled, else :func:`mm`."""
+    if (PLAIN_BLAS and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+        A = a.t() if trans_a else a
+        B = b.t() if trans_b else b
+        if out_dtype == torch.bfloat16:
+            return torch.mm(A, B)
+        return torch.mm(A, B, out_dtype=out_dtype)
+    return mm(a, b, trans_a=trans_a, trans_b=trans_b, out_dtype=out_dtype)
+

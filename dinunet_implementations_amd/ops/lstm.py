@@ -32,7 +32,7 @@ from . import _grad
 from . import _lib
 from . import _streams
 from . import capture as _cap
-from .gemm import mm, mm_grouped
+from .gemm import mm, mm_grouped, mm_plain
 
 Tensor = torch.Tensor
 
@@ -104,7 +104,7 @@ class _BiLSTMFn(torch.autograd.Function):
                 raise ValueError("precomputed LSTM input projection has the wrong shape/dtype")
             xp = xp_pre
         else:
-            xp = mm(x2d, wih_p, trans_b=True, out_dtype=torch.float32)   # [B*S, ndir*GP]
+            xp = mm_plain(x2d, wih_p, trans_b=True, out_dtype=torch.float32)  # [B*S, ndir*GP]
         c_save = torch.empty(ndir, Bp, S, HD, dtype=torch.float32, device=dev)
         hprev = torch.empty(ndir, Bp, S, HD, dtype=torch.bfloat16, device=dev)
         hT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
@@ -178,7 +178,7 @@ class _BiLSTMFn(torch.autograd.Function):
         # (7) input grad
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = mm(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
+            dx = mm_plain(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
             if enc_dtype != torch.bfloat16:
                 dx = dx.to(enc_dtype)
         if capturing:
