@@ -51,6 +51,21 @@ relu_bwd_colsum_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
   }
 }
 
+// dym = dy * (y > 0), elementwise over n bf16 values (n % 8 == 0, 16-B aligned): the encoder
+// backward's mask when its bias gradient rides in the weight-gradient GEMM (dym^T @ ones)
+__global__ void __launch_bounds__(256)
+relu_bwd_kernel(const bf16x8* __restrict__ dy, const bf16x8* __restrict__ y,
+                bf16x8* __restrict__ dym, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    const bf16x8 g = dy[i], a = y[i];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (float)a[e] > 0.f ? g[e] : (bf16)0.f;
+    dym[i] = o;
+  }
+}
+
 // out[c] = sum_s part[s][c]  (fixed order -> bit-reproducible)
 __global__ void colsum_slabs_kernel(const float* __restrict__ part, int slabs, int O,
                                     float* __restrict__ out, int accumulate) {
@@ -105,6 +120,16 @@ DN_API int dn_step_prologue(const float* x, long nx, void* xb, const long long* 
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, nx / 8,
                      (bf16*)xb, y, ny, yd, g, ng / 4);
+  return dn_launch_status();
+}
+
+DN_API int dn_relu_bwd(const void* dy, const void* y, void* dym, long n, hipStream_t st) {
+  if (n <= 0 || n % 8) return DN_BAD_SHAPE;
+  if ((((uintptr_t)dy) | ((uintptr_t)y) | ((uintptr_t)dym)) & 15) return DN_BAD_SHAPE;
+  const long n8 = n / 8;
+  const long blocks = (n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048;
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     (const bf16x8*)dy, (const bf16x8*)y, (bf16x8*)dym, n8);
   return dn_launch_status();
 }
 

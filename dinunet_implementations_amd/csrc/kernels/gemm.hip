@@ -209,9 +209,10 @@ struct Epi {
   float alpha, beta;
   int relu;
   int out_bf16;
+  int ncol;  // > 0: only output columns < ncol are stored (e.g. a ones-operand column sum)
 };
 
-constexpr int GMAX = 8;  // problems per grouped launch
+constexpr int GMAX = 12;  // problems per grouped launch (kernarg: ~1.6 KB)
 
 // One GEMM problem of a (possibly grouped) launch.
 struct GemmProb {
@@ -354,12 +355,13 @@ gemm_kernel(GemmGroup g) {
 #undef Bs
   // epilogue
   float* slab = P.slab;
+  const int nst = (slab || P.epi.ncol <= 0) ? N : min(N, P.epi.ncol);
 #pragma unroll
   for (int i = 0; i < T::FM; ++i)
 #pragma unroll
     for (int j = 0; j < T::FN; ++j) {
       const int col = col0 + wn * T::WN + 16 * j + (lane & 15);
-      if (col >= N) continue;
+      if (col >= nst) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = row0 + wm * T::WM + 16 * i + 4 * (lane >> 4) + r;
@@ -370,8 +372,41 @@ gemm_kernel(GemmGroup g) {
     }
 }
 
+// 4 consecutive outputs of one row: v (already alpha-free split sum) -> epilogue -> vector store
+__device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, int row, int col, f32x4 v) {
+  const long orow = epi.row_map ? epi.row_map[row] : row;
+  if (orow < 0) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] *= epi.alpha;
+    if (epi.bias) v[e] += epi.bias[col + e];
+    if (epi.relu) v[e] = fmaxf(v[e], 0.f);
+  }
+  if (epi.out_bf16) {
+    bf16x4* cp = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(C) + orow * ldc + col);
+    if (epi.beta != 0.f) {
+      const bf16x4 o = *cp;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += epi.beta * (float)o[e];
+    }
+    bf16x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = (bf16)v[e];
+    *cp = w;
+  } else {
+    f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + orow * ldc + col);
+    if (epi.beta != 0.f) {
+      const f32x4 o = *cp;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += epi.beta * o[e];
+    }
+    *cp = v;
+  }
+}
+
 // deterministic split-K combine + epilogue over every problem of a group; each thread handles
-// 4 consecutive columns of one row
+// 4 consecutive columns of one row.  Rows of N % 4 == 0 problems (every ICA shape) take 16-B
+// slab loads (all splits issued together) and 16-B stores; others the scalar path.
 __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
   const long total = g.elem_start[g.n];
   for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; 4 * i4 < total;
@@ -382,14 +417,40 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
     const GemmProb& P = g.p[pi];
     const long base = g.elem_start[pi];
     const long mn = (long)P.M * P.N;
+    const long idx = idx0 - base;
+    if (idx >= mn) continue;
+    const bool vec = P.epi.ncol <= 0 && (P.N & 3) == 0 && (P.ldc & 3) == 0 &&
+                     ((((uintptr_t)P.C) & 15) == 0) &&
+                     ((((uintptr_t)P.slab) & 15) == 0);
+    if (vec) {
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      int s = 0;
+      for (; s + 4 <= g.splits; s += 4) {  // four slab loads in flight per round
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(P.slab + (long)s * mn + idx);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(P.slab + (long)(s + 1) * mn + idx);
+        const f32x4 a2 = *reinterpret_cast<const f32x4*>(P.slab + (long)(s + 2) * mn + idx);
+        const f32x4 a3 = *reinterpret_cast<const f32x4*>(P.slab + (long)(s + 3) * mn + idx);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += ((a0[e] + a1[e]) + a2[e]) + a3[e];
+      }
+      for (; s < g.splits; ++s) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(P.slab + (long)s * mn + idx);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += a[e];
+      }
+      const int row = (int)(idx / P.N), col = (int)(idx - (long)row * P.N);
+      epi_store4(P.epi, P.C, P.ldc, row, col, v);
+      continue;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const long idx = idx0 + e - base;
-      if (idx >= mn) break;  // (problems are padded to multiples of 4 elements in elem_start)
-      float v = 0.f;
-      for (int s = 0; s < g.splits; ++s) v += P.slab[(long)s * mn + idx];
-      const int row = (int)(idx / P.N), col = (int)(idx - (long)row * P.N);
-      epi_store(P.epi, P.C, P.ldc, row, col, v);
+      const long ie = idx + e;
+      if (ie < mn && (P.epi.ncol <= 0 || ie % P.N < P.epi.ncol)) {
+        float v = 0.f;
+        for (int s = 0; s < g.splits; ++s) v += P.slab[(long)s * mn + ie];
+        const int row = (int)(ie / P.N), col = (int)(ie - (long)row * P.N);
+        epi_store(P.epi, P.C, P.ldc, row, col, v);
+      }
     }
   }
 }
@@ -486,17 +547,19 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   P.kchunk = kchunk_for(K, g.splits);
   if (g.splits > 1) g.splits = (K + P.kchunk - 1) / P.kchunk;
   P.slab = g.splits > 1 ? slab : nullptr;
-  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16};
+  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0};
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }
 
-// Grouped GEMM: n <= 8 independent problems with the same operand layouts / element types /
-// output type in ONE launch (+ one split-K reduce).  Per-problem arrays; `slab` holds
+// Grouped GEMM: n <= GMAX (12) independent problems with the same operand layouts / element types /
+// output type in ONE launch (+ one split-K reduce).  Per-problem arrays (`ncol` may be null: see
+// Epi::ncol); `slab` holds
 // splits * sum(M_i * N_i) fp32 when splits > 1.  Every problem uses the same K split count.
 DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const void* const* B,
                            const long* ldb, void* const* C, const long* ldc, const int* M,
                            const int* N, const int* K, const float* alpha, const float* beta,
-                           const void* const* bias, const void* const* row_map, int relu,
+                           const void* const* bias, const void* const* row_map,
+                           const int* ncol, int relu,
                            int a_bf16, int b_bf16, int ta, int tb, int c_bf16, int tile,
                            int splits, float* slab, hipStream_t st) {
   if (n < 1 || n > GMAX) return DN_BAD_SHAPE;
@@ -515,7 +578,8 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
     P.kchunk = kchunk_for(K[i], sp);
     P.slab = g.splits > 1 ? slab + soff : nullptr;
     soff += (long)g.splits * M[i] * N[i];
-    P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16};
+    P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16,
+                ncol ? ncol[i] : 0};
   }
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }

@@ -481,35 +481,6 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
 #endif
 }
 
-// deterministic column sums of a bf16 [N][C] matrix into slab partials [slabs][C] (fp32)
-__global__ void __launch_bounds__(256)
-colsum_bf16_kernel(const bf16* __restrict__ x, int N, int C, float* __restrict__ part) {
-  const int cg = blockIdx.x * 32 + (threadIdx.x & 31);
-  const int rl = threadIdx.x >> 5;
-  const int c0 = cg * 8;
-  const int rows_per = (N + gridDim.y - 1) / gridDim.y;
-  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (c0 + 8 <= C) {
-    for (int r = r0 + rl; r < r1; r += 8) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (long)r * C + c0);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
-    }
-  }
-  __shared__ float red[8][32 * 8 + 4];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) red[rl][(threadIdx.x & 31) * 8 + e] = s[e];
-  __syncthreads();
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col < C) {
-    float t = 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) t += red[r][threadIdx.x];
-    part[(long)blockIdx.y * C + col] = t;
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 // weight pack: reference layout ([i|f|o|g] rows, fp32) -> kernel layouts (bf16, m = 4u+g,
 // units zero-padded to HD)
@@ -557,26 +528,6 @@ __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
       whhT_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][(g * Hd + u) * Hd + k] : 0.f);
     }
   }
-}
-
-// bias grads: sum the column-sum slabs of dpre and ACCUMULATE into b_ih and b_hh (same grad)
-__global__ void lstm_bias_grad_kernel(const float* __restrict__ part, int slabs, int Hd, int HD,
-                                      int ndir, LstmParams out) {
-  const int G = 4 * Hd;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= ndir * G) return;
-  const int d = idx / G, r = idx % G, g = r / Hd, u = r % Hd;
-  const int col = d * 4 * HD + 4 * u + g;
-  const long C = (long)ndir * 4 * HD;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // independent chains: loads in flight
-  int k = 0;
-  for (; k + 8 <= slabs; k += 8)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += part[(long)(k + e) * C + col];
-  for (; k < slabs; ++k) acc[0] += part[(long)k * C + col];
-  const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  if (out.bih[d]) const_cast<float*>(out.bih[d])[r] += s;
-  if (out.bhh[d]) const_cast<float*>(out.bhh[d])[r] += s;
 }
 
 // rows per workgroup: spread small batches over more CUs (the gate phase is VALU-bound per CU)
@@ -735,18 +686,3 @@ DN_API int dn_lstm_bwd(const float* pre, const float* c_save, const void* whhT_p
   return DN_UNSUPPORTED;
 }
 
-// bias grads from dpre [N][ndir*4HD] bf16: slab column sums (ws: [64][ndir*4HD] fp32), then
-// accumulate into b_ih / b_hh of each direction (reference layout)
-DN_API int dn_lstm_bias_grad(const void* dpre, int N, int Hd, int ndir, float* ws, float* dbih0,
-                             float* dbhh0, float* dbih1, float* dbhh1, hipStream_t st) {
-  const int HD = dn_lstm_padded_hidden(Hd);
-  if (!HD || N <= 0) return DN_BAD_SHAPE;
-  const int C = ndir * 4 * HD;
-  const int slabs = N < 64 ? N : 64;
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((C + 255) / 256, slabs), dim3(256), 0, st,
-                     (const bf16*)dpre, N, C, ws);
-  LstmParams o{{nullptr, nullptr}, {dbih0, dbih1}, {nullptr, nullptr}, {dbhh0, dbhh1}};
-  hipLaunchKernelGGL(lstm_bias_grad_kernel, dim3((ndir * 4 * Hd + 255) / 256), dim3(256), 0, st,
-                     ws, slabs, Hd, HD, ndir, o);
-  return dn_launch_status();
-}

@@ -12,6 +12,10 @@ from typing import Callable, Iterable, List
 
 import torch
 
+# deferred weight-gradient GEMM problems of the current backward pass (see :func:`defer`)
+_pending: List[dict] = []
+_pending_params: List[torch.Tensor] = []
+
 _callbacks: List[Callable[[torch.nn.Parameter], None]] = []
 
 
@@ -41,3 +45,42 @@ def notify(params: Iterable[torch.Tensor]) -> None:
     for p in params:
         for cb in list(_callbacks):
             cb(p)
+
+
+def defer(problems: Iterable[dict], params: Iterable[torch.Tensor]) -> None:
+    """Queue weight-gradient GEMM problems (``mm_grouped`` dicts, all ``trans_a=True``:
+    ``out += a^T @ b``) instead of launching them now.  Every problem queued during one
+    backward pass is issued by :func:`flush` as ONE grouped launch (per dtype/layout class) on
+    the backward's stream when the pass ends, and only then are ``params`` reported final.
+
+    Why: the ICA step's weight gradients (LSTM dW_ih / dW_hh / biases, encoder dW / bias) are
+    long-K (K = B*S) GEMMs of few tiles each; issued separately they either serialise or need a
+    side stream, and every cross-stream edge of a HIP graph costs ~5-12 us of signalling.  One
+    grouped launch puts all ~280 tiles on the 256 CUs at once.
+    """
+    first = not _pending
+    _pending.extend(problems)
+    _pending_params.extend(params)
+    if first:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(flush)
+        except RuntimeError:  # not inside a backward pass: nothing to batch with
+            flush()
+
+
+def flush() -> None:
+    """Issue every deferred gradient GEMM (grouped by operand dtypes / layouts) and notify."""
+    if not _pending:
+        return
+    from .gemm import mm_grouped
+    probs, params = list(_pending), list(_pending_params)
+    _pending.clear()
+    _pending_params.clear()
+    groups = {}
+    for q in probs:
+        key = (q["a"].dtype, q["b"].dtype, q["out"].dtype, q["a"].stride(-1) == 1,
+               q["b"].stride(-1) == 1, q["a"].device)
+        groups.setdefault(key, []).append(q)
+    for g in groups.values():
+        mm_grouped(g, trans_a=True)
+    notify(params)

@@ -24,10 +24,11 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
                           _lib.c_int, _lib.c_void_p, _lib.c_void_p])
 
-_lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 13 + [_lib.c_int] * 8
+_lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 14 + [_lib.c_int] * 8
               + [_lib.c_void_p, _lib.c_void_p])
 
 _NCU = 256
+GMAX = 12  # problems per grouped launch (csrc/kernels/gemm.hip)
 
 
 def _layout(t: Tensor, rows_first: bool):
@@ -49,6 +50,10 @@ def _layout(t: Tensor, rows_first: bool):
     return t, 0, t.stride(0)
 
 
+# tuning override of the grouped launches' split-K (0 = heuristic); tools/gpu sweeps
+_GROUP_SPLITS = int(__import__("os").environ.get("DINUNET_GROUP_SPLITS", "0"))
+
+
 def choose_tiling(M: int, N: int, K: int):
     """(tile, split-K).  Few-tile long-K GEMMs (the weight gradients, 64 tiles of K = 3136) cut K
     into ~384-deep chunks on separate workgroups; from ~128 tiles on, the deterministic slab
@@ -58,10 +63,20 @@ def choose_tiling(M: int, N: int, K: int):
     t64 = ((M + 63) // 64) * ((N + 63) // 64)
     if t128 >= 2 * _NCU:
         return 1, 1
-    splits = 1
-    if K >= 768 and t64 < _NCU // 2:  # measured: at ~200 tiles the slab reduce costs more
-        splits = max(1, min(8, round(K / 384), (4 * _NCU) // max(t64, 1)))
-    return 0, splits
+    return 0, _split_rule(t64, K)
+
+
+def _split_rule(t64: int, K: int) -> int:
+    """Split-K count for ``t64`` 64x64 tiles of depth K.  A tile's K loop is latency-bound (one
+    workgroup keeps ~32 KB in flight), so long-K problems cut K until ~3 workgroups share each
+    CU; medium K only splits when few tiles exist (a second ~5 us reduce launch otherwise eats
+    the gain).  Measured on MI355X (bench.py, merged ICA weight-gradient launch: 284 tiles of
+    K = 3136): 1 split 0.4156 ms/step, 2: 0.4045, 3: 0.4010, 4: 0.4024."""
+    if K >= 2048:
+        return max(1, min(8, round(3 * _NCU / max(t64, 1)), K // 512))
+    if K >= 768 and t64 < _NCU // 2:
+        return max(1, min(8, round(K / 384), (4 * _NCU) // max(t64, 1)))
+    return 1
 
 
 def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
@@ -126,26 +141,31 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
     """Several independent ``out_i (+)= alpha_i * op(a_i) @ op(b_i)`` in ONE launch.
 
     ``problems``: sequence of dicts with keys ``a``, ``b``, ``out`` (required, fp32 or bf16 like
-    every other ``out`` of the group) and optional ``alpha``, ``beta``, ``bias``, ``row_map``.
+    every other ``out`` of the group) and optional ``alpha``, ``beta``, ``bias``, ``row_map``,
+    ``ncol`` (store only the first ``ncol`` result columns into ``out``; lets a column sum ride
+    along as ``a^T @ ones[K, 8]`` with the vectorised operand path).
     All ``a`` (and all ``b``) share dtype and memory layout.  On CPU runs :func:`mm` per problem.
     """
     import ctypes
     probs = list(problems)
     if not probs:
         return
-    if len(probs) > 8:
-        for i in range(0, len(probs), 8):
-            mm_grouped(probs[i:i + 8], trans_a, trans_b, splits, tile)
+    if len(probs) > GMAX:
+        for i in range(0, len(probs), GMAX):
+            mm_grouped(probs[i:i + GMAX], trans_a, trans_b, splits, tile)
         return
     if not probs[0]["a"].is_cuda:
         for q in probs:
+            if q.get("ncol"):
+                nc = int(q["ncol"])
+                q = dict(q, b=(q["b"][:nc] if trans_b else q["b"][:, :nc]))
             mm(q["a"], q["b"], trans_a=trans_a, trans_b=trans_b, out=q["out"],
                alpha=q.get("alpha", 1.0), beta=q.get("beta", 0.0), bias=q.get("bias"),
                row_map=q.get("row_map"))
         return
     n = len(probs)
     arrs = {k: [] for k in ("A", "lda", "B", "ldb", "C", "ldc", "M", "N", "K", "alpha", "beta",
-                            "bias", "rmap")}
+                            "bias", "rmap", "ncol")}
     keep = []
     ta = tb = None
     a_bf = b_bf = c_bf = None
@@ -177,14 +197,15 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         for k, v in (("A", A.data_ptr()), ("lda", lda), ("B", B.data_ptr()), ("ldb", ldb),
                      ("C", out.data_ptr()), ("ldc", out.stride(0)), ("M", M), ("N", N), ("K", K),
                      ("alpha", float(q.get("alpha", 1.0))), ("beta", float(q.get("beta", 0.0))),
-                     ("bias", _lib.ptr(bias)), ("rmap", _lib.ptr(rmap))):
+                     ("bias", _lib.ptr(bias)), ("rmap", _lib.ptr(rmap)),
+                     ("ncol", int(q.get("ncol", 0) or 0))):
             arrs[k].append(v)
         maxk = max(maxk, K)
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
+    if splits is None and _GROUP_SPLITS:
+        splits = _GROUP_SPLITS
     if splits is None:
-        splits = 1
-        if maxk >= 768 and t64 < _NCU // 2:
-            splits = max(1, min(8, round(maxk / 384), (4 * _NCU) // max(t64, 1)))
+        splits = _split_rule(t64, maxk)
     sp = max(1, int(splits))
     dev = probs[0]["out"].device
     slab = None
@@ -199,7 +220,8 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               (P * n)(*arrs["B"]), (L * n)(*arrs["ldb"]), (P * n)(*arrs["C"]),
               (L * n)(*arrs["ldc"]), (I * n)(*arrs["M"]), (I * n)(*arrs["N"]),
               (I * n)(*arrs["K"]), (F * n)(*arrs["alpha"]), (F * n)(*arrs["beta"]),
-              (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), 0, int(a_bf), int(b_bf), ta, tb,
+              (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), (I * n)(*arrs["ncol"]), 0,
+              int(a_bf), int(b_bf), ta, tb,
               int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.stream())
 
 

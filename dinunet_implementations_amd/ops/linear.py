@@ -2,8 +2,9 @@
 
 Forward is ONE MFMA GEMM with the bias+ReLU epilogue, reading the fp32 input windows and fp32
 master weights directly (rounded to bf16 while staging) and storing bf16 activations.  Backward
-masks the incoming gradient with the stored activations, then runs the weight-gradient GEMM
-(split-K over the B*S rows) and, only when required, the input-gradient GEMM.
+masks the incoming gradient with the stored activations, defers the weight / bias gradient
+GEMMs (``dym^T x``, ``dym^T 1``) to the end-of-backward grouped launch (``ops._grad.defer``)
+and, only when required, runs the input-gradient GEMM.
 """
 from __future__ import annotations
 
@@ -23,6 +24,8 @@ _lib.register("dn_relu_bwd_colsum", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p
 _lib.register("dn_enc_proj", [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_relu_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                              _lib.c_void_p])
 _RB_SLABS = 64
 
 
@@ -46,14 +49,25 @@ def _relu_linear_backward(ctx, dy):
     N, O = y.shape
     dy = dy.to(torch.bfloat16).contiguous()
     dym = torch.empty_like(dy)
-    ws = torch.empty(_RB_SLABS * O, dtype=torch.float32, device=dy.device)
-    # bias grad accumulated straight into .grad; weight grad by a beta=1 GEMM epilogue
-    db = _grad.grad_buffer(bias) if bias is not None else \
-        torch.empty(O, dtype=torch.float32, device=dy.device)
-    _lib.call("dn_relu_bwd_colsum", dy.data_ptr(), y.data_ptr(), dym.data_ptr(),
-              db.data_ptr(), ws.data_ptr(), N, O, int(bias is not None), _lib.stream())
-    mm(dym, x2d, trans_a=True, out=_grad.grad_buffer(weight), beta=1.0)
-    _grad.notify([weight] + ([bias] if bias is not None else []))
+    if (N * O) % 8 == 0:
+        # mask only; dW += dym^T x and db += dym^T 1 are deferred into the end-of-backward
+        # grouped launch with the LSTM's weight gradients (ops._grad.defer)
+        _lib.call("dn_relu_bwd", dy.data_ptr(), y.data_ptr(), dym.data_ptr(), N * O,
+                  _lib.stream())
+        probs = [dict(a=dym, b=x2d, out=_grad.grad_buffer(weight), beta=1.0)]
+        if bias is not None:
+            from .lstm import _ones
+            probs.append(dict(a=dym, b=_ones(N, dy.device), out=_grad.grad_buffer(bias).view(-1, 1),
+                              beta=1.0, ncol=1))
+        _grad.defer(probs, [weight] + ([bias] if bias is not None else []))
+    else:
+        ws = torch.empty(_RB_SLABS * O, dtype=torch.float32, device=dy.device)
+        db = _grad.grad_buffer(bias) if bias is not None else \
+            torch.empty(O, dtype=torch.float32, device=dy.device)
+        _lib.call("dn_relu_bwd_colsum", dy.data_ptr(), y.data_ptr(), dym.data_ptr(),
+                  db.data_ptr(), ws.data_ptr(), N, O, int(bias is not None), _lib.stream())
+        mm(dym, x2d, trans_a=True, out=_grad.grad_buffer(weight), beta=1.0)
+        _grad.notify([weight] + ([bias] if bias is not None else []))
     dx = None
     if ctx.needs_input_grad[0]:
         dx = mm(dym, weight, out_dtype=x2d.dtype)

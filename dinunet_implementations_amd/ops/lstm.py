@@ -15,10 +15,10 @@ backward
   5. ``dn_lstm_bwd``: reverse-time recurrence -> gate grads ``dpre`` (bf16, original time order).
   6. parameter grads ACCUMULATED straight into ``.grad`` (flat buffer) by GEMM epilogues with a
      row map back to the reference ``[i|f|o|g]`` layout: ``dW_ih += dpre^T x``,
-     ``dW_hh += dpre^T h_{t-1}``; bias grads from a deterministic column sum of ``dpre``.
+     ``dW_hh += dpre^T h_{t-1}``, bias grads ``+= dpre^T 1`` (all in one grouped launch).
   7. ``dx = dpre W_ih`` only when the input needs a gradient.  The weight-gradient GEMMs of (6)
-     run on the side stream beside (7) and the encoder backward that follows; the side stream
-     is joined (and the engines notified) when the autograd pass ends.
+     are deferred (``ops._grad.defer``) and issued with the encoder's as ONE grouped launch when
+     the autograd pass ends; the engines are notified then.
 
 Reference math: ``comps/icalstm/models.py:5-66`` (oracle: ``ops.reference.bilstm``).
 """
@@ -46,8 +46,6 @@ _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
                               _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_lstm_rows_per_wg", [_lib.c_int])
-_lib.register("dn_lstm_bias_grad", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
-                                    _lib.c_void_p] + [_lib.c_void_p] * 4 + [_lib.c_void_p])
 
 _ROWMAP_CACHE: Dict[Tuple[int, int, str], Tensor] = {}
 
@@ -75,6 +73,19 @@ def _row_map(Hd: int, HD: int, device) -> Tensor:
         rm = torch.where(u < Hd, g * Hd + u, torch.full_like(m, -1)).to(torch.int32).to(device)
         _ROWMAP_CACHE[key] = rm
     return rm
+
+
+_ONES = {}
+
+
+def _ones(n: int, device) -> Tensor:
+    """bf16 ones ``[n, 8]`` (8 columns: the 16-B operand path), cached per (n, device)."""
+    key = (n, str(device))
+    t = _ONES.get(key)
+    if t is None:
+        t = torch.ones(n, 8, dtype=torch.bfloat16, device=device)
+        _ONES[key] = t
+    return t
 
 
 class _BiLSTMFn(torch.autograd.Function):
@@ -156,25 +167,10 @@ class _BiLSTMFn(torch.autograd.Function):
                   dpre.data_ptr(), st)
         dpre_v = dpre[:N]
         capturing = _cap.active() is not None and ctx.modules is not None
-        # (6) parameter grads accumulated into .grad (reference layout via row map), on the side
-        # stream unless rank-dAD is capturing activations
-        overlap = not capturing
-        if overlap:
-            side = _streams.fork(dev)
-            with torch.cuda.stream(side):
-                _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
-                done = torch.cuda.Event()
-                done.record(side)
-            _streams.keep_alive(side, (dpre, x2d, hprev))
-            live = [p for p in params if p is not None]
-
-            def _join():
-                torch.cuda.current_stream(dev).wait_event(done)
-                _grad.notify(live)
-            torch.autograd.Variable._execution_engine.queue_callback(_join)
-        else:
-            _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
-            _grad.notify([p for p in params if p is not None])
+        # (6) parameter grads accumulated into .grad (reference layout via row map): queued for
+        # the end-of-backward grouped launch together with the encoder's (ops._grad.defer)
+        probs = _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
+        _grad.defer(probs, [p for p in params if p is not None])
         # (7) input grad
         dx = None
         if ctx.needs_input_grad[0]:
@@ -230,20 +226,14 @@ class _nullctx:
         return False
 
 
-def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
-    """Accumulate dW_ih, dW_hh, b_ih, b_hh gradients of every direction into ``.grad``."""
+def _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
+    """Grouped-GEMM problems accumulating dW_ih, dW_hh, b_ih, b_hh of every direction into
+    ``.grad`` (``out += dpre^T @ operand``, gate rows mapped back to the reference layout)."""
     GP = 4 * HD
     N = B * S
     Bp = hprev.shape[1]
     rmap = _row_map(Hd, HD, dev)
-    ws = torch.empty(64 * ndir * GP, dtype=torch.float32, device=dev)
-    gb = [None] * 8
-    for d in range(ndir):
-        w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
-        gb[4 * d + 1] = _grad.grad_buffer(b_ih) if b_ih is not None else None
-        gb[4 * d + 3] = _grad.grad_buffer(b_hh) if b_hh is not None else None
-    _lib.call("dn_lstm_bias_grad", dpre_v.data_ptr(), N, Hd, ndir, ws.data_ptr(),
-              _lib.ptr(gb[1]), _lib.ptr(gb[3]), _lib.ptr(gb[5]), _lib.ptr(gb[7]), _lib.stream())
+    ones = _ones(N, dev)
     probs = []
     for d in range(ndir):
         w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
@@ -251,7 +241,12 @@ def _param_grads(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
         probs.append(dict(a=dsl, b=x2d, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap))
         probs.append(dict(a=dsl, b=hprev[d].view(Bp * S, HD)[:N, :Hd],
                           out=_grad.grad_buffer(w_hh), beta=1.0, row_map=rmap))
-    mm_grouped(probs, trans_a=True)  # every direction's dW_ih and dW_hh in one launch
+        # bias grads = column sums of dpre = dpre^T @ ones: extra problems of the same launch
+        for b in (b_ih, b_hh):
+            if b is not None:
+                probs.append(dict(a=dsl, b=ones, out=_grad.grad_buffer(b).view(-1, 1), beta=1.0,
+                                  row_map=rmap, ncol=1))
+    return probs
 
 
 def bilstm(x: Tensor, params: Sequence[Tuple[Tensor, Tensor, Tensor, Tensor]],

@@ -34,7 +34,18 @@ def _entry(rank, world, port, fn, args, outdir):
         pickle.dump(res, f)
 
 
-def run_world(fn, world, *args):
+def run_world(fn, world, *args, _retry=True):
+    try:
+        return _run_world(fn, world, *args)
+    except AssertionError as e:
+        # free_port() -> bind is racy against other processes on the host: retry once on a
+        # rendezvous port collision, never on a real failure
+        if _retry and ("Address already in use" in str(e) or "EADDRINUSE" in str(e)):
+            return run_world(fn, world, *args, _retry=False)
+        raise
+
+
+def _run_world(fn, world, *args):
     outdir = tempfile.mkdtemp()
     # spawn (not fork): the pytest parent has live OpenMP/autograd threads; workers must be
     # module-level functions of an importable test module

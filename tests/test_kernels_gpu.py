@@ -184,6 +184,56 @@ def test_ica_model_gpu_matches_cpu_oracle():
     assert rel(out.cpu(), ref) < 3e-2
 
 
+def test_lstm_bias_grads_deterministic_and_accumulating():
+    """LSTM bias grads ride in the weight-gradient grouped GEMM (dpre^T @ ones, ncol = 1):
+    bitwise reproducible, accumulated into .grad across backward calls, b_ih == b_hh."""
+    from dinunet_implementations_amd.ops import lstm as L
+    B, S, I, Hd = 33, 11, 64, 174
+    ps = _lstm_params(I, Hd, 2)
+    x = torch.randn(B, S, I, device=DEV)
+    grads = []
+    for rep in range(2):
+        out, _ = L.bilstm(x, ps, reduce="mean")
+        out.sum().backward()
+        grads.append([p[1].grad.clone() for p in ps] + [p[3].grad.clone() for p in ps])
+    torch.cuda.synchronize()
+    for a, b in zip(*grads):
+        assert torch.allclose(b, 2 * a, rtol=1e-5, atol=1e-6)
+    for p in ps:
+        assert torch.equal(p[1].grad, p[3].grad)
+    runs = []
+    for rep in range(2):
+        for p in ps:
+            for t in p:
+                t.grad = None
+        out, _ = L.bilstm(x, ps, reduce="mean")
+        out.sum().backward()
+        runs.append([p[1].grad.clone() for p in ps])
+    assert all(torch.equal(a, b) for a, b in zip(*runs))
+
+
+def test_gemm_grouped_ncol_stores_only_leading_columns():
+    from dinunet_implementations_amd.ops.gemm import mm_grouped
+    a = torch.randn(300, 96, device=DEV).to(torch.bfloat16)
+    ones = torch.ones(300, 8, device=DEV, dtype=torch.bfloat16)
+    out = torch.full((96, 1), 2.0, device=DEV)
+    guard = torch.full((96, 8), 7.0, device=DEV)
+    w = torch.randn(300, 64, device=DEV).to(torch.bfloat16)
+    gw = torch.zeros(96, 64, device=DEV)
+    for splits in (1, 3):
+        o = out.clone()
+        g = guard.clone()
+        mm_grouped([dict(a=a, b=w, out=gw, beta=0.0),
+                    dict(a=a, b=ones, out=o, beta=1.0, ncol=1),
+                    dict(a=a, b=ones, out=g[:, :1], beta=0.0, ncol=1)], trans_a=True,
+                   splits=splits)
+        ref = a.float().sum(0, keepdim=True).t()
+        assert torch.allclose(o, 2.0 + ref, rtol=1e-4, atol=1e-3)
+        assert torch.allclose(g[:, :1], ref, rtol=1e-4, atol=1e-3)
+        assert torch.equal(g[:, 1:], guard[:, 1:]), "columns >= ncol must not be written"
+        assert torch.allclose(gw, a.float().t() @ w.float(), rtol=1e-3, atol=1e-2)
+
+
 @pytest.mark.parametrize("br", ["4", "8", "16"])
 def test_lstm_rows_per_workgroup_variants(br, monkeypatch):
     """Every rows-per-workgroup instantiation (column redistribution) matches the oracle."""
