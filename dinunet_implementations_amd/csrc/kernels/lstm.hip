@@ -492,18 +492,35 @@ struct LstmParams {
   const float* bhh[2];
 };
 
+// extra fp32 -> bf16 casts riding in the pack launch (e.g. the encoder weights, whose GEMM
+// goes to hipBLASLt with bf16 operands): saves a launch at the head of every step
+constexpr int PACK_CASTS = 4;
+struct CastJobs {
+  const float* src[PACK_CASTS];
+  bf16* dst[PACK_CASTS];
+  int n[PACK_CASTS];
+  int cnt;
+};
+
 __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
                                  bf16* __restrict__ wih_p,    // [ndir*4HD][I]
                                  float* __restrict__ bias_p,  // [ndir*4HD]
                                  bf16* __restrict__ whh_p,    // [ndir][4HD][HD]
-                                 bf16* __restrict__ whhT_p) { // [ndir][HD][4HD]
+                                 bf16* __restrict__ whhT_p,   // [ndir][HD][4HD]
+                                 CastJobs cj) {
   // 32-bit index math throughout (every extent < 2^31): 64-bit div/mod per element made this
   // ~1M-element repack a 6 us kernel at the head of every step
   const int GP = 4 * HD;
   const int n_wih = ndir * GP * I, n_b = ndir * GP, n_whh = ndir * GP * HD;
-  const int total = n_wih + n_b + 2 * n_whh;
+  const int n_pack = n_wih + n_b + 2 * n_whh;
+  int total = n_pack;
+  for (int j = 0; j < cj.cnt; ++j) total += cj.n[j];
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-    if (idx < n_wih) {
+    if (idx >= n_pack) {
+      int r = idx - n_pack, j = 0;
+      while (j + 1 < cj.cnt && r >= cj.n[j]) r -= cj.n[j++];
+      cj.dst[j][r] = (bf16)cj.src[j][r];
+    } else if (idx < n_wih) {
       const int r = idx / I, k = idx - r * I;
       const int d = r / GP, m = r - d * GP, u = m >> 2, g = m & 3;
       wih_p[idx] = (bf16)(u < Hd ? p.wih[d][(g * Hd + u) * I + k] : 0.f);
@@ -641,14 +658,25 @@ DN_API int dn_lstm_padded_hidden(int Hd) {
 DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0, const float* bhh0,
                         const float* wih1, const float* bih1, const float* whh1, const float* bhh1,
                         int I, int Hd, int ndir, void* wih_p, float* bias_p, void* whh_p,
-                        void* whhT_p, hipStream_t st) {
+                        void* whhT_p, int ncast, const float* const* cast_src,
+                        void* const* cast_dst, const int* cast_n, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
-  if (!HD || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
+  if (!HD || ndir < 1 || ndir > 2 || ncast < 0 || ncast > PACK_CASTS) return DN_BAD_SHAPE;
   LstmParams p{{wih0, wih1}, {bih0, bih1}, {whh0, whh1}, {bhh0, bhh1}};
-  const long total = ndir * 4L * HD * I + ndir * 4L * HD + 2L * ndir * 4 * HD * HD;
+  CastJobs cj{};
+  cj.cnt = ncast;
+  long total = ndir * 4L * HD * I + ndir * 4L * HD + 2L * ndir * 4 * HD * HD;
+  for (int j = 0; j < ncast; ++j) {
+    if (cast_n[j] <= 0) return DN_BAD_SHAPE;
+    cj.src[j] = cast_src[j];
+    cj.dst[j] = (bf16*)cast_dst[j];
+    cj.n[j] = cast_n[j];
+    total += cast_n[j];
+  }
+  if (total >= (1L << 31)) return DN_BAD_SHAPE;
   const int blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
   hipLaunchKernelGGL(lstm_pack_kernel, dim3(blocks), dim3(256), 0, st, p, I, Hd, HD, ndir,
-                     (bf16*)wih_p, bias_p, (bf16*)whh_p, (bf16*)whhT_p);
+                     (bf16*)wih_p, bias_p, (bf16*)whh_p, (bf16*)whhT_p, cj);
   return dn_launch_status();
 }
 

@@ -75,12 +75,13 @@ class LSTM(nn.Module):
                 and ops.lstm_supported(x.shape[0], self.input_size, self.hidden_size,
                                        self.num_direction))
 
-    def prepack(self, device, side: bool = True):
+    def prepack(self, device, side: bool = True, casts=(), cast_out=None):
         """Pack the LSTM weights into the kernel layouts ahead of the forward (on the side
-        stream when ``side``)."""
+        stream when ``side``); ``casts`` get bf16 copies from the same launch."""
         from ..ops.lstm import pack_params
         flat = [t for cell in self.lstms for t in cell.params()]
-        return pack_params(flat, self.input_size, device, side=side)
+        return pack_params(flat, self.input_size, device, side=side, casts=casts,
+                           cast_out=cast_out)
 
     def forward(self, x: torch.Tensor, h=None, reduce: str = "none", packed=None, xp=None):
         """``reduce='none'`` returns ``(hidden_seq [B,S,H*dirs], (h, c))`` like the reference;
@@ -170,10 +171,18 @@ class ICALstm(nn.Module):
         if self.use_fused and x.is_cuda and self.lstm.fused_ok(x) and ops.capture.active() is None:
             # in-stream: as a side-stream branch of the step graph the pack saved nothing (it
             # fills the chip anyway) and added a cross-queue wait before the input projection
-            self._packed = self.lstm.prepack(x.device, side=False)
+            lin = self.encoder[0]
+            casts = []
+            want = lin.bias is not None and ops.PLAIN_BLAS
+            if want and x.dtype == torch.float32:
+                # eager callers: same operand values as the step graph's bf16 input (every GEMM
+                # rounds to bf16 while staging), so eager and replayed steps agree
+                x = x.to(torch.bfloat16)
+            self._packed = self.lstm.prepack(
+                x.device, side=False, casts=(lin.weight, lin.bias) if want else (),
+                cast_out=casts)
             B, S = x.shape[:2]
             flat = x.reshape(B * S, -1)
-            lin = self.encoder[0]
             wih_p = self._packed[0]
             if _FUSED_ENCPROJ and ops.enc_proj_supported(flat, lin.weight, lin.bias, wih_p):
                 # encoder + LSTM input projection in ONE launch (csrc/kernels/encproj.hip);
@@ -181,6 +190,10 @@ class ICALstm(nn.Module):
                 # row-chunk workgroups each stream all weights: per-CU bandwidth bound)
                 enc, self._xp = ops.encoder_projection(flat, lin.weight, lin.bias, wih_p,
                                                        module=lin)
+                return enc.view(B, S, -1)
+            if casts:
+                enc = ops.linear_bias_relu(flat, lin.weight, lin.bias, module=lin,
+                                           bf16_params=tuple(casts))
                 return enc.view(B, S, -1)
         return self.encode(x)
 

@@ -2,7 +2,7 @@
 (``_native/libdinunet_kernels.so``); on CPU they run the reference math (``ops.reference``)."""
 from . import _lib, capture, reference
 from ._lib import native_available
-from .gemm import mm
+from .gemm import PLAIN_BLAS, mm, mm_grouped, mm_plain
 from .linear import encoder_projection, enc_proj_supported, linear_bias_relu
 from .lstm import bilstm as _bilstm_fused, lstm_supported, padded_hidden
 from .optim import FlatParams, FusedAdam, cast_bf16_to_f32, cast_f32_to_bf16, step_prologue

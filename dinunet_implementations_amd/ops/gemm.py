@@ -52,6 +52,7 @@ def _layout(t: Tensor, rows_first: bool):
 
 # tuning override of the grouped launches' split-K (0 = heuristic); tools/gpu sweeps
 _GROUP_SPLITS = int(__import__("os").environ.get("DINUNET_GROUP_SPLITS", "0"))
+_GROUP_TILE = int(__import__("os").environ.get("DINUNET_GROUP_TILE", "-1"))
 
 
 def choose_tiling(M: int, N: int, K: int):
@@ -204,6 +205,8 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
     if splits is None and _GROUP_SPLITS:
         splits = _GROUP_SPLITS
+    if tile is None and _GROUP_TILE >= 0:
+        tile = _GROUP_TILE
     if splits is None:
         splits = _split_rule(t64, maxk)
     sp = max(1, int(splits))

@@ -16,7 +16,7 @@ import torch.nn as nn
 from . import _grad
 from . import _lib
 from . import capture as _cap
-from .gemm import mm
+from .gemm import PLAIN_BLAS, mm
 
 _lib.register("dn_relu_bwd_colsum", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                                      _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
@@ -31,8 +31,14 @@ _RB_SLABS = 64
 
 class _LinearBiasReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2d, weight, bias, module):
-        y = mm(x2d, weight, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16)
+    def forward(ctx, x2d, weight, bias, module, w_bf16=None, b_bf16=None):
+        if w_bf16 is not None:
+            # bf16 input and bf16 weight/bias copies (made by the LSTM pack launch): hipBLASLt
+            # with its fused RELU_BIAS epilogue, 11.2 us vs 19.7 us for csrc/kernels/gemm.hip at
+            # 3136x256x1000 (tools/enc_gemm_probe.py, rocprofv3 on MI355X)
+            y = torch._addmm_activation(b_bf16, x2d, w_bf16.t())
+        else:
+            y = mm(x2d, weight, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16)
         ctx.save_for_backward(x2d, y)
         ctx.weight, ctx.bias = weight, bias
         ctx.module = module
@@ -40,7 +46,7 @@ class _LinearBiasReLU(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        return _relu_linear_backward(ctx, dy)
+        return _relu_linear_backward(ctx, dy) + (None, None)
 
 
 def _relu_linear_backward(ctx, dy):
@@ -119,9 +125,16 @@ def encoder_projection(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tens
 
 
 def linear_bias_relu(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
-                     module: Optional[nn.Module] = None) -> torch.Tensor:
+                     module: Optional[nn.Module] = None,
+                     bf16_params: Optional[tuple] = None) -> torch.Tensor:
+    """``relu(x W^T + b)`` -> bf16.  ``bf16_params = (W_bf16, b_bf16)``: rounded copies of the
+    parameters made for this step; with a bf16 input the forward then runs on hipBLASLt."""
     if not x2d.is_cuda:
         return torch.relu(torch.nn.functional.linear(x2d, weight, bias))
     if not _lib.native_available():
         raise RuntimeError("linear_bias_relu on GPU needs the gfx950 kernel library")
-    return _LinearBiasReLU.apply(x2d.contiguous(), weight, bias, module)
+    wb = bb = None
+    if (bf16_params is not None and bias is not None and x2d.dtype == torch.bfloat16
+            and PLAIN_BLAS):
+        wb, bb = bf16_params
+    return _LinearBiasReLU.apply(x2d.contiguous(), weight, bias, module, wb, bb)

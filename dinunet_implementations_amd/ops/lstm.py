@@ -24,6 +24,8 @@ Reference math: ``comps/icalstm/models.py:5-66`` (oracle: ``ops.reference.bilstm
 """
 from __future__ import annotations
 
+import ctypes
+
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -36,7 +38,8 @@ from .gemm import mm, mm_grouped, mm_plain
 
 Tensor = torch.Tensor
 
-_lib.register("dn_lstm_pack", [_lib.c_void_p] * 8 + [_lib.c_int] * 3 + [_lib.c_void_p] * 5)
+_lib.register("dn_lstm_pack", [_lib.c_void_p] * 8 + [_lib.c_int] * 3 + [_lib.c_void_p] * 4
+              + [_lib.c_int] + [_lib.c_void_p] * 3 + [_lib.c_void_p])
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
@@ -185,11 +188,14 @@ class _BiLSTMFn(torch.autograd.Function):
         return (dx, None, None, None, None) + (None,) * len(params)
 
 
-def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = False):
+def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = False,
+                casts: Sequence[Tensor] = (), cast_out: Optional[List[Tensor]] = None):
     """``dn_lstm_pack``: fp32 reference-layout params -> bf16 kernel layouts + fused bias.
 
     With ``side=True`` the pack runs on the side stream (it depends only on the parameters, so
     it overlaps the encoder GEMM) and the returned event orders the consumer after it.
+    ``casts`` (<= 4 fp32 tensors) are rounded to bf16 by the same launch; the copies are
+    appended to ``cast_out``.
     """
     ndir = len(params) // 4
     Hd = params[2].shape[1]
@@ -204,8 +210,19 @@ def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = 
         whh_p = torch.empty(ndir, GP, HD, dtype=torch.bfloat16, device=device)
         whhT_p = torch.empty(ndir, HD, GP, dtype=torch.bfloat16, device=device)
         ps = [p.detach().contiguous() for p in params] + [None] * (8 - len(params))
+        if len(casts) > 4:
+            raise ValueError("pack_params: at most 4 extra casts")
+        srcs = [c.detach().contiguous() for c in casts]
+        dsts = [torch.empty(c.shape, dtype=torch.bfloat16, device=device) for c in srcs]
+        nc = len(srcs)
+        P, I_ = ctypes.c_void_p, ctypes.c_int
         _lib.call("dn_lstm_pack", *[_lib.ptr(p) for p in ps], I, Hd, ndir, wih_p.data_ptr(),
-                  bias_p.data_ptr(), whh_p.data_ptr(), whhT_p.data_ptr(), _lib.stream())
+                  bias_p.data_ptr(), whh_p.data_ptr(), whhT_p.data_ptr(), nc,
+                  (P * max(nc, 1))(*[c.data_ptr() for c in srcs]),
+                  (P * max(nc, 1))(*[d.data_ptr() for d in dsts]),
+                  (I_ * max(nc, 1))(*[c.numel() for c in srcs]), _lib.stream())
+        if cast_out is not None:
+            cast_out.extend(dsts)
         ev = None
         if side:
             ev = torch.cuda.Event()

@@ -212,6 +212,32 @@ def test_lstm_bias_grads_deterministic_and_accumulating():
     assert all(torch.equal(a, b) for a, b in zip(*runs))
 
 
+def test_encoder_hipblaslt_path_matches_hand_gemm_and_pack_casts():
+    """The ICA encoder forward on hipBLASLt (bf16 copies of W, b made by the LSTM pack launch)
+    matches the hand-written bias+ReLU GEMM; the pack's extra casts are exact bf16 roundings."""
+    from dinunet_implementations_amd.ops import linear_bias_relu
+    from dinunet_implementations_amd.ops.lstm import pack_params
+    torch.manual_seed(0)
+    x = torch.randn(300, 1000, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(256, 1000, device=DEV) * 0.03).requires_grad_()
+    b = torch.randn(256, device=DEV).requires_grad_()
+    ps = [t.to(DEV) for t in _lstm_params(256, 64, 1)[0]]
+    out = []
+    pack_params(ps, 256, torch.device(DEV), casts=(w, b), cast_out=out)
+    assert torch.equal(out[0], w.detach().to(torch.bfloat16))
+    assert torch.equal(out[1], b.detach().to(torch.bfloat16))
+    y_lt = linear_bias_relu(x, w, b, bf16_params=tuple(out))
+    y_hand = linear_bias_relu(x, w, b)
+    assert y_lt.dtype == y_hand.dtype == torch.bfloat16
+    assert rel(y_lt, y_hand) < 1e-2
+    g = torch.randn_like(y_lt.float())
+    (y_lt.float() * g).sum().backward()
+    gw, gb = w.grad.clone(), b.grad.clone()
+    w.grad = b.grad = None
+    (y_hand.float() * g).sum().backward()
+    assert rel(gw, w.grad) < 2e-2 and rel(gb, b.grad) < 2e-2
+
+
 def test_gemm_grouped_ncol_stores_only_leading_columns():
     from dinunet_implementations_amd.ops.gemm import mm_grouped
     a = torch.randn(300, 96, device=DEV).to(torch.bfloat16)
@@ -297,33 +323,49 @@ def test_encoder_projection_fused_matches_two_gemms(N, KX, N2):
 
 def test_ica_step_with_fused_encoder_projection_matches_unfused():
     """ICALstm at input_size 256 with a bf16 batch takes the fused encoder+projection launch;
-    loss and every gradient match the two-GEMM path (same bf16 operand rounding)."""
+    the default path runs the encoder on hipBLASLt (bf16-rounded bias).  Both match the fp32
+    CPU oracle (same bf16 input values) and each other; the bf16 rounding of recurrent states
+    makes small LSTM gradients differ by a few percent between two valid bf16 paths."""
+    import copy
     from dinunet_implementations_amd.models import ICALstm
     from dinunet_implementations_amd.models import ica as ica_mod
     from dinunet_implementations_amd.ops import linear as lin_mod
-    ica_mod._FUSED_ENCPROJ = True  # opt-in path (see models/ica.py)
     torch.manual_seed(0)
-    m = ICALstm(input_size=256, hidden_size=128, num_comps=20, window_size=10).to(DEV).train()
+    m = ICALstm(input_size=256, hidden_size=128, num_comps=20, window_size=10).train()
     m.classifier[0].p = 0.0
+    mc = copy.deepcopy(m)
+    m = m.to(DEV)
     x = torch.randn(8, 12, 20, 10, device=DEV).to(torch.bfloat16)
     y = torch.randint(0, 2, (8,), device=DEV)
+    _, lref, _ = mc.forward_loss(x.float().cpu(), y.cpu())
+    lref.backward()
+    gref = [p.grad.clone() for p in mc.parameters()]
     grads = []
-    for fused in (True, False):
-        for p in m.parameters():
-            p.grad = None
-        orig = lin_mod.enc_proj_supported
-        if not fused:
-            import dinunet_implementations_amd.ops as ops_pkg
-            ops_pkg.enc_proj_supported = lambda *a, **k: False
-        try:
-            _, loss, _ = m.forward_loss(x, y)
-            loss.backward()
-        finally:
-            import dinunet_implementations_amd.ops as ops_pkg
-            ops_pkg.enc_proj_supported = orig
-        grads.append((float(loss), [p.grad.clone() for p in m.parameters()]))
-    ica_mod._FUSED_ENCPROJ = False
+    ica_mod._FUSED_ENCPROJ = True  # opt-in path (see models/ica.py)
+    try:
+        for fused in (True, False):
+            for p in m.parameters():
+                p.grad = None
+            orig = lin_mod.enc_proj_supported
+            if not fused:
+                import dinunet_implementations_amd.ops as ops_pkg
+                ops_pkg.enc_proj_supported = lambda *a, **k: False
+            try:
+                _, loss, _ = m.forward_loss(x, y)
+                loss.backward()
+            finally:
+                import dinunet_implementations_amd.ops as ops_pkg
+                ops_pkg.enc_proj_supported = orig
+            grads.append((float(loss.detach()), [p.grad.clone() for p in m.parameters()]))
+    finally:
+        ica_mod._FUSED_ENCPROJ = False
     (l1, g1), (l2, g2) = grads
-    assert abs(l1 - l2) < 1e-3
-    for a, b in zip(g1, g2):
-        assert rel(a, b) < 2e-2
+    assert abs(l1 - l2) < 1e-3 and abs(l1 - float(lref)) < 1e-2
+    for a, b, r in zip(g1, g2, gref):
+        if r.norm() < 1e-6:  # analytically ~0 (bias in front of BatchNorm): noise either way
+            assert a.norm() < 1e-5 and b.norm() < 1e-5
+            continue
+        assert rel(a.cpu(), r) < 0.15 and rel(b.cpu(), r) < 0.15  # bf16 end to end
+        assert rel(a, b) < 8e-2
+
+

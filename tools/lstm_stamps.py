@@ -33,7 +33,7 @@ def main():
     from dinunet_implementations_amd.ops.lstm import padded_hidden
     lib = ctypes.CDLL(OUT)
     V, I_, F, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
-    lib.dn_lstm_pack.argtypes = [V] * 8 + [I_] * 3 + [V] * 5
+    lib.dn_lstm_pack.argtypes = [V] * 8 + [I_] * 3 + [V] * 4 + [I_, V, V, V, V]
     lib.dn_lstm_fwd.argtypes = [V, V, V, I_, I_, I_, I_, V, V, V, V, F, V, V, I_, V]
     lib.dn_lstm_bwd.argtypes = [V, V, V, V, L, L, F, V, V, I_, I_, I_, I_, V, V]
     lib.dn_set_stamp_buf.argtypes = [V]
@@ -55,7 +55,7 @@ def main():
     whhT_p = torch.empty(ndir, HD, GP, dtype=torch.bfloat16, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     lib.dn_lstm_pack(*[p.data_ptr() for p in ps], I, Hd, ndir, wih_p.data_ptr(), bias_p.data_ptr(),
-                     whh_p.data_ptr(), whhT_p.data_ptr(), st)
+                     whh_p.data_ptr(), whhT_p.data_ptr(), 0, None, None, None, st)
     x = torch.randn(B * S, I, device=dev).to(torch.bfloat16)
     xp = mm(x, wih_p, trans_b=True)
     c_save = torch.empty(ndir, Bp, S, HD, device=dev)
