@@ -112,7 +112,9 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+    # DINUNET_BACKEND=gloo rehearses the multi-site GPU path with several ranks on ONE GPU
+    # (RCCL needs one device per rank); production multi-GPU runs use nccl (= RCCL)
+    be = backend or os.environ.get("DINUNET_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
     pg = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
