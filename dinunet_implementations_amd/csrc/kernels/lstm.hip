@@ -96,10 +96,12 @@ template <> struct LdsSplit<192, 4> { static constexpr int FWD_MT = 0, BWD_KS = 
 template <> struct LdsSplit<192, 8> { static constexpr int FWD_MT = 0, BWD_KS = 6; };
 template <> struct LdsSplit<192, 16> { static constexpr int FWD_MT = 1, BWD_KS = 9; };
 
-// Column of the all-zero 16 B slot (row BR of the h / dpre exchange tile) that MFMA lanes of
-// padded batch columns read: its banks (16 + 32 = 48..51 for every HD the kernels take) are not
-// touched by the valid lanes of the same ds_read_b128 lane group.
-constexpr int ZCOL = 64;
+// MFMA columns >= BR (padded batch columns of the 16-wide B operand) are never consumed: the
+// row_gather / slot redistribution only takes columns < BR.  Their lanes therefore read row
+// n % BR -- the same 16 B as a valid lane, an LDS broadcast -- so every lane group of a
+// ds_read_b128 touches only BR distinct addresses on disjoint banks (rows are 4 banks apart).
+// The former all-zero slot (row BR, column 64) shared banks with valid rows at some k-steps:
+// rocprofv3 SQ_LDS_BANK_CONFLICT was ~90% of SQ_ACTIVE_INST_LDS in the backward.
 
 // BR = batch rows per workgroup (4, 8 or 16).  The recurrent MFMA always computes 16 columns;
 // columns >= BR are zero.  For the gate phase the BR valid columns are redistributed over all
@@ -132,7 +134,10 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   constexpr int NT = NW * 64;
   constexpr int MT = 4 * UG;   // m-tiles per wave
   constexpr int KS = HD / 32;
-  constexpr int LDH = HD + 8;  // +16 B per row: the 16 rows land on distinct bank quads
+  // row stride = 16 or 48 dwords mod 64 banks (HD % 64 == 0): the 4 rows x 4 k-quads of a
+  // ds_read_b128 lane group land on 16 distinct bank quads (HD + 8 left rows 4 banks apart,
+  // colliding with the k-quad offsets)
+  constexpr int LDH = HD + 32;
   constexpr int NLM = UG == 1 ? LdsSplit<HD, BR>::FWD_MT : 0, NRM = MT - NLM;
   constexpr int G16 = 16 / BR, NSL1 = BR / 4, NSL = UG * NSL1;
   constexpr int EPT = BR * HD / NT;  // h_{t-1} copy: elements per thread
@@ -211,13 +216,9 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      // columns >= BR must be zero: those lanes read one all-zero 16 B slot (row BR is never
-      // written) instead of being exec-masked -- every lane group of ds_read_b128 holds valid
-      // lanes anyway, so masking saved no LDS cycle but made the compiler branch and drain
-      // lgkmcnt before every MFMA; unmasked, the reads of later k-steps issue ahead
-      const bool hv = BR == 16 || n < BR;
-      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(
-          &hbuf[cur][hv ? n : (BR & 15)][hv ? 32 * ks + 8 * q : ZCOL]);
+      // unmasked (exec-masking made the compiler branch and drain lgkmcnt before every MFMA):
+      // lanes of padded columns re-read a valid row, see above
+      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
       for (int mt = 0; mt < NRM; ++mt) acc[mt] = mfma16(wf[mt][ks], hb, acc[mt]);
 #pragma unroll
@@ -316,7 +317,7 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
                 int B, int S, int Hd, int ndir,
                 bf16* __restrict__ dpre) {          // [Bp*S][ndir][4*HD] permuted, original time
   constexpr int KS = 4 * HD / 32;
-  constexpr int LDD = 4 * HD + 8;
+  constexpr int LDD = 4 * HD + 32;  // 16 dwords mod 64 banks: see LDH in the forward
   constexpr int NLK = UG == 1 ? LdsSplit<HD, BR>::BWD_KS : 0, NRK = KS - NLK;
   constexpr int NW = HD / (16 * UG);
   constexpr int NT = NW * 64;
@@ -407,9 +408,8 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     for (int g = 0; g < UG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const bool dv = BR == 16 || n < BR;  // see the forward: unmasked zero-slot reads
-      const bf16x8 db = *reinterpret_cast<const bf16x8*>(
-          &dbuf[cur][dv ? n : (BR & 15)][dv ? 32 * ks + 8 * q : ZCOL]);
+      // see the forward: padded columns read (broadcast) a valid row; never consumed
+      const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
       for (int g = 0; g < UG; ++g)
         acc[g] = mfma16(ks < NRK ? af[g][ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane],
