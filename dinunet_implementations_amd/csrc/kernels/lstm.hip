@@ -91,6 +91,9 @@ __device__ __forceinline__ float row_gather(const float (&v)[16 / BR]) {
 // At BR = 4 / 8 a lane owns 1-2 gate slots, which leaves room for all of W_hh in VGPRs in the
 // forward and all but 4 k-steps of W_hh^T in the backward (whose exchange-tile reads run ahead
 // of the MFMA chain and need the registers): spill-free at 168.
+#ifndef BWD_CHAINS
+#define BWD_CHAINS 2
+#endif
 template <int HD, int BR> struct LdsSplit { static constexpr int FWD_MT = 0, BWD_KS = 0; };
 template <> struct LdsSplit<192, 4> { static constexpr int FWD_MT = 0, BWD_KS = 4; };
 template <> struct LdsSplit<192, 8> { static constexpr int FWD_MT = 0, BWD_KS = 6; };
@@ -403,17 +406,31 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
         dx[s] += dhT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s];
       }
     }
-    f32x4 acc[UG];
+    // K = 4*HD runs as BWD_CHAINS independent accumulator chains per unit group (summed after
+    // the loop): one chain of 24 dependent MFMAs left the SIMD waiting on its own results
+    constexpr int NCH = BWD_CHAINS;
+    f32x4 acc[UG], accp[UG][NCH];
 #pragma unroll
-    for (int g = 0; g < UG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < UG; ++g)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) accp[g][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       // see the forward: padded columns read (broadcast) a valid row; never consumed
       const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
       for (int g = 0; g < UG; ++g)
-        acc[g] = mfma16(ks < NRK ? af[g][ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane],
-                        db, acc[g]);
+        accp[g][ks % NCH] = mfma16(
+            ks < NRK ? af[g][ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db,
+            accp[g][ks % NCH]);
+    }
+#pragma unroll
+    for (int g = 0; g < UG; ++g) {
+      acc[g] = accp[g][0];
+#pragma unroll
+      for (int c = 1; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[g][j] += accp[g][c][j];
     }
     float dhr[NSL];
     if constexpr (BR == 16) {

@@ -18,6 +18,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "_native", "libdinunet_kernels.so")
+# tuning: a variant build of the same sources (tools/build_variant.py) in place of the default
+LIB_PATH = os.environ.get("DINUNET_KERNEL_LIB") or LIB_PATH
 
 _lib: Optional[ctypes.CDLL] = None
 _lock = threading.Lock()
