@@ -186,10 +186,11 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   float* csv = c_save + hplane + (long)b * S * HD;
 
   float c[NSL], hs[NSL], hl[NSL];
-  f32x4 xn[NSL];
+  f32x4 xn[NSL], bbr[NSL];
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
     c[s] = hs[s] = hl[s] = 0.f;
+    if constexpr (NSL == 1) bbr[s] = *reinterpret_cast<const f32x4*>(&bias_s[4 * uu[s]]);
     const int tau0 = dir == 0 ? 0 : S - 1;
     xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau0 * rowX + 4 * uu[s]);
   }
@@ -204,6 +205,16 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
     const int tau = dir == 0 ? t : S - 1 - t;
     const int t1 = t + 1 < S ? t + 1 : t;
     const int tau1 = dir == 0 ? t1 : S - 1 - t1;
+    // step t+1's projection, requested before this step's MFMAs: its address math and issue
+    // stay off the gate phase, which is the tail of the step's critical path
+    // (one gate slot per lane only: at BR >= 8 the extra registers spill)
+    constexpr bool EARLY = NSL == 1;
+    f32x4 xnn[NSL];
+    if constexpr (EARLY) {
+#pragma unroll
+      for (int s = 0; s < NSL; ++s)
+        xnn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 4 * uu[s]);
+    }
     // h_{t-1} (the tile every wave reads below) -> global for the weight-gradient GEMMs
     if constexpr (EPT == 4) {
       *reinterpret_cast<bf16x4*>(hcp + (long)tau * HD) = *reinterpret_cast<const bf16x4*>(&hbuf[cur][cp_r][cp_c]);
@@ -253,7 +264,7 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
 #pragma unroll
     for (int s = 0; s < NSL; ++s) {
       const int u = uu[s];
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(&bias_s[4 * u]);
+      const f32x4 bb = EARLY ? bbr[s] : *reinterpret_cast<const f32x4*>(&bias_s[4 * u]);
       const float p0 = pa[s][0] + xn[s][0] + bb[0];
       const float p1 = pa[s][1] + xn[s][1] + bb[1];
       const float p2 = pa[s][2] + xn[s][2] + bb[2];
@@ -261,8 +272,8 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
       // the gate pre-activations x W_ih^T + h W_hh^T + b, in place of the projection they were
       // built from: the backward reads them instead of re-running a time-parallel GEMM
       if (wpre) *reinterpret_cast<f32x4*>(xrow + (long)tau * rowX + 4 * u) = f32x4{p0, p1, p2, p3};
-      // consumed: issue step t+1's projection (hidden by its MFMA phase)
-      xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 4 * u);
+      if constexpr (EARLY) xn[s] = xnn[s];
+      else xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 4 * u);
       const float gi = dn_sigmoid(dn_sigmoid(p0));
       const float gf = dn_sigmoid(dn_sigmoid(p1));
       const float go = dn_sigmoid(dn_sigmoid(p2));
@@ -390,6 +401,23 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     STAMP(ts0);
 #endif
     const int tau = dir == 0 ? t : S - 1 - t;
+    // step t-1's pre-activations and c_{t-2}, requested before this step's MFMAs (their
+    // address math and issue stay off the gate phase at the tail of the step)
+    const int t1 = t > 0 ? t - 1 : 0;
+    const int tau1 = dir == 0 ? t1 : S - 1 - t1;
+    const int t2 = t > 1 ? t - 2 : 0;
+    const int tau2 = dir == 0 ? t2 : S - 1 - t2;
+    // (one gate slot per lane, no per-step dh loads only: otherwise the registers spill)
+    constexpr bool EARLY = NSL == 1 && !DSEQ;
+    f32x4 pnn[NSL];
+    float cpnn[NSL];
+    if constexpr (EARLY) {
+#pragma unroll
+      for (int s = 0; s < NSL; ++s) {
+        pnn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
+        cpnn[s] = crow[(long)tau2 * HD + uu[s]];
+      }
+    }
     float dx[NSL];
 #pragma unroll
     for (int s = 0; s < NSL; ++s) {
@@ -450,17 +478,17 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     STAMP(ts1);
 #endif
     const int nxt = cur ^ 1;
-    const int t1 = t > 0 ? t - 1 : 0;
-    const int tau1 = dir == 0 ? t1 : S - 1 - t1;
-    const int t2 = t > 1 ? t - 2 : 0;
-    const int tau2 = dir == 0 ? t2 : S - 1 - t2;
 #pragma unroll
     for (int s = 0; s < NSL; ++s) {
       const f32x4 pc = pn[s];
       const float cp = t > 0 ? cpn[s] : 0.f;
-      // consumed: issue step t-1's pre and c_{t-2} (hidden by the next MFMA phase)
-      pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
-      cpn[s] = crow[(long)tau2 * HD + uu[s]];
+      if constexpr (EARLY) {
+        pn[s] = pnn[s];
+        cpn[s] = cpnn[s];
+      } else {  // consumed: issue step t-1's pre and c_{t-2} (hidden by the next MFMA phase)
+        pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
+        cpn[s] = crow[(long)tau2 * HD + uu[s]];
+      }
       const float si = dn_sigmoid(pc[0]), sf = dn_sigmoid(pc[1]), so = dn_sigmoid(pc[2]);
       const float gi = dn_sigmoid(si), gf = dn_sigmoid(sf), go = dn_sigmoid(so);
       const float gg = dn_tanh(pc[3]);
