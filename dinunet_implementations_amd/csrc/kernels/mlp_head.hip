@@ -55,6 +55,7 @@ struct HLayer {
   int S_z;   // row stride of the output-gradient image                = rup32(out) + 8
   int Np;    // rup32(out)
   long a_off, xhat_off, rstd_off, dz_off;  // byte offsets into the workspace
+  long st_off;  // stash of the bias / BatchNorm grads [gb | ggamma | gbeta] (fused fwd+bwd1)
 };
 
 struct HArgs {
@@ -425,12 +426,12 @@ head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
 // ---------------------------------------------------------------------------------------------
 // fwd1: layers 1.. and the loss in one workgroup.
 template <int MT, bool VECW>
-__global__ void __launch_bounds__(HS_NT)
-head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ out,
-                 float* __restrict__ loss, long long* __restrict__ pred,
-                 unsigned long long* __restrict__ rng, char* __restrict__ ws,
-                 unsigned long long* __restrict__ stamps) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void fwd1_body(const HArgs& a, const long long* __restrict__ y,
+                                          float* __restrict__ out, float* __restrict__ loss,
+                                          long long* __restrict__ pred,
+                                          unsigned long long* __restrict__ rng,
+                                          char* __restrict__ ws,
+                                          unsigned long long* __restrict__ stamps, char* smem) {
   constexpr int Mp = 16 * MT, NT = HS_NT, NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int B = a.B;
@@ -543,13 +544,25 @@ head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ o
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// bwd1: output-gradient chain down to dZ_0 (+ bias / BatchNorm parameter gradients).
-template <int MT>
+template <int MT, bool VECW>
 __global__ void __launch_bounds__(HS_NT)
-head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss,
+head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ out,
+                 float* __restrict__ loss, long long* __restrict__ pred,
+                 unsigned long long* __restrict__ rng, char* __restrict__ ws,
                  unsigned long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  fwd1_body<MT, VECW>(a, y, out, loss, pred, rng, ws, stamps, smem);
+}
+
+// ---------------------------------------------------------------------------------------------
+// bwd1: output-gradient chain down to dZ_0 (+ bias / BatchNorm parameter gradients).
+// stash = 1 (fused forward): the bias / BatchNorm gradients go to the workspace stash (not
+// accumulated: bwd0 adds them into .grad once the backward is known to use this d loss)
+template <int MT>
+__device__ __forceinline__ void bwd1_body(const HArgs& a, char* __restrict__ ws,
+                                          const float* __restrict__ dloss,
+                                          unsigned long long* __restrict__ stamps, char* smem,
+                                          int stash) {
   constexpr int Mp = 16 * MT, NT = HS_NT, NW = NT / 64;
   constexpr int CB = MT == 2 ? 4 : 2;  // weight-column k-steps per load batch
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -566,8 +579,9 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
     const int C = L.out, Cp = rup32(C), S = L.S_z;
     bf16* wdz = reinterpret_cast<bf16*>(ws + L.dz_off);
     float gbold = 0.f, colv[Mp];
+    float* const gbw = stash ? reinterpret_cast<float*>(ws + L.st_off) : L.gb;
     if (L.gb && tid < C) {  // bias-gradient loads first (old value + the column of dL/dz)
-      gbold = L.gb[tid];
+      gbold = stash ? 0.f : L.gb[tid];
 #pragma unroll
       for (int m = 0; m < Mp; ++m) colv[m] = dzl[m * 16 + tid];
     }
@@ -581,7 +595,7 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
       float s = 0.f;
 #pragma unroll
       for (int m = 0; m < Mp; ++m) s += m < B ? colv[m] : 0.f;
-      L.gb[tid] = gbold + gs * s;
+      gbw[tid] = gbold + gs * s;
     }
   }
   for (int l = a.nl - 1; l >= 1; --l) {
@@ -593,6 +607,10 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
     const float* xhat_ws = reinterpret_cast<const float*>(ws + P.xhat_off);
     const float* rstd_ws = reinterpret_cast<const float*>(ws + P.rstd_off);
     bf16* wdz = reinterpret_cast<bf16*>(ws + P.dz_off);
+    float* const st = reinterpret_cast<float*>(ws + P.st_off);
+    float* const gbw = stash ? st : P.gb;
+    float* const ggw = stash ? st + P.out : P.ggamma;
+    float* const gbew = stash ? st + 2 * P.out : P.gbeta;
 
     // Everything a tile needs from global memory, requested in one go (clamped addresses, no
     // use until the MFMAs / epilogue): weight columns of the first CB k-steps, the saved
@@ -619,10 +637,10 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
           for (int r = 0; r < 4; ++r) xhp[mt][r] = xhat_ws[(16 * mt + 4 * (lane >> 4) + r) * P.Np + kk];
         rsp = rstd_ws[kk];
         gap = P.gamma[kc];
-        ggo = P.ggamma[kc];
-        gbeo = P.gbeta[kc];
+        ggo = stash ? 0.f : P.ggamma[kc];
+        gbeo = stash ? 0.f : P.gbeta[kc];
       }
-      if (P.gb) gbo = P.gb[kc];
+      if (P.gb) gbo = stash ? 0.f : P.gb[kc];
     };
     if (wid < ntl) prefetch(wid);
     ws_to_lds<NT>(abuf, ws + L.a_off, Mp * Sa, tid);  // relu mask of the layer below
@@ -673,8 +691,8 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
         s1 = colsum4(s1);
         s2 = colsum4(s2);
         if (lane < 16 && kv) {
-          P.ggamma[kk] = ggo + s2;
-          P.gbeta[kk] = gbeo + s1;
+          ggw[kk] = ggo + s2;
+          gbew[kk] = gbeo + s1;
         }
         const float ga = kv ? gap : 0.f;
         const float m1 = s1 / (float)B, m2 = s2 / (float)B;
@@ -693,7 +711,7 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
 #pragma unroll
           for (int r = 0; r < 4; ++r) sb += d[mt][r];
         sb = colsum4(sb);
-        if (lane < 16 && kv) P.gb[kk] = gbo + sb;
+        if (lane < 16 && kv) gbw[kk] = gbo + sb;
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -713,13 +731,37 @@ head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss
   }
 }
 
+template <int MT>
+__global__ void __launch_bounds__(HS_NT)
+head_bwd1_kernel(HArgs a, char* __restrict__ ws, const float* __restrict__ dloss,
+                 unsigned long long* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bwd1_body<MT>(a, ws, dloss, stamps, smem, 0);
+}
+
+// Training step whose d loss is known at forward time (a persistent 1 the step's backward
+// passes): fwd1 and bwd1 in ONE single-workgroup launch, so the output-gradient chain starts
+// without a kernel boundary and on an L2-hot workspace.
+template <int MT, bool VECW>
+__global__ void __launch_bounds__(HS_NT)
+head_fwd1_bwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ out,
+                      float* __restrict__ loss, long long* __restrict__ pred,
+                      unsigned long long* __restrict__ rng, char* __restrict__ ws,
+                      const float* __restrict__ dloss, unsigned long long* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  fwd1_body<MT, VECW>(a, y, out, loss, pred, rng, ws, stamps, smem);
+  __threadfence_block();
+  __syncthreads();
+  bwd1_body<MT>(a, ws, dloss, stamps, smem, 1);
+}
+
 // ---------------------------------------------------------------------------------------------
 // bwd0: blocks [0, dw_jobs[nl]) -> 16-row slices of every layer's dW (read-modify-write into the
 // fp32 gradient); blocks after that -> 16-column slices of dX = dZ_0 W_0 (+ layer-0 dropout).
 template <int MT>
 __global__ void __launch_bounds__(HW_NT)
 head_bwd0_kernel(HArgs a, const char* __restrict__ ws, float* __restrict__ dx, long lddx,
-                 unsigned long long* __restrict__ stamps) {
+                 int apply_stash, unsigned long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int Mp = 16 * MT, NT = HW_NT, NW = NT / 64;
   constexpr int G = 6;  // dW tiles per wave batch (global read-modify-write in flight together)
@@ -727,6 +769,19 @@ head_bwd0_kernel(HArgs a, const char* __restrict__ ws, float* __restrict__ dx, l
   const int B = a.B;
   const int job = blockIdx.x;
   if (job == 0) HSTAMP(24);
+  if (apply_stash && job == gridDim.x - 1) {  // bias / BatchNorm grads of the fused forward
+    for (int l = 0; l < a.nl; ++l) {
+      const HLayer& L = a.L[l];
+      const float* st = reinterpret_cast<const float*>(ws + L.st_off);
+      for (int i = tid; i < L.out; i += NT) {
+        if (L.gb) L.gb[i] += st[i];
+        if (L.bn) {
+          L.ggamma[i] += st[L.out + i];
+          L.gbeta[i] += st[2 * L.out + i];
+        }
+      }
+    }
+  }
   if (job < a.dw_jobs[a.nl]) {
     int l = 0;
     while (job >= a.dw_jobs[l + 1]) ++l;
@@ -901,6 +956,8 @@ static bool make_plan(int nl, const int* dims, const int* flags, const float* dr
     if (L.bn) off = al256(off + 4L * L.Np);
     L.dz_off = off;
     off = al256(off + 2L * Mp * L.S_z);
+    L.st_off = off;
+    off = al256(off + 12L * L.out);
     if (l >= 1) buf_a1 = buf_a1 > Mp * L.S_a ? buf_a1 : Mp * L.S_a;
     buf_aall = buf_aall > Mp * L.S_a ? buf_aall : Mp * L.S_a;
     buf_z = buf_z > Mp * L.S_z ? buf_z : Mp * L.S_z;
@@ -949,31 +1006,44 @@ static void head_init() {
   allow_lds(head_bwd1_kernel<4>);
   allow_lds(head_bwd0_kernel<2>);
   allow_lds(head_bwd0_kernel<4>);
+  allow_lds(head_fwd1_bwd1_kernel<2, true>);
+  allow_lds(head_fwd1_bwd1_kernel<2, false>);
   g_head_init = true;
 }
 
 template <int MT, bool V0, bool V1>
 static void launch_fwd_t(const Plan& p, const float* x, long ldx, const long long* y, float* out,
                          float* loss, long long* pred, unsigned long long* rng, void* ws,
-                         hipStream_t st) {
+                         const float* dloss, hipStream_t st) {
   hipLaunchKernelGGL((head_fwd0_kernel<MT, V0>), dim3(p.grid_fwd0), dim3(HW_NT), p.lds_fwd0, st,
                      p.a, x, ldx, rng, (char*)ws, g_head_stamps);
-  hipLaunchKernelGGL((head_fwd1_kernel<MT, V1>), dim3(1), dim3(HS_NT), p.lds_fwd1, st, p.a, y,
-                     out, loss, pred, rng, (char*)ws, g_head_stamps);
+  // (no fused variant for 64-row batches: the bwd1 phase spills at MT = 4)
+  if constexpr (MT == 2) {
+    if (dloss) {
+      const long lds = p.lds_fwd1 > p.lds_bwd1 ? p.lds_fwd1 : p.lds_bwd1;
+      hipLaunchKernelGGL((head_fwd1_bwd1_kernel<MT, V1>), dim3(1), dim3(HS_NT), lds, st, p.a, y,
+                         out, loss, pred, rng, (char*)ws, dloss, g_head_stamps);
+      return;
+    }
+  }
+  {
+    hipLaunchKernelGGL((head_fwd1_kernel<MT, V1>), dim3(1), dim3(HS_NT), p.lds_fwd1, st, p.a, y,
+                       out, loss, pred, rng, (char*)ws, g_head_stamps);
+  }
 }
 
 // weight rows may be read as 16-B vectors when every K of the launch is a multiple of 8
 template <int MT>
 static void launch_fwd(const Plan& p, const float* x, long ldx, const long long* y, float* out,
                        float* loss, long long* pred, unsigned long long* rng, void* ws,
-                       hipStream_t st) {
+                       const float* dloss, hipStream_t st) {
   const bool v0 = p.a.L[0].in % 8 == 0;
   bool v1 = true;
   for (int l = 1; l < p.a.nl; ++l) v1 = v1 && p.a.L[l].in % 8 == 0;
-  if (v0 && v1) launch_fwd_t<MT, true, true>(p, x, ldx, y, out, loss, pred, rng, ws, st);
-  else if (v1) launch_fwd_t<MT, false, true>(p, x, ldx, y, out, loss, pred, rng, ws, st);
-  else if (v0) launch_fwd_t<MT, true, false>(p, x, ldx, y, out, loss, pred, rng, ws, st);
-  else launch_fwd_t<MT, false, false>(p, x, ldx, y, out, loss, pred, rng, ws, st);
+  if (v0 && v1) launch_fwd_t<MT, true, true>(p, x, ldx, y, out, loss, pred, rng, ws, dloss, st);
+  else if (v1) launch_fwd_t<MT, false, true>(p, x, ldx, y, out, loss, pred, rng, ws, dloss, st);
+  else if (v0) launch_fwd_t<MT, true, false>(p, x, ldx, y, out, loss, pred, rng, ws, dloss, st);
+  else launch_fwd_t<MT, false, false>(p, x, ldx, y, out, loss, pred, rng, ws, dloss, st);
 }
 
 }  // namespace
@@ -1014,9 +1084,59 @@ DN_API int dn_head_fwd(int nl, const int* dims, const int* flags, const float* d
   p.a.train = train;
   p.a.log_out = log_out;
   if (p.Mp == 32)
-    launch_fwd<2>(p, x, ldx, y, out, loss, pred, rng, ws, st);
+    launch_fwd<2>(p, x, ldx, y, out, loss, pred, rng, ws, nullptr, st);
   else
-    launch_fwd<4>(p, x, ldx, y, out, loss, pred, rng, ws, st);
+    launch_fwd<4>(p, x, ldx, y, out, loss, pred, rng, ws, nullptr, st);
+  return dn_launch_status();
+}
+
+// Training forward that also runs the output-gradient chain (bwd1) for the d loss already held
+// at `dloss` (the step's persistent 1): ptrs must carry the gradient buffers; the bias /
+// BatchNorm gradients wait in the workspace stash until dn_head_bwd0 (apply_stash = 1) adds
+// them, so a backward with a different d loss can still run the full dn_head_bwd instead.
+DN_API int dn_head_fwd_train(int nl, const int* dims, const int* flags, const float* drops,
+                             const float* bnp, void* const* ptrs, const float* x, long ldx, int B,
+                             const long long* y, float* out, float* loss, long long* pred,
+                             unsigned long long* rng, void* ws, int log_out, const float* dloss,
+                             hipStream_t st) {
+  Plan p;
+  if (!dloss || !make_plan(nl, dims, flags, drops, bnp, ptrs, B, p)) return DN_UNSUPPORTED;
+  if (p.Mp != 32) return DN_UNSUPPORTED;  // B <= 32 only; the caller runs dn_head_fwd instead
+  for (int l = 0; l < nl; ++l) {
+    const HLayer& L = p.a.L[l];
+    if (!L.gW || (L.b && !L.gb) || (L.bn && (!L.ggamma || !L.gbeta))) return DN_BAD_SHAPE;
+  }
+  head_init();
+  p.a.train = 1;
+  p.a.log_out = log_out;
+  if (p.Mp == 32)
+    launch_fwd<2>(p, x, ldx, y, out, loss, pred, rng, ws, dloss, st);
+  else
+    launch_fwd<4>(p, x, ldx, y, out, loss, pred, rng, ws, dloss, st);
+  return dn_launch_status();
+}
+
+// The rest of the backward after dn_head_fwd_train: dW of every layer, dX, and the stashed bias
+// / BatchNorm gradients added into .grad.
+DN_API int dn_head_bwd0(int nl, const int* dims, const int* flags, const float* drops,
+                        const float* bnp, void* const* ptrs, int B, void* ws, float* dx, long lddx,
+                        hipStream_t st) {
+  Plan p;
+  if (!make_plan(nl, dims, flags, drops, bnp, ptrs, B, p)) return DN_UNSUPPORTED;
+  for (int l = 0; l < nl; ++l) {
+    const HLayer& L = p.a.L[l];
+    if (!L.gW || (L.b && !L.gb) || (L.bn && (!L.ggamma || !L.gbeta))) return DN_BAD_SHAPE;
+  }
+  head_init();
+  p.a.train = 1;
+  p.a.log_out = 0;
+  const int grid0 = p.grid_bwd0_dw + (dx ? p.grid_bwd0_dx : 0);
+  if (p.Mp == 32)
+    hipLaunchKernelGGL(head_bwd0_kernel<2>, dim3(grid0), dim3(HW_NT), p.lds_bwd0, st, p.a,
+                       (const char*)ws, dx, lddx, 1, g_head_stamps);
+  else
+    hipLaunchKernelGGL(head_bwd0_kernel<4>, dim3(grid0), dim3(HW_NT), p.lds_bwd0, st, p.a,
+                       (const char*)ws, dx, lddx, 1, g_head_stamps);
   return dn_launch_status();
 }
 
@@ -1039,12 +1159,12 @@ DN_API int dn_head_bwd(int nl, const int* dims, const int* flags, const float* d
     hipLaunchKernelGGL(head_bwd1_kernel<2>, dim3(1), dim3(HS_NT), p.lds_bwd1, st, p.a, (char*)ws,
                        dloss, g_head_stamps);
     hipLaunchKernelGGL(head_bwd0_kernel<2>, dim3(grid0), dim3(HW_NT), p.lds_bwd0, st, p.a,
-                       (const char*)ws, dx, lddx, g_head_stamps);
+                       (const char*)ws, dx, lddx, 0, g_head_stamps);
   } else {
     hipLaunchKernelGGL(head_bwd1_kernel<4>, dim3(1), dim3(HS_NT), p.lds_bwd1, st, p.a, (char*)ws,
                        dloss, g_head_stamps);
     hipLaunchKernelGGL(head_bwd0_kernel<4>, dim3(grid0), dim3(HW_NT), p.lds_bwd0, st, p.a,
-                       (const char*)ws, dx, lddx, g_head_stamps);
+                       (const char*)ws, dx, lddx, 0, g_head_stamps);
   }
   return dn_launch_status();
 }

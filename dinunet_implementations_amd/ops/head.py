@@ -44,6 +44,36 @@ _lib.register("dn_head_fwd", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _
                               _P, _P, _P, _P, _lib.c_int, _lib.c_int, _P])
 _lib.register("dn_head_bwd", [_lib.c_int, _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _P, _lib.c_long,
                               _P])
+_lib.register("dn_head_fwd_train", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int,
+                                    _P, _P, _P, _P, _P, _P, _lib.c_int, _P, _P])
+_lib.register("dn_head_bwd0", [_lib.c_int, _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long,
+                               _P])
+
+# d(loss) tensor of the running training step, when the step will backpropagate exactly that
+# tensor (runtime.step.TrainStep's persistent 1): the forward then runs the head's output-gradient
+# chain in the same launch (dn_head_fwd_train).  DINUNET_FUSED_HEAD=0 disables.
+_HINT: Optional[torch.Tensor] = None
+import os as _os
+_FUSED_HEAD = _os.environ.get("DINUNET_FUSED_HEAD", "1") == "1"
+
+
+class loss_grad_hint:
+    """``with loss_grad_hint(one): out, loss, pred = head_loss(...)`` -- then
+    ``loss.backward(one)``.  A backward with any other gradient tensor stays correct (it runs
+    the unfused chain); it only loses the saving."""
+
+    def __init__(self, t: Optional[torch.Tensor]):
+        self.t = t
+
+    def __enter__(self):
+        global _HINT
+        self.prev, _HINT = _HINT, self.t
+        return self
+
+    def __exit__(self, *a):
+        global _HINT
+        _HINT = self.prev
+        return False
 
 
 class _Layer:
@@ -192,7 +222,7 @@ class HeadSpec:
 
 class _HeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, y, spec: HeadSpec, log_out: bool, *params):
+    def forward(ctx, x, y, spec: HeadSpec, log_out: bool, hint, *params):
         ctx.set_materialize_grads(False)  # no zero-filled grads for out / pred
         x = x.float().contiguous()
         y = y.long().contiguous()
@@ -205,10 +235,22 @@ class _HeadFn(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=x.device)
         pred = torch.empty(B, dtype=torch.long, device=x.device)
         rng = spec.rng(x.device)
-        _lib.call("dn_head_fwd", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
-                  spec.ptrs(False), x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(),
-                  loss.data_ptr(), pred.data_ptr(), rng.data_ptr(), ws.data_ptr(), int(train),
-                  int(log_out), _lib.stream())
+        ctx.hint_ptr = None
+        if train and hint is not None:
+            rc = _lib.lib().dn_head_fwd_train(
+                spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True),
+                x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(), loss.data_ptr(),
+                pred.data_ptr(), rng.data_ptr(), ws.data_ptr(), int(log_out), hint.data_ptr(),
+                _lib.stream())
+            if rc == 0:
+                ctx.hint_ptr = hint.data_ptr()
+            elif rc != 3:  # 3 = unsupported shape: the classic launches below
+                raise RuntimeError(f"dn_head_fwd_train failed with status {rc}")
+        if ctx.hint_ptr is None:
+            _lib.call("dn_head_fwd", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
+                      spec.ptrs(False), x.data_ptr(), x.stride(0), B, y.data_ptr(),
+                      out.data_ptr(), loss.data_ptr(), pred.data_ptr(), rng.data_ptr(),
+                      ws.data_ptr(), int(train), int(log_out), _lib.stream())
         ctx.spec, ctx.B, ctx.D0, ctx.train = spec, B, x.shape[1], train
         ctx.ws = ws if train else None
         ctx.mark_non_differentiable(out, pred)
@@ -216,7 +258,7 @@ class _HeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, dloss, dpred):
-        n_in = 4 + len(ctx.spec.params())
+        n_in = 5 + len(ctx.spec.params())
         if dloss is None:
             return (None,) * n_in
         if not ctx.train:
@@ -225,9 +267,15 @@ class _HeadFn(torch.autograd.Function):
         dloss = dloss.float().contiguous()
         dx = torch.empty(B, ctx.D0, dtype=torch.float32, device=dloss.device) \
             if ctx.needs_input_grad[0] else None
-        _lib.call("dn_head_bwd", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
-                  spec.ptrs(True), B, ctx.ws.data_ptr(), dloss.data_ptr(), _lib.ptr(dx),
-                  ctx.D0, _lib.stream())
+        if ctx.hint_ptr is not None and dloss.data_ptr() == ctx.hint_ptr:
+            # the forward already ran the output-gradient chain for exactly this d loss
+            _lib.call("dn_head_bwd0", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
+                      spec.ptrs(True), B, ctx.ws.data_ptr(), _lib.ptr(dx), ctx.D0,
+                      _lib.stream())
+        else:
+            _lib.call("dn_head_bwd", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
+                      spec.ptrs(True), B, ctx.ws.data_ptr(), dloss.data_ptr(), _lib.ptr(dx),
+                      ctx.D0, _lib.stream())
         params = spec.params()
         _grad.notify(params)
         if _cap.active() is not None:
@@ -248,7 +296,12 @@ def _ws_image(ws: Tensor, off: int, rows: int, stride: int) -> Tensor:
 def head_loss(x: Tensor, spec: HeadSpec, y: Tensor, log_out: bool):
     """``(out, loss, pred)`` of ``loss(modules(x), y)``; fused on a GPU when supported."""
     if spec.supported(x):
-        return _HeadFn.apply(x, y, spec, bool(log_out), *spec.params())
+        hint = _HINT
+        if hint is not None and not (_FUSED_HEAD and torch.is_grad_enabled() and spec.training
+                                     and hint.device == x.device and hint.numel() == 1
+                                     and hint.dtype == torch.float32 and x.shape[0] <= 32):
+            hint = None
+        return _HeadFn.apply(x, y, spec, bool(log_out), hint, *spec.params())
     logits = spec.run_modules(x)
     if logits.is_cuda:
         from .heads import log_softmax_nll, softmax_ce

@@ -82,17 +82,24 @@ class TrainStep:
         self._cap_lr = None
         self._bf16_in = False
 
-    def _backward(self, loss):
+    def _grad_one(self, device, dtype=torch.float32):
         # a persistent d(loss)/d(loss) = 1: loss.backward() would launch a fill kernel for it
         # inside every replay
         one = self._one
-        if one is None or one.device != loss.device or one.dtype != loss.dtype:
-            one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
-        torch.autograd.backward(loss, one)
+        if one is None or one.device != device or one.dtype != dtype:
+            one = self._one = torch.ones((), dtype=dtype, device=device)
+        return one
+
+    def _backward(self, loss):
+        torch.autograd.backward(loss, self._grad_one(loss.device, loss.dtype))
 
     def _fwd_bwd(self, x, y):
         with self.engine.step_context():
-            out, loss, pred = self.forward_loss(self.model, x, y)
+            # the step backpropagates exactly this tensor: fused ops may start their backward
+            # inside the forward (ops.head.loss_grad_hint)
+            hint = self._grad_one(x.device) if x.is_cuda else None
+            with ops.head.loss_grad_hint(hint):
+                out, loss, pred = self.forward_loss(self.model, x, y)
             self._backward(loss)
         return out, loss, pred
 
@@ -178,7 +185,8 @@ class TrainStep:
                 with self.engine.step_context():
                     h = self.model.stem(sx)
                     hd = h.detach().requires_grad_(h.requires_grad)
-                    out, loss, pred = self.model.body_loss(hd, sy)
+                    with ops.head.loss_grad_hint(self._grad_one(sx.device)):
+                        out, loss, pred = self.model.body_loss(hd, sy)
                     self._backward(loss)
             with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):
                 if h.requires_grad:

@@ -245,3 +245,35 @@ def test_fs_backward_exact_given_forward_state(B):
         dz = P.bn.weight.detach() * rstd * (d - d.mean(0) - xh * (d * xh).mean(0))
         kd = img(pdz_off, pS_z, P.linear.out_features)
         assert rel(kd, dz.to(torch.bfloat16).float()) < 1e-3, l
+
+
+@pytest.mark.parametrize("scale", [1.0, 2.5])
+def test_fused_forward_backward_chain_matches_two_phase(scale):
+    """With a d(loss) hint the forward also runs the output-gradient chain (one launch) and
+    the backward only dW / dX + the stashed bias / BatchNorm grads: bitwise the unfused result
+    when the backward uses the hinted tensor; a backward with another tensor (scale 2.5) falls
+    back to the full chain and stays exact."""
+    from dinunet_implementations_amd.ops.head import HeadSpec, head_loss, loss_grad_hint
+    torch.manual_seed(0)
+    mods = _ica_head(p=0.0).to(DEV).train()
+    ref_mods = copy.deepcopy(mods)
+    x = torch.randn(32, 384, device=DEV)
+    y = torch.randint(0, 2, (32,), device=DEV)
+    one = torch.ones((), device=DEV)
+    g = one if scale == 1.0 else torch.full((), scale, device=DEV)
+    res = []
+    for fused, m in ((True, mods), (False, ref_mods)):
+        xi = x.clone().requires_grad_()
+        spec = HeadSpec(list(m))
+        with loss_grad_hint(one if fused else None):
+            out, loss, _ = head_loss(xi, spec, y, log_out=False)
+        torch.autograd.backward(loss, g)
+        torch.cuda.synchronize()
+        res.append((out.clone(), xi.grad.clone(), [p.grad.clone() for p in m.parameters()],
+                    [b.clone() for b in m.buffers()]))
+    (o1, dx1, g1, b1), (o2, dx2, g2, b2) = res
+    assert torch.equal(o1, o2) and torch.equal(dx1, dx2)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+    for a, b in zip(b1, b2):
+        assert torch.equal(a, b)
