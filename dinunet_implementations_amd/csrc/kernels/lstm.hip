@@ -547,20 +547,52 @@ struct CastJobs {
   int cnt;
 };
 
+// The training step's prologue riding in the same launch (runtime.step.TrainStep before a graph
+// replay): batch -> bf16 static input (8 per item), labels copy, gradient buffer zeroing (4 per
+// item).  ux = ug = ny = 0 when unused.
+struct StepPrologue {
+  const float* x;
+  bf16* xb;
+  const long long* y;
+  long long* yd;
+  float* g;
+  long ux, ug, ny;
+};
+
 __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
                                  bf16* __restrict__ wih_p,    // [ndir*4HD][I]
                                  float* __restrict__ bias_p,  // [ndir*4HD]
                                  bf16* __restrict__ whh_p,    // [ndir][4HD][HD]
                                  bf16* __restrict__ whhT_p,   // [ndir][HD][4HD]
-                                 CastJobs cj) {
+                                 CastJobs cj, StepPrologue sp) {
   // 32-bit index math throughout (every extent < 2^31): 64-bit div/mod per element made this
   // ~1M-element repack a 6 us kernel at the head of every step
   const int GP = 4 * HD;
   const int n_wih = ndir * GP * I, n_b = ndir * GP, n_whh = ndir * GP * HD;
   const int n_pack = n_wih + n_b + 2 * n_whh;
-  int total = n_pack;
-  for (int j = 0; j < cj.cnt; ++j) total += cj.n[j];
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+  int n_pc = n_pack;
+  for (int j = 0; j < cj.cnt; ++j) n_pc += cj.n[j];
+  const long total = n_pc + sp.ux + sp.ug + sp.ny;
+  for (long li = blockIdx.x * (long)blockDim.x + threadIdx.x; li < total;
+       li += (long)gridDim.x * blockDim.x) {
+    if (li >= n_pc) {  // step prologue
+      long i = li - n_pc;
+      if (i < sp.ux) {
+        const f32x4 a = reinterpret_cast<const f32x4*>(sp.x)[2 * i];
+        const f32x4 b = reinterpret_cast<const f32x4*>(sp.x)[2 * i + 1];
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] = (bf16)a[e]; o[4 + e] = (bf16)b[e]; }
+        reinterpret_cast<bf16x8*>(sp.xb)[i] = o;
+      } else if ((i -= sp.ux) < sp.ug) {
+        reinterpret_cast<f32x4*>(sp.g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        i -= sp.ug;
+        sp.yd[i] = sp.y[i];
+      }
+      continue;
+    }
+    const int idx = (int)li;
     if (idx >= n_pack) {
       int r = idx - n_pack, j = 0;
       while (j + 1 < cj.cnt && r >= cj.n[j]) r -= cj.n[j++];
@@ -700,11 +732,12 @@ DN_API int dn_lstm_padded_hidden(int Hd) {
   return 0;
 }
 
-DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0, const float* bhh0,
-                        const float* wih1, const float* bih1, const float* whh1, const float* bhh1,
-                        int I, int Hd, int ndir, void* wih_p, float* bias_p, void* whh_p,
-                        void* whhT_p, int ncast, const float* const* cast_src,
-                        void* const* cast_dst, const int* cast_n, hipStream_t st) {
+static int lstm_pack_launch(const float* wih0, const float* bih0, const float* whh0,
+                            const float* bhh0, const float* wih1, const float* bih1,
+                            const float* whh1, const float* bhh1, int I, int Hd, int ndir,
+                            void* wih_p, float* bias_p, void* whh_p, void* whhT_p, int ncast,
+                            const float* const* cast_src, void* const* cast_dst,
+                            const int* cast_n, const StepPrologue& sp, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || ndir < 1 || ndir > 2 || ncast < 0 || ncast > PACK_CASTS) return DN_BAD_SHAPE;
   LstmParams p{{wih0, wih1}, {bih0, bih1}, {whh0, whh1}, {bhh0, bhh1}};
@@ -719,11 +752,41 @@ DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0,
     total += cast_n[j];
   }
   if (total >= (1L << 31)) return DN_BAD_SHAPE;
-  const int blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+  total += sp.ux + sp.ug + sp.ny;
+  // the batch conversion is HBM-bound: as many workgroups as the standalone prologue had
+  const long cap = sp.ux ? 4096 : 2048;
+  const int blocks = (int)((total + 255) / 256 < cap ? (total + 255) / 256 : cap);
   hipLaunchKernelGGL(lstm_pack_kernel, dim3(blocks), dim3(256), 0, st, p, I, Hd, HD, ndir,
-                     (bf16*)wih_p, bias_p, (bf16*)whh_p, (bf16*)whhT_p, cj);
+                     (bf16*)wih_p, bias_p, (bf16*)whh_p, (bf16*)whhT_p, cj, sp);
   return dn_launch_status();
 }
+
+DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0, const float* bhh0,
+                        const float* wih1, const float* bih1, const float* whh1, const float* bhh1,
+                        int I, int Hd, int ndir, void* wih_p, float* bias_p, void* whh_p,
+                        void* whhT_p, int ncast, const float* const* cast_src,
+                        void* const* cast_dst, const int* cast_n, hipStream_t st) {
+  const StepPrologue sp{};
+  return lstm_pack_launch(wih0, bih0, whh0, bhh0, wih1, bih1, whh1, bhh1, I, Hd, ndir, wih_p,
+                          bias_p, whh_p, whhT_p, ncast, cast_src, cast_dst, cast_n, sp, st);
+}
+
+// dn_lstm_pack + dn_step_prologue in ONE launch (x: nx fp32 -> xb bf16, nx % 8 == 0; y: ny int64
+// -> yd; g: ng floats zeroed, ng % 4 == 0; 16-B aligned x, xb, g)
+DN_API int dn_lstm_pack_prologue(const float* wih0, const float* bih0, const float* whh0,
+                                 const float* bhh0, const float* wih1, const float* bih1,
+                                 const float* whh1, const float* bhh1, int I, int Hd, int ndir,
+                                 void* wih_p, float* bias_p, void* whh_p, void* whhT_p, int ncast,
+                                 const float* const* cast_src, void* const* cast_dst,
+                                 const int* cast_n, const float* x, long nx, void* xb,
+                                 const long long* y, long ny, long long* yd, float* g, long ng,
+                                 hipStream_t st) {
+  if (nx % 8 || ng % 4 || (((uintptr_t)x | (uintptr_t)xb | (uintptr_t)g) & 15)) return DN_BAD_SHAPE;
+  const StepPrologue sp{x, (bf16*)xb, y, yd, g, nx / 8, ng / 4, ny};
+  return lstm_pack_launch(wih0, bih0, whh0, bhh0, wih1, bih1, whh1, bhh1, I, Hd, ndir, wih_p,
+                          bias_p, whh_p, whhT_p, ncast, cast_src, cast_dst, cast_n, sp, st);
+}
+
 
 // rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
 DN_API int dn_lstm_rows_per_wg(int B) { return pick_br(B); }

@@ -40,6 +40,10 @@ Tensor = torch.Tensor
 
 _lib.register("dn_lstm_pack", [_lib.c_void_p] * 8 + [_lib.c_int] * 3 + [_lib.c_void_p] * 4
               + [_lib.c_int] + [_lib.c_void_p] * 3 + [_lib.c_void_p])
+_lib.register("dn_lstm_pack_prologue", [_lib.c_void_p] * 8 + [_lib.c_int] * 3
+              + [_lib.c_void_p] * 4 + [_lib.c_int] + [_lib.c_void_p] * 3
+              + [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                 _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p])
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
@@ -216,11 +220,17 @@ def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = 
         dsts = [torch.empty(c.shape, dtype=torch.bfloat16, device=device) for c in srcs]
         nc = len(srcs)
         P, I_ = ctypes.c_void_p, ctypes.c_int
-        _lib.call("dn_lstm_pack", *[_lib.ptr(p) for p in ps], I, Hd, ndir, wih_p.data_ptr(),
-                  bias_p.data_ptr(), whh_p.data_ptr(), whhT_p.data_ptr(), nc,
-                  (P * max(nc, 1))(*[c.data_ptr() for c in srcs]),
-                  (P * max(nc, 1))(*[d.data_ptr() for d in dsts]),
-                  (I_ * max(nc, 1))(*[c.numel() for c in srcs]), _lib.stream())
+        args = ([_lib.ptr(p) for p in ps] + [I, Hd, ndir, wih_p.data_ptr(), bias_p.data_ptr(),
+                whh_p.data_ptr(), whhT_p.data_ptr(), nc,
+                (P * max(nc, 1))(*[c.data_ptr() for c in srcs]),
+                (P * max(nc, 1))(*[d.data_ptr() for d in dsts]),
+                (I_ * max(nc, 1))(*[c.numel() for c in srcs])])
+        if _DEFERRED is not None and not side:
+            # recorded, launched before each replay (run_deferred_pack); the record keeps every
+            # operand alive so the graph pool never hands the packed buffers to another tensor
+            _DEFERRED.append((args, (ps, srcs, dsts, wih_p, bias_p, whh_p, whhT_p)))
+        else:
+            _lib.call("dn_lstm_pack", *args, _lib.stream())
         if cast_out is not None:
             cast_out.extend(dsts)
         ev = None
@@ -241,6 +251,43 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
+
+
+_DEFERRED: Optional[list] = None
+
+
+class defer_pack:
+    """While active (a graph capture in ``runtime.step.TrainStep``), ``pack_params`` allocates
+    its outputs but records its launch instead of issuing it: the pack depends only on the
+    parameters, so it runs before each replay in the same launch as the step prologue
+    (``run_deferred_pack``), and the graph starts at the encoder GEMM.  The packed layouts are
+    identical either way."""
+
+    def __init__(self):
+        self.records: list = []
+
+    def __enter__(self):
+        global _DEFERRED
+        self._prev, _DEFERRED = _DEFERRED, self.records
+        return self
+
+    def __exit__(self, *a):
+        global _DEFERRED
+        _DEFERRED = self._prev
+        return False
+
+
+def run_deferred_pack(records: list, prologue=None) -> None:
+    """Issue the recorded pack launches; the LAST one also runs the step prologue
+    ``(x fp32, xb bf16, y int64, yd int64, grad fp32)`` when given (``dn_lstm_pack_prologue``)."""
+    for k, (args, _keep) in enumerate(records):
+        if prologue is not None and k == len(records) - 1:
+            x, xb, y, yd, g = prologue
+            _lib.call("dn_lstm_pack_prologue", *args, x.data_ptr(), x.numel(), xb.data_ptr(),
+                      y.data_ptr(), y.numel(), yd.data_ptr(), g.data_ptr(), g.numel(),
+                      _lib.stream())
+        else:
+            _lib.call("dn_lstm_pack", *args, _lib.stream())
 
 
 def _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):

@@ -25,6 +25,7 @@ from typing import Callable, Optional
 import torch
 
 from .. import ops
+from ..ops.lstm import defer_pack, run_deferred_pack
 from .timers import NULL, PhaseTimer, enabled_by_env
 
 
@@ -43,6 +44,20 @@ HEADS = {"ica": ica_forward_loss, "fs": fs_forward_loss}
 # query from another thread while this thread captures invalidates the capture and kills the
 # watchdog (hipErrorStreamCaptureUnsupported -> abort).
 CAPTURE_MODE = "thread_local"
+
+# The LSTM weight repack leaves the graph and rides in the step prologue's launch
+# (DINUNET_DEFER_PACK=0 keeps it captured)
+DEFER_PACK = os.environ.get("DINUNET_DEFER_PACK", "1") != "0"
+
+
+class _NoDefer:
+    records: list = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 class TrainStep:
@@ -81,6 +96,7 @@ class TrainStep:
         self.graph_opt = False
         self._cap_lr = None
         self._bf16_in = False
+        self._packs: list = []  # LSTM repacks deferred out of the captured graph
 
     def _grad_one(self, device, dtype=torch.float32):
         # a persistent d(loss)/d(loss) = 1: loss.backward() would launch a fill kernel for it
@@ -126,8 +142,14 @@ class TrainStep:
         return sx, sy
 
     def _feed(self, x, y, sx, sy):
-        """Before a replay, in ONE launch when possible: inputs into the static buffers and the
-        gradient buffer zeroed (the graphs no longer contain the zeroing)."""
+        """Before a replay, in ONE launch when possible: inputs into the static buffers, the
+        gradient buffer zeroed (the graphs no longer contain the zeroing) and the LSTM weight
+        repack the capture deferred out of the graph (``ops.lstm.defer_pack``)."""
+        if self._packs:
+            if self._bf16_in:
+                run_deferred_pack(self._packs, (x, sx, y, sy, self.flat.grad))
+                return
+            run_deferred_pack(self._packs)
         if self._bf16_in:
             ops.step_prologue(x, sx, y, sy, self.flat.grad)
             return
@@ -161,7 +183,7 @@ class TrainStep:
             self.opt.sync_device_step()
             self._cap_lr = self.opt.lr
         try:
-            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE), self._defer_pack() as dp:
                 out, loss, pred = self._fwd_bwd(sx, sy)
                 if self._pre_reduce is not None:
                     self._pre_reduce()
@@ -174,6 +196,10 @@ class TrainStep:
                 self.engine.sync_enabled = prev
         self.graph = g
         self.static = (sx, sy, out, loss, pred)
+        self._packs = dp.records
+
+    def _defer_pack(self):
+        return defer_pack() if DEFER_PACK else _NoDefer()
 
     def _capture_split(self, x, y):
         sx, sy = self._static_inputs(x, y)
@@ -181,7 +207,7 @@ class TrainStep:
         self.engine.sync_enabled = False
         self.graph_opt = False
         try:
-            with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
+            with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE), self._defer_pack() as dp:
                 with self.engine.step_context():
                     h = self.model.stem(sx)
                     hd = h.detach().requires_grad_(h.requires_grad)
@@ -195,6 +221,7 @@ class TrainStep:
             self.engine.sync_enabled = True
         self.graph, self.graph_b = ga, gb
         self.static = (sx, sy, out, loss, pred)
+        self._packs = dp.records
         self._keep = (h, hd)  # the graphs replay into these buffers
 
     def __call__(self, x, y):

@@ -57,6 +57,21 @@ def test_graph_replay_matches_eager():
     assert torch.allclose(fe.data, fg.data, rtol=1e-5, atol=1e-6)
 
 
+def test_deferred_pack_prologue_is_bit_identical(monkeypatch):
+    """The LSTM repack taken out of the graph and fused into the step prologue's launch
+    (ops.lstm.defer_pack + dn_lstm_pack_prologue) trains bit-identically to the captured pack."""
+    import dinunet_implementations_amd.runtime.step as st
+    xs, ys = _batches()
+    monkeypatch.setattr(st, "DEFER_PACK", False)
+    _, f0, s0 = _trainer(0, use_graph=True)
+    _run(s0, xs, ys)
+    monkeypatch.setattr(st, "DEFER_PACK", True)
+    _, f1, s1 = _trainer(0, use_graph=True)
+    _run(s1, xs, ys)
+    assert not s0._packs and len(s1._packs) == 1 and s1._bf16_in
+    assert torch.equal(f0.data, f1.data)
+
+
 def test_split_capture_matches_single_graph():
     xs, ys = _batches()
     _, f1, s1 = _trainer(0, use_graph=True, split=False)
