@@ -110,6 +110,18 @@ def build_host(force: bool = False, verbose: bool = True) -> str:
     return HOST_LIB
 
 
+def build_host_sanitized(out_path: str, sanitizers: str = "address,undefined") -> str:
+    """Debug target: the host runtime sources linked with the edge-case driver
+    ``host/check/sanitize_dataio.cpp`` into one executable under ASan + UBSan.  GPU ASan is not
+    available for gfx950 here, so the sanitized target is the host code only.  Not part of
+    :func:`build_all`; ``tests/test_host_sanitize.py`` builds and runs it."""
+    srcs = _sources("cpp") + [os.path.join(HERE, "host", "check", "sanitize_dataio.cpp")]
+    flags = ["-O1", "-g", "-std=c++17", "-fopenmp", f"-fsanitize={sanitizers}",
+             "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"]
+    _run([CXX, *flags, "-I", os.path.join(HERE, "host"), *srcs, "-o", out_path])
+    return out_path
+
+
 def build_all(force: bool = False, jobs: int = 4, verbose: bool = True):
     return build_kernels(force, jobs, verbose), build_host(force, verbose)
 
