@@ -440,6 +440,11 @@ __device__ __forceinline__ void fwd1_body(const HArgs& a, const long long* __res
   bf16* nxt = cur + a.buf_a1;
   float* logit = reinterpret_cast<float*>(nxt + a.buf_a1);  // [Mp][16]
   const uint64_t seed = rng ? *rng : 0ull;
+  // labels requested now and parked in LDS with the activation image: the loss phase at the end
+  // no longer waits on a global round trip
+  int* ylds = reinterpret_cast<int*>(logit + Mp * 16);  // [64] (no static LDS: see lds_fwd1)
+  // (MT 4 has no register to spare for it: the label load stays in the loss phase)
+  const long long ypre = (MT <= 2 && wid == 0 && lane < B) ? y[lane] : 0ll;
   HSTAMP(3);
   // this wave's first layer-1 tile: weights (first 8 k-steps) and epilogue parameters are
   // requested before the activation image is copied in, so their latency overlaps it
@@ -465,6 +470,7 @@ __device__ __forceinline__ void fwd1_body(const HArgs& a, const long long* __res
     const float* src = reinterpret_cast<const float*>(ws + a.logit_off);
     for (int i = tid; i < Mp * 16; i += NT) logit[i] = src[i];
   }
+  if (MT <= 2 && wid == 0) ylds[lane] = (int)(ypre < 0 ? -1 : (ypre > 0x7fffffffll ? 0x7fffffff : ypre));
   __syncthreads();
   HSTAMP(4);
   for (int l = 1; l < a.nl; ++l) {
@@ -517,7 +523,7 @@ __device__ __forceinline__ void fwd1_body(const HArgs& a, const long long* __res
       float se = 0.f;
       for (int c = 0; c < C; ++c) se += expf(logit[m * 16 + c] - mx);
       const float lse = mx + logf(se);
-      long long yc = y[m];
+      long long yc = MT <= 2 ? (long long)ylds[m] : y[m];
       yc = yc < 0 ? 0 : (yc >= C ? C - 1 : yc);
       float* dzl = reinterpret_cast<float*>(ws + a.dzl_off);
       for (int c = 0; c < C; ++c) {
@@ -564,7 +570,7 @@ __device__ __forceinline__ void bwd1_body(const HArgs& a, char* __restrict__ ws,
                                           unsigned long long* __restrict__ stamps, char* smem,
                                           int stash) {
   constexpr int Mp = 16 * MT, NT = HS_NT, NW = NT / 64;
-  constexpr int CB = MT == 2 ? 4 : 2;  // weight-column k-steps per load batch
+  constexpr int CB = 2;  // weight-column k-steps per load batch (x2 register sets: see pipe)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int B = a.B;
   bf16* dz = reinterpret_cast<bf16*>(smem);
@@ -615,38 +621,58 @@ __device__ __forceinline__ void bwd1_body(const HArgs& a, char* __restrict__ ws,
     // Everything a tile needs from global memory, requested in one go (clamped addresses, no
     // use until the MFMAs / epilogue): weight columns of the first CB k-steps, the saved
     // BatchNorm xhat / rstd, gamma and the old values of the parameter gradients it updates.
+    // One column batch covers the whole K loop (Np <= CB * 32, the ICA head): the NEXT tile's
+    // operands are requested into a second register set before this tile's MFMAs, so a wave's
+    // later tiles do not start with a global round trip.  Otherwise the K loop reloads wc.
+    const bool pipe = Np <= CB * 32;
     float wc[CB][8], xhp[MT][4];
     float rsp = 0.f, gap = 0.f, ggo = 0.f, gbeo = 0.f, gbo = 0.f;
-    auto load_wc = [&](int nb, int kk) {
-#pragma unroll
-      for (int u = 0; u < CB; ++u)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int n = nb + 32 * u + 8 * (lane >> 4) + j;
-          wc[u][j] = L.W[(n < N && kk < K) ? n * K + kk : 0];
-        }
-    };
-    auto prefetch = [&](int t) {
-      const int kk = 16 * t + (lane & 15);
-      const int kc = kk < K ? kk : 0;
-      load_wc(0, kk);
-      if (P.bn) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) xhp[mt][r] = xhat_ws[(16 * mt + 4 * (lane >> 4) + r) * P.Np + kk];
-        rsp = rstd_ws[kk];
-        gap = P.gamma[kc];
-        ggo = stash ? 0.f : P.ggamma[kc];
-        gbeo = stash ? 0.f : P.gbeta[kc];
-      }
-      if (P.gb) gbo = stash ? 0.f : P.gb[kc];
-    };
+    float wn[CB][8], xhn[MT][4];
+    float rsn = 0.f, gan = 0.f, ggn = 0.f, gben = 0.f, gbn = 0.f;
+#define HB1_LOAD_W(w, nb, kk)                                                   \
+  _Pragma("unroll") for (int u = 0; u < CB; ++u)                                \
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) {                               \
+    const int n_ = (nb) + 32 * u + 8 * (lane >> 4) + j;                         \
+    w[u][j] = L.W[(n_ < N && (kk) < K) ? n_ * K + (kk) : 0];                    \
+  }
+#define HB1_PREFETCH(t, w, xh, rs, ga, gg, gbe, gbv)                            \
+  do {                                                                          \
+    const int kk_ = 16 * (t) + (lane & 15);                                     \
+    const int kc_ = kk_ < K ? kk_ : 0;                                          \
+    HB1_LOAD_W(w, 0, kk_)                                                       \
+    if (P.bn) {                                                                 \
+      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                         \
+      _Pragma("unroll") for (int r = 0; r < 4; ++r)                             \
+        xh[mt][r] = xhat_ws[(16 * mt + 4 * (lane >> 4) + r) * P.Np + kc_];      \
+      rs = rstd_ws[kc_];                                                        \
+      ga = P.gamma[kc_];                                                        \
+      gg = stash ? 0.f : P.ggamma[kc_];                                         \
+      gbe = stash ? 0.f : P.gbeta[kc_];                                         \
+    }                                                                           \
+    if (P.gb) gbv = stash ? 0.f : P.gb[kc_];                                    \
+  } while (0)
+    auto load_wc = [&](int nb, int kk) { HB1_LOAD_W(wc, nb, kk) };
+    auto prefetch = [&](int t) { HB1_PREFETCH(t, wc, xhp, rsp, gap, ggo, gbeo, gbo); };
     if (wid < ntl) prefetch(wid);
     ws_to_lds<NT>(abuf, ws + L.a_off, Mp * Sa, tid);  // relu mask of the layer below
     __syncthreads();
     for (int t = wid; t < ntl; t += NW) {
-      if (t != wid) prefetch(t);
+      if (t != wid) {
+        if (pipe) {
+#pragma unroll
+          for (int u = 0; u < CB; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wc[u][j] = wn[u][j];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xhp[mt][r] = xhn[mt][r];
+          rsp = rsn; gap = gan; ggo = ggn; gbeo = gben; gbo = gbn;
+        } else {
+          prefetch(t);
+        }
+      }
+      if (pipe && t + NW < ntl) HB1_PREFETCH(t + NW, wn, xhn, rsn, gan, ggn, gben, gbn);
       const int kk = 16 * t + (lane & 15);
       const bool kv = kk < K;
       f32x4 acc[MT];
@@ -976,7 +1002,7 @@ static bool make_plan(int nl, const int* dims, const int* flags, const float* dr
   p.grid_bwd0_dx = (a.L[0].in + 15) / 16;
   const long red = 4L * (HW_NT / 64) * (Mp / 16) * 4 * 64;
   p.lds_fwd0 = ((2L * Mp * a.L[0].S_a + 15) & ~15L) + red;
-  p.lds_fwd1 = 2L * 2 * a.buf_a1 + 4L * Mp * 16;
+  p.lds_fwd1 = 2L * 2 * a.buf_a1 + 4L * Mp * 16 + 4L * 64;  // + the label slots
   p.lds_bwd1 = 2L * (2 * a.buf_z + a.buf_a1);
   const long dwl = 2L * (a.buf_aall + Mp * 24);
   p.lds_bwd0 = dwl > red ? dwl : red;
