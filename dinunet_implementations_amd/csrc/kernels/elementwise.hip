@@ -90,7 +90,8 @@ __global__ void colsum_slabs_kernel(const float* __restrict__ part, int slabs, i
 __global__ void __launch_bounds__(256)
 step_prologue_kernel(const float* __restrict__ x, long ux, bf16* __restrict__ xb,
                      const long long* __restrict__ y, long ny, long long* __restrict__ yd,
-                     float* __restrict__ g, long ug) {
+                     float* __restrict__ g, long ug, int* __restrict__ bump) {
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;  // armed Adam step counter
   const long total = ux + ug + ny;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
@@ -119,7 +120,7 @@ DN_API int dn_step_prologue(const float* x, long nx, void* xb, const long long* 
   long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, nx / 8,
-                     (bf16*)xb, y, ny, yd, g, ng / 4);
+                     (bf16*)xb, y, ny, yd, g, ng / 4, dn_take_step_bump());
   return dn_launch_status();
 }
 

@@ -557,6 +557,7 @@ struct StepPrologue {
   long long* yd;
   float* g;
   long ux, ug, ny;
+  int* bump;  // armed Adam step counter (dn_set_step_bump), advanced once by the launch
 };
 
 __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
@@ -565,6 +566,7 @@ __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
                                  bf16* __restrict__ whh_p,    // [ndir][4HD][HD]
                                  bf16* __restrict__ whhT_p,   // [ndir][HD][4HD]
                                  CastJobs cj, StepPrologue sp) {
+  if (sp.bump && blockIdx.x == 0 && threadIdx.x == 0) *sp.bump += 1;
   // 32-bit index math throughout (every extent < 2^31): 64-bit div/mod per element made this
   // ~1M-element repack a 6 us kernel at the head of every step
   const int GP = 4 * HD;
@@ -782,7 +784,7 @@ DN_API int dn_lstm_pack_prologue(const float* wih0, const float* bih0, const flo
                                  const long long* y, long ny, long long* yd, float* g, long ng,
                                  hipStream_t st) {
   if (nx % 8 || ng % 4 || (((uintptr_t)x | (uintptr_t)xb | (uintptr_t)g) & 15)) return DN_BAD_SHAPE;
-  const StepPrologue sp{x, (bf16*)xb, y, yd, g, nx / 8, ng / 4, ny};
+  const StepPrologue sp{x, (bf16*)xb, y, yd, g, nx / 8, ng / 4, ny, dn_take_step_bump()};
   return lstm_pack_launch(wih0, bih0, whh0, bhh0, wih1, bih1, whh1, bhh1, I, Hd, ndir, wih_p,
                           bias_p, whh_p, whhT_p, ncast, cast_src, cast_dst, cast_n, sp, st);
 }

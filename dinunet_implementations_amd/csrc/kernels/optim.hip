@@ -12,10 +12,10 @@ __global__ void __launch_bounds__(256)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
             float bc1, float inv_sqrt_bc2, float grad_scale, const int* __restrict__ tdev,
-            double b1d, double b2d) {
+            double b1d, double b2d, int tofs) {
   if (tdev) {  // graph-replayable form: the step number lives on the device (adam_bump_kernel);
                // double math as on the host, so both forms round to the same fp32 corrections
-    const double t = (double)(*tdev + 1);
+    const double t = (double)(*tdev + tofs);  // tofs 0: the step prologue advanced it
     bc1 = (float)(1.0 - pow(b1d, t));
     inv_sqrt_bc2 = (float)(1.0 / sqrt(1.0 - pow(b2d, t)));
   }
@@ -90,19 +90,20 @@ DN_API int dn_adam(float* p, const float* g, float* m, float* v, long n, float l
   if (n <= 0) return DN_OK;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, n, lr,
-                     b1, b2, eps, wd, bc1, inv_sqrt_bc2, grad_scale, (const int*)nullptr, 0.0, 0.0);
+                     b1, b2, eps, wd, bc1, inv_sqrt_bc2, grad_scale, (const int*)nullptr, 0.0, 0.0, 1);
   return dn_launch_status();
 }
 
 // Adam whose step number t is read from (and then advanced in) device memory: capturable in a
 // HIP graph and replayed every step with the right bias corrections.  *tdev = completed steps.
 DN_API int dn_adam_dev(float* p, const float* g, float* m, float* v, long n, float lr, double b1,
-                       double b2, float eps, float wd, float grad_scale, int* tdev, hipStream_t st) {
+                       double b2, float eps, float wd, float grad_scale, int* tdev, int prebumped,
+                       hipStream_t st) {
   if (n <= 0) return DN_OK;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, n, lr,
-                     (float)b1, (float)b2, eps, wd, 0.f, 0.f, grad_scale, (const int*)tdev, b1, b2);
-  hipLaunchKernelGGL(adam_bump_kernel, dim3(1), dim3(1), 0, st, tdev);
+                     (float)b1, (float)b2, eps, wd, 0.f, 0.f, grad_scale, (const int*)tdev, b1, b2, prebumped ? 0 : 1);
+  if (!prebumped) hipLaunchKernelGGL(adam_bump_kernel, dim3(1), dim3(1), 0, st, tdev);
   return dn_launch_status();
 }
 
@@ -126,4 +127,20 @@ DN_API int dn_cast_bf16_f32(const void* in, float* out, long n, float scale, hip
   hipLaunchKernelGGL(cast_scale_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)in,
                      out, n, scale);
   return dn_launch_status();
+}
+
+static int* g_step_bump = nullptr;
+int* dn_take_step_bump() {
+  int* p = g_step_bump;
+  g_step_bump = nullptr;
+  return p;
+}
+
+// Arm (tdev) or disarm (null) the one-shot step-counter advance of the next step-prologue
+// launch (dn_step_prologue / dn_lstm_pack_prologue).  Returns 1 when a previously armed counter
+// was never consumed (the caller's feed path launched no prologue), else 0.
+DN_API int dn_set_step_bump(int* tdev) {
+  const int stale = g_step_bump != nullptr;
+  g_step_bump = tdev;
+  return stale;
 }

@@ -24,7 +24,8 @@ _lib.register("dn_adam", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_vo
 _lib.register("dn_adam_dev", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_long, _lib.c_float, _lib.c_double, _lib.c_double,
                               _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_void_p,
-                              _lib.c_void_p])
+                              _lib.c_int, _lib.c_void_p])
+_lib.register("dn_set_step_bump", [_lib.c_void_p])
 _lib.register("dn_step_prologue", [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p,
                                    _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                                    _lib.c_void_p])
@@ -123,17 +124,32 @@ class FusedAdam:
             self._tdev = torch.zeros(1, dtype=torch.int32, device=self.flat.data.device)
         self._tdev.fill_(self.step_count)
 
-    def step_graphable(self, grad_scale: float = 1.0):
+    def step_graphable(self, grad_scale: float = 1.0, prebumped: bool = False):
         """One Adam step whose bias corrections come from the device step counter (advanced by
         the same launch), so it can be captured once and replayed every step.  The caller keeps
-        ``step_count`` in sync (one increment per replay)."""
+        ``step_count`` in sync (one increment per replay).  ``prebumped``: the caller advances
+        the counter in its step prologue instead (:meth:`arm_step_bump` before each replay), so
+        the update is ONE graph node, not Adam + a one-thread bump kernel."""
         d = self.flat.data
         if self._tdev is None:
             self.sync_device_step()
         b1, b2 = self.betas
         _lib.call("dn_adam_dev", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
                   self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
-                  self.weight_decay, grad_scale, self._tdev.data_ptr(), _lib.stream())
+                  self.weight_decay, grad_scale, self._tdev.data_ptr(), int(prebumped),
+                  _lib.stream())
+
+    def arm_step_bump(self):
+        """The next step-prologue launch advances the device step counter (one-shot)."""
+        if self._tdev is None:
+            self.sync_device_step()
+        _lib.lib().dn_set_step_bump(self._tdev.data_ptr())
+
+    @staticmethod
+    def disarm_step_bump():
+        """Clear an armed advance; raises when no prologue launch consumed it."""
+        if _lib.lib().dn_set_step_bump(None):
+            raise RuntimeError("step counter armed but no step-prologue launch consumed it")
 
     def state_dict(self) -> Dict:
         return {"lr": self.lr, "betas": self.betas, "eps": self.eps,

@@ -94,6 +94,7 @@ class TrainStep:
         self.graph_b = None
         self._one = None
         self.graph_opt = False
+        self._prebump = False
         self._cap_lr = None
         self._bf16_in = False
         self._packs: list = []  # LSTM repacks deferred out of the captured graph
@@ -179,6 +180,10 @@ class TrainStep:
         if prev is not None:
             self.engine.sync_enabled = False  # no collectives inside the captured region
         self.graph_opt = self._graph_opt_ok()
+        # the feed before each replay always launches a step prologue on this path, and that
+        # launch advances Adam's device step counter: no one-thread bump node in the graph
+        self._prebump = self.graph_opt and (
+            self._bf16_in or (y.dtype == torch.int64 and self.flat.grad.numel() % 4 == 0))
         if self.graph_opt:
             self.opt.sync_device_step()
             self._cap_lr = self.opt.lr
@@ -190,7 +195,7 @@ class TrainStep:
                 if self.graph_opt:
                     scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
                              else self.engine.reduce())
-                    self.opt.step_graphable(grad_scale=scale)
+                    self.opt.step_graphable(grad_scale=scale, prebumped=self._prebump)
         finally:
             if prev is not None:
                 self.engine.sync_enabled = prev
@@ -244,7 +249,14 @@ class TrainStep:
             return self._eager(x, y)
         T = self.timers
         with T.phase("fwd_bwd"):
-            self._feed(x, y, sx, sy)
+            if self.graph_opt and self._prebump:
+                self.opt.arm_step_bump()
+                try:
+                    self._feed(x, y, sx, sy)
+                finally:
+                    self.opt.disarm_step_bump()
+            else:
+                self._feed(x, y, sx, sy)
             self.graph.replay()
             if self.graph_b is not None:
                 for b in self._first_buckets:  # all-reduce under the stem backward
