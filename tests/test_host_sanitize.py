@@ -33,3 +33,19 @@ def test_host_runtime_under_sanitizers(tmp_path, sanitizers):
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "host sanitizer checks passed" in r.stdout
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr
+
+
+def test_sanitizer_toolchain_reports_heap_overflow(tmp_path):
+    """Negative control: the same flags do catch an out-of-bounds write, so a clean run of the
+    driver above means something."""
+    src = tmp_path / "oob.cpp"
+    src.write_text("#include <vector>\nint main(int c, char**) { std::vector<int> v(4);"
+                   " int* p = v.data(); p[c + 3] = 1; return p[0]; }\n")
+    exe = str(tmp_path / "oob")
+    r = subprocess.run([b.CXX, "-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer",
+                        str(src), "-o", exe], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("sanitizer runtime not installed: " + r.stderr[-200:])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=60)
+    assert r.returncode != 0 and "heap-buffer-overflow" in r.stderr, r.stderr[-2000:]
