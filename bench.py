@@ -87,12 +87,14 @@ def main():
     dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
     grp.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
     dt = float(dt.item())
-    loss = float(step.last_loss)
+    loss = float(step.last_loss.detach())
     n = grp.world
     total = n * args.batch * args.steps / dt
     if grp.is_master:
         rec = {
-            "metric": BASELINE_METRIC,
+            # the headline metric names dSGD; other engines report the same quantity under
+            # their own name (never mistaken for the dSGD headline)
+            "metric": BASELINE_METRIC.replace("dSGD", args.engine),
             "value": round(total, 2),
             "unit": "samples/s (whole job: sum over the N sites)",
             "n_gpus": n,

@@ -35,11 +35,6 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// One-shot device step counter the next step-prologue launch advances (dn_set_step_bump in
-// optim.hip): the graph-captured Adam then reads an already advanced step number and the step
-// graph needs no one-thread bump node.  Host-side state; consumed (reset) by the launch.
-int* dn_take_step_bump();
-
 static inline int dn_launch_status() {
   return hipGetLastError() == hipSuccess ? DN_OK : DN_LAUNCH_FAILED;
 }

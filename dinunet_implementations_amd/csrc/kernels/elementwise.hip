@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256)
 step_prologue_kernel(const float* __restrict__ x, long ux, bf16* __restrict__ xb,
                      const long long* __restrict__ y, long ny, long long* __restrict__ yd,
                      float* __restrict__ g, long ug, int* __restrict__ bump) {
-  if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;  // armed Adam step counter
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;  // Adam's device step counter
   const long total = ux + ug + ny;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
@@ -112,15 +112,16 @@ step_prologue_kernel(const float* __restrict__ x, long ux, bf16* __restrict__ xb
 
 }  // namespace
 
+// bump: the graph-captured Adam's device step counter, advanced once by this launch (null: none)
 DN_API int dn_step_prologue(const float* x, long nx, void* xb, const long long* y, long ny,
-                            long long* yd, float* g, long ng, hipStream_t st) {
+                            long long* yd, float* g, long ng, int* bump, hipStream_t st) {
   if (nx % 8 || ng % 4 || (((uintptr_t)x | (uintptr_t)xb | (uintptr_t)g) & 15)) return DN_BAD_SHAPE;
   const long total = nx / 8 + ng / 4 + ny;
   if (total <= 0) return DN_OK;
   long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, nx / 8,
-                     (bf16*)xb, y, ny, yd, g, ng / 4, dn_take_step_bump());
+                     (bf16*)xb, y, ny, yd, g, ng / 4, bump);
   return dn_launch_status();
 }
 

@@ -557,7 +557,7 @@ struct StepPrologue {
   long long* yd;
   float* g;
   long ux, ug, ny;
-  int* bump;  // armed Adam step counter (dn_set_step_bump), advanced once by the launch
+  int* bump;  // Adam's device step counter (graph-captured update), advanced once; null: none
 };
 
 __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
@@ -774,7 +774,8 @@ DN_API int dn_lstm_pack(const float* wih0, const float* bih0, const float* whh0,
 }
 
 // dn_lstm_pack + dn_step_prologue in ONE launch (x: nx fp32 -> xb bf16, nx % 8 == 0; y: ny int64
-// -> yd; g: ng floats zeroed, ng % 4 == 0; 16-B aligned x, xb, g)
+// -> yd; g: ng floats zeroed, ng % 4 == 0; 16-B aligned x, xb, g; bump: Adam's device step
+// counter advanced once, or null)
 DN_API int dn_lstm_pack_prologue(const float* wih0, const float* bih0, const float* whh0,
                                  const float* bhh0, const float* wih1, const float* bih1,
                                  const float* whh1, const float* bhh1, int I, int Hd, int ndir,
@@ -782,9 +783,9 @@ DN_API int dn_lstm_pack_prologue(const float* wih0, const float* bih0, const flo
                                  const float* const* cast_src, void* const* cast_dst,
                                  const int* cast_n, const float* x, long nx, void* xb,
                                  const long long* y, long ny, long long* yd, float* g, long ng,
-                                 hipStream_t st) {
+                                 int* bump, hipStream_t st) {
   if (nx % 8 || ng % 4 || (((uintptr_t)x | (uintptr_t)xb | (uintptr_t)g) & 15)) return DN_BAD_SHAPE;
-  const StepPrologue sp{x, (bf16*)xb, y, yd, g, nx / 8, ng / 4, ny, dn_take_step_bump()};
+  const StepPrologue sp{x, (bf16*)xb, y, yd, g, nx / 8, ng / 4, ny, bump};
   return lstm_pack_launch(wih0, bih0, whh0, bhh0, wih1, bih1, whh1, bhh1, I, Hd, ndir, wih_p,
                           bias_p, whh_p, whhT_p, ncast, cast_src, cast_dst, cast_n, sp, st);
 }

@@ -128,19 +128,3 @@ DN_API int dn_cast_bf16_f32(const void* in, float* out, long n, float scale, hip
                      out, n, scale);
   return dn_launch_status();
 }
-
-static int* g_step_bump = nullptr;
-int* dn_take_step_bump() {
-  int* p = g_step_bump;
-  g_step_bump = nullptr;
-  return p;
-}
-
-// Arm (tdev) or disarm (null) the one-shot step-counter advance of the next step-prologue
-// launch (dn_step_prologue / dn_lstm_pack_prologue).  Returns 1 when a previously armed counter
-// was never consumed (the caller's feed path launched no prologue), else 0.
-DN_API int dn_set_step_bump(int* tdev) {
-  const int stale = g_step_bump != nullptr;
-  g_step_bump = tdev;
-  return stale;
-}

@@ -43,7 +43,7 @@ _lib.register("dn_lstm_pack", [_lib.c_void_p] * 8 + [_lib.c_int] * 3 + [_lib.c_v
 _lib.register("dn_lstm_pack_prologue", [_lib.c_void_p] * 8 + [_lib.c_int] * 3
               + [_lib.c_void_p] * 4 + [_lib.c_int] + [_lib.c_void_p] * 3
               + [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
-                 _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p])
+                 _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
@@ -277,15 +277,18 @@ class defer_pack:
         return False
 
 
-def run_deferred_pack(records: list, prologue=None) -> None:
+def run_deferred_pack(records: list, prologue=None, bump: Optional[Tensor] = None) -> None:
     """Issue the recorded pack launches; the LAST one also runs the step prologue
-    ``(x fp32, xb bf16, y int64, yd int64, grad fp32)`` when given (``dn_lstm_pack_prologue``)."""
+    ``(x fp32, xb bf16, y int64, yd int64, grad fp32)`` when given (``dn_lstm_pack_prologue``),
+    advancing the int32 counter ``bump`` once when given."""
+    if bump is not None and prologue is None:
+        raise ValueError("run_deferred_pack: a step-counter bump rides on the prologue only")
     for k, (args, _keep) in enumerate(records):
         if prologue is not None and k == len(records) - 1:
             x, xb, y, yd, g = prologue
             _lib.call("dn_lstm_pack_prologue", *args, x.data_ptr(), x.numel(), xb.data_ptr(),
                       y.data_ptr(), y.numel(), yd.data_ptr(), g.data_ptr(), g.numel(),
-                      _lib.stream())
+                      _lib.ptr(bump), _lib.stream())
         else:
             _lib.call("dn_lstm_pack", *args, _lib.stream())
 

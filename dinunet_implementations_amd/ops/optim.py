@@ -25,10 +25,9 @@ _lib.register("dn_adam_dev", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.
                               _lib.c_long, _lib.c_float, _lib.c_double, _lib.c_double,
                               _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_void_p,
                               _lib.c_int, _lib.c_void_p])
-_lib.register("dn_set_step_bump", [_lib.c_void_p])
 _lib.register("dn_step_prologue", [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p,
                                    _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
-                                   _lib.c_void_p])
+                                   _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_sgd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                          _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_int,
                          _lib.c_void_p])
@@ -128,8 +127,9 @@ class FusedAdam:
         """One Adam step whose bias corrections come from the device step counter (advanced by
         the same launch), so it can be captured once and replayed every step.  The caller keeps
         ``step_count`` in sync (one increment per replay).  ``prebumped``: the caller advances
-        the counter in its step prologue instead (:meth:`arm_step_bump` before each replay), so
-        the update is ONE graph node, not Adam + a one-thread bump kernel."""
+        the counter in its step prologue instead (it passes :meth:`device_step` to the
+        prologue launch before each replay), so the update is ONE graph node, not Adam + a
+        one-thread bump kernel."""
         d = self.flat.data
         if self._tdev is None:
             self.sync_device_step()
@@ -139,17 +139,12 @@ class FusedAdam:
                   self.weight_decay, grad_scale, self._tdev.data_ptr(), int(prebumped),
                   _lib.stream())
 
-    def arm_step_bump(self):
-        """The next step-prologue launch advances the device step counter (one-shot)."""
+    def device_step(self) -> torch.Tensor:
+        """The device step counter (int32[1]) the graph-captured update reads; a step prologue
+        given it advances it once per launch."""
         if self._tdev is None:
             self.sync_device_step()
-        _lib.lib().dn_set_step_bump(self._tdev.data_ptr())
-
-    @staticmethod
-    def disarm_step_bump():
-        """Clear an armed advance; raises when no prologue launch consumed it."""
-        if _lib.lib().dn_set_step_bump(None):
-            raise RuntimeError("step counter armed but no step-prologue launch consumed it")
+        return self._tdev
 
     def state_dict(self) -> Dict:
         return {"lr": self.lr, "betas": self.betas, "eps": self.eps,
@@ -168,15 +163,16 @@ class FusedAdam:
 
 
 def step_prologue(x: torch.Tensor, xb: Optional[torch.Tensor], y: torch.Tensor,
-                  yd: torch.Tensor, grad: torch.Tensor):
+                  yd: torch.Tensor, grad: torch.Tensor, bump: Optional[torch.Tensor] = None):
     """ONE launch before a graph replay: ``xb <- bf16(x)`` (skipped when ``xb`` is None),
-    ``yd <- y`` (int64) and ``grad <- 0``."""
+    ``yd <- y`` (int64), ``grad <- 0`` and, when given, ``bump += 1`` (the captured Adam's
+    device step counter, :meth:`FusedAdam.device_step`)."""
     nx = x.numel() if xb is not None else 0
     if nx % 8 or grad.numel() % 4 or y.dtype != torch.int64 or yd.dtype != torch.int64:
         raise ValueError("step_prologue: x numel % 8, grad numel % 4 and int64 labels required")
     _lib.call("dn_step_prologue", x.data_ptr() if nx else None, nx,
               xb.data_ptr() if nx else None, y.data_ptr(), y.numel(), yd.data_ptr(),
-              grad.data_ptr(), grad.numel(), _lib.stream())
+              grad.data_ptr(), grad.numel(), _lib.ptr(bump), _lib.stream())
 
 
 def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):

@@ -144,20 +144,22 @@ class TrainStep:
 
     def _feed(self, x, y, sx, sy):
         """Before a replay, in ONE launch when possible: inputs into the static buffers, the
-        gradient buffer zeroed (the graphs no longer contain the zeroing) and the LSTM weight
-        repack the capture deferred out of the graph (``ops.lstm.defer_pack``)."""
+        gradient buffer zeroed (the graphs no longer contain the zeroing), the LSTM weight
+        repack the capture deferred out of the graph (``ops.lstm.defer_pack``) and, when the
+        update is captured (``_prebump``), the advance of Adam's device step counter."""
+        bump = self.opt.device_step() if (self.graph_opt and self._prebump) else None
         if self._packs:
             if self._bf16_in:
-                run_deferred_pack(self._packs, (x, sx, y, sy, self.flat.grad))
+                run_deferred_pack(self._packs, (x, sx, y, sy, self.flat.grad), bump)
                 return
             run_deferred_pack(self._packs)
         if self._bf16_in:
-            ops.step_prologue(x, sx, y, sy, self.flat.grad)
+            ops.step_prologue(x, sx, y, sy, self.flat.grad, bump)
             return
         if sx.data_ptr() != x.data_ptr():
             sx.copy_(x, non_blocking=True)
         if y.dtype == torch.int64 and self.flat.grad.numel() % 4 == 0:
-            ops.step_prologue(x, None, y, sy, self.flat.grad)
+            ops.step_prologue(x, None, y, sy, self.flat.grad, bump)
         else:
             if sy.data_ptr() != y.data_ptr():
                 sy.copy_(y, non_blocking=True)
@@ -246,17 +248,15 @@ class TrainStep:
             (self._capture_split if self.split else self._capture)(x, y)
         sx, sy, out, loss, pred = self.static
         if sx.shape != x.shape or sy.shape != y.shape:  # e.g. a ragged last batch
-            return self._eager(x, y)
+            loss = self._eager(x, y)
+            if self.graph_opt:
+                # the eager update advanced only the host step count: the captured update reads
+                # the device counter
+                self.opt.sync_device_step()
+            return loss
         T = self.timers
         with T.phase("fwd_bwd"):
-            if self.graph_opt and self._prebump:
-                self.opt.arm_step_bump()
-                try:
-                    self._feed(x, y, sx, sy)
-                finally:
-                    self.opt.disarm_step_bump()
-            else:
-                self._feed(x, y, sx, sy)
+            self._feed(x, y, sx, sy)
             self.graph.replay()
             if self.graph_b is not None:
                 for b in self._first_buckets:  # all-reduce under the stem backward

@@ -39,8 +39,10 @@ def test_sanitizer_toolchain_reports_heap_overflow(tmp_path):
     """Negative control: the same flags do catch an out-of-bounds write, so a clean run of the
     driver above means something."""
     src = tmp_path / "oob.cpp"
+    # the overflowed slot is written through a volatile pointer and read back into the exit
+    # code, so no optimisation level can drop the store before ASan instruments it
     src.write_text("#include <vector>\nint main(int c, char**) { std::vector<int> v(4);"
-                   " int* p = v.data(); p[c + 3] = 1; return p[0]; }\n")
+                   " volatile int* p = v.data(); p[c + 3] = 1; return p[c + 3] + p[0]; }\n")
     exe = str(tmp_path / "oob")
     r = subprocess.run([b.CXX, "-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer",
                         str(src), "-o", exe], capture_output=True, text=True)

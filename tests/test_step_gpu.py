@@ -220,9 +220,9 @@ def test_rankdad_step_graph_matches_eager():
     assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5)
 
 
-def test_step_counter_bump_is_one_shot():
-    """The armed Adam step counter is advanced by exactly one step-prologue launch; an armed
-    counter no prologue consumed is reported when disarmed."""
+def test_step_counter_bump_is_explicit():
+    """The step prologue advances exactly the counter it is given, once per launch, and
+    nothing when given none."""
     from dinunet_implementations_amd.ops import FlatParams, FusedAdam, step_prologue
     lin = torch.nn.Linear(8, 4).cuda()
     flat = FlatParams(lin.parameters())
@@ -233,13 +233,47 @@ def test_step_counter_bump_is_one_shot():
     y = torch.randint(0, 2, (4,), device="cuda")
     yd = torch.empty_like(y)
     xb = torch.empty_like(x, dtype=torch.bfloat16)
-    opt.arm_step_bump()
-    step_prologue(x, xb, y, yd, flat.grad)
-    FusedAdam.disarm_step_bump()
-    step_prologue(x, xb, y, yd, flat.grad)  # not armed: no advance
+    step_prologue(x, xb, y, yd, flat.grad, opt.device_step())
+    step_prologue(x, xb, y, yd, flat.grad)  # no counter: no advance
     torch.cuda.synchronize()
-    assert int(opt._tdev.item()) == 6
+    assert int(opt.device_step().item()) == 6
     assert torch.equal(yd, y) and torch.equal(xb, x.to(torch.bfloat16))
-    opt.arm_step_bump()
-    with pytest.raises(RuntimeError, match="no step-prologue"):
-        FusedAdam.disarm_step_bump()
+
+
+def test_ragged_batch_keeps_device_step_in_sync():
+    """A ragged batch after capture runs eagerly; the captured Adam's device counter must follow
+    the host step count so later replays match torch.optim.Adam's bias corrections."""
+    from dinunet_implementations_amd.ops import FlatParams, FusedAdam
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    from dinunet_implementations_amd.runtime.step import TrainStep
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 2)).cuda()
+    ref = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 2)).cuda()
+    ref.load_state_dict(net.state_dict())
+    flat = FlatParams(net.parameters())
+    opt = FusedAdam(flat, lr=1e-2)
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-2)
+    grp = SiteGroup(device=torch.device("cuda"))
+    eng = make_engine("dSGD", net, flat, grp, {"precision_bits": "32"})
+
+    def fl(model, x, y):
+        out = model(x)
+        loss = torch.nn.functional.cross_entropy(out, y)
+        return out, loss, out.argmax(1)
+
+    step = TrainStep(net, flat, opt, eng, forward_loss=fl, use_graph=True, eager_warmup=1)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    sizes = [8, 8, 8, 5, 8, 8]
+    for n in sizes:
+        x = torch.randn(n, 16, device="cuda", generator=g)
+        y = torch.randint(0, 2, (n,), device="cuda", generator=g)
+        step(x, y)
+        ropt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(x), y).backward()
+        ropt.step()
+    torch.cuda.synchronize()
+    assert step.graph is not None and step.graph_opt
+    assert int(opt.device_step().item()) == opt.step_count == len(sizes)
+    for p, q in zip(net.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, rtol=1e-4, atol=1e-5)
