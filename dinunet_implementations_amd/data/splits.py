@@ -35,8 +35,10 @@ def ratio_split(items: Sequence[Any], ratio: Sequence[float], seed: int = 0) -> 
 
 
 def kfold_splits(items: Sequence[Any], k: int, seed: int = 0) -> List[Dict[str, List[Any]]]:
-    if k < 2:
-        raise ValueError("num_folds must be >= 2")
+    if k < 3:
+        # fold i is the test set and fold i+1 the validation set: with k=2 nothing is left to
+        # train on
+        raise ValueError("num_folds must be >= 3")
     it = _shuffled(items, seed)
     folds = [it[i::k] for i in range(k)]
     out = []

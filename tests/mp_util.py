@@ -24,14 +24,26 @@ def _entry(rank, world, port, fn, args, outdir):
     torch.set_num_threads(2)
     from dinunet_implementations_amd.parallel import init_sites, shutdown
     res = None
+    grp = None
     try:
         grp = init_sites(backend="gloo", device="cpu")
         res = ("ok", fn(grp, *args))
-        shutdown()
     except Exception:  # pragma: no cover - surfaced by the parent
         res = ("err", traceback.format_exc())
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
+    # Tear down only after every rank has written its result: a rank that destroys its gloo
+    # context while a peer is still sending aborts ("terminate called without an active
+    # exception") in gloo's transport threads.  os._exit skips interpreter-exit destructors of
+    # those threads for the same reason; the result file is already on disk.
+    try:
+        if grp is not None and res[0] == "ok":
+            import torch.distributed as dist
+            dist.barrier()
+            shutdown()
+    except Exception:  # pragma: no cover
+        pass
+    os._exit(0)
 
 
 def run_world(fn, world, *args, _retry=True):
