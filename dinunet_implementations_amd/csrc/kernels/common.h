@@ -35,6 +35,22 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Buffer-resource stores (gfx950 raw buffer ops, 32-bit per-lane byte offset, hardware range
+// check): a lane whose offset is >= the descriptor's byte count is dropped by the hardware.  That
+// masks a store WITHOUT a branch, so hipcc keeps counting vmcnt exactly across it (a divergent
+// `if` around a store makes every later wait in the loop a conservative vmcnt(0)).
+constexpr uint32_t DN_OOB = 0x80000000u;
+// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt(0) only: the builtin form is seen by
+// hipcc's waitcnt bookkeeping (an asm wait is not)
+constexpr int DN_VMCNT0 = 0x0F70;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dn_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void dn_store_f32x4(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         r, (int)off, 0, 0);
+}
+
 static inline int dn_launch_status() {
   return hipGetLastError() == hipSuccess ? DN_OK : DN_LAUNCH_FAILED;
 }

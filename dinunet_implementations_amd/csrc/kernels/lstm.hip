@@ -83,6 +83,24 @@ __device__ __forceinline__ float row_gather(const float (&v)[16 / BR]) {
   }
 }
 
+// In-workgroup step hand-off without a barrier (LDS only).  A producer wave writes its h (or
+// dpre) tile to LDS, makes those writes complete (LDS-only release: s_waitcnt lgkmcnt(0)) and
+// adds 1 to its group's counter (4 producer waves per group, so after step t the counter is
+// 4 (t + 1)); a consumer polls that ONE word (relaxed atomic LDS load, wave-uniform) until it
+// reaches the step it needs, then reads the tile.  LDS services a wave's requests in order, so
+// a consumer that has seen the count reads the published data.  (A `volatile` poll would make
+// hipcc wait for every outstanding global load and store at each poll.)
+__device__ __forceinline__ void publish_count(int* ctr, bool leader) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (leader) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wait_count(int* ctr, int need) {
+  while (__builtin_amdgcn_readfirstlane(
+             __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+    __builtin_amdgcn_s_sleep(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
@@ -94,6 +112,32 @@ __device__ __forceinline__ float row_gather(const float (&v)[16 / BR]) {
 #ifndef BWD_CHAINS
 #define BWD_CHAINS 2
 #endif
+// LSTM_FLAGS: forward step hand-off through LDS counters (1) or a workgroup barrier (0);
+// LSTM_PRIO: wave priority raised over the gate phase (the step's critical path) when > 0
+#ifndef LSTM_FLAGS
+#define LSTM_FLAGS 0
+#endif
+#ifndef LSTM_PRIO
+#define LSTM_PRIO 0
+#endif
+// LSTM_POLY: the outer sigmoid of the reference's double sigmoid, sigmoid(s) for s = sigmoid(x)
+// in (0, 1), as a degree-5 polynomial (max abs error 6.2e-7 on [0, 1]: 5 FMAs instead of
+// mul + exp + add + rcp)
+#ifndef LSTM_POLY
+#define LSTM_POLY 0
+#endif
+__device__ __forceinline__ float sigmoid_unit(float s) {
+  if constexpr (LSTM_POLY) {
+    float v = 0.0011067962041124701f;
+    v = __builtin_fmaf(v, s, 0.0014183232560753822f);
+    v = __builtin_fmaf(v, s, -0.021660439670085907f);
+    v = __builtin_fmaf(v, s, 0.00021609874966088682f);
+    v = __builtin_fmaf(v, s, 0.24997784197330475f);
+    return __builtin_fmaf(v, s, 0.500000536441803f);
+  } else {
+    return dn_sigmoid(s);
+  }
+}
 template <int HD, int BR> struct LdsSplit { static constexpr int FWD_MT = 0, BWD_KS = 0; };
 template <> struct LdsSplit<192, 4> { static constexpr int FWD_MT = 0, BWD_KS = 4; };
 template <> struct LdsSplit<192, 8> { static constexpr int FWD_MT = 0, BWD_KS = 6; };
@@ -143,8 +187,9 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   constexpr int LDH = HD + 32;
   constexpr int NLM = UG == 1 ? LdsSplit<HD, BR>::FWD_MT : 0, NRM = MT - NLM;
   constexpr int G16 = 16 / BR, NSL1 = BR / 4, NSL = UG * NSL1;
-  constexpr int EPT = BR * HD / NT;  // h_{t-1} copy: elements per thread
   __shared__ __attribute__((aligned(16))) bf16 hbuf[2][16][LDH];
+  // hcnt[g] = h_t tiles published by producer group g (4 waves): 4 (t + 1) after step t
+  __shared__ __attribute__((aligned(16))) int hcnt[NW / 4];
   __shared__ __attribute__((aligned(16))) float bias_s[4 * HD];
   // lane-linear fragment image: one 1 KiB row per (wave, m-tile, k-step) -> conflict-free b128
   __shared__ __attribute__((aligned(16))) bf16x8 wlds[NLM > 0 ? NW : 1][NLM > 0 ? NLM : 1][NLM > 0 ? KS : 1][64];
@@ -172,64 +217,91 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   }
   for (int i = tid; i < 4 * HD; i += NT) bias_s[i] = bias[dir * 4 * HD + i];
   for (int i = tid; i < 2 * 16 * LDH; i += NT) (&hbuf[0][0][0])[i] = (bf16)0.f;
+  if (tid < NW / 4) hcnt[tid] = 0;
   __syncthreads();
 
   int uu[NSL];  // slot (group gu, s1) -> unit of m-tile 4*gu + r + s1*G16 of this wave
 #pragma unroll
   for (int s = 0; s < NSL; ++s)
     uu[s] = 16 * (UG * w + s / NSL1) + 4 * (r + (s % NSL1) * G16) + q;
-  float* xrow = xp + (long)bc * S * rowX + (long)dir * 4 * HD;
-  const bool wpre = store_pre && b < B;  // padded rows alias row B-1: never store them
-  const long hplane = (long)dir * Bp * S * HD;
-  const int cp_r = (tid * EPT) / HD, cp_c = (tid * EPT) % HD;
-  bf16* hcp = hprev + hplane + ((long)(blockIdx.x * BR + cp_r) * S) * HD + cp_c;
-  float* csv = c_save + hplane + (long)b * S * HD;
+  // Every per-step global access goes through a buffer descriptor with a 32-bit per-lane byte
+  // offset (host guarantees every buffer < 2 GiB): the step part of an address is one scalar
+  // multiply, no 64-bit address math per access.  Gate pre-activation stores of padded rows
+  // (b >= B) get an out-of-range offset and are dropped (no branch, see common.h); without a
+  // backward the descriptor has no records and every such store is dropped.
+  const int rowXi = ndir * 4 * HD;
+  const __amdgpu_buffer_rsrc_t x_rs = dn_rsrc(xp, (uint32_t)(B * S * rowXi * 4));
+  const __amdgpu_buffer_rsrc_t pre_rs = dn_rsrc(xp, store_pre ? (uint32_t)(B * S * rowXi * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t c_rs = dn_rsrc(c_save, (uint32_t)(ndir * Bp * S * HD * 4));
+  const __amdgpu_buffer_rsrc_t hp_rs = dn_rsrc(hprev, (uint32_t)(ndir * Bp * S * HD * 2));
+  uint32_t xo[NSL], po[NSL], co[NSL], ho[NSL];  // per-lane byte offsets at time index 0
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) {
+    xo[s] = (uint32_t)((bc * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 4);
+    po[s] = b < B ? (uint32_t)((b * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 4) : DN_OOB;
+    co[s] = (uint32_t)((((dir * Bp + b) * S) * HD + uu[s]) * 4);
+    ho[s] = (uint32_t)((((dir * Bp + b) * S) * HD + uu[s]) * 2);
+  }
+  const uint32_t xstep = (uint32_t)(rowXi * 4);  // bytes per time index
+  auto load_x = [&](int s, int tau) {  // time index -1 / S wraps out of range: reads 0
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+        x_rs, (int)(xo[s] + (uint32_t)tau * xstep), 0, 0));
+  };
+  // h_{t-1} for the weight-gradient GEMMs: each lane stores the h it produces into step t+1's
+  // slot (the last step's h has no slot: out-of-range offset, dropped); slot 0 holds h_{-1} = 0
+  {
+    const int tau0 = dir == 0 ? 0 : S - 1;
+#pragma unroll
+    for (int s = 0; s < NSL; ++s)
+      __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, hp_rs,
+                                            (int)(ho[s] + (uint32_t)(tau0 * HD * 2)), 0, 0);
+  }
 
   float c[NSL], hs[NSL], hl[NSL];
-  f32x4 xn[NSL], bbr[NSL];
+  // xa / xb: the input projection of the current / next step, ping-ponged over a 2-step
+  // unrolled loop so that no register copy (and no vmcnt wait) sits between a prefetch and its
+  // use one step later
+  f32x4 xa[NSL], xb[NSL], bbr[NSL];
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
     c[s] = hs[s] = hl[s] = 0.f;
     if constexpr (NSL == 1) bbr[s] = *reinterpret_cast<const f32x4*>(&bias_s[4 * uu[s]]);
-    const int tau0 = dir == 0 ? 0 : S - 1;
-    xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau0 * rowX + 4 * uu[s]);
+    xa[s] = load_x(s, dir == 0 ? 0 : S - 1);
   }
   int cur = 0;
+  // the resident-weight loads have all landed before the time loop: without this the loop's
+  // waitcnt bookkeeping (merged over the loop entry) keeps waiting on the previous step's stores
+  // in the MFMA phase
+  __builtin_amdgcn_s_waitcnt(DN_VMCNT0);
 #ifdef DN_STAMPS
   unsigned long long st_a = 0, st_b = 0, st_c = 0, ts0, ts1, ts2, ts3;
 #endif
-  for (int t = 0; t < S; ++t) {
+  // step t+1's projection is requested before this step's MFMAs (one gate slot per lane only:
+  // at BR >= 8 the second register set spills; those lanes re-load in place after the use)
+  constexpr bool EARLY = NSL == 1;
+  auto step = [&](const int t, f32x4 (&xn)[NSL], f32x4 (&xnn)[NSL]) {
+    __builtin_amdgcn_sched_barrier(0);  // step boundary for the scheduler (see the backward)
 #ifdef DN_STAMPS
     STAMP(ts0);
 #endif
     const int tau = dir == 0 ? t : S - 1 - t;
-    const int t1 = t + 1 < S ? t + 1 : t;
-    const int tau1 = dir == 0 ? t1 : S - 1 - t1;
-    // step t+1's projection, requested before this step's MFMAs: its address math and issue
-    // stay off the gate phase, which is the tail of the step's critical path
-    // (one gate slot per lane only: at BR >= 8 the extra registers spill)
-    constexpr bool EARLY = NSL == 1;
-    f32x4 xnn[NSL];
+    const int tau1 = dir == 0 ? t + 1 : S - 2 - t;  // past the end at the last step: reads 0
     if constexpr (EARLY) {
 #pragma unroll
-      for (int s = 0; s < NSL; ++s)
-        xnn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 4 * uu[s]);
+      for (int s = 0; s < NSL; ++s) xnn[s] = load_x(s, tau1);
     }
-    // h_{t-1} (the tile every wave reads below) -> global for the weight-gradient GEMMs
-    if constexpr (EPT == 4) {
-      *reinterpret_cast<bf16x4*>(hcp + (long)tau * HD) = *reinterpret_cast<const bf16x4*>(&hbuf[cur][cp_r][cp_c]);
-    } else if constexpr (EPT == 2) {
-      *reinterpret_cast<unsigned*>(hcp + (long)tau * HD) = *reinterpret_cast<const unsigned*>(&hbuf[cur][cp_r][cp_c]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < EPT; ++e) hcp[(long)tau * HD + e] = hbuf[cur][cp_r][cp_c + e];
-    }
-    // recurrent GEMM  pre^T[m][b] = sum_k W[m][k] h[b][k]  (W resident)
+    // recurrent GEMM  pre^T[m][b] = sum_k W[m][k] h[b][k]  (W resident).  No workgroup
+    // barrier: before the k-steps of a group of 4 producer waves (64*UG units of h_{t-1}) the
+    // wave polls that group's counter, so its MFMAs start on the units already published
+    // while the slower waves still run the gate math of step t-1
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      if constexpr (LSTM_FLAGS) {
+        if (ks % (2 * UG) == 0) wait_count(&hcnt[ks / (2 * UG)], 4 * t);
+      }
       // unmasked (exec-masking made the compiler branch and drain lgkmcnt before every MFMA):
       // lanes of padded columns re-read a valid row, see above
       const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
@@ -260,6 +332,7 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
     { float z = pa[0][0]; asm volatile("" :: "v"(z)); }
     STAMP(ts1);
 #endif
+    if constexpr (LSTM_PRIO > 0) __builtin_amdgcn_s_setprio(LSTM_PRIO);
     const int nxt = cur ^ 1;
 #pragma unroll
     for (int s = 0; s < NSL; ++s) {
@@ -271,31 +344,47 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
       const float p3 = pa[s][3] + xn[s][3] + bb[3];
       // the gate pre-activations x W_ih^T + h W_hh^T + b, in place of the projection they were
       // built from: the backward reads them instead of re-running a time-parallel GEMM
-      if (wpre) *reinterpret_cast<f32x4*>(xrow + (long)tau * rowX + 4 * u) = f32x4{p0, p1, p2, p3};
-      if constexpr (EARLY) xn[s] = xnn[s];
-      else xn[s] = *reinterpret_cast<const f32x4*>(xrow + (long)tau1 * rowX + 4 * u);
-      const float gi = dn_sigmoid(dn_sigmoid(p0));
-      const float gf = dn_sigmoid(dn_sigmoid(p1));
-      const float go = dn_sigmoid(dn_sigmoid(p2));
+      dn_store_f32x4(pre_rs, po[s] + (uint32_t)tau * xstep, f32x4{p0, p1, p2, p3});
+      if constexpr (!EARLY) xn[s] = load_x(s, tau1);
+      const float gi = sigmoid_unit(dn_sigmoid(p0));
+      const float gf = sigmoid_unit(dn_sigmoid(p1));
+      const float go = sigmoid_unit(dn_sigmoid(p2));
       const float gg = dn_tanh(p3);
       c[s] = gf * c[s] + gi * gg;
       const float h = go * dn_tanh(c[s]);
-      csv[(long)tau * HD + u] = c[s];
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, c[s]), c_rs,
+                                            (int)(co[s] + (uint32_t)(tau * HD * 4)), 0, 0);
       if constexpr (SEQ) hseq[((long)b * S + t) * ndir * HD + dir * HD + u] = h;
       hs[s] += h;
       hl[s] = h;
-      hbuf[nxt][bl][u] = (bf16)h;
+      const bf16 hb16 = (bf16)h;
+      hbuf[nxt][bl][u] = hb16;
+      __builtin_amdgcn_raw_buffer_store_b16(
+          __builtin_bit_cast(unsigned short, hb16), hp_rs,
+          (int)(t + 1 < S ? ho[s] + (uint32_t)(tau1 * HD * 2) : DN_OOB), 0, 0);
     }
 #ifdef DN_STAMPS
     STAMP(ts2);
 #endif
-    __syncthreads();
+    if constexpr (LSTM_FLAGS) publish_count(&hcnt[w / 4], lane == 0);
+    else __syncthreads();
+    if constexpr (LSTM_PRIO > 0) __builtin_amdgcn_s_setprio(0);
 #ifdef DN_STAMPS
     STAMP(ts3);
     st_a += ts1 - ts0; st_b += ts2 - ts1; st_c += ts3 - ts2;
 #endif
     cur = nxt;
+  };
+  int t = 0;
+  if constexpr (EARLY) {
+    for (; t + 1 < S; t += 2) {
+      step(t, xa, xb);
+      step(t + 1, xb, xa);
+    }
+  } else {
+    for (; t < S; ++t) step(t, xa, xa);
   }
+  if (t < S) step(t, xa, xb);
 #ifdef DN_STAMPS
   if (lane == 0 && blockIdx.x == 0) {
     unsigned long long* o = dn_stamp_buf + (blockIdx.y * 64 + w) * 4;
@@ -382,42 +471,59 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   const int tauL = dir == 0 ? S - 1 : 0;
   const int tp0 = S >= 2 ? S - 2 : 0;
   const int tauP = dir == 0 ? tp0 : S - 1 - tp0;
-  float cc[NSL], cpn[NSL];
+  // pn: step t's gate pre-activations; ca / cb: c_t and c_{t-1}, alternating roles over a 2-step
+  // unrolled loop.  Each step turns pn and c_t into gate activations FIRST (they need no MFMA
+  // result), then reloads the same registers with step t-1's pre-activations and c_{t-2}: the
+  // loads fly during this step's MFMAs and gate phase, and nothing copies a register that a load
+  // is still filling (such a copy is a vmcnt wait at the end of the step)
+  float ca[NSL], cb[NSL], dTl[NSL];
   f32x4 pn[NSL];
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
-    cc[s] = crow[(long)tauL * HD + uu[s]];
-    cpn[s] = crow[(long)tauP * HD + uu[s]];
+    const int uc = uu[s] < Hd ? uu[s] : Hd - 1;
+    dTl[s] = dhT ? dhT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s] : 0.f;  // dL/dh_T
+    ca[s] = crow[(long)tauL * HD + uu[s]];
+    cb[s] = crow[(long)tauP * HD + uu[s]];
     pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tauL * rowX + 4 * uu[s]);
   }
   __syncthreads();
+  __builtin_amdgcn_s_waitcnt(DN_VMCNT0);  // resident weights landed (see the forward)
 
   int cur = 0;
 #ifdef DN_STAMPS
   unsigned long long st_a = 0, st_b = 0, st_c = 0, ts0, ts1, ts2, ts3;
 #endif
-  for (int t = S - 1; t >= 0; --t) {
+  auto step = [&](const int t, float (&ccur)[NSL], float (&cprv)[NSL]) {
+    // nothing of a later step is scheduled above this point: hipcc otherwise hoists the next
+    // step's gate math (which needs only the loads issued here) into this step's MFMA phase
+    // and waits there for a load it has just issued
+    __builtin_amdgcn_sched_barrier(0);
 #ifdef DN_STAMPS
     STAMP(ts0);
 #endif
     const int tau = dir == 0 ? t : S - 1 - t;
-    // step t-1's pre-activations and c_{t-2}, requested before this step's MFMAs (their
-    // address math and issue stay off the gate phase at the tail of the step)
     const int t1 = t > 0 ? t - 1 : 0;
     const int tau1 = dir == 0 ? t1 : S - 1 - t1;
     const int t2 = t > 1 ? t - 2 : 0;
     const int tau2 = dir == 0 ? t2 : S - 1 - t2;
-    // (one gate slot per lane, no per-step dh loads only: otherwise the registers spill)
-    constexpr bool EARLY = NSL == 1 && !DSEQ;
-    f32x4 pnn[NSL];
-    float cpnn[NSL];
-    if constexpr (EARLY) {
+    float si[NSL], sf[NSL], so[NSL], gi[NSL], gf[NSL], go[NSL], gg[NSL], tc[NSL], cp[NSL];
+    auto activations = [&]() {
 #pragma unroll
       for (int s = 0; s < NSL; ++s) {
-        pnn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
-        cpnn[s] = crow[(long)tau2 * HD + uu[s]];
+        const f32x4 pc = pn[s];
+        cp[s] = t > 0 ? cprv[s] : 0.f;
+        si[s] = dn_sigmoid(pc[0]); sf[s] = dn_sigmoid(pc[1]); so[s] = dn_sigmoid(pc[2]);
+        gi[s] = sigmoid_unit(si[s]); gf[s] = sigmoid_unit(sf[s]); go[s] = sigmoid_unit(so[s]);
+        gg[s] = dn_tanh(pc[3]);
+        tc[s] = dn_tanh(ccur[s]);
+        pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
+        ccur[s] = crow[(long)tau2 * HD + uu[s]];
       }
-    }
+    };
+    // up to 2 gate slots per lane the activations are live across the MFMAs; at 4 (BR = 16)
+    // they would spill, so they follow the MFMAs there
+    constexpr bool HOIST = NSL <= 2;
+    if constexpr (HOIST) activations();
     float dx[NSL];
 #pragma unroll
     for (int s = 0; s < NSL; ++s) {
@@ -426,13 +532,7 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
         const int uc = uu[s] < Hd ? uu[s] : Hd - 1;
         dx[s] = dhrow[(long)t * dh_st + uc] * dh_scale * msk[s];
       }
-    }
-    if (t == S - 1 && dhT) {
-#pragma unroll
-      for (int s = 0; s < NSL; ++s) {
-        const int uc = uu[s] < Hd ? uu[s] : Hd - 1;
-        dx[s] += dhT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s];
-      }
+      dx[s] += t == S - 1 ? dTl[s] : 0.f;  // select: no load in the loop
     }
     // K = 4*HD runs as BWD_CHAINS independent accumulator chains per unit group (summed after
     // the loop): one chain of 24 dependent MFMAs left the SIMD waiting on its own results
@@ -477,34 +577,21 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     { float z = dhr[0]; asm volatile("" :: "v"(z)); }
     STAMP(ts1);
 #endif
+    if constexpr (!HOIST) activations();
     const int nxt = cur ^ 1;
 #pragma unroll
     for (int s = 0; s < NSL; ++s) {
-      const f32x4 pc = pn[s];
-      const float cp = t > 0 ? cpn[s] : 0.f;
-      if constexpr (EARLY) {
-        pn[s] = pnn[s];
-        cpn[s] = cpnn[s];
-      } else {  // consumed: issue step t-1's pre and c_{t-2} (hidden by the next MFMA phase)
-        pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
-        cpn[s] = crow[(long)tau2 * HD + uu[s]];
-      }
-      const float si = dn_sigmoid(pc[0]), sf = dn_sigmoid(pc[1]), so = dn_sigmoid(pc[2]);
-      const float gi = dn_sigmoid(si), gf = dn_sigmoid(sf), go = dn_sigmoid(so);
-      const float gg = dn_tanh(pc[3]);
-      const float tc = dn_tanh(cc[s]);
       const float dh = dhr[s] + dx[s];
-      const float dc = dcc[s] + dh * go * (1.f - tc * tc);
-      const float d_o = dh * tc;
-      const float d_i = dc * gg, d_g = dc * gi, d_f = dc * cp;
+      const float dc = dcc[s] + dh * go[s] * (1.f - tc[s] * tc[s]);
+      const float d_o = dh * tc[s];
+      const float d_i = dc * gg[s], d_g = dc * gi[s], d_f = dc * cp[s];
       const float m = msk[s];
-      dcc[s] = dc * gf * m;
-      cc[s] = cp;
+      dcc[s] = dc * gf[s] * m;
       bf16x4 e;
-      e[0] = (bf16)(m * d_i * gi * (1.f - gi) * si * (1.f - si));
-      e[1] = (bf16)(m * d_f * gf * (1.f - gf) * sf * (1.f - sf));
-      e[2] = (bf16)(m * d_o * go * (1.f - go) * so * (1.f - so));
-      e[3] = (bf16)(m * d_g * (1.f - gg * gg));
+      e[0] = (bf16)(m * d_i * gi[s] * (1.f - gi[s]) * si[s] * (1.f - si[s]));
+      e[1] = (bf16)(m * d_f * gf[s] * (1.f - gf[s]) * sf[s] * (1.f - sf[s]));
+      e[2] = (bf16)(m * d_o * go[s] * (1.f - go[s]) * so[s] * (1.f - so[s]));
+      e[3] = (bf16)(m * d_g * (1.f - gg[s] * gg[s]));
       *reinterpret_cast<bf16x4*>(&dbuf[nxt][bl][4 * uu[s]]) = e;
       *reinterpret_cast<bf16x4*>(drow + (long)tau * rowX + 4 * uu[s]) = e;
     }
@@ -517,7 +604,13 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     st_a += ts1 - ts0; st_b += ts2 - ts1; st_c += ts3 - ts2;
 #endif
     cur = nxt;
+  };
+  int t = S - 1;
+  for (; t >= 1; t -= 2) {
+    step(t, ca, cb);
+    step(t - 1, cb, ca);
   }
+  if (t >= 0) step(t, ca, cb);
 #ifdef DN_STAMPS
   if (lane == 0 && blockIdx.x == 0) {
     unsigned long long* o = dn_stamp_buf + (256 + blockIdx.y * 64 + w) * 4;

@@ -21,7 +21,9 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 
 # (kernel-name regex) -> max tolerated private segment bytes
 ALLOWED = {
-    r"lstm_bwd_kernelILi192ELi(8|16)E": 64,  # BR = 8 / 16 backward (batch > 128 only)
+    # BR = 16 backward with a per-step output gradient (sequence-output mode, batch > 512 only;
+    # the ICA model's temporal-mean mode does not spill)
+    r"lstm_bwd_kernelILi192ELi16ELb1E": 96,
 }
 
 
