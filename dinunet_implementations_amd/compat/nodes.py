@@ -388,8 +388,22 @@ class RemoteNode:
         self.step += 1
         steps = max(self.steps_per_epoch, 1)
         if self.step >= steps:
-            self.phase = "validation"
-            return {"output": {"command": "validate", "apply_file": apply_file, "cfg": self.cfg}}
+            # validation every `validation_epochs` epochs (compspec.json:149-160), the same rule
+            # as the collective runtime (runtime/site.py); patience counts validations
+            ve = max(1, int(self.cfg.get("validation_epochs", 1)))
+            if self.epoch % ve == 0:
+                self.phase = "validation"
+                return {"output": {"command": "validate", "apply_file": apply_file, "cfg": self.cfg}}
+            last = self.epoch >= int(self.cfg.get("epochs", 1))
+            self.rlogs["cumulative_total_duration"].append(time.time() - self.t_start)
+            self.epoch += 1
+            self.step = 0
+            out = {"command": "train_round", "apply_file": apply_file, "cfg": self.cfg,
+                   "epoch_end": True}
+            if last:  # sites apply the last update and stop; the next round is the test
+                self.phase = "test"
+                out["stop"] = True
+            return {"output": out}
         return {"output": {"command": "train_round", "apply_file": apply_file, "cfg": self.cfg}}
 
     @property

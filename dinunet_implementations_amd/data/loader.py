@@ -30,6 +30,7 @@ class DeviceLoader:
         # with batch stats even in eval): fold it into the previous batch instead
         self.merge_singleton = merge_singleton
         self._gen = torch.Generator(device="cpu")
+        self._pos = 0  # batches yielded by the current pass (resume position)
 
     def __len__(self):
         n = self.inputs.shape[0]
@@ -56,8 +57,10 @@ class DeviceLoader:
         else:
             perm = None
         self.epoch += 1
+        self._pos = 0
         nb = len(self)
         for b in range(nb):
+            self._pos = b + 1
             s = b * self.batch_size
             e = n if b == nb - 1 and not self.drop_last else min(n, s + self.batch_size)
             if perm is None:
@@ -66,3 +69,17 @@ class DeviceLoader:
             else:
                 ix = perm[s:e]
                 yield self.inputs.index_select(0, ix), self.labels.index_select(0, ix), ix
+
+    # ---- resume ------------------------------------------------------------------------------
+    def state(self) -> dict:
+        """Position for an exact resume: passes started and batches consumed in the current one
+        (the shuffle of a pass is a pure function of ``seed`` and its pass number)."""
+        return {"epoch": int(self.epoch), "pos": int(self._pos)}
+
+    def resume_iter(self, state: dict):
+        """An iterator that continues where :meth:`state` was taken."""
+        self.epoch = max(0, int(state.get("epoch", 0)) - 1)
+        it = iter(self)
+        for _ in range(int(state.get("pos", 0))):
+            next(it, None)
+        return it

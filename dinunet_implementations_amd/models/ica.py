@@ -17,6 +17,7 @@ launch per direction (``ops.head``).  On CPU the module runs the reference math
 from __future__ import annotations
 
 import os
+import warnings
 from typing import Optional, Tuple
 
 import torch
@@ -91,6 +92,8 @@ class LSTM(nn.Module):
             params = [cell.params() for cell in self.lstms]
             return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms), packed=packed,
                               xp=xp)
+        if x.is_cuda and self.use_fused:
+            _slow_lstm_gate(self.hidden_size, x.shape[0])
         if h is not None:
             hs, (h_t, c_t) = self.lstms[0](x, h)
             if self.bidirectional:
@@ -103,6 +106,24 @@ class LSTM(nn.Module):
         if reduce == "mean":
             return hs.mean(1), (h_t, c_t)
         return hs, (h_t, c_t)
+
+
+_SLOW_WARNED = False
+
+
+def _slow_lstm_gate(hidden: int, batch: int):
+    """A GPU LSTM the persistent kernels do not cover (per-direction hidden > 192: W_hh no longer
+    fits the register file of one CU) runs the reference's per-step loop of library ops, ~100x
+    slower.  That is never silent: it raises unless ``DINUNET_ALLOW_SLOW_LSTM=1`` opts in, and
+    then warns once."""
+    global _SLOW_WARNED
+    msg = (f"LSTM hidden {hidden} (batch {batch}) is outside the fused gfx950 kernels "
+           f"(per-direction hidden <= 192); the step-by-step reference loop would run instead")
+    if os.environ.get("DINUNET_ALLOW_SLOW_LSTM", "0") != "1":
+        raise NotImplementedError(msg + ": set DINUNET_ALLOW_SLOW_LSTM=1 to accept it")
+    if not _SLOW_WARNED:
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
+        _SLOW_WARNED = True
 
 
 class ICALstm(nn.Module):

@@ -57,6 +57,15 @@ class Engine:
     def reduce(self) -> float:
         raise NotImplementedError
 
+    # resume ------------------------------------------------------------------------------------
+    def state_dict(self) -> Dict[str, object]:
+        """Engine state a resumed run needs to continue the same curve (warm-started factors,
+        error feedback); empty for stateless engines."""
+        return {}
+
+    def load_state_dict(self, sd: Dict[str, object]):
+        pass
+
     # file-transport path (COINSTAC compat) ---------------------------------------------------
     def payload(self) -> Dict[str, Tensor]:
         raise NotImplementedError
@@ -347,6 +356,13 @@ class RankDADEngine(Engine):
         self._act_ptrs = torch.tensor([self._active.data_ptr() + 4 * i for i in range(n)],
                                       dtype=torch.int64).to(dev)
 
+    def state_dict(self):
+        return {"q": [q.detach().cpu().clone() for q in getattr(self, "_q", [])]}
+
+    def load_state_dict(self, sd):
+        for q, v in zip(getattr(self, "_q", []), sd.get("q", [])):
+            q.copy_(v.to(q.device))
+
     def pre_reduce(self):
         """Local rank-r factors of every large Linear's gradient into the send buffer: one
         ``dn_pi_iterate`` (4 launches, all layers) per power iteration, no host sync
@@ -525,6 +541,15 @@ class PowerSGDEngine(Engine):
         dev = flat.data.device
         self.Q = [torch.randn(c, r, generator=gen).to(dev) for _, _, c, r in self.mats]
         self.err = [torch.zeros(rw, c, device=dev) for _, rw, c, _ in self.mats]
+
+    def state_dict(self):
+        return {"Q": [q.detach().cpu().clone() for q in self.Q],
+                "err": [e.detach().cpu().clone() for e in self.err]}
+
+    def load_state_dict(self, sd):
+        for dst, key in ((self.Q, "Q"), (self.err, "err")):
+            for t, v in zip(dst, sd.get(key, [])):
+                t.copy_(v.to(t.device))
 
     def _dense_pack(self):
         g = self.flat.grad

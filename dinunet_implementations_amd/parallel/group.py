@@ -100,9 +100,16 @@ _GROUP: Optional[SiteGroup] = None
 
 
 def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
-               timeout_s: int = 1800) -> SiteGroup:
-    """Initialise from torchrun-style env vars; world 1 when they are absent."""
+               timeout_s: Optional[int] = None) -> SiteGroup:
+    """Initialise from torchrun-style env vars; world 1 when they are absent.
+
+    ``timeout_s`` (default ``DINUNET_PG_TIMEOUT``, else 1800 s) bounds every collective: a site
+    that dies or hangs makes the survivors' next collective fail (gloo: at once when the peer's
+    socket closes; RCCL: the process-group watchdog after the timeout) instead of waiting
+    forever; ``run.py`` then reports the failure and exits non-zero."""
     global _GROUP
+    if timeout_s is None:
+        timeout_s = int(os.environ.get("DINUNET_PG_TIMEOUT", "1800"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))

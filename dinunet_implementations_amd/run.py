@@ -51,7 +51,15 @@ def main(argv=None):
     state = {"baseDirectory": base, "clientId": f"local{grp.rank}"}
     out = a.out or os.path.join(a.data_path, "output")
     T, D, H = get_task(cfg["task_id"])
-    FederatedSite(cfg, grp, T, D, H, state, out, site_name=f"local{grp.rank}").run()
+    try:
+        FederatedSite(cfg, grp, T, D, H, state, out, site_name=f"local{grp.rank}").run()
+    except Exception as e:  # a peer site died / timed out, or this site failed
+        # report and leave without tearing the process group down: a destroy that waits on a
+        # dead peer would hang this survivor too
+        print(f"[local{grp.rank}] site failure ({type(e).__name__}): {e}", file=sys.stderr,
+              flush=True)
+        sys.stdout.flush()
+        os._exit(3)
     shutdown()
     return 0
 

@@ -25,6 +25,7 @@ from __future__ import annotations
 import copy
 import math
 import os
+import signal
 import time
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -38,6 +39,16 @@ from ..utils import logs as L
 from ..utils.metrics import Averages, Metrics, improved, metric_value
 from .step import TrainStep
 from .trainer import NNTrainer, set_seed
+
+
+def _fault_step(rank: int) -> Optional[int]:
+    """``DINUNET_FAULT=<rank>:<step>``: that rank kills itself (SIGKILL, no cleanup) before its
+    <step>-th training step -- the dead-site case the failure-path test exercises."""
+    spec = os.environ.get("DINUNET_FAULT", "")
+    if not spec:
+        return None
+    r, _, s = spec.partition(":")
+    return int(s or 0) if int(r) == rank else None
 
 
 class FederatedSite:
@@ -117,7 +128,8 @@ class FederatedSite:
     # ---- train loops ------------------------------------------------------------------------
     def _train_epochs(self, trainer: NNTrainer, engine, data, cfg: Dict[str, Any], group: SiteGroup,
                       fold_dir: str, seed: int, logs: Dict[str, Any], tag: str = "",
-                      start_epoch: int = 1, best: Optional[Dict[str, Any]] = None):
+                      start_epoch: int = 1, best: Optional[Dict[str, Any]] = None,
+                      resume: Optional[Dict[str, Any]] = None):
         bs = int(cfg.get("batch_size", 16))
         li = max(1, int(cfg.get("local_iterations", 1)))
         tr = self._loader(*data["train"], "train", bs, seed)
@@ -146,20 +158,25 @@ class FederatedSite:
                 step = TrainStep(trainer.modules(), trainer.flat, trainer.optimizer, engine,
                                  use_graph=use_graph,
                                  forward_loss=lambda m, x, y: trainer.forward_loss(x, y))
-        it = iter(tr)
+        it = tr.resume_iter(resume["loader"]) if resume and resume.get("loader") else iter(tr)
+        fault_at = _fault_step(group.rank)
         tl = logs.setdefault(f"{tag}train_log", [])
         vl = logs.setdefault(f"{tag}validation_log", [])
         lvl = logs.setdefault(f"{tag}local_validation_log", [])
         comp = logs.setdefault("time_spent_on_computation", [])
         cum = logs.setdefault("cumulative_total_duration", [])
         itd = logs.setdefault("local_iter_duration", [])
-        t_run = time.time()
+        t_run = time.time() - (cum[-1] if cum else 0.0)  # a resumed run continues the clock
         trainer.train()
         for epoch in range(start_epoch, epochs + 1):
             t0 = time.time()
             avg, met = trainer.new_averages(), trainer.new_metrics()
             nsamp = 0
             for _ in range(steps):
+                if fault_at is not None:  # failure-path tests (DINUNET_FAULT=<rank>:<step>)
+                    fault_at -= 1
+                    if fault_at < 0:
+                        os.kill(os.getpid(), signal.SIGKILL)
                 if step is not None:
                     try:
                         x, y, _ix = next(it)
@@ -220,14 +237,19 @@ class FederatedSite:
                         stop = True
                 self.log(f"{tag}epoch {epoch} train_loss {avg.average:.4f} val_loss {r['loss']:.4f} "
                          f"val_{monitor} {score:.4f} best@{best['epoch']}")
-                if cfg.get("checkpoint_every_validation", True):
-                    trainer.save_checkpoint(os.path.join(fold_dir, f"{tag}checkpoint_last.pt"),
-                                            epoch=epoch, best=dict(best), logs=None)
                 if cfg.get("check_replicas") and group.distributed and engine.name != "dSGD-local":
                     ok = self._replica_checksum(trainer)
                     logs.setdefault("replica_check", []).append(bool(ok))
             comp.append(time.time() - t0)
             cum.append(time.time() - t_run)
+            if epoch % val_every == 0 and cfg.get("checkpoint_every_validation", True):
+                # everything a resume needs to continue this exact curve:
+                # weights + optimizer, best/patience, the log history, every RNG, the train
+                # loader's position and the engine's warm-start / error-feedback state
+                trainer.save_checkpoint(os.path.join(fold_dir, f"{tag}checkpoint_last.pt"),
+                                        epoch=epoch, best=dict(best), logs=copy.deepcopy(logs),
+                                        rng=trainer.rng_state(), loader=tr.state(),
+                                        engine=engine.state_dict(), stopped=bool(stop))
             if stop:
                 logs[f"{tag}stopped_epoch"] = epoch
                 break
@@ -280,7 +302,7 @@ class FederatedSite:
         trainer = self.Trainer(cache=cfg, state=self.state, device=self.device)
         trainer.init_nn(seed=int(cfg.get("seed", 0) or 0) + fold)  # same init on every site
         self._broadcast_model(trainer, 0)
-        start_epoch, best = 1, None
+        start_epoch, best, resume = 1, None, None
         last = os.path.join(fdir, "checkpoint_last.pt")
         if cfg.get("mode") == "test":
             path = cfg.get("pretrained_path") or os.path.join(fdir, "checkpoint_best.pt")
@@ -288,16 +310,26 @@ class FederatedSite:
             best = {"epoch": 0, "score": None}
         else:
             if cfg.get("resume") and os.path.exists(last):
-                st = trainer.load_checkpoint(last, load_optimizer=True)
-                start_epoch = int(st.get("epoch", 0)) + 1
-                best = st.get("best")
+                resume = trainer.load_checkpoint(last, load_optimizer=True)
+                start_epoch = int(resume.get("epoch", 0)) + 1
+                best = resume.get("best")
+                if resume.get("stopped"):  # early stopping had already ended this fold
+                    logs["stopped_epoch"] = int(resume.get("epoch", 0))
+                    start_epoch = int(cfg.get("epochs", 1)) + 1
+                for k, v in (resume.get("logs") or {}).items():
+                    logs.setdefault(k, v)
                 self.log(f"resuming fold {fold} at epoch {start_epoch}")
             elif cfg.get("pretrain"):
                 self._pretrain(trainer, data, fdir, seed, logs)
             engine = make_engine(str(cfg.get("agg_engine", "dSGD")), trainer.modules(), trainer.flat,
                                  self.group, cfg)
+            if resume is not None:
+                if resume.get("engine"):
+                    engine.load_state_dict(resume["engine"])
+                if resume.get("rng"):
+                    trainer.load_rng_state(resume["rng"])
             best = self._train_epochs(trainer, engine, data, cfg, self.group, fdir, seed, logs,
-                                      start_epoch=start_epoch, best=best)
+                                      start_epoch=start_epoch, best=best, resume=resume)
             if hasattr(engine, "close"):
                 engine.close()
             trainer.load_checkpoint(os.path.join(fdir, "checkpoint_best.pt"))

@@ -136,6 +136,43 @@ class NNTrainer:
         st.update(extra)
         return st
 
+    # ---- random state (resume continues the same training curve) -------------
+    def rng_state(self) -> Dict[str, Any]:
+        """Every generator a training step draws from: torch (CPU, and the device's when on a
+        GPU), Python ``random``, NumPy, and the device-side dropout counters of fused heads."""
+        npst = np.random.get_state()
+        st: Dict[str, Any] = {
+            "torch": torch.get_rng_state(),
+            "python": random.getstate(),
+            "numpy": {"keys": torch.from_numpy(npst[1].astype(np.int64)), "pos": int(npst[2]),
+                      "has_gauss": int(npst[3]), "cached": float(npst[4])},
+        }
+        dev = self.device["gpu"]
+        if dev.type == "cuda":
+            st["cuda"] = torch.cuda.get_rng_state(dev)
+        heads = {}
+        for k, m in self.nn.items():
+            spec = getattr(m, "_head", None)
+            if spec is not None and getattr(spec, "_rng", None) is not None:
+                heads[k] = spec._rng.detach().cpu().clone()
+        st["heads"] = heads
+        return st
+
+    def load_rng_state(self, st: Dict[str, Any]):
+        torch.set_rng_state(st["torch"])
+        py = st["python"]
+        random.setstate((py[0], tuple(py[1]), py[2]))
+        n = st["numpy"]
+        np.random.set_state(("MT19937", n["keys"].numpy().astype(np.uint32), n["pos"],
+                             n["has_gauss"], n["cached"]))
+        dev = self.device["gpu"]
+        if dev.type == "cuda" and "cuda" in st:
+            torch.cuda.set_rng_state(st["cuda"], dev)
+        for k, t in (st.get("heads") or {}).items():
+            spec = getattr(self.nn.get(k), "head_spec", None)
+            if spec is not None:
+                spec().rng(dev).copy_(t.to(dev))
+
     def save_checkpoint(self, path: str, **extra):
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         tmp = path + ".tmp"

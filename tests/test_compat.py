@@ -55,3 +55,22 @@ def test_reference_entry_callbacks_and_stdio(fs_data_root, tmp_path):
           stdout=buf)
     lines = [json.loads(l) for l in buf.getvalue().splitlines()]
     assert lines == [{"output": {"echo": 1}}, {"output": "r"}]
+
+
+def test_simulator_validation_epochs(fs_data_root, tmp_path):
+    """The remote validates every `validation_epochs` epochs (compspec.json:149-160), like the
+    collective runtime; training still runs every epoch and ends with a test."""
+    from dinunet_implementations_amd.compat.nodes import LocalNode, RemoteNode
+    from dinunet_implementations_amd.compat.simulator import simulate
+    it, locs, rem = simulate(fs_data_root, str(tmp_path), lambda: LocalNode(device="cpu"), RemoteNode,
+                             overrides={"epochs": 5, "validation_epochs": 2, "patience": 100})
+    r = json.load(open(os.path.join(str(tmp_path), "output", "remote", "simulatorRun",
+                                    "FS-Classification", "fold_0", "logs.json")))
+    assert len(r["validation_log"]) == 2           # epochs 2 and 4
+    assert r["best_val_epoch"] in (2, 4)
+    assert len(r["cumulative_total_duration"]) == 5  # every epoch ends once
+    site = json.load(open(os.path.join(str(tmp_path), "output", "local0", "simulatorRun",
+                                       "FS-Classification", "fold_0", "logs.json")))
+    assert len(site["train_log"]) == 5 and len(site["validation_log"]) == 2
+    ws = [locs[s].trainer.flat.data for s in sorted(locs)]
+    assert all(torch.equal(w, ws[0]) for w in ws)

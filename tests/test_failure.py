@@ -1,0 +1,42 @@
+"""Failure path: a site that dies mid-epoch makes the surviving sites stop with a
+non-zero exit and a failure report, within the configured collective timeout, instead of hanging.
+
+Two independent site processes (no torchrun agent, which would kill the survivors itself) train
+FS-Classification over gloo on the CPU; ``DINUNET_FAULT=1:25`` SIGKILLs site 1 before its 25th
+training step.
+"""
+import os
+import signal
+import subprocess
+import sys
+import time
+
+from mp_util import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_dead_site_makes_survivor_exit_nonzero(fs_data_root, tmp_path):
+    port = free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT,
+                   OMP_NUM_THREADS="1", DINUNET_FAULT="1:25", DINUNET_PG_TIMEOUT="30")
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "dinunet_implementations_amd.run", "--data-path", fs_data_root,
+             "--out", str(tmp_path / "out"), "--device", "cpu", "--set", "epochs=50",
+             "--set", "patience=100"],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    t0 = time.time()
+    try:
+        outs = [p.communicate(timeout=120) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.time() - t0
+    assert procs[1].returncode == -signal.SIGKILL, (procs[1].returncode, outs[1][1][-2000:])
+    assert procs[0].returncode == 3, (procs[0].returncode, outs[0][1][-3000:])
+    assert "site failure" in outs[0][1]
+    assert elapsed < 90

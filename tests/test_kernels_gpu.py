@@ -369,3 +369,22 @@ def test_ica_step_with_fused_encoder_projection_matches_unfused():
         assert rel(a, b) < 8e-2
 
 
+
+
+@pytest.mark.gpu
+def test_lstm_outside_fused_kernels_is_loud(monkeypatch):
+    """Per-direction hidden > 192 has no persistent kernel: the GPU refuses the ~100x slower
+    reference loop unless DINUNET_ALLOW_SLOW_LSTM=1 opts in (then it warns and runs)."""
+    import warnings
+    from dinunet_implementations_amd.models import ica as ica_mod
+    m = ica_mod.ICALstm(input_size=32, hidden_size=512, num_comps=4, window_size=5).cuda()
+    x = torch.randn(2, 6, 4, 5, device="cuda")
+    monkeypatch.delenv("DINUNET_ALLOW_SLOW_LSTM", raising=False)
+    with pytest.raises(NotImplementedError, match="DINUNET_ALLOW_SLOW_LSTM"):
+        m(x)
+    monkeypatch.setenv("DINUNET_ALLOW_SLOW_LSTM", "1")
+    monkeypatch.setattr(ica_mod, "_SLOW_WARNED", False)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        logits, _ = m(x)
+    assert logits.shape == (2, 2) and any("outside the fused" in str(i.message) for i in w)
