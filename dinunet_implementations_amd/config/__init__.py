@@ -69,6 +69,12 @@ FRAMEWORK_DEFAULTS: Dict[str, Any] = {
     "dad_tol": 1e-3,
     "powersgd_rank": 4,
     "powersgd_warm_start": True,
+    # collective plan for the xGMI mesh (README "Collective plan"): dSGD bucket size, RCCL
+    # algorithm / protocol (None = RCCL's own choice), per-collective timeout
+    "dsgd_bucket_mb": 4.0,
+    "rccl_algo": None,
+    "rccl_proto": None,
+    "collective_timeout_s": 1800,
 }
 
 TASK_DEFAULTS: Dict[str, Dict[str, Any]] = {

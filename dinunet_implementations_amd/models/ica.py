@@ -94,6 +94,7 @@ class LSTM(nn.Module):
                               xp=xp)
         if x.is_cuda and self.use_fused:
             _slow_lstm_gate(self.hidden_size, x.shape[0])
+        x = x.to(self.lstms[0].i2h.weight.dtype)  # the fused encoder hands over bf16
         if h is not None:
             hs, (h_t, c_t) = self.lstms[0](x, h)
             if self.bidirectional:

@@ -34,7 +34,7 @@ from ..ops import capture as _cap
 from ..ops.optim import FlatParams, cast_bf16_to_f32, cast_f32_to_bf16
 from .group import SiteGroup
 from .lowrank import EPS as EPS_MGS
-from .lowrank import _mgs_torch_, dad_factors, orthonormalize_
+from .lowrank import LowRankTable, _mgs_torch_, dad_factors, orthonormalize_
 
 Tensor = torch.Tensor
 
@@ -108,10 +108,13 @@ class DSGDEngine(Engine):
     """
     name = "dSGD"
 
-    def __init__(self, model, flat, group, cfg=None, bucket_mb: float = 4.0, overlap: bool = True):
+    def __init__(self, model, flat, group, cfg=None, bucket_mb: Optional[float] = None,
+                 overlap: bool = True):
         super().__init__(model, flat, group, cfg)
-        self.overlap = overlap and group.distributed
+        self.overlap = overlap and group.distributed and bool(self.cfg.get("dsgd_overlap", True))
         self.sync_enabled = True
+        if bucket_mb is None:
+            bucket_mb = float(self.cfg.get("dsgd_bucket_mb", 4.0))
         cap = int(bucket_mb * (1 << 20) / 4)
         self.buckets: List[Tuple[int, int]] = []
         self._param_bucket: Dict[int, int] = {}
@@ -136,15 +139,46 @@ class DSGDEngine(Engine):
         self._handles: Dict[int, object] = {}
         self._half_bufs: Dict[int, Tensor] = {}
         self._hooks = []
+        self._delivered = set()
         if self.overlap:
+            # autograd fires a parameter's post-accumulate hook even when its producer returned
+            # no gradient for it -- which is what the fused ops do: they accumulate into .grad
+            # themselves, possibly later (deferred grouped GEMM at the end of the backward), and
+            # notify through ops._grad.  A tensor hook sees whether a real gradient arrived, and
+            # only then does the post-accumulate hook count the parameter as ready.
             for p, _, _ in segs:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                self._hooks.append(p.register_hook(self._marker(id(p))))
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulated))
             _gradreg.register(self._on_grad)  # fused ops write .grad directly and notify
         self._reset()
+
+    def _marker(self, pid: int):
+        def hook(g):
+            if g is not None:
+                self._delivered.add(pid)
+        return hook
+
+    def _on_accumulated(self, p):
+        if id(p) in self._delivered:
+            self._delivered.discard(id(p))
+            self._on_grad(p)
 
     def _reset(self):
         self._pending = list(self._expected)
         self._handles.clear()
+        self._ready = [False] * len(self.buckets)
+        self._next = 0
+        self._seen = set()
+
+    def _drain(self):
+        """Launch ready buckets strictly in bucket order.  Every rank then issues the same
+        collective sequence whatever path produced its gradients: an eager step (autograd hooks,
+        e.g. a ragged last batch), a graph replay (``launch_bucket`` / ``reduce``), or a split
+        replay.  Out-of-order launches across ranks would pair different buckets in RCCL."""
+        while self._next < len(self.buckets) and self._ready[self._next]:
+            if self._next not in self._handles:
+                self._launch(self._next)
+            self._next += 1
 
     def split_buckets(self, stem_params) -> List[int]:
         """Re-bucket for a step whose backward is replayed in two parts (``TrainStep`` split
@@ -173,9 +207,11 @@ class DSGDEngine(Engine):
         return list(range(len(body)))
 
     def launch_bucket(self, b: int):
-        """Start bucket ``b``'s all-reduce now (RCCL stream ordered after the current stream)."""
-        if self.group.distributed and b not in self._handles:
-            self._launch(b)
+        """Mark bucket ``b`` ready and start every ready bucket up to it, in order (RCCL stream
+        ordered after the current stream)."""
+        if self.group.distributed:
+            self._ready[b] = True
+            self._drain()
 
     def _launch(self, b: int):
         if not self._handles:  # first bucket of this step
@@ -197,20 +233,21 @@ class DSGDEngine(Engine):
         if not self.sync_enabled:
             return
         b = self._param_bucket.get(id(p))
-        if b is None:
+        if b is None or id(p) in self._seen:  # each parameter counts once per step
             return
+        self._seen.add(id(p))
         self._pending[b] -= 1
-        if self._pending[b] == 0 and b not in self._handles:
-            self._launch(b)
+        if self._pending[b] == 0:
+            self._ready[b] = True
+            self._drain()
 
     def reduce(self) -> float:
         g = self.group
         if not g.distributed:
             self._reset()
             return 1.0
-        for b in range(len(self.buckets)):
-            if b not in self._handles:
-                self._launch(b)
+        self._ready = [True] * len(self.buckets)
+        self._drain()
         for b, h in self._handles.items():
             h.wait()
             if self.half:
@@ -271,7 +308,9 @@ class RankDADEngine(Engine):
 
     # ---- gradient-space path ---------------------------------------------------------------
     def _init_fast(self):
-        """Device tables for the batched power-iteration kernels (csrc/kernels/lowrank.hip)."""
+        """Device tables of the factorisation kernels (csrc/kernels/lowrank.hip): per large
+        Linear, its gradient view, the warm-start / candidate Q, and the P and Q slots of the
+        send buffer that the factor all-gather ships."""
         import ctypes
         segs = {id(p): o for p, o, _ in self.flat.segments()}
         dev = self.flat.data.device
@@ -294,87 +333,56 @@ class RankDADEngine(Engine):
         W = self.group.world
         self._gathered = (torch.zeros(W * self._send.numel(), dtype=torch.float32, device=dev)
                           if self.group.distributed else self._send)
-        self._pc, self._qc, self._q = [], [], []
-        lib = _lib.lib()
-        self._splits = int(lib.dn_pi_splits())  # row-split partials of G^T P per layer
-        for _, _, out_f, in_f, rr, _, _ in self.fast_layers:
+        layers = []
+        self._praw = []
+        for _, o, out_f, in_f, rr, po, qo in self.fast_layers:
             q = torch.randn(in_f, rr, generator=gen)  # identical on every site (same seed)
             _mgs_torch_(q)
-            self._q.append(q.to(dev))
-            self._pc.append(torch.empty(out_f, rr, dtype=torch.float32, device=dev))
-            self._qc.append(torch.empty(self._splits, in_f, rr, dtype=torch.float32, device=dev))
-        self._active = torch.ones(n, dtype=torch.int32, device=dev)
-
-        class PiLayer(ctypes.Structure):
-            _fields_ = [(k, ctypes.c_void_p) for k in ("G", "Pc", "Q", "Qc", "Psend", "Qsend",
-                                                     "active")] + \
-                       [(k, ctypes.c_int) for k in ("out", "inn", "r", "row0", "col0")]
+            qsend = self._send[qo:qo + in_f * rr].view(in_f, rr)
+            qsend.copy_(q.to(dev))  # the send slot doubles as the next step's warm start
+            praw = torch.empty(out_f, rr, dtype=torch.float32, device=dev)
+            self._praw.append(praw)
+            G = self.flat.grad[o:o + out_f * in_f].view(out_f, in_f)
+            layers.append((G, None, praw, self._send[po:po + out_f * rr].view(out_f, rr), qsend))
+        self._table = LowRankTable(layers, dev)
 
         class PiRecon(ctypes.Structure):
             _fields_ = [("G", ctypes.c_void_p), ("P", ctypes.c_void_p), ("Q", ctypes.c_void_p),
                         ("out", ctypes.c_int), ("inn", ctypes.c_int), ("r", ctypes.c_int),
                         ("start", ctypes.c_long)]
         L = _lib.lib()
-        L.dn_pi_layer_size.restype = ctypes.c_long
         L.dn_pi_recon_size.restype = ctypes.c_long
-        if ctypes.sizeof(PiLayer) != L.dn_pi_layer_size() or \
-                ctypes.sizeof(PiRecon) != L.dn_pi_recon_size():
-            raise RuntimeError("power-iteration table layout mismatch with the kernel library")
-        tab = (PiLayer * n)()
+        if ctypes.sizeof(PiRecon) != L.dn_pi_recon_size():
+            raise RuntimeError("reconstruction table layout mismatch with the kernel library")
         rec = (PiRecon * n)()
-        rows, cols, start = 0, 0, 0
-        row_starts, col_starts = [], []
-        G0 = self.flat.grad.data_ptr()
-        send0, gat0 = self._send.data_ptr(), self._gathered.data_ptr()
+        start = 0
+        G0, gat0 = self.flat.grad.data_ptr(), self._gathered.data_ptr()
         for i, (_, o, out_f, in_f, rr, po, qo) in enumerate(self.fast_layers):
-            t = tab[i]
-            t.G = G0 + 4 * o
-            t.Pc, t.Q, t.Qc = self._pc[i].data_ptr(), self._q[i].data_ptr(), self._qc[i].data_ptr()
-            t.Psend, t.Qsend = send0 + 4 * po, send0 + 4 * qo
-            t.active = self._active.data_ptr() + 4 * i
-            t.out, t.inn, t.r, t.row0, t.col0 = out_f, in_f, rr, rows, cols
-            row_starts.append(rows)
-            col_starts.append(cols)
-            rows += out_f
-            cols += (in_f + 63) // 64
             c = rec[i]
             c.G, c.P, c.Q = G0 + 4 * o, gat0 + 4 * po, gat0 + 4 * qo
             c.out, c.inn, c.r, c.start = out_f, in_f, rr, start
             start += out_f * in_f
-        self._rows, self._cols, self._recon_total = rows, cols, start
-
-        def dev_bytes(obj):
-            raw = bytes(obj)
-            return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
-        self._tab = dev_bytes(tab)
-        self._rec = dev_bytes(rec)
-        self._row_starts = torch.tensor(row_starts, dtype=torch.int32).to(dev)
-        self._col_starts = torch.tensor(col_starts, dtype=torch.int32).to(dev)
-        self._mgs_ptrs = torch.tensor([t.data_ptr() for t in self._pc], dtype=torch.int64).to(dev)
-        self._mgs_dims = torch.tensor([[t.shape[0], t.shape[1], t.stride(0)] for t in self._pc],
-                                      dtype=torch.int32).to(dev)
-        self._act_ptrs = torch.tensor([self._active.data_ptr() + 4 * i for i in range(n)],
-                                      dtype=torch.int64).to(dev)
+        self._recon_total = start
+        self._rec = torch.frombuffer(bytearray(bytes(rec)), dtype=torch.uint8).to(dev)
 
     def state_dict(self):
-        return {"q": [q.detach().cpu().clone() for q in getattr(self, "_q", [])]}
+        if self.fast and getattr(self, "fast_layers", None):
+            return {"send": self._send.detach().cpu().clone()}  # holds every warm-start Q
+        return {}
 
     def load_state_dict(self, sd):
-        for q, v in zip(getattr(self, "_q", []), sd.get("q", [])):
-            q.copy_(v.to(q.device))
+        if "send" in sd and getattr(self, "fast_layers", None):
+            self._send.copy_(sd["send"].to(self._send.device))
 
     def pre_reduce(self):
-        """Local rank-r factors of every large Linear's gradient into the send buffer: one
-        ``dn_pi_iterate`` (4 launches, all layers) per power iteration, no host sync
-        (HIP-graph capturable)."""
+        """Local rank-r factors of every large Linear's gradient into the send buffer: two
+        launches per power iteration for all layers (``G Q``; CholeskyQR2 + ``G^T P``), the
+        ``dad_tol`` stop decided on the device: no host sync, HIP-graph capturable."""
         if not self.fast or not self.fast_layers:
             return
         for it in range(max(1, self.iters)):
-            _lib.call("dn_pi_iterate", self._tab.data_ptr(), self._row_starts.data_ptr(),
-                      self._col_starts.data_ptr(), len(self.fast_layers), self._rows, self._cols,
-                      self._mgs_ptrs.data_ptr(), self._mgs_dims.data_ptr(),
-                      self._act_ptrs.data_ptr(), max(l[2] for l in self.fast_layers),
-                      float(self.tol), int(it == 0), _lib.stream())
+            self._table.gq(it, self.tol)
+            self._table.orth_gtp(it)
 
     def _fast_reduce(self) -> float:
         g = self.group
@@ -539,8 +547,41 @@ class PowerSGDEngine(Engine):
         self.dense_segs = dense
         gen = torch.Generator(device="cpu").manual_seed(int(self.cfg.get("seed", 0)) + 12345)
         dev = flat.data.device
-        self.Q = [torch.randn(c, r, generator=gen).to(dev) for _, _, c, r in self.mats]
-        self.err = [torch.zeros(rw, c, device=dev) for _, rw, c, _ in self.mats]
+        # GPU: every matrix of the model per launch (csrc/kernels/lowrank.hip): P = M Q with
+        # M = G + err formed in the same pass, CholeskyQR2 + Q = M^T P, then G = P Q^T and the
+        # error feedback -- three launches and two all-reduces per step, no host sync
+        self.fast = bool(flat.data.is_cuda and self.warm and _lib.native_available()
+                         and self.cfg.get("powersgd_device", True) and self.mats)
+        qs = [torch.randn(c, r, generator=gen) for _, _, c, r in self.mats]
+        if not self.fast:
+            self.Q = [q.to(dev) for q in qs]
+            self.err = [torch.zeros(rw, c, device=dev) for _, rw, c, _ in self.mats]
+            return
+        seg = {id(p): o for p, o, _ in flat.segments()}
+        rows_r = sum(rw * r for _, rw, _, r in self.mats)
+        self._qbuf = torch.cat([q.reshape(-1) for q in qs]).to(dev)  # Q: warm start + Q all-reduce
+        self._pbuf = torch.zeros(rows_r, dtype=torch.float32, device=dev)   # raw P: all-reduce
+        self._psend = torch.zeros(rows_r, dtype=torch.float32, device=dev)  # orthonormal P
+        self._ebuf = torch.zeros(sum(rw * c for _, rw, c, _ in self.mats), dtype=torch.float32,
+                                 device=dev)
+        self.Q, self.err, layers = [], [], []
+        po = qo = eo = 0
+        for p, rw, c, r in self.mats:
+            Q = self._qbuf[qo:qo + c * r].view(c, r)
+            E = self._ebuf[eo:eo + rw * c].view(rw, c)
+            P = self._pbuf[po:po + rw * r].view(rw, r)
+            Ps = self._psend[po:po + rw * r].view(rw, r)
+            G = flat.grad[seg[id(p)]:seg[id(p)] + rw * c].view(rw, c)
+            self.Q.append(Q)
+            self.err.append(E)
+            layers.append((G, E, P, Ps, Q))
+            po, qo, eo = po + rw * r, qo + c * r, eo + rw * c
+        self._table = LowRankTable(layers, dev)
+
+    def pre_reduce(self):
+        """M = G + err and the local P = M Q of every matrix (one launch, graph-capturable)."""
+        if self.fast:
+            self._table.gq(0)
 
     def state_dict(self):
         return {"Q": [q.detach().cpu().clone() for q in self.Q],
@@ -562,14 +603,24 @@ class PowerSGDEngine(Engine):
             g[o:o + n].copy_(buf[off:off + n])
             off += n
 
-    def reduce(self) -> float:
+    def reduce(self, factorized: bool = False) -> float:
+        """``factorized``: :meth:`pre_reduce` already ran (inside the captured step)."""
         g = self.group
         W = g.world
         self.comm_bytes = 0
-        dense = self._dense_pack()
-        self._allreduce_mean_(dense)
-        self._dense_unpack(dense)
+        if g.distributed:
+            dense = self._dense_pack()
+            self._allreduce_mean_(dense)
+            self._dense_unpack(dense)
         if not self.mats:
+            return 1.0
+        if self.fast:
+            if not factorized:
+                self.pre_reduce()
+            self._allreduce_mean_(self._pbuf)   # round 1: P (mean over sites)
+            self._table.orth_gtp(0)             # orthonormalise P, Q = M^T P
+            self._allreduce_mean_(self._qbuf)   # round 2: Q (mean); also the next warm start
+            self._table.recon_ef()              # G = P Q^T, err = M - G
             return 1.0
         Ms = []
         for (p, rows, cols, r), e in zip(self.mats, self.err):

@@ -65,6 +65,12 @@ class SiteGroup:
         if not self.distributed:
             out.copy_(t.reshape(-1))
             return None
+        if self.backend == "gloo" and t.is_cuda:
+            # gloo has no device all_gather_into_tensor: stage through the host (multi-site
+            # rehearsal on one GPU only; production GPU runs use RCCL)
+            parts = self.all_gather(t.detach().reshape(-1).cpu())
+            out.copy_(torch.cat(parts).to(out.device))
+            return None
         return dist.all_gather_into_tensor(out, t.contiguous().reshape(-1), group=self.pg,
                                            async_op=async_op)
 

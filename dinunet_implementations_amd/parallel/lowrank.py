@@ -19,9 +19,9 @@ from ..ops import _lib
 
 _lib.register("dn_mgs_batched", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
                                   _lib.c_int, _lib.c_float, _lib.c_void_p])
-_lib.register("dn_pi_iterate", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
-                                 _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_int,
+_lib.register("dn_lr_stage", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
+                              _lib.c_int, _lib.c_float, _lib.c_void_p])
+_lib.register("dn_lr_recon_ef", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long,
                                  _lib.c_void_p])
 _lib.register("dn_pi_reconstruct", [_lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_long,
                                      _lib.c_int, _lib.c_void_p])
@@ -82,3 +82,81 @@ def dad_factors(delta: torch.Tensor, act: torch.Tensor, rank: int, num_iters: in
 def _rel_change(a: torch.Tensor, b: torch.Tensor) -> float:
     # a single host sync per iteration only on the convergence check path
     return float((a - b).norm() / (a.norm() + EPS))
+
+
+class LowRankTable:
+    """Device-side descriptor table of the ``csrc/kernels/lowrank.hip`` factorisation kernels:
+    every large gradient matrix of a model, all handled by each launch.
+
+    ``layers``: ``[(G view [out, in], err [out, in] or None, P [out, r], Psend [out, r],
+    Qsend [in, r])]`` (fp32 CUDA tensors, contiguous).  ``Qsend`` holds the committed Q: the
+    input of every iteration and the next step's warm start (initialise it).  The
+    change norms and an ``active`` flag per layer are allocated here.  One power iteration =
+    :meth:`gq` (1 launch) + :meth:`orth_gtp` (2 launches), all layers each."""
+
+    def __init__(self, layers, device):
+        import ctypes
+        L = _lib.lib()
+        L.dn_lr_layer_size.restype = ctypes.c_long
+        maxr, plds, qlds = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        L.dn_lr_limits(ctypes.byref(maxr), ctypes.byref(plds), ctypes.byref(qlds))
+
+        class LrLayer(ctypes.Structure):
+            _fields_ = [(k, ctypes.c_void_p) for k in ("G", "err", "P", "Psend", "Qsend", "norms",
+                                                     "active")] + \
+                       [(k, ctypes.c_int) for k in ("out", "in_", "r", "b1", "n1", "b3", "n3")]
+        if ctypes.sizeof(LrLayer) != L.dn_lr_layer_size():
+            raise RuntimeError("low-rank table layout mismatch with the kernel library")
+        n = len(layers)
+        if n > 256:
+            raise ValueError("at most 256 low-rank layers per table")
+        self.n = n
+        self._keep = []
+        self.active = torch.ones(max(n, 1), dtype=torch.int32, device=device)
+        tab = (LrLayer * max(n, 1))()
+        b1 = b3 = 0
+        starts = []
+        total = 0
+        for i, (G, err, P, ps, qs) in enumerate(layers):
+            out_f, in_f = G.shape
+            r = P.shape[1]
+            if r > maxr.value or out_f * r > plds.value:
+                raise ValueError(f"low-rank layer [{out_f}, {in_f}] rank {r} exceeds the kernel "
+                                 f"limits (r <= {maxr.value}, out * r <= {plds.value})")
+            n1 = -(-out_f // 16)
+            n3 = -(-in_f // 16)
+            norms = torch.zeros(2 * n3, dtype=torch.float32, device=device)
+            self._keep.append(norms)
+            t = tab[i]
+            t.G, t.err = G.data_ptr(), (err.data_ptr() if err is not None else None)
+            t.P, t.Psend, t.Qsend = P.data_ptr(), ps.data_ptr(), qs.data_ptr()
+            t.norms = norms.data_ptr()
+            t.active = self.active.data_ptr() + 4 * i
+            t.out, t.in_, t.r, t.b1, t.n1, t.b3, t.n3 = out_f, in_f, r, b1, n1, b3, n3
+            b1 += n1
+            b3 += n3
+            starts.append(total)
+            total += out_f * in_f
+        self.blocks1, self.blocks3, self.total = b1, b3, total
+        self.table = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
+        self.starts = torch.tensor(starts or [0], dtype=torch.int64).to(device)
+
+    def _stage(self, stage: int, it: int, tol: float = 0.0):
+        if self.n:
+            _lib.call("dn_lr_stage", self.table.data_ptr(), self.n, self.blocks1, self.blocks3,
+                      stage, int(it), float(tol), _lib.stream())
+
+    def gq(self, it: int, tol: float = 0.0):
+        """P = G Q (PowerSGD: M = G + err first).  Iteration 0 re-activates every layer; later
+        ones first stop a layer whose last Q changed by less than ``tol`` (rank-dAD dad_tol)."""
+        self._stage(0, it, tol)
+
+    def orth_gtp(self, it: int):
+        """Pn = CholeskyQR2(P) -> Psend, Q = G^T Pn -> Qsend (2 launches, all layers)."""
+        self._stage(1, it)
+
+    def recon_ef(self):
+        """PowerSGD: G <- Psend Qsend^T, err <- M - G (M = G + err left by :meth:`gq`)."""
+        if self.n:
+            _lib.call("dn_lr_recon_ef", self.table.data_ptr(), self.starts.data_ptr(), self.n,
+                      self.total, _lib.stream())

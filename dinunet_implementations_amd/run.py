@@ -29,6 +29,16 @@ def parse_sets(items: List[str]) -> Dict[str, Any]:
     return out
 
 
+def apply_collective_plan(cfg: Dict[str, Any]):
+    """RCCL algorithm / protocol for the xGMI mesh from the config (``rccl_algo``,
+    ``rccl_proto``; see README "Collective plan"), exported before the process group is
+    created.  An explicit NCCL_ALGO / NCCL_PROTO in the environment wins."""
+    for key, env in (("rccl_algo", "NCCL_ALGO"), ("rccl_proto", "NCCL_PROTO")):
+        v = cfg.get(key)
+        if v:
+            os.environ.setdefault(env, str(v))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--data-path", required=True)
@@ -41,10 +51,12 @@ def main(argv=None):
     from .runtime.site import FederatedSite
     from .tasks import get_task
 
-    grp = init_sites(device=a.device)
     specs = load_inputspec(os.path.join(a.data_path, "inputspec.json"))
-    site_in = specs[grp.rank % len(specs)]
+    rank = int(os.environ.get("RANK", "0"))
+    site_in = specs[rank % len(specs)]
     cfg = build_config(site_input=site_in, overrides=parse_sets(a.set))
+    apply_collective_plan(cfg)  # before the communicator exists
+    grp = init_sites(device=a.device, timeout_s=cfg.get("collective_timeout_s"))
     base = os.path.join(a.data_path, "input", f"local{grp.rank}", "simulatorRun")
     if not os.path.isdir(base):
         base = os.path.join(a.data_path, "input", f"local{grp.rank % len(specs)}", "simulatorRun")

@@ -147,16 +147,20 @@ class FederatedSite:
         if monitor.lower() == "loss":
             direction = "minimize"
         best = best or {"score": None, "epoch": 0, "wait": 0}
-        use_fast = trainer.has_fast_path and li == 1
+        # gradient accumulation runs on the fast path too (TrainStep accum) unless the engine
+        # captures per-micro-batch activations (rank-dAD's CPU activation-space form)
+        use_fast = trainer.has_fast_path and (li == 1 or getattr(engine, "fast", True)
+                                               or engine.name != "rankDAD")
         step = None
         if use_fast:
             use_graph = bool(cfg.get("use_graph", True)) and self.device.type == "cuda"
             sm = trainer.split_module()
             if sm is not None:  # stem/body model: split capture overlaps the all-reduce
-                step = TrainStep(sm, trainer.flat, trainer.optimizer, engine, use_graph=use_graph)
+                step = TrainStep(sm, trainer.flat, trainer.optimizer, engine, use_graph=use_graph,
+                                 accum=li)
             else:
                 step = TrainStep(trainer.modules(), trainer.flat, trainer.optimizer, engine,
-                                 use_graph=use_graph,
+                                 use_graph=use_graph, accum=li,
                                  forward_loss=lambda m, x, y: trainer.forward_loss(x, y))
         it = tr.resume_iter(resume["loader"]) if resume and resume.get("loader") else iter(tr)
         fault_at = _fault_step(group.rank)
@@ -178,16 +182,17 @@ class FederatedSite:
                     if fault_at < 0:
                         os.kill(os.getpid(), signal.SIGKILL)
                 if step is not None:
-                    try:
-                        x, y, _ix = next(it)
-                    except StopIteration:
-                        it = iter(tr)
-                        x, y, _ix = next(it)
-                    loss = step(x, y)
-                    avg.add(loss.detach(), len(y))
-                    # clone: a graph replay overwrites its static outputs next step
-                    met.add(trainer.score(step.last_out, step.last_pred).detach().clone(), y)
-                    nsamp += len(y)
+                    for k in range(li):
+                        try:
+                            x, y, _ix = next(it)
+                        except StopIteration:
+                            it = iter(tr)
+                            x, y, _ix = next(it)
+                        loss = step(x, y, first=k == 0, last=k == li - 1)
+                        avg.add(loss.detach(), len(y))
+                        # clone: a graph replay overwrites its static outputs next step
+                        met.add(trainer.score(step.last_out, step.last_pred).detach().clone(), y)
+                        nsamp += len(y)
                     continue
                 trainer.flat.zero_grad()
                 if hasattr(engine, "sync_enabled"):

@@ -63,8 +63,13 @@ class _NoDefer:
 class TrainStep:
     def __init__(self, model, flat, opt, engine, task: str = "ica", use_graph: bool = True,
                  eager_warmup: int = 3, forward_loss: Optional[Callable] = None,
-                 timers: Optional[PhaseTimer] = None, split: Optional[bool] = None):
+                 timers: Optional[PhaseTimer] = None, split: Optional[bool] = None,
+                 accum: int = 1):
         self.model = model
+        # gradient accumulation (``local_iterations``): a step is ``accum`` calls; the first
+        # zeroes the gradient, every call backpropagates d(loss)/accum (the reference's
+        # (loss / local_iterations).backward()), the last one reduces and updates
+        self.accum = max(1, int(accum))
         self.flat = flat
         self.opt = opt
         self.engine = engine
@@ -104,7 +109,7 @@ class TrainStep:
         # inside every replay
         one = self._one
         if one is None or one.device != device or one.dtype != dtype:
-            one = self._one = torch.ones((), dtype=dtype, device=device)
+            one = self._one = torch.full((), 1.0 / self.accum, dtype=dtype, device=device)
         return one
 
     def _backward(self, loss):
@@ -120,15 +125,20 @@ class TrainStep:
             self._backward(loss)
         return out, loss, pred
 
-    def _eager(self, x, y):
+    def _eager(self, x, y, first: bool = True, last: bool = True):
         T = self.timers
+        sync = getattr(self.engine, "sync_enabled", None)
         with T.phase("fwd_bwd"):
-            self.flat.zero_grad()
+            if first:
+                self.flat.zero_grad()
+            if sync is not None:
+                self.engine.sync_enabled = last  # collectives only with the last micro-batch
             out, loss, pred = self._fwd_bwd(x, y)
-        with T.phase("reduce"):
-            scale = self.engine.reduce()
-        with T.phase("optim"):
-            self.opt.step(grad_scale=scale)
+        if last:
+            with T.phase("reduce"):
+                scale = self.engine.reduce()
+            with T.phase("optim"):
+                self.opt.step(grad_scale=scale)
         self.last_out, self.last_loss, self.last_pred = out.detach(), loss.detach(), pred
         return loss
 
@@ -142,33 +152,37 @@ class TrainStep:
         self._bf16_in = bf
         return sx, sy
 
-    def _feed(self, x, y, sx, sy):
+    def _feed(self, x, y, sx, sy, zero: bool = True):
         """Before a replay, in ONE launch when possible: inputs into the static buffers, the
-        gradient buffer zeroed (the graphs no longer contain the zeroing), the LSTM weight
-        repack the capture deferred out of the graph (``ops.lstm.defer_pack``) and, when the
-        update is captured (``_prebump``), the advance of Adam's device step counter."""
+        gradient buffer zeroed (the graphs no longer contain the zeroing; not for the later
+        micro-batches of an accumulated step), the LSTM weight repack the capture deferred out
+        of the graph (``ops.lstm.defer_pack``) and, when the update is captured
+        (``_prebump``), the advance of Adam's device step counter."""
         bump = self.opt.device_step() if (self.graph_opt and self._prebump) else None
+        g = self.flat.grad if zero else self.flat.grad[:0]
         if self._packs:
             if self._bf16_in:
-                run_deferred_pack(self._packs, (x, sx, y, sy, self.flat.grad), bump)
+                run_deferred_pack(self._packs, (x, sx, y, sy, g), bump)
                 return
             run_deferred_pack(self._packs)
         if self._bf16_in:
-            ops.step_prologue(x, sx, y, sy, self.flat.grad, bump)
+            ops.step_prologue(x, sx, y, sy, g, bump)
             return
         if sx.data_ptr() != x.data_ptr():
             sx.copy_(x, non_blocking=True)
         if y.dtype == torch.int64 and self.flat.grad.numel() % 4 == 0:
-            ops.step_prologue(x, None, y, sy, self.flat.grad, bump)
+            ops.step_prologue(x, None, y, sy, g, bump)
         else:
             if sy.data_ptr() != y.data_ptr():
                 sy.copy_(y, non_blocking=True)
-            self.flat.grad.zero_()
+            if zero:
+                self.flat.grad.zero_()
 
     def _graph_opt_ok(self) -> bool:
         # the optimizer joins the graph when no collective sits between backward and update
+        # (and every replay is a whole step: no accumulation)
         return (not self.engine.group.distributed and isinstance(self.opt, ops.FusedAdam)
-                and self.flat.data.is_cuda)
+                and self.flat.data.is_cuda and self.accum == 1)
 
     def _reduce_after_replay(self):
         if self._pre_reduce is not None:
@@ -231,24 +245,25 @@ class TrainStep:
         self._packs = dp.records
         self._keep = (h, hd)  # the graphs replay into these buffers
 
-    def __call__(self, x, y):
+    def __call__(self, x, y, first: bool = True, last: bool = True):
+        """One micro-batch; ``first`` / ``last`` delimit an accumulated step (``accum`` > 1)."""
         self.calls += 1
         if not self.use_graph:
-            return self._eager(x, y)
+            return self._eager(x, y, first, last)
         if self.graph is not None and self.graph_opt and self.opt.lr != self._cap_lr:
             self.graph = None  # the learning rate is baked into the captured update
         if self.graph is None:
-            if self.calls <= self.eager_warmup:
+            if self.calls <= self.eager_warmup * self.accum:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
-                    loss = self._eager(x, y)
+                    loss = self._eager(x, y, first, last)
                 torch.cuda.current_stream().wait_stream(s)
                 return loss
             (self._capture_split if self.split else self._capture)(x, y)
         sx, sy, out, loss, pred = self.static
         if sx.shape != x.shape or sy.shape != y.shape:  # e.g. a ragged last batch
-            loss = self._eager(x, y)
+            loss = self._eager(x, y, first, last)
             if self.graph_opt:
                 # the eager update advanced only the host step count: the captured update reads
                 # the device counter
@@ -256,12 +271,16 @@ class TrainStep:
             return loss
         T = self.timers
         with T.phase("fwd_bwd"):
-            self._feed(x, y, sx, sy)
+            self._feed(x, y, sx, sy, zero=first)
             self.graph.replay()
             if self.graph_b is not None:
-                for b in self._first_buckets:  # all-reduce under the stem backward
-                    self.engine.launch_bucket(b)
+                if last:
+                    for b in self._first_buckets:  # all-reduce under the stem backward
+                        self.engine.launch_bucket(b)
                 self.graph_b.replay()
+        if not last:
+            self.last_out, self.last_loss, self.last_pred = out, loss, pred
+            return loss
         if hasattr(self.engine, "sync_enabled"):
             self.engine.sync_enabled = True
         if self.graph_opt:

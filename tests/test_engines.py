@@ -177,3 +177,65 @@ def test_dsgd_split_buckets_partition_flat_buffer():
     for p, o, n in flat.segments():
         b = eng._param_bucket[id(p)]
         assert (b not in first) == (id(p) in stem_ids)
+
+
+class _DeferredLinear(torch.autograd.Function):
+    """Mimics the fused ops: returns no gradient for the weight to autograd and writes it into
+    .grad only at the end of the backward pass (ops._grad.defer/flush), then notifies."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        from dinunet_implementations_amd.ops import _grad
+        x, w = ctx.saved_tensors
+
+        def flush():
+            w.grad.add_(g.t() @ x)
+            _grad.notify([w])
+        torch.autograd.Variable._execution_engine.queue_callback(flush)
+        return g @ w, None
+
+
+class _RecordingGroup:
+    """A 2-site group whose all-reduce records what it was handed at launch time."""
+    distributed, world, rank, backend = True, 2, 0, "gloo"
+
+    def __init__(self):
+        self.launched = []
+
+    def all_reduce(self, t, op=None, async_op=False):
+        self.launched.append(t.detach().clone())
+
+        class _Done:
+            def wait(self_inner):
+                return None
+        return _Done()
+
+
+def test_dsgd_waits_for_deferred_fused_gradients():
+    """A parameter whose producer hands autograd no gradient (fused op writing .grad at the end
+    of the backward) must not be reported ready by autograd's post-accumulate hook, which
+    fires anyway: its bucket would be all-reduced before the gradient exists.  Every bucket
+    must be launched with its final local gradient."""
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import DSGDEngine
+    torch.manual_seed(0)
+    lin1, lin2 = torch.nn.Linear(6, 5), torch.nn.Linear(5, 3)
+    m = torch.nn.Sequential(lin1, lin2)
+    flat = FlatParams(m.parameters())
+    grp = _RecordingGroup()
+    eng = DSGDEngine(m, flat, grp, {}, bucket_mb=1e-5)  # a bucket per parameter
+    x = torch.randn(4, 6)
+    flat.zero_grad()
+    with eng.step_context():
+        h = _DeferredLinear.apply(x, lin1.weight) + lin1.bias
+        lin2(h).pow(2).sum().backward()
+    final = flat.grad.clone()
+    eng.reduce()
+    assert len(grp.launched) == len(eng.buckets)
+    for (s0, e0), sent in zip(eng.buckets, grp.launched):
+        assert torch.equal(sent, final[s0:e0]), (s0, e0)

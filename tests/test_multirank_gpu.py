@@ -1,0 +1,44 @@
+"""Multi-site correctness on the GPU: 2 and 4 ranks share one MI355X over gloo
+(``DINUNET_BACKEND=gloo``), train through the production HIP-graph TrainStep with every engine,
+both payload precisions, a ragged batch on one rank (eager step beside graph replays: the dSGD
+bucket launch order must still agree) and local_iterations = 2; all replicas must end
+bit-identical (``tools/multirank_check.py``).  Each case is a fresh ``torch.distributed.run``
+started before any GPU use in this process's children."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    (2, ["--engine", "dSGD", "--precision", "32"]),
+    (2, ["--engine", "dSGD", "--precision", "16", "--ragged"]),
+    (2, ["--engine", "dSGD", "--precision", "32", "--accum", "2", "--ragged"]),
+    (2, ["--engine", "rankDAD", "--precision", "32", "--ragged"]),
+    (2, ["--engine", "powerSGD", "--precision", "16", "--accum", "2"]),
+    (4, ["--engine", "dSGD", "--precision", "16", "--accum", "2", "--ragged"]),
+    (4, ["--engine", "rankDAD", "--precision", "16"]),
+]
+
+
+@pytest.mark.parametrize("world,args", CASES, ids=[f"w{w}-" + "-".join(a[1::2]) +
+                                                   ("-ragged" if "--ragged" in a else "")
+                                                   for w, a in CASES])
+def test_replicas_bit_identical(world, args):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from mp_util import free_port
+    env = dict(os.environ, DINUNET_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(world), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tools", "multirank_check.py")] + args
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    res = json.loads(lines[-1])
+    assert res["ok"], res
+    assert res["graph"] and res["world"] == world
+    assert r.returncode == 0, r.stderr[-3000:]

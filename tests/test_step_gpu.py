@@ -277,3 +277,58 @@ def test_ragged_batch_keeps_device_step_in_sync():
     assert int(opt.device_step().item()) == opt.step_count == len(sizes)
     for p, q in zip(net.parameters(), ref.parameters()):
         assert torch.allclose(p, q, rtol=1e-4, atol=1e-5)
+
+
+def test_accumulated_graph_step_matches_eager():
+    """local_iterations = 2 on the HIP-graph path: the second micro-batch's replay accumulates
+    into the gradient (no zeroing prologue), the update runs after it; equals the eager
+    accumulation (reference (loss / li).backward())."""
+    xs, ys = _batches(n=10)
+    _, fe, se = _trainer(0, use_graph=False, accum=2)
+    _, fg, sg = _trainer(0, use_graph=True, accum=2)
+    for st in (se, sg):
+        for i in range(xs.shape[0]):
+            st(xs[i], ys[i], first=i % 2 == 0, last=i % 2 == 1)
+    torch.cuda.synchronize()
+    assert sg.graph is not None and not sg.graph_opt
+    assert se.opt.step_count == sg.opt.step_count == 5
+    assert torch.allclose(fe.data, fg.data, rtol=1e-5, atol=1e-6)
+
+
+def test_powersgd_device_matches_reference_math():
+    """Device PowerSGD (csrc/kernels/lowrank.hip: P = M Q with M = G + err, CholeskyQR2,
+    Q = M^T P, G = P Q^T, err = M - G) == the same algorithm in torch ops (MGS), over 3
+    steps of error feedback and warm-started Q."""
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import PowerSGDEngine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    grp = SiteGroup(device=torch.device("cuda"))
+    m = _model(0)
+    fa = FlatParams(m.parameters())
+    ea = PowerSGDEngine(m, fa, grp, {"powersgd_rank": 4})
+    mb = _model(0)
+    fb = FlatParams(mb.parameters())
+    eb = PowerSGDEngine(mb, fb, grp, {"powersgd_rank": 4, "powersgd_device": False})
+    assert ea.fast and not eb.fast
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for _ in range(3):
+        gr = torch.randn(fa.grad.shape, device="cuda", generator=g)
+        fa.grad.copy_(gr)
+        fb.grad.copy_(gr)
+        ea.reduce()
+        eb.reduce()
+        torch.cuda.synchronize()
+        assert torch.allclose(fa.grad, fb.grad, rtol=1e-3, atol=1e-4), \
+            (fa.grad - fb.grad).abs().max()
+        for x, y in zip(ea.err, eb.err):
+            assert torch.allclose(x, y, rtol=1e-3, atol=1e-4)
+
+
+def test_powersgd_step_graph_matches_eager():
+    xs, ys = _batches()
+    _, fe, se = _trainer(0, engine="powerSGD", use_graph=False)
+    _, fg, sg = _trainer(0, engine="powerSGD", use_graph=True)
+    _run(se, xs, ys)
+    _run(sg, xs, ys)
+    assert sg.graph is not None and sg.graph_opt
+    assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5)

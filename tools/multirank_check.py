@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Multi-site replica check on ONE GPU: N ranks (torch.distributed.run, ``DINUNET_BACKEND=gloo``,
+every rank on cuda:0) train the ICA-LSTM through the production TrainStep (HIP-graph replay,
+split capture with the all-reduce between the replays for dSGD) on rank-specific data, then
+compare every rank's flat parameters bit for bit.  Replicas of a synchronous engine must stay
+identical; any divergence means two ranks applied different updates.
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
+        tools/multirank_check.py --engine dSGD --precision 16 --ragged --accum 2
+
+Prints one JSON line (rank 0); exit status 0 iff all ranks are bit-identical.
+"""
+import argparse
+import json
+import os
+import sys
+
+os.environ.setdefault("DINUNET_BACKEND", "gloo")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--engine", default="dSGD")
+    ap.add_argument("--precision", default="32")
+    ap.add_argument("--accum", type=int, default=1)
+    ap.add_argument("--ragged", action="store_true",
+                    help="rank 1 feeds one short batch mid-run (eager fallback beside replays)")
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=24)
+    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--overlap", type=int, default=1, help="dSGD all-reduce under the backward")
+    ap.add_argument("--diag", action="store_true", help="report dSGD gradient-ready counts")
+    ap.add_argument("--split", type=int, default=-1, help="-1: TrainStep's default")
+    a = ap.parse_args()
+
+    import torch
+    from dinunet_implementations_amd.models import ICALstm
+    from dinunet_implementations_amd.ops import FlatParams, FusedAdam
+    from dinunet_implementations_amd.parallel import init_sites, make_engine, shutdown
+    from dinunet_implementations_amd.runtime.step import TrainStep
+
+    grp = init_sites()
+    dev = grp.device
+    torch.manual_seed(1234)  # identical init on every site
+    m = ICALstm(input_size=128, hidden_size=384, num_comps=50, window_size=10).to(dev).train()
+    m.classifier[0].p = 0.0
+    flat = FlatParams(m.parameters())
+    opt = FusedAdam(flat, lr=1e-3)
+    cfg = {"precision_bits": a.precision, "dad_reduction_rank": 8, "powersgd_rank": 4, "seed": 5,
+           "dsgd_overlap": bool(a.overlap)}
+    eng = make_engine(a.engine, m, flat, grp, cfg)
+    counts = {}
+    if a.diag and hasattr(eng, "_on_grad"):
+        names = {id(p): n for n, p in m.named_parameters()}
+        orig = eng._on_grad
+
+        def spy(p):
+            if eng.sync_enabled:
+                counts[names.get(id(p), "?")] = counts.get(names.get(id(p), "?"), 0) + 1
+            return orig(p)
+        eng._on_grad = spy
+        import dinunet_implementations_amd.ops._grad as _gr
+        _gr.unregister(orig)
+        _gr.register(spy)
+        for h in eng._hooks:
+            h.remove()
+        eng._hooks = [p.register_post_accumulate_grad_hook(spy) for p in m.parameters()]
+    step = TrainStep(m, flat, opt, eng, task="ica", use_graph=bool(a.graph), accum=a.accum,
+                     split=None if a.split < 0 else bool(a.split))
+    g = torch.Generator(device=dev).manual_seed(100 + grp.rank)  # site-specific data
+    n_micro = a.steps * a.accum
+    ragged_at = (n_micro // 2) // a.accum * a.accum + a.accum - 1  # a last micro-batch
+    for i in range(n_micro):
+        B = a.batch - 5 if (a.ragged and grp.rank == 1 and i == ragged_at) else a.batch
+        x = torch.randn(B, a.seq, 50, 10, device=dev, generator=g)
+        y = torch.randint(0, 2, (B,), device=dev, generator=g)
+        step(x, y, first=i % a.accum == 0, last=i % a.accum == a.accum - 1)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    mine = flat.data.detach().cpu()
+    allp = grp.all_gather(mine)
+    same = all(torch.equal(p, allp[0]) for p in allp)
+    maxdiff = max(float((p - allp[0]).abs().max()) for p in allp)
+    res = {"ok": bool(same), "world": grp.world, "engine": a.engine, "precision": a.precision,
+           "accum": a.accum, "ragged": a.ragged, "graph": step.graph is not None,
+           "split": bool(step.split), "steps": opt.step_count, "max_abs_diff": maxdiff,
+           "param_sum": float(mine.double().sum())}
+    if a.diag:
+        res["notify_counts_per_param"] = {k: v / n_micro for k, v in counts.items() if v != n_micro}
+        res["params_never_notified"] = [n for n, _ in m.named_parameters() if n not in counts]
+    if grp.rank == 0:
+        print(json.dumps(res), flush=True)
+    shutdown()
+    return 0 if same else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
