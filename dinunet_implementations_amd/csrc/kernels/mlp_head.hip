@@ -23,7 +23,7 @@
 // synchronisation.  Dropout masks come from a counter-based hash of (seed, layer, row, col); the
 // seed is a device word bumped by fwd1, so a captured HIP graph draws fresh masks on every replay,
 // and the backward regenerates the mask from the seed saved in the workspace.
-#include "common.h"
+#include "head_common.h"
 
 namespace {
 
@@ -31,8 +31,6 @@ constexpr int HMAXL = 6;
 constexpr int HW_NT = 256;  // fwd0 / bwd0 workgroups (4 waves)
 constexpr int HS_NT = 512;  // fwd1 / bwd1 single workgroup (8 waves, 256-VGPR budget)
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 struct HLayer {
   const float* W;  // [out][in]
@@ -74,33 +72,7 @@ struct HArgs {
 // installed with dn_head_set_stamps (diagnostics: tools/bench_head.py --stamps).
 #define HSTAMP(i) do { if (stamps && threadIdx.x == 0) stamps[(i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-__host__ __device__ constexpr int rup32(int v) { return (v + 31) & ~31; }
 
-// 32-bit counter hash (Wellons' lowbias32 finaliser over idx ^ key(seed, layer)): two 32-bit
-// multiplies per element.  The former 64-bit splitmix finaliser (six 64-bit multiplies, each a
-// chain of quarter-rate 32-bit ones) made the layer-0 dropout the longest phase of the forward.
-__device__ __forceinline__ uint32_t hmix(uint64_t seed, uint32_t layer, uint32_t idx) {
-  const uint32_t key = (uint32_t)seed * 0x9E3779B9u ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu ^
-                       (layer + 1u) * 0xC2B2AE35u;
-  uint32_t x = idx ^ key;
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return x >> 8;  // 24 uniform bits
-}
-
-__device__ __forceinline__ bool hkeep(uint64_t seed, int layer, int m, int k, int K, float p) {
-  return (float)hmix(seed, (uint32_t)layer, (uint32_t)(m * K + k)) * (1.f / 16777216.f) >= p;
-}
-
-// sum over the four lanes holding one accumulator column (l, l^16, l^32, l^48)
-__device__ __forceinline__ float colsum4(float v) {
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
-}
 
 // B fragment from weight ROWS: lane -> row n, k .. k+7 (contiguous).  Branchless (clamped
 // address + select) so a batch of these issues all its loads before the first use.
@@ -193,15 +165,6 @@ __device__ __forceinline__ ColP load_colp(const HLayer& L, int n, bool train) {
   return c;
 }
 
-// Fragment with lane i <- column c0 + (i & 15) and element j <- row k0 + 8 * (i >> 4) + j of a
-// row-major LDS image (row stride S elements): two hardware-transposed 4x16 reads.
-__device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int S, int c0, int k0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const bf16* a0 = img + (k0 + 8 * g + q) * S + c0 + 4 * p;
-  const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-  const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * S));
-  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
-}
 
 
 // bias -> BatchNorm -> ReLU -> (next layer's dropout) epilogue of one 16-column tile of layer l,
@@ -1086,6 +1049,7 @@ DN_API int dn_head_set_stamps(void* p) {
 // the head does not fit the fused kernels.
 // Per layer: dims[l] -> dims[l+1]; flags[l] = bn (0 none / 1 batch stats / 2 running) | relu << 2.
 DN_API int dn_head_layout(int nl, const int* dims, const int* flags, int B, long* out) {
+  if (B > 64) return headb_layout(nl, dims, flags, B, out);
   Plan p;
   if (!make_plan(nl, dims, flags, nullptr, nullptr, nullptr, B, p)) return DN_UNSUPPORTED;
   out[0] = p.ws_bytes;
@@ -1104,6 +1068,9 @@ DN_API int dn_head_fwd(int nl, const int* dims, const int* flags, const float* d
                        const float* bnp, void* const* ptrs, const float* x, long ldx, int B,
                        const long long* y, float* out, float* loss, long long* pred,
                        unsigned long long* rng, void* ws, int train, int log_out, hipStream_t st) {
+  if (B > 64)
+    return headb_fwd(nl, dims, flags, drops, bnp, ptrs, x, ldx, B, y, out, loss, pred, rng, ws,
+                     train, log_out, st);
   Plan p;
   if (!make_plan(nl, dims, flags, drops, bnp, ptrs, B, p)) return DN_UNSUPPORTED;
   head_init();
@@ -1171,6 +1138,7 @@ DN_API int dn_head_bwd0(int nl, const int* dims, const int* flags, const float* 
 DN_API int dn_head_bwd(int nl, const int* dims, const int* flags, const float* drops,
                        const float* bnp, void* const* ptrs, int B, void* ws, const float* dloss,
                        float* dx, long lddx, hipStream_t st) {
+  if (B > 64) return headb_bwd(nl, dims, flags, drops, bnp, ptrs, B, ws, dloss, dx, lddx, st);
   Plan p;
   if (!make_plan(nl, dims, flags, drops, bnp, ptrs, B, p)) return DN_UNSUPPORTED;
   for (int l = 0; l < nl; ++l) {

@@ -11,9 +11,17 @@ Covers the two classifier heads of the reference:
 
 A :class:`HeadSpec` is parsed from the module sequence itself, so the fused path always matches
 what the modules would compute (parameters, BN eps/momentum/mode, dropout placement); anything the
-kernel does not cover (batch > 64, > 16 classes, unknown modules) runs the modules + the loss op.
+kernels do not cover (> 16 classes, layers wider than 2048, unknown modules) runs the modules +
+the loss op.
 
-The forward is two launches (the wide first layer over many workgroups, then the narrow tail +
+Batches above 64 rows run ``csrc/kernels/head_big.hip`` behind the same C entry points: one
+launch per layer forward (row blocks x 64-column blocks, the previous layer's BatchNorm + ReLU and
+this layer's dropout applied while staging the input tile) + one loss launch, one launch per
+layer backward (dA and dW jobs in one grid) + one per BatchNorm layer; BatchNorm statistics are
+deterministic per-row-block partials merged in a fixed order (SURVEY K7 at the large batches of
+the reference's pretrain config).
+
+For batches <= 64 the forward is two launches (the wide first layer over many workgroups, then the narrow tail +
 loss in one): loss, outputs, argmax, BatchNorm running-stat update and the dropout masks
 (counter-based hash; the seed is a device counter the kernel bumps, so HIP-graph replays draw
 fresh masks).  The backward is two launches (the output-gradient chain, then every dW slice and

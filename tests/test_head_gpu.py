@@ -1,4 +1,6 @@
-"""Fused MLP head + loss (csrc/kernels/mlp_head.hip) against the plain module path in fp32."""
+"""Fused MLP head + loss against the plain module path in fp32: csrc/kernels/mlp_head.hip for
+batches <= 64, csrc/kernels/head_big.hip (row-block tiling, cross-workgroup BatchNorm statistics)
+above."""
 import copy
 
 import pytest
@@ -91,7 +93,7 @@ def _compare(mods_fused, mods_ref, fused_fn, x, y, log_out, train=True, emulate=
     return xf, xr
 
 
-@pytest.mark.parametrize("B", [32, 7, 50])
+@pytest.mark.parametrize("B", [32, 7, 50, 65, 300, 2048])
 def test_ica_head_train_matches_modules(B):
     torch.manual_seed(0)
     head = _ica_head(p=0.0).to(DEV).train()
@@ -110,26 +112,28 @@ def test_ica_head_train_matches_modules(B):
     assert int(bn.num_batches_tracked) == int(rbn.num_batches_tracked) == 1
 
 
-def test_ica_head_eval_uses_running_stats():
+@pytest.mark.parametrize("B", [20, 500])
+def test_ica_head_eval_uses_running_stats(B):
     torch.manual_seed(1)
     head = _ica_head().to(DEV)
     head[2].running_mean.uniform_(-0.5, 0.5)
     head[2].running_var.uniform_(0.5, 2.0)
     head.eval()
     ref_head = copy.deepcopy(head)
-    x = torch.randn(20, 384, device=DEV)
-    y = torch.randint(0, 2, (20,), device=DEV)
+    x = torch.randn(B, 384, device=DEV)
+    y = torch.randint(0, 2, (B,), device=DEV)
     with torch.no_grad():
         _compare(list(head), list(ref_head), None, x, y, log_out=False, train=False, emulate=False)
 
 
-def test_ica_head_dropout_statistics_and_fresh_masks():
+@pytest.mark.parametrize("B", [32, 256])
+def test_ica_head_dropout_statistics_and_fresh_masks(B):
     from dinunet_implementations_amd.ops.head import HeadSpec, head_loss
     torch.manual_seed(2)
     head = _ica_head(p=0.25).to(DEV).train()
     spec = HeadSpec(list(head))
-    x = torch.randn(32, 384, device=DEV).abs() + 0.1
-    y = torch.randint(0, 2, (32,), device=DEV)
+    x = torch.randn(B, 384, device=DEV).abs() + 0.1
+    y = torch.randint(0, 2, (B,), device=DEV)
     masks = []
     for _ in range(2):
         xf = x.clone().requires_grad_()
@@ -142,7 +146,8 @@ def test_ica_head_dropout_statistics_and_fresh_masks():
     assert not torch.equal(masks[0], masks[1])
 
 
-@pytest.mark.parametrize("B,dropout_in", [(16, ()), (45, ()), (16, (1,))])
+@pytest.mark.parametrize("B,dropout_in", [(16, ()), (45, ()), (16, (1,)), (130, ()), (1000, ()),
+                                         (130, (1,))])
 def test_fs_network_fused_matches_modules(B, dropout_in):
     torch.manual_seed(3)
     net = _fs_head(dropout_in=dropout_in).to(DEV).train()
@@ -169,14 +174,15 @@ def test_fs_network_fused_matches_modules(B, dropout_in):
     assert errs[len(errs) // 2] < 6e-2 and errs[-1] < 0.1, errs
 
 
-def test_head_grads_accumulate_and_scale():
+@pytest.mark.parametrize("B", [32, 300])
+def test_head_grads_accumulate_and_scale(B):
     """Gradients add into existing .grad and scale with d loss (loss * 3)."""
     from dinunet_implementations_amd.ops.head import HeadSpec, head_loss
     torch.manual_seed(4)
     head = _ica_head(p=0.0).to(DEV).train()
     spec = HeadSpec(list(head))
-    x = torch.randn(32, 384, device=DEV)
-    y = torch.randint(0, 2, (32,), device=DEV)
+    x = torch.randn(B, 384, device=DEV)
+    y = torch.randint(0, 2, (B,), device=DEV)
     _, loss, _ = head_loss(x, spec, y, log_out=False)
     loss.backward()
     g1 = [p.grad.clone() for p in head.parameters()]
@@ -203,7 +209,7 @@ def test_ica_model_forward_loss_fused_vs_cpu():
     assert abs(loss.item() - rl.item()) < 3e-2
 
 
-@pytest.mark.parametrize("B", [16, 45])
+@pytest.mark.parametrize("B", [16, 45, 200])
 def test_fs_backward_exact_given_forward_state(B):
     """Each backward layer (dA = dZ W, ReLU mask, batch-statistics BatchNorm backward) reproduces
     the fp32 math applied to the kernel's own saved forward state."""
@@ -227,7 +233,7 @@ def test_fs_backward_exact_given_forward_state(B):
     dx = torch.empty_like(x)
     _lib.call("dn_head_bwd", spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp,
               spec.ptrs(True), B, ws.data_ptr(), one.data_ptr(), dx.data_ptr(), 66, _lib.stream())
-    Mp = 32 if B <= 32 else 64
+    Mp = 32 if B <= 32 else (64 if B <= 64 else B)  # image rows (big batches: exactly B)
 
     def img(off, S, n):
         return ws[off: off + 2 * Mp * S].view(torch.bfloat16).view(Mp, S)[:B, :n].float()
