@@ -233,6 +233,7 @@ struct GemmGroup {
   long elem_start[GMAX + 1];  // split-K reduce: prefix of M*N
   int n, splits;
   int vec;  // every operand satisfies stage_load_vec's alignment contract
+  int vepi;  // every problem can take the LDS-staged vector epilogue (see gemm_dma_kernel)
 };
 
 __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int row, int col, float v) {
@@ -372,6 +373,253 @@ gemm_kernel(GemmGroup g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA GEMM for bf16 operands (the common case: every ICA-step GEMM).  Tiles go global -> LDS
+// by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip, no conversion pass), into two
+// LDS stages: tile t+1's DMA is in flight under tile t's MFMAs, one vmcnt(0) + barrier per K tile.
+// The DMA writes LDS lane-linearly (1 KB per wave instruction), so the bank-conflict swizzles are
+// applied on the per-lane SOURCE address and undone on the read:
+//  k-contiguous image [rows][64 k] (128-B rows): chunk slot = chunk ^ ((row >> 1) & 7) -> the 16
+//    rows of a ds_read_b128 group hit 16 distinct bank quads;
+//  k-major image [64 k][C cols]: C = 128 (256-B rows) slot = chunk ^ sw256(k), C = 64 (128-B rows)
+//    slot = chunk ^ sw128(k) -> each 32-lane half of a ds_read_b64_tr_b16 fragment read (8 k-rows x
+//    2 chunks) covers 64 distinct banks.
+// Out-of-range 16-B chunks (ragged M / N / K, split-K slice ends) read a zero page instead, so the
+// loop carries no masks.  Contract (host-checked): both operands bf16, GemmGroup::vec.
+__device__ const uint4 g_gemm_zero[1] = {};
+
+__device__ __forceinline__ int sw_kc(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int sw_km256(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+__device__ __forceinline__ int sw_km128(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int ROWS, bool KCONTIG>
+struct DmaImg {
+  static constexpr int BYTES = ROWS * 64 * 2;    // one 64-deep K tile
+  static constexpr int PER_WAVE = BYTES / 1024 / 4;
+};
+
+// This wave's share of the DMA of operand rows [row0, row0 + ROWS) x k [k, k + 64), as per-lane
+// source pointers fixed for the whole K loop (row / column part and swizzle folded in once; a K
+// tile only adds its k offset).  A lane whose row (column) is out of range keeps a null pointer
+// and reads the zero page; the k range is checked per tile (K % 8 == 0: chunks are all in or out).
+template <int ROWS, bool KCONTIG>
+struct DmaStream {
+  static constexpr int PW = DmaImg<ROWS, KCONTIG>::PER_WAVE;
+  const bf16* p[PW];
+  int kofs[PW];  // the chunk's k offset within the tile
+  long kstep;    // elements per unit of k
+  int ins0;
+  __device__ __forceinline__ void init(const bf16* __restrict__ base, long ld, int row0, int nrows,
+                                       int wid, int lane) {
+    ins0 = wid * PW;
+    kstep = KCONTIG ? 1 : ld;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int ins = ins0 + j;
+      if constexpr (KCONTIG) {
+        const int r = ins * 8 + (lane >> 3);
+        const int ch = (lane & 7) ^ sw_kc(r);
+        const int gr = row0 + r;
+        kofs[j] = 8 * ch;
+        p[j] = gr < nrows ? base + (long)gr * ld + 8 * ch : nullptr;
+      } else {
+        constexpr int CPR = ROWS / 8;
+        constexpr int RPI = 64 / CPR;
+        const int kr = ins * RPI + lane / CPR;
+        const int ch = (lane % CPR) ^ (ROWS == 128 ? sw_km256(kr) : sw_km128(kr));
+        const int gc = row0 + 8 * ch;
+        kofs[j] = kr;
+        p[j] = gc < nrows ? base + (long)kr * ld + gc : nullptr;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(int k0, int K, char* img) const {
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const bool ok = p[j] != nullptr && k0 + kofs[j] < K;
+      const bf16* src = ok ? p[j] + (long)k0 * kstep : reinterpret_cast<const bf16*>(g_gemm_zero);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(img + (ins0 + j) * 1024), 16, 0, 0);
+    }
+  }
+};
+
+// 16x32 MFMA operand fragment (operand rows r0 .. r0 + 15, k = 32 ks .. +31) from a DMA image
+template <int ROWS, bool KCONTIG>
+__device__ __forceinline__ bf16x8 dma_frag(const char* img, int r0, int ks, int lane) {
+  if constexpr (KCONTIG) {
+    const int r = r0 + (lane & 15);
+    const int ch = 4 * ks + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * (ch ^ sw_kc(r)));
+  } else {
+    constexpr int RB = ROWS * 2;
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k0 = 32 * ks + 8 * g + q, k1 = k0 + 4;
+    const int ch = (r0 >> 3) + (p >> 1);
+    const int s0 = ROWS == 128 ? sw_km256(k0) : sw_km128(k0);
+    const int s1 = ROWS == 128 ? sw_km256(k1) : sw_km128(k1);
+    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(img + k0 * RB + 16 * (ch ^ s0) + 8 * (p & 1)));
+    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(img + k1 * RB + 16 * (ch ^ s1) + 8 * (p & 1)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+template <int BM, int BN, bool TA, bool TB>
+__global__ void __launch_bounds__(256)
+gemm_dma_kernel(GemmGroup g) {
+  typedef DmaImg<BM, !TA> IA;
+  typedef DmaImg<BN, TB> IB;
+  constexpr int STAGE = IA::BYTES + IB::BYTES;
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int ES = WN + 4;                 // fp32 epilogue row stride (per-wave WM x WN block)
+  constexpr int EBYTES = 4 * WM * ES * 4;    // four waves
+  constexpr int SMEM = 2 * STAGE > EBYTES ? 2 * STAGE : EBYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int ntiles = g.tile_start[g.n];
+  const int bid = (int)blockIdx.x;
+  const int gtile = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);  // XCD-contiguous tiles
+  if (gtile >= ntiles) return;
+  int pi = 0;
+  while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
+  const GemmProb& P = g.p[pi];
+  const bf16* __restrict__ A = reinterpret_cast<const bf16*>(P.A);
+  const bf16* __restrict__ B = reinterpret_cast<const bf16*>(P.B);
+  const int M = P.M, N = P.N, K = P.K;
+  const int tile = gtile - g.tile_start[pi];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: the DMA's LDS base (M0)
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int row0 = (tile / tiles_n) * BM, col0 = (tile % tiles_n) * BN;
+  const int kbeg = blockIdx.z * P.kchunk;
+  const int kend = min(K, kbeg + P.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  DmaStream<BM, !TA> sa;
+  DmaStream<BN, TB> sb;
+  sa.init(A, P.lda, row0, M, wid, lane);
+  sb.init(B, P.ldb, col0, N, wid, lane);
+  if (nk > 0) {
+    sa.issue(kbeg, kend, smem);
+    sb.issue(kbeg, kend, smem + IA::BYTES);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t & 1) * STAGE;
+    if (t + 1 < nk) {
+      char* nxt = smem + ((t + 1) & 1) * STAGE;
+      sa.issue(kbeg + 64 * (t + 1), kend, nxt);
+      sb.issue(kbeg + 64 * (t + 1), kend, nxt + IA::BYTES);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = dma_frag<BM, !TA>(cur, wm * WM + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = dma_frag<BN, TB>(cur + IA::BYTES, wn * WN + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (g.vepi) {
+    // LDS-staged epilogue: alpha / bias / ReLU applied in registers, the wave's WM x WN block
+    // goes through LDS (the K loop's last barrier freed it), then out as 16-B row vectors (the
+    // MFMA layout alone would store 2- or 4-byte pieces, 16 lanes per row segment)
+    float* E = reinterpret_cast<float*>(smem) + wid * WM * ES;
+    const Epi& ep = P.epi;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int lc = 16 * j + (lane & 15);
+      const int col = col0 + wn * WN + lc;
+      const float bias = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] * ep.alpha + bias;
+          if (ep.relu) v = fmaxf(v, 0.f);
+          E[(16 * i + 4 * (lane >> 4) + r) * ES + lc] = v;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    const int gr0 = row0 + wm * WM, gc0 = col0 + wn * WN;
+    if (ep.out_bf16) {
+      constexpr int CPR = WN / 8, RPI = 64 / CPR;  // 8-column vectors per row, rows per pass
+#pragma unroll
+      for (int it = 0; it < WM / RPI; ++it) {
+        const int lr = it * RPI + lane / CPR, lc = 8 * (lane % CPR);
+        const int row = gr0 + lr, col = gc0 + lc;
+        if (row >= M || col >= N) continue;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(E + lr * ES + lc);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(E + lr * ES + lc + 4);
+        bf16x8* cp = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(P.C) + (long)row * P.ldc + col);
+        float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        if (ep.beta != 0.f) {
+          const bf16x8 o = *cp;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += ep.beta * (float)o[e];
+        }
+        bf16x8 w;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = (bf16)v[e];
+        *cp = w;
+      }
+    } else {
+      constexpr int CPR = WN / 4, RPI = 64 / CPR;
+#pragma unroll
+      for (int it = 0; it < WM / RPI; ++it) {
+        const int lr = it * RPI + lane / CPR, lc = 4 * (lane % CPR);
+        const int row = gr0 + lr, col = gc0 + lc;
+        if (row >= M || col >= N) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(E + lr * ES + lc);
+        f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + (long)row * P.ldc + col);
+        if (ep.beta != 0.f) {
+          const f32x4 o = *cp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += ep.beta * o[e];
+        }
+        *cp = v;
+      }
+    }
+    return;
+  }
+  float* slab = P.slab;
+  const int nst = (slab || P.epi.ncol <= 0) ? N : min(N, P.epi.ncol);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = col0 + wn * WN + 16 * j + (lane & 15);
+      if (col >= nst) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= M) continue;
+        if (slab) slab[((long)blockIdx.z * M + row) * N + col] = acc[i][j][r];
+        else epi_store(P.epi, P.C, P.ldc, row, col, acc[i][j][r]);
+      }
+    }
+}
+
 // 4 consecutive outputs of one row: v (already alpha-free split sum) -> epilogue -> vector store
 __device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, int row, int col, f32x4 v) {
   const long orow = epi.row_map ? epi.row_map[row] : row;
@@ -455,6 +703,8 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
   }
 }
 
+static int g_gemm_dma = 1;  // bf16 x bf16 aligned groups take gemm_dma_kernel (A/B switch)
+
 static int kchunk_for(int K, int& splits) {
   int kchunk = K;
   if (splits > 1) {
@@ -477,7 +727,14 @@ int launch(GemmGroup& g, hipStream_t st) {
   g.tile_start[g.n] = tiles;
   g.elem_start[g.n] = elems;
   dim3 grid((tiles + 7) / 8 * 8, 1, g.splits);
-  if (g.vec)
+  if constexpr (sizeof(TAe) == 2 && sizeof(TBe) == 2) {
+    if (g.vec && g_gemm_dma)
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB>), grid, dim3(256), 0, st, g);
+    else if (g.vec)
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, true>), grid, dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, false>), grid, dim3(256), 0, st, g);
+  } else if (g.vec)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, true>), grid, dim3(256), 0, st, g);
   else
     hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, false>), grid, dim3(256), 0, st, g);
@@ -515,15 +772,26 @@ static bool vec_ok(const void* base, int kcontig, int rows, int K, long ld) {
 
 static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int tile, hipStream_t st) {
   g.vec = 1;
+  g.vepi = 1;
   for (int i = 0; i < g.n; ++i) {
     const GemmProb& P = g.p[i];
     if (!vec_ok(P.A, !ta, P.M, P.K, P.lda) || !vec_ok(P.B, tb, P.N, P.K, P.ldb)) g.vec = 0;
+    // 16-B output vectors: 8 columns (bf16) / 4 (fp32) never straddle N or a misaligned row
+    const int cv = P.epi.out_bf16 ? 8 : 4;
+    if (P.slab || P.epi.row_map || P.epi.ncol > 0 || P.N % cv || P.ldc % cv || !aligned16(P.C))
+      g.vepi = 0;
   }
   if (tile == 1) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
   return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, g, st);
 }
 
 }  // namespace
+
+// 1: bf16 x bf16 GEMMs use the LDS-DMA kernel (default); 0: the register-staged kernel.
+DN_API int dn_gemm_set_dma(int on) {
+  g_gemm_dma = on != 0;
+  return DN_OK;
+}
 
 // Returns the fp32 slab elements the caller must provide for a split-K launch (0 if none).
 DN_API long dn_gemm_workspace(int M, int N, int K, int splits) {

@@ -75,15 +75,63 @@ def ica_timecourses(n: int, comps: int = 100, T: int = 980, seed: int = 0, signa
     return x.astype(np.float32), y.astype(np.int64)
 
 
+def ica_cohort_hard(n: int, comps: int = 100, T: int = 980, seed: int = 0, site: int = 0,
+                    signal: float = 0.5, label_noise: float = 0.1, n_net: int = 8,
+                    cohort_seed: int = 7):
+    """A cohort where the label is a CONNECTIVITY pattern, not a spectral one (time-to-AUC and
+    fidelity benchmarks; the easy :func:`ica_timecourses` is separable within ~30 steps).
+
+    * Both classes carry the same oscillation power in the ``n_net`` network components (subject
+      frequency ~ U(0.02, 0.06), so the spectrum says nothing about the label).  In class 1 one
+      latent oscillation drives all of them with cohort-fixed loadings (coherent network); in
+      class 0 every component oscillates with its own phase.
+    * Subject-level nuisance: AR(1) coefficient ~ N(0.55, 0.1) per subject.
+    * Site shift: per-site component gains (log-normal, sigma 0.3) and a site-specific mean AR
+      coefficient offset, applied before the per-component standardisation.
+    * ``label_noise`` of the labels are flipped (caps the attainable AUC below 1).
+    The network components and loadings depend only on ``cohort_seed`` (shared by all sites)."""
+    crng = np.random.default_rng(cohort_seed)
+    net = crng.choice(comps, n_net, replace=False)
+    load = crng.choice([-1.0, 1.0], n_net) * crng.uniform(0.7, 1.3, n_net)
+    srng = np.random.default_rng(cohort_seed * 1000 + site + 1)
+    gain = np.exp(srng.normal(0, 0.3, comps)).astype(np.float32)
+    ar_site = srng.normal(0, 0.05)
+    rng = np.random.default_rng(seed)
+    y_true = rng.integers(0, 2, n)
+    ar = np.clip(rng.normal(0.55 + ar_site, 0.1, (n, 1)), 0.05, 0.9).astype(np.float32)
+    x = rng.normal(0, 1, (n, comps, T)).astype(np.float32)
+    for k in range(1, T):
+        x[:, :, k] = ar * x[:, :, k - 1] + x[:, :, k]
+    x /= np.sqrt(1.0 / (1.0 - ar[:, :, None] ** 2))  # unit variance noise
+    t = np.arange(T, dtype=np.float32)
+    f = rng.uniform(0.02, 0.06, (n, 1, 1)).astype(np.float32)
+    shared = rng.uniform(0, 2 * np.pi, (n, 1, 1))
+    own = rng.uniform(0, 2 * np.pi, (n, n_net, 1))
+    phase = np.where(y_true[:, None, None] == 1, shared, own).astype(np.float32)
+    osc = np.sin(2 * np.pi * f * t[None, None, :] + phase)
+    x[:, net, :] += signal * load[None, :, None].astype(np.float32) * osc
+    x *= gain[None, :, None]
+    x = (x - x.mean(-1, keepdims=True)) / (x.std(-1, keepdims=True) + 1e-6)
+    flip = rng.random(n) < label_noise
+    y = np.where(flip, 1 - y_true, y_true)
+    return x.astype(np.float32), y.astype(np.int64)
+
+
 def make_ica_sites(root: str, sites: int = 2, subjects: Sequence[int] = (64, 64), comps: int = 100,
                    T: int = 980, seed: int = 0, window_size: int = 10, window_stride: int = 10,
-                   hidden_size: int = 384, input_size: int = 256) -> str:
+                   hidden_size: int = 384, input_size: int = 256, cohort: str = "easy",
+                   **cohort_kw) -> str:
+    """Per-site ICA data + inputspec in the reference layout; ``cohort="hard"`` draws
+    :func:`ica_cohort_hard` (site-shifted, connectivity labels, label noise)."""
     specs = []
     for s in range(sites):
         d = os.path.join(root, "input", f"local{s}", "simulatorRun")
         os.makedirs(d, exist_ok=True)
         n = subjects[s % len(subjects)]
-        x, y = ica_timecourses(n, comps, T, seed=seed * 100 + s)
+        if cohort == "hard":
+            x, y = ica_cohort_hard(n, comps, T, seed=seed * 100 + s, site=s, **cohort_kw)
+        else:
+            x, y = ica_timecourses(n, comps, T, seed=seed * 100 + s)
         np.save(os.path.join(d, "ica_data.npy"), x)
         with open(os.path.join(d, "labels.csv"), "w", newline="") as f:
             w = csv.writer(f)

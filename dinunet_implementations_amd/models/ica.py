@@ -195,7 +195,7 @@ class ICALstm(nn.Module):
             # fills the chip anyway) and added a cross-queue wait before the input projection
             lin = self.encoder[0]
             casts = []
-            want = lin.bias is not None and ops.PLAIN_BLAS
+            want = lin.bias is not None
             if want and x.dtype == torch.float32:
                 # eager callers: same operand values as the step graph's bf16 input (every GEMM
                 # rounds to bf16 while staging), so eager and replayed steps agree

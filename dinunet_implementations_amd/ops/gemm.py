@@ -24,6 +24,7 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
                           _lib.c_int, _lib.c_void_p, _lib.c_void_p])
 
+_lib.register("dn_gemm_set_dma", [_lib.c_int])
 _lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 14 + [_lib.c_int] * 8
               + [_lib.c_void_p, _lib.c_void_p])
 
@@ -228,13 +229,14 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.stream())
 
 
-# Plain GEMMs (no fused epilogue: bf16 operands, fp32 or bf16 output, no bias / beta / row map)
-# may go to the vendor library (hipBLASLt through torch), which at these skinny shapes measures
-# ~2x faster than the hand-written tile loop (tools/bench_gemm.py / rocprof: 3136x1536x256
-# 9.2 vs 18 us).  Every GEMM with a fused epilogue stays on csrc/kernels/gemm.hip.
+# Plain GEMMs (bf16 operands, no row map) run on csrc/kernels/gemm.hip's LDS-DMA kernel, which
+# beats hipBLASLt at every ICA-step shape at B = 32 (tools/bench_gemm.py on MI355X, us: encoder
+# 12.7 vs 19.0, projection 13.0 vs 18.7, dX 14.4 vs 19.0) and is within 1.1-1.3x of it at
+# B = 2048 (profiles/r2_gemm_shapes.md).  DINUNET_PLAIN_BLAS=1 routes them to hipBLASLt through
+# torch instead (A/B switch).
 import os as _os
 
-PLAIN_BLAS = _os.environ.get("DINUNET_PLAIN_BLAS", "1") == "1"
+PLAIN_BLAS = _os.environ.get("DINUNET_PLAIN_BLAS", "0") == "1"
 
 
 def mm_plain(a: Tensor, b: Tensor, trans_b: bool = False, out_dtype: torch.dtype = torch.float32,

@@ -1,7 +1,8 @@
 """Fused ``relu(x W^T + b)`` (the ICA encoder, reference ``comps/icalstm/models.py:87,107``).
 
-Forward is ONE MFMA GEMM with the bias+ReLU epilogue, reading the fp32 input windows and fp32
-master weights directly (rounded to bf16 while staging) and storing bf16 activations.  Backward
+Forward is ONE MFMA GEMM with the bias+ReLU epilogue storing bf16 activations: on the training
+step the input windows and the weight arrive as bf16 (cast by the LSTM pack launch) and take the
+LDS-DMA kernel; otherwise fp32 operands are rounded to bf16 while staging.  Backward
 masks the incoming gradient with the stored activations, defers the weight / bias gradient
 GEMMs (``dym^T x``, ``dym^T 1``) to the end-of-backward grouped launch (``ops._grad.defer``)
 and, only when required, runs the input-gradient GEMM.
@@ -32,11 +33,13 @@ _RB_SLABS = 64
 class _LinearBiasReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, weight, bias, module, w_bf16=None, b_bf16=None):
-        if w_bf16 is not None:
-            # bf16 input and bf16 weight/bias copies (made by the LSTM pack launch): hipBLASLt
-            # with its fused RELU_BIAS epilogue, 11.2 us vs 19.7 us for csrc/kernels/gemm.hip at
-            # 3136x256x1000 (tools/enc_gemm_probe.py, rocprofv3 on MI355X)
+        if w_bf16 is not None and PLAIN_BLAS:
+            # A/B switch: hipBLASLt with its fused RELU_BIAS epilogue
             y = torch._addmm_activation(b_bf16, x2d, w_bf16.t())
+        elif w_bf16 is not None:
+            # bf16 input and the bf16 weight copy made by the LSTM pack launch: both operands
+            # take the LDS-DMA kernel; bias + ReLU in its epilogue (fp32 bias)
+            y = mm(x2d, w_bf16, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16)
         else:
             y = mm(x2d, weight, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16)
         ctx.save_for_backward(x2d, y)
@@ -134,7 +137,6 @@ def linear_bias_relu(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[tor
     if not _lib.native_available():
         raise RuntimeError("linear_bias_relu on GPU needs the gfx950 kernel library")
     wb = bb = None
-    if (bf16_params is not None and bias is not None and x2d.dtype == torch.bfloat16
-            and PLAIN_BLAS):
+    if bf16_params is not None and bias is not None and x2d.dtype == torch.bfloat16:
         wb, bb = bf16_params
     return _LinearBiasReLU.apply(x2d.contiguous(), weight, bias, module, wb, bb)

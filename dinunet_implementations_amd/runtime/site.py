@@ -153,7 +153,8 @@ class FederatedSite:
                                                or engine.name != "rankDAD")
         step = None
         if use_fast:
-            use_graph = bool(cfg.get("use_graph", True)) and self.device.type == "cuda"
+            use_graph = (bool(cfg.get("use_graph", True)) and self.device.type == "cuda"
+                         and not trainer.reference_math)
             sm = trainer.split_module()
             if sm is not None:  # stem/body model: split capture overlaps the all-reduce
                 step = TrainStep(sm, trainer.flat, trainer.optimizer, engine, use_graph=use_graph,

@@ -71,6 +71,12 @@ class NNTrainer:
         return pred
 
     @property
+    def reference_math(self) -> bool:
+        """``compute_path = "reference"``: every model runs the fp32 oracle math
+        (``ops/reference.py``) instead of the fused kernels, on whatever device it lives on."""
+        return str(self.cache.get("compute_path", "fused")) == "reference"
+
+    @property
     def has_fast_path(self) -> bool:
         return type(self).forward_loss is not NNTrainer.forward_loss
 
@@ -89,6 +95,11 @@ class NNTrainer:
             self._init_nn_model()
             for k in self.nn:
                 self.nn[k] = self.nn[k].to(self.device["gpu"])
+            if self.reference_math:
+                for net in self.nn.values():
+                    for m in net.modules():
+                        if hasattr(m, "use_fused"):
+                            m.use_fused = False
         if init_optimizer:
             self._init_optimizer()
 

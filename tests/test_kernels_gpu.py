@@ -54,6 +54,46 @@ def test_gemm_tile_shapes(tile, splits, ta, tb, M, N, K):
     assert rel(out, ref) < 2e-3
 
 
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(328, 200, 416), (3136, 256, 1000), (256, 1000, 3136), (64, 64, 64)])
+def test_gemm_lds_dma_bf16(tile, splits, ta, tb, M, N, K):
+    """bf16 x bf16 aligned GEMMs take the LDS-DMA kernel (global_load_lds, swizzled images,
+    zero-page edges): fp32 reference of the same bf16 operands, and bitwise agreement with the
+    register-staged kernel (same MFMA k order)."""
+    from dinunet_implementations_amd.ops import _lib, mm
+    a = (torch.randn(K, M, device=DEV) if ta else torch.randn(M, K, device=DEV)).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV) if tb else torch.randn(K, N, device=DEV)).to(torch.bfloat16)
+    ref = (a.t() if ta else a).float() @ (b.t() if tb else b).float()
+    out = mm(a, b, trans_a=ta, trans_b=tb, tile=tile, splits=splits)
+    assert rel(out, ref) < 2e-3
+    _lib.call("dn_gemm_set_dma", 0)
+    try:
+        old = mm(a, b, trans_a=ta, trans_b=tb, tile=tile, splits=splits)
+    finally:
+        _lib.call("dn_gemm_set_dma", 1)
+    assert torch.equal(out, old)
+
+
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 128), (3136, 1536, 256)])
+def test_gemm_lds_dma_vector_epilogue(tile, M, N, K):
+    """The DMA kernel's LDS-staged 16-B epilogue: bias + ReLU into bf16, alpha + beta
+    accumulation into fp32, ragged M."""
+    from dinunet_implementations_amd.ops import mm
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    y = mm(a, w, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16, tile=tile)
+    ref = torch.relu(a.float() @ w.float().t() + bias)
+    assert y.dtype == torch.bfloat16 and rel(y, ref) < 1e-2
+    c = torch.randn(M, N, device=DEV)
+    c0 = c.clone()
+    mm(a, w, trans_b=True, out=c, beta=1.0, alpha=0.5, tile=tile)
+    assert rel(c, c0 + 0.5 * (a.float() @ w.float().t())) < 2e-3
+
+
 def test_gemm_epilogue_bias_relu_bf16_out_and_beta():
     from dinunet_implementations_amd.ops import mm
     M, N, K = 300, 200, 128
@@ -213,8 +253,9 @@ def test_lstm_bias_grads_deterministic_and_accumulating():
 
 
 def test_encoder_hipblaslt_path_matches_hand_gemm_and_pack_casts():
-    """The ICA encoder forward on hipBLASLt (bf16 copies of W, b made by the LSTM pack launch)
-    matches the hand-written bias+ReLU GEMM; the pack's extra casts are exact bf16 roundings."""
+    """The ICA encoder forward from the bf16 copies of W, b made by the LSTM pack launch (the
+    LDS-DMA kernel; hipBLASLt under DINUNET_PLAIN_BLAS=1) matches the fp32-operand bias+ReLU
+    GEMM; the pack's extra casts are exact bf16 roundings."""
     from dinunet_implementations_amd.ops import linear_bias_relu
     from dinunet_implementations_amd.ops.lstm import pack_params
     torch.manual_seed(0)

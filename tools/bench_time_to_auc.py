@@ -10,6 +10,11 @@ the clock stops when it reaches ``--target``.  Prints one JSON line (rank 0).
     python tools/bench_time_to_auc.py [--target 0.9]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
         tools/bench_time_to_auc.py
+
+``--cohort hard`` (``data.synthetic.ica_cohort_hard``: connectivity labels, site shifts, label
+noise) is the cohort that separates engines / precisions; ``--compute-path reference`` runs the
+fp32 oracle math (``ops/reference.py``, no fused kernels, eager) on the same device as the
+bf16-fidelity baseline.  The JSON line carries the whole validation-AUC curve.
 """
 from __future__ import annotations
 
@@ -33,11 +38,17 @@ def main():
     ap.add_argument("--eval-every", type=int, default=16)
     ap.add_argument("--max-steps", type=int, default=4000)
     ap.add_argument("--lr", type=float, default=1e-3)
-    ap.add_argument("--signal", type=float, default=0.6)
+    ap.add_argument("--effect", "--signal", dest="signal", type=float, default=0.6,
+                    help="class-signal amplitude (--effect under torchrun: --signal is ambiguous there)")
     ap.add_argument("--engine", default="dSGD", choices=["dSGD", "rankDAD", "powerSGD"])
+    ap.add_argument("--cohort", default="easy", choices=["easy", "hard"])
+    ap.add_argument("--label-noise", type=float, default=0.1, help="hard cohort")
+    ap.add_argument("--compute-path", default="fused", choices=["fused", "reference"])
+    ap.add_argument("--seed", type=int, default=0, help="model init / batch order")
+    ap.add_argument("--full", action="store_true", help="run max-steps even after the target")
     a = ap.parse_args()
 
-    from dinunet_implementations_amd.data.synthetic import ica_timecourses
+    from dinunet_implementations_amd.data.synthetic import ica_cohort_hard, ica_timecourses
     from dinunet_implementations_amd.models import ICALstm
     from dinunet_implementations_amd.ops import FlatParams, FusedAdam
     from dinunet_implementations_amd.ops.reference import ica_windows
@@ -48,20 +59,30 @@ def main():
     grp = init_sites()
     dev = grp.device
     C, T, W = 100, 980, 10
-    x, y = ica_timecourses(a.subjects + a.val, C, T, seed=1000 + grp.rank, signal=a.signal)
+    if a.cohort == "hard":
+        x, y = ica_cohort_hard(a.subjects + a.val, C, T, seed=1000 + grp.rank, site=grp.rank,
+                               signal=a.signal, label_noise=a.label_noise)
+    else:
+        x, y = ica_timecourses(a.subjects + a.val, C, T, seed=1000 + grp.rank, signal=a.signal)
     xw = ica_windows(torch.from_numpy(x), W, W, T)  # [N, S, C, W]
     X = xw.to(dev)
     Y = torch.from_numpy(y).to(dev)
     Xtr, Ytr, Xva, Yva = X[:a.subjects], Y[:a.subjects], X[a.subjects:], Y[a.subjects:]
 
-    torch.manual_seed(0)  # same init everywhere
+    torch.manual_seed(a.seed)  # same init everywhere
     model = ICALstm(input_size=256, hidden_size=384, num_comps=C, window_size=W).to(dev).train()
+    ref_math = a.compute_path == "reference"
+    if ref_math:
+        for m in model.modules():
+            if hasattr(m, "use_fused"):
+                m.use_fused = False
     flat = FlatParams(model.parameters())
     grp.broadcast(flat.data, 0)
     opt = FusedAdam(flat, lr=a.lr)
     engine = make_engine(a.engine, model, flat, grp, {"precision_bits": "32", "seed": 0})
-    step = TrainStep(model, flat, opt, engine, task="ica", use_graph=dev.type == "cuda")
-    g = torch.Generator(device=dev).manual_seed(7 + grp.rank)
+    step = TrainStep(model, flat, opt, engine, task="ica",
+                     use_graph=dev.type == "cuda" and not ref_math)
+    g = torch.Generator(device=dev).manual_seed(7 + grp.rank + 100 * a.seed)
 
     def global_auc():
         model.eval()
@@ -81,26 +102,42 @@ def main():
     grp.barrier()
     t0 = time.perf_counter()
     auc, steps = 0.5, 0
+    curve = []
+    t_hit, s_hit = None, None
     while steps < a.max_steps:
         idx = torch.randint(0, len(Xtr), (a.batch,), device=dev, generator=g)
         step(Xtr[idx], Ytr[idx])
         steps += 1
         if steps % a.eval_every == 0:
             auc = global_auc()
-            if auc >= a.target:
-                break
+            curve.append([steps, round(auc, 4)])
+            if auc >= a.target and t_hit is None:
+                if dev.type == "cuda":
+                    torch.cuda.synchronize()
+                t_hit, s_hit = time.perf_counter() - t0, steps
+                if not a.full:
+                    break
+            if grp.is_master and steps % (a.eval_every * 16) == 0:
+                print(f"# step {steps} auc {auc:.4f}", file=sys.stderr, flush=True)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     grp.barrier()
-    dt = time.perf_counter() - t0
+    dt = time.perf_counter() - t0 if t_hit is None else t_hit
     if grp.is_master:
         print(json.dumps({
             "metric": "wall-clock to target validation AUC, ICA-LSTM " + a.engine,
             "value": round(dt, 3), "unit": "s", "higher_is_better": False,
-            "target_auc": a.target, "reached_auc": round(auc, 4), "reached": auc >= a.target,
-            "steps": steps, "samples_per_site": steps * a.batch, "n_sites": grp.world,
-            "data": "synthetic ICA time courses (ica_timecourses, signal=%g)" % a.signal,
-            "dtype": "bf16",
+            "target_auc": a.target, "reached": t_hit is not None,
+            "steps": s_hit if s_hit is not None else steps,
+            "samples_per_site": (s_hit if s_hit is not None else steps) * a.batch,
+            "final_auc": round(auc, 4), "best_auc": max([c[1] for c in curve] or [0.5]),
+            "n_sites": grp.world, "seed": a.seed, "engine": a.engine,
+            "data": ("synthetic ICA cohort %s (signal=%g%s)" % (
+                a.cohort, a.signal,
+                ", label_noise=%g" % a.label_noise if a.cohort == "hard" else "")),
+            "compute_path": a.compute_path,
+            "dtype": "fp32" if ref_math else "bf16",
+            "curve": curve,
         }), flush=True)
     shutdown()
     return 0
