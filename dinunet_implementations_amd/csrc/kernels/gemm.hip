@@ -445,6 +445,17 @@ struct DmaStream {
   }
 };
 
+// ds_read_b64_tr_b16 as inline asm: hipcc treats the builtin as an LDS read it cannot alias-check
+// against the LDS-DMA ring, and waits vmcnt(0) before it -- draining the prefetched tiles.  The
+// asm form is invisible to that bookkeeping, so the caller waits lgkmcnt(0) (+ sched_barrier)
+// itself before the MFMAs consume the result.
+__device__ __forceinline__ s16x4 tr16_asm(const char* p) {
+  s16x4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+
 // 16x32 MFMA operand fragment (operand rows r0 .. r0 + 15, k = 32 ks .. +31) from a DMA image
 template <int ROWS, bool KCONTIG>
 __device__ __forceinline__ bf16x8 dma_frag(const char* img, int r0, int ks, int lane) {
@@ -459,24 +470,23 @@ __device__ __forceinline__ bf16x8 dma_frag(const char* img, int r0, int ks, int 
     const int ch = (r0 >> 3) + (p >> 1);
     const int s0 = ROWS == 128 ? sw_km256(k0) : sw_km128(k0);
     const int s1 = ROWS == 128 ? sw_km256(k1) : sw_km128(k1);
-    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s16x4*)(img + k0 * RB + 16 * (ch ^ s0) + 8 * (p & 1)));
-    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s16x4*)(img + k1 * RB + 16 * (ch ^ s1) + 8 * (p & 1)));
+    const s16x4 x0 = tr16_asm(img + k0 * RB + 16 * (ch ^ s0) + 8 * (p & 1));
+    const s16x4 x1 = tr16_asm(img + k1 * RB + 16 * (ch ^ s1) + 8 * (p & 1));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
   }
 }
 
-template <int BM, int BN, bool TA, bool TB>
+template <int BM, int BN, bool TA, bool TB, int S>
 __global__ void __launch_bounds__(256)
 gemm_dma_kernel(GemmGroup g) {
+  static_assert(S >= 2 && S <= 4, "ring depth");
   typedef DmaImg<BM, !TA> IA;
   typedef DmaImg<BN, TB> IB;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int ES = WN + 4;                 // fp32 epilogue row stride (per-wave WM x WN block)
   constexpr int EBYTES = 4 * WM * ES * 4;    // four waves
-  constexpr int SMEM = 2 * STAGE > EBYTES ? 2 * STAGE : EBYTES;
+  constexpr int SMEM = S * STAGE > EBYTES ? S * STAGE : EBYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int ntiles = g.tile_start[g.n];
@@ -509,19 +519,30 @@ gemm_dma_kernel(GemmGroup g) {
   DmaStream<BN, TB> sb;
   sa.init(A, P.lda, row0, M, wid, lane);
   sb.init(B, P.ldb, col0, N, wid, lane);
-  if (nk > 0) {
-    sa.issue(kbeg, kend, smem);
-    sb.issue(kbeg, kend, smem + IA::BYTES);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const char* cur = smem + (t & 1) * STAGE;
-    if (t + 1 < nk) {
-      char* nxt = smem + ((t + 1) & 1) * STAGE;
-      sa.issue(kbeg + 64 * (t + 1), kend, nxt);
-      sb.issue(kbeg + 64 * (t + 1), kend, nxt + IA::BYTES);
+  // S-stage ring, tiles prefetched D = S - 1 ahead: at the top of iteration t this wave waits
+  // until only the glds of tiles t+1 .. t+D-1 are outstanding (counted vmcnt, never 0 in the
+  // steady state), one raw barrier makes every wave's share of tile t visible and retires the
+  // reads of iteration t-1 (whose buffer tile t+D then refills), then the MFMAs run on tile t.
+  constexpr int D = S - 1;
+  constexpr int G = DmaStream<BM, !TA>::PW + DmaStream<BN, TB>::PW;  // glds per wave per tile
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < nk) {
+      sa.issue(kbeg + 64 * d, kend, smem + d * STAGE);
+      sb.issue(kbeg + 64 * d, kend, smem + d * STAGE + IA::BYTES);
     }
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = min(D - 1, nk - 1 - t);  // tiles after t already issued
+    if (ahead >= 2) __builtin_amdgcn_s_waitcnt(DN_VMCNT0 | (2 * G));
+    else if (ahead == 1) __builtin_amdgcn_s_waitcnt(DN_VMCNT0 | G);
+    else __builtin_amdgcn_s_waitcnt(DN_VMCNT0);
+    __builtin_amdgcn_s_barrier();
+    if (t + D < nk) {
+      char* nxt = smem + ((t + D) % S) * STAGE;
+      sa.issue(kbeg + 64 * (t + D), kend, nxt);
+      sb.issue(kbeg + 64 * (t + D), kend, nxt + IA::BYTES);
+    }
+    const char* cur = smem + (t % S) * STAGE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[FM], bfr[FN];
@@ -529,14 +550,18 @@ gemm_dma_kernel(GemmGroup g) {
       for (int i = 0; i < FM; ++i) af[i] = dma_frag<BM, !TA>(cur, wm * WM + 16 * i, ks, lane);
 #pragma unroll
       for (int j = 0; j < FN; ++j) bfr[j] = dma_frag<BN, TB>(cur + IA::BYTES, wn * WN + 16 * j, ks, lane);
+      if constexpr (TA || !TB) {  // asm transposed reads: retire them before the MFMAs
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the ring
 
   if (g.vepi) {
     // LDS-staged epilogue: alpha / bias / ReLU applied in registers, the wave's WM x WN block
@@ -728,8 +753,13 @@ int launch(GemmGroup& g, hipStream_t st) {
   g.elem_start[g.n] = elems;
   dim3 grid((tiles + 7) / 8 * 8, 1, g.splits);
   if constexpr (sizeof(TAe) == 2 && sizeof(TBe) == 2) {
-    if (g.vec && g_gemm_dma)
-      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB>), grid, dim3(256), 0, st, g);
+    // ring depth: a grid that fills the chip several times over hides the DMA latency with
+    // resident workgroups (2 stages, 32 KB at 64x64 -> 5 per CU); a small grid (the B = 32
+    // step's ~200-tile GEMMs) needs the deeper 4-stage ring inside each workgroup
+    if (g.vec && g_gemm_dma && BM == 64 && (long)tiles * g.splits < 512)
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 4>), grid, dim3(256), 0, st, g);
+    else if (g.vec && g_gemm_dma)
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 2>), grid, dim3(256), 0, st, g);
     else if (g.vec)
       hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, true>), grid, dim3(256), 0, st, g);
     else

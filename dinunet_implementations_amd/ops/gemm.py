@@ -74,6 +74,10 @@ def _split_rule(t64: int, K: int) -> int:
     CU; medium K only splits when few tiles exist (a second ~5 us reduce launch otherwise eats
     the gain).  Measured on MI355X (bench.py, merged ICA weight-gradient launch: 284 tiles of
     K = 3136): 1 split 0.4156 ms/step, 2: 0.4045, 3: 0.4010, 4: 0.4024."""
+    if K >= 16384:
+        # very long K (large-batch weight gradients, K = B*S): ~8 workgroups per CU, each still
+        # >= 2048 deep (B = 2048 ICA step, grouped dW: 3 splits 1556 us, see profiles/r2_*)
+        return max(1, min(32, -(-8 * _NCU // max(t64, 1)), K // 2048))
     if K >= 2048:
         return max(1, min(8, round(3 * _NCU / max(t64, 1)), K // 512))
     if K >= 768 and t64 < _NCU // 2:
