@@ -26,8 +26,6 @@ import torch.nn as nn
 from .. import ops
 from ..ops import reference as ref
 
-_FUSED_ENCPROJ = os.environ.get("DINUNET_FUSED_ENCPROJ", "0") == "1"
-
 
 class LSTMCell(nn.Module):
     """One LSTM direction built from two ``nn.Linear`` (``models.py:5-45``).
@@ -189,7 +187,6 @@ class ICALstm(nn.Module):
         if x.dtype not in (torch.float32, torch.bfloat16):
             x = x.float()  # host datasets are float64 (reference comps/icalstm/__init__.py:29)
         self._packed = None
-        self._xp = None
         if self.use_fused and x.is_cuda and self.lstm.fused_ok(x) and ops.capture.active() is None:
             # in-stream: as a side-stream branch of the step graph the pack saved nothing (it
             # fills the chip anyway) and added a cross-queue wait before the input projection
@@ -205,14 +202,6 @@ class ICALstm(nn.Module):
                 cast_out=casts)
             B, S = x.shape[:2]
             flat = x.reshape(B * S, -1)
-            wih_p = self._packed[0]
-            if _FUSED_ENCPROJ and ops.enc_proj_supported(flat, lin.weight, lin.bias, wih_p):
-                # encoder + LSTM input projection in ONE launch (csrc/kernels/encproj.hip);
-                # opt-in: measured 63 us vs 38 us for the two GEMM launches at B=32 (49
-                # row-chunk workgroups each stream all weights: per-CU bandwidth bound)
-                enc, self._xp = ops.encoder_projection(flat, lin.weight, lin.bias, wih_p,
-                                                       module=lin)
-                return enc.view(B, S, -1)
             if casts:
                 enc = ops.linear_bias_relu(flat, lin.weight, lin.bias, module=lin,
                                            bf16_params=tuple(casts))
@@ -225,8 +214,7 @@ class ICALstm(nn.Module):
     def body_loss(self, enc: torch.Tensor, y: torch.Tensor):
         """Second half of :meth:`forward_loss`: bi-LSTM, classifier, softmax-CE on ``enc``."""
         packed, self._packed = getattr(self, "_packed", None), None
-        xp, self._xp = getattr(self, "_xp", None), None
-        o, _ = self.lstm(enc, reduce="mean", packed=packed, xp=xp)
+        o, _ = self.lstm(enc, reduce="mean", packed=packed)
         o = o.flatten(1).to(self.classifier[1].weight.dtype)
         if self.use_fused and o.is_cuda:
             return ops.head_loss(o, self.head_spec(), y, log_out=False)

@@ -3,7 +3,7 @@
 from . import _lib, capture, reference
 from ._lib import native_available
 from .gemm import PLAIN_BLAS, mm, mm_grouped, mm_plain
-from .linear import encoder_projection, enc_proj_supported, linear_bias_relu
+from .linear import linear_bias_relu
 from .lstm import bilstm as _bilstm_fused, lstm_supported, padded_hidden
 from .optim import FlatParams, FusedAdam, cast_bf16_to_f32, cast_f32_to_bf16, step_prologue
 from .heads import softmax_ce, log_softmax_nll
@@ -15,7 +15,7 @@ def bilstm(x, params, reduce: str = "none", modules=None, packed=None, xp=None):
 
 
 __all__ = [
-    "mm", "linear_bias_relu", "encoder_projection", "enc_proj_supported", "bilstm", "lstm_supported", "padded_hidden", "FlatParams",
+    "mm", "linear_bias_relu", "bilstm", "lstm_supported", "padded_hidden", "FlatParams",
     "FusedAdam", "cast_bf16_to_f32", "cast_f32_to_bf16", "step_prologue", "HeadSpec", "head_loss",
     "softmax_ce", "log_softmax_nll", "native_available", "capture", "reference",
 ]

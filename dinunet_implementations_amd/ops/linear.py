@@ -22,9 +22,6 @@ from .gemm import PLAIN_BLAS, mm
 _lib.register("dn_relu_bwd_colsum", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                                      _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
                                      _lib.c_void_p])
-_lib.register("dn_enc_proj", [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_void_p,
-                              _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
-                              _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_relu_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                               _lib.c_void_p])
 _RB_SLABS = 64
@@ -83,48 +80,6 @@ def _relu_linear_backward(ctx, dy):
     if ctx.module is not None and _cap.active() is not None:
         _cap.record(ctx.module, x2d, dym)
     return dx, None, None, None
-
-
-class _EncProjFn(torch.autograd.Function):
-    """``enc = relu(x W^T + b)`` and, in the same launch, the LSTM input projection
-    ``xp = enc W_ih^T`` (``csrc/kernels/encproj.hip``).  ``enc`` is the differentiable output
-    (same backward as :class:`_LinearBiasReLU`); ``xp`` is handed to the fused LSTM, which
-    differentiates w.r.t. ``enc`` itself."""
-
-    @staticmethod
-    def forward(ctx, x2d, weight, bias, module, wih_p, xp_out):
-        N, KX = x2d.shape
-        I = weight.shape[0]
-        enc = torch.empty(N, I, dtype=torch.bfloat16, device=x2d.device)
-        _lib.call("dn_enc_proj", x2d.data_ptr(), x2d.stride(0), N, KX, weight.data_ptr(),
-                  bias.data_ptr(), wih_p.data_ptr(), wih_p.shape[0], enc.data_ptr(),
-                  xp_out.data_ptr(), _lib.stream())
-        ctx.save_for_backward(x2d, enc)
-        ctx.weight, ctx.bias = weight, bias
-        ctx.module = module
-        return enc
-
-    @staticmethod
-    def backward(ctx, dy):
-        dx, _, _, _ = _relu_linear_backward(ctx, dy)
-        return dx, None, None, None, None, None
-
-
-def enc_proj_supported(x2d: torch.Tensor, weight: torch.Tensor, bias, wih_p) -> bool:
-    """The fused encoder + projection kernel's contract (width 256, bf16 input, K % 8 == 0)."""
-    return (x2d.is_cuda and x2d.dtype == torch.bfloat16 and bias is not None
-            and weight.shape[0] == 256 and weight.dtype == torch.float32
-            and weight.is_contiguous() and x2d.stride(1) == 1 and x2d.shape[1] % 8 == 0
-            and x2d.stride(0) % 8 == 0 and wih_p is not None and wih_p.shape[1] == 256
-            and wih_p.shape[0] % 64 == 0 and _lib.native_available())
-
-
-def encoder_projection(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor,
-                       wih_p: torch.Tensor, module: Optional[nn.Module] = None):
-    """``(enc, xp)``: the encoder output (autograd) and its LSTM input projection."""
-    xp = torch.empty(x2d.shape[0], wih_p.shape[0], dtype=torch.float32, device=x2d.device)
-    enc = _EncProjFn.apply(x2d, weight, bias, module, wih_p, xp)
-    return enc, xp
 
 
 def linear_bias_relu(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],

@@ -117,7 +117,7 @@ class _BiLSTMFn(torch.autograd.Function):
         if x2d.dtype != torch.bfloat16:
             x2d = x2d.to(torch.bfloat16)
         x2d = x2d.contiguous()
-        if xp_pre is not None:  # projected together with the encoder (ops.encoder_projection)
+        if xp_pre is not None:  # the caller's own input projection (same layout as below)
             if xp_pre.shape != (B * S, ndir * GP) or xp_pre.dtype != torch.float32:
                 raise ValueError("precomputed LSTM input projection has the wrong shape/dtype")
             xp = xp_pre

@@ -346,72 +346,6 @@ def test_gemm_grouped_matches_per_problem(splits):
         assert rel(q["out"], ref) < 2e-3
 
 
-@pytest.mark.parametrize("N,KX,N2", [(3136, 1000, 1536), (200, 64, 512), (70, 1000, 1024)])
-def test_encoder_projection_fused_matches_two_gemms(N, KX, N2):
-    """csrc/kernels/encproj.hip: enc = relu(X We^T + be), xp = enc Wp^T in one launch, against
-    the fp32 reference of the same bf16-rounded operands (ragged row tails included)."""
-    from dinunet_implementations_amd.ops import encoder_projection
-    x = torch.randn(N, KX, device=DEV).to(torch.bfloat16)
-    w = torch.randn(256, KX, device=DEV) / KX ** 0.5
-    b = torch.randn(256, device=DEV) * 0.1
-    wp = (torch.randn(N2, 256, device=DEV) / 16).to(torch.bfloat16)
-    enc, xp = encoder_projection(x, w, b, wp)
-    ref_enc = torch.relu(x.float() @ bf(w).t() + b)
-    assert rel(enc, ref_enc) < 1e-2
-    ref_xp = enc.float() @ wp.float().t()  # phase 2 consumes the bf16 enc tile
-    assert rel(xp, ref_xp) < 2e-3
-
-
-def test_ica_step_with_fused_encoder_projection_matches_unfused():
-    """ICALstm at input_size 256 with a bf16 batch takes the fused encoder+projection launch;
-    the default path runs the encoder on hipBLASLt (bf16-rounded bias).  Both match the fp32
-    CPU oracle (same bf16 input values) and each other; the bf16 rounding of recurrent states
-    makes small LSTM gradients differ by a few percent between two valid bf16 paths."""
-    import copy
-    from dinunet_implementations_amd.models import ICALstm
-    from dinunet_implementations_amd.models import ica as ica_mod
-    from dinunet_implementations_amd.ops import linear as lin_mod
-    torch.manual_seed(0)
-    m = ICALstm(input_size=256, hidden_size=128, num_comps=20, window_size=10).train()
-    m.classifier[0].p = 0.0
-    mc = copy.deepcopy(m)
-    m = m.to(DEV)
-    x = torch.randn(8, 12, 20, 10, device=DEV).to(torch.bfloat16)
-    y = torch.randint(0, 2, (8,), device=DEV)
-    _, lref, _ = mc.forward_loss(x.float().cpu(), y.cpu())
-    lref.backward()
-    gref = [p.grad.clone() for p in mc.parameters()]
-    grads = []
-    ica_mod._FUSED_ENCPROJ = True  # opt-in path (see models/ica.py)
-    try:
-        for fused in (True, False):
-            for p in m.parameters():
-                p.grad = None
-            orig = lin_mod.enc_proj_supported
-            if not fused:
-                import dinunet_implementations_amd.ops as ops_pkg
-                ops_pkg.enc_proj_supported = lambda *a, **k: False
-            try:
-                _, loss, _ = m.forward_loss(x, y)
-                loss.backward()
-            finally:
-                import dinunet_implementations_amd.ops as ops_pkg
-                ops_pkg.enc_proj_supported = orig
-            grads.append((float(loss.detach()), [p.grad.clone() for p in m.parameters()]))
-    finally:
-        ica_mod._FUSED_ENCPROJ = False
-    (l1, g1), (l2, g2) = grads
-    assert abs(l1 - l2) < 1e-3 and abs(l1 - float(lref)) < 1e-2
-    for a, b, r in zip(g1, g2, gref):
-        if r.norm() < 1e-6:  # analytically ~0 (bias in front of BatchNorm): noise either way
-            assert a.norm() < 1e-5 and b.norm() < 1e-5
-            continue
-        assert rel(a.cpu(), r) < 0.15 and rel(b.cpu(), r) < 0.15  # bf16 end to end
-        assert rel(a, b) < 8e-2
-
-
-
-
 @pytest.mark.gpu
 def test_lstm_outside_fused_kernels_is_loud(monkeypatch):
     """Per-direction hidden > 192 has no persistent kernel: the GPU refuses the ~100x slower
