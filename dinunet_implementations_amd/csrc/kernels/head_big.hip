@@ -21,8 +21,10 @@
 //         and layer l-1's ReLU mask.  If layer l-1 has BatchNorm the result (dy) goes out in fp32
 //         with per-row-block column sums (sum dy, sum dy xhat); otherwise it IS dZ_{l-1} (bf16
 //         image + fp32 column partials for the bias gradient).  For l = 0 it is d input.
-//       bwd(l) dW jobs (64 x 64 weight tiles): gW += dZ_l^T A_l over every row, operands from
-//         the CDNA4 LDS transpose read; column-block-0 jobs add the bias gradient.
+//       bwd(l) dW jobs (64 x 64 weight tiles x row splits): dZ_l^T A_l over the split's rows,
+//         operands from the CDNA4 LDS transpose read, into gW (one split) or fp32 partials that
+//         a small reduce launch adds in split order; the first split of column block 0 adds the
+//         bias gradient.
 //       bn(l) (row blocks): merges the column sums (= d beta, d gamma) and writes
 //         dZ_l = gamma rstd (dy - mean(dy) - xhat mean(dy xhat)).
 // The last layer must be a plain Linear (no BatchNorm / ReLU after the logits), as in both heads.
@@ -77,7 +79,17 @@ struct BArgs {
   int nl, B, nrb, train, log_out;
   long g_off;   // fp32 [B][C] p - onehot
   long gs_off;  // fp32 [16] its column sums
+  long dwp_off; // fp32 [rs][out][in] row-split partial weight gradients (one layer at a time)
 };
+
+// Row splits of one layer's dW reduction: enough (tile, split) jobs for ~2 per CU, each split at
+// least one 64-row block.
+static inline int dw_splits(int nW, int nrb) {
+  int rs = (512 + nW - 1) / nW;
+  if (rs > 16) rs = 16;
+  if (rs > nrb) rs = nrb;
+  return rs < 1 ? 1 : rs;
+}
 
 template <bool V>
 __device__ __forceinline__ void load4(const float* __restrict__ p, long ld, int r, int c, int R,
@@ -397,7 +409,7 @@ headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws) {
 template <bool LAST, bool VW>
 __global__ void __launch_bounds__(BNT)
 headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict__ dloss,
-                 float* __restrict__ dx, long lddx, int nA) {
+                 float* __restrict__ dx, long lddx, int nA, int RS) {
   __shared__ __attribute__((aligned(16))) bf16 T0[RB * LS];
   __shared__ __attribute__((aligned(16))) bf16 T1[RB * LS];
   const BLayer& L = a.L[l];
@@ -524,15 +536,20 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
     return;
   }
 
-  // dW job: gW[n0 .. n0 + 64)[k0 .. k0 + 64) += sum over rows of dZ_l[b][n] A_l[b][k]
-  const int n0 = (job / nkb) * TB;
+  // dW job (tile, split): sum over split `sp`'s rows of dZ_l[b][n] A_l[b][k] for the 64 x 64
+  // tile n0.., k0..; one split accumulates into gW directly, several write partials that
+  // headb_dw_reduce adds in split order
+  const int tile = job / RS, sp = job - tile * RS;
+  const int kbw = tile % nkb, k0w = kbw * TB;
+  const int n0 = (tile / nkb) * TB;
+  const int rb0 = sp * a.nrb / RS, rb1 = (sp + 1) * a.nrb / RS;
   const bf16* aimg = reinterpret_cast<const bf16*>(ws + L.a_off);
   f32x4 acc[4] = {};
-  for (int r0 = 0; r0 < B; r0 += RB) {
+  for (int r0 = rb0 * RB; r0 < rb1 * RB; r0 += RB) {
     stage_dz(r0, n0, false);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const int row = sr + 16 * p, gr = r0 + row, c = k0 + sq;
+      const int row = sr + 16 * p, gr = r0 + row, c = k0w + sq;
       const bool ok = gr < B && c < L.S_a;
       const bf16x4 q = *reinterpret_cast<const bf16x4*>(aimg + (ok ? (long)gr * L.S_a + c : 0));
       const bf16x4 zero = {};
@@ -547,15 +564,19 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
     }
     __syncthreads();
   }
-  const int k = k0 + 16 * wid + (lane & 15);
+  const int k = k0w + 16 * wid + (lane & 15);
+  float* part = reinterpret_cast<float*>(ws + a.dwp_off) + (long)sp * N * K;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + 16 * mt + 4 * (lane >> 4) + r;
-      if (n < N && k < K) L.gW[(long)n * K + k] += acc[mt][r];
+      if (n < N && k < K) {
+        if (RS == 1) L.gW[(long)n * K + k] += acc[mt][r];
+        else part[(long)n * K + k] = acc[mt][r];
+      }
     }
-  if (kb == 0 && L.gb && tid < TB && n0 + tid < N) {
+  if (sp == 0 && kbw == 0 && L.gb && tid < TB && n0 + tid < N) {
     const int n = n0 + tid;
     float db;
     if constexpr (LAST) {
@@ -566,6 +587,19 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
       for (int rb = 0; rb < a.nrb; ++rb) db += dbp[(long)rb * N + n];
     }
     L.gb[n] += db;
+  }
+}
+
+// gW of layer l += the RS row-split partials, added in split order (deterministic)
+__global__ void __launch_bounds__(256)
+headb_dw_reduce_kernel(BArgs a, int l, const char* __restrict__ ws, int RS) {
+  const BLayer& L = a.L[l];
+  const long NK = (long)L.out * L.in;
+  const float* part = reinterpret_cast<const float*>(ws + a.dwp_off);
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < NK; e += (long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int sp = 0; sp < RS; ++sp) v += part[sp * NK + e];
+    L.gW[e] += v;
   }
 }
 
@@ -642,6 +676,15 @@ static bool bplan(int nl, const int* dims, const int* flags, const float* drops,
   off = al256(off + 4L * B * dims[nl]);
   a.gs_off = off;
   off = al256(off + 4L * 16);
+  long dwp = 0;
+  for (int l = 0; l < nl; ++l) {
+    const BLayer& L = a.L[l];
+    const int nkb = (L.in + TB - 1) / TB, nW = ((L.out + TB - 1) / TB) * nkb;
+    const long need = (long)dw_splits(nW, a.nrb) * L.out * L.in;
+    dwp = dwp > need ? dwp : need;
+  }
+  a.dwp_off = off;
+  off = al256(off + 4L * dwp);
   p.ws_bytes = off;
   return true;
 }
@@ -709,15 +752,24 @@ int headb_bwd(int nl, const int* dims, const int* flags, const float* drops, con
                          (char*)ws);
     const int nkb = (L.in + TB - 1) / TB;
     const int nA = (l > 0 || dx) ? p.a.nrb * nkb : 0;
-    const int nW = ((L.out + TB - 1) / TB) * nkb;
+    const int nWt = ((L.out + TB - 1) / TB) * nkb;
+    const int RS = dw_splits(nWt, p.a.nrb);
+    const int nW = nWt * RS;
     const bool vw = L.in % 4 == 0;
     const dim3 grid(nA + nW);
     if (l == nl - 1) {
-      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<true, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA);
-      else hipLaunchKernelGGL((headb_bwd_kernel<true, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA);
+      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<true, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
+      else hipLaunchKernelGGL((headb_bwd_kernel<true, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
     } else {
-      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<false, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA);
-      else hipLaunchKernelGGL((headb_bwd_kernel<false, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA);
+      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<false, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
+      else hipLaunchKernelGGL((headb_bwd_kernel<false, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
+    }
+    if (RS > 1) {
+      const long NK = (long)L.out * L.in;
+      long blocks = (NK + 255) / 256;
+      if (blocks > 1024) blocks = 1024;
+      hipLaunchKernelGGL(headb_dw_reduce_kernel, dim3((unsigned)blocks), dim3(BNT), 0, st, p.a, l,
+                         (const char*)ws, RS);
     }
   }
   return dn_launch_status();

@@ -77,26 +77,33 @@ DN_API int dn_mgs_batched(float* const* mats, const int* dims, void* unused, int
 
 // ---------------------------------------------------------------------------------------------
 // Low-rank factorisation of every large Linear's gradient G [out, in], all layers per launch.
-// One power iteration (rank-dAD) or one PowerSGD round is three short launches:
+// One power iteration (rank-dAD) or one PowerSGD round is TWO short launches:
 //
 //   lr_gq      P = G Q           16 rows per block, f32 MFMA 16x16x4 over K (4 waves split K),
 //                                Q staged in LDS.  PowerSGD: M = G + err is formed in the same
-//                                pass and written back.
-//   lr_orth    Pn = CholQR2(P)   one workgroup per layer: Gram P^T P by f32 MFMA, Cholesky by one
-//                                wave in registers (lane = row of the r x r Gram, shuffles),
-//                                R^{-1} by back substitution, P R^{-1} by f32 MFMA; twice
-//                                (CholeskyQR2).  A pivot that vanishes (rank(P) < r) drops its
-//                                column.
-//   lr_gtp     Q = G^T Pn        16 columns per block over all rows, f32 MFMA, Pn in LDS; the
-//                                block commits its Q slice to Qsend with the change norms the
-//                                next lr_gq turns into the dad_tol decision (`active` flag)
+//                                pass and written back.  (PowerSGD all-reduces P here.)
+//   lr_gtp     Pn = P R^{-1}, Q = G^T Pn
+//                                16 columns per block over all rows.  Every block forms the Gram
+//                                P^T P of the LDS-staged P in fp64 (a few us of redundant work
+//                                instead of a serial per-layer launch), factors R^T R = P^T P
+//                                (fp64 Cholesky by one wave, lane = row; a vanishing pivot drops
+//                                its column) and inverts R in fp64 -- the same bits in every
+//                                block -- then forms Pn in LDS by f32 MFMA and Q by f32 MFMA.  Column
+//                                block 0 writes Pn (Psend).  The block commits its Q slice to
+//                                Qsend with the change norms the next lr_gq turns into the
+//                                dad_tol decision (`active` flag).
 //
+// Cholesky QR with an fp64 Gram and fp64 factor: the orthogonality loss of plain CholQR is the
+// Gram's rounding times cond(P)^2, which fp64 keeps far below fp32 resolution for the condition
+// numbers of these factors; the fp32 product P R^{-1} then leaves ~eps32 * cond(P).  This replaced
+// a per-layer CholeskyQR2 workgroup in fp32 (two serial one-wave factorisations per iteration,
+// 38 us per launch for the 768-row LSTM gradients, `tools/lowrank_bench.py`).
 // Qsend is the committed Q: the next iteration's input and the next step's warm start.  The
 // `active` flag (device memory) stops a converged layer without a host sync.
 namespace {
 
 constexpr int LR_MAXR = 16;
-constexpr int LR_PLDS = 16384;  // floats of P staged by lr_orth (out * r)
+constexpr int LR_PLDS = 16384;  // floats of P staged by lr_gtp (out * r)
 
 struct LrLayer {
   float* G;        // [out][in] gradient view (PowerSGD: becomes M = G + err)
@@ -112,11 +119,19 @@ struct LrLayer {
 };
 
 constexpr int LR_QLDS = 16384;  // floats of Q staged by lr_gq (in * r)
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+__device__ __forceinline__ double shfl_d(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __shfl((int)(b & 0xffffffffLL), src, 64);
+  const int hi = __shfl((int)(b >> 32), src, 64);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 // grid = sum of n1, block 256: 16 rows of one layer per block.  At it > 0 the layer's dad_tol
@@ -168,17 +183,32 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
   float* gw = X.G + (long)(rv ? row : row0) * in;
   const float* erow = X.err ? X.err + (long)(rv ? row : row0) * in : nullptr;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int k0 = 4 * w; k0 < in; k0 += 16) {
-    const int k = k0 + kr;
-    const bool kv = k < in;
-    float av = (rv && kv) ? grow[k] : 0.f;
-    if (erow && rv && kv) {  // PowerSGD: M = G + error feedback, kept in the gradient buffer
-      av += erow[k];
-      gw[k] = av;
+  // 16 chunks per round: all their G loads are issued before the first MFMA (a K loop with a
+  // few loads in flight was latency-bound: ~1 us per round trip)
+  constexpr int U = 16;
+  for (int kb = 4 * w; kb < in; kb += 16 * U) {
+    float av[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = kb + 16 * u + kr;
+      av[u] = (rv && k < in) ? grow[k] : 0.f;
     }
-    const float bv = (kv && c < r) ? q[k * r + c] : 0.f;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    if (erow) {  // PowerSGD: M = G + error feedback, kept in the gradient buffer
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = kb + 16 * u + kr;
+        if (rv && k < in) {
+          av[u] += erow[k];
+          gw[k] = av[u];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = kb + 16 * u + kr;
+      const float bv = (k < in && c < r) ? q[k * r + c] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv, acc, 0, 0, 0);
+    }
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][i][c]
@@ -190,138 +220,6 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
   }
 }
 
-// P [n, r] in LDS <- P R^{-1}, R^T R = P^T P.  256 threads.
-__device__ __forceinline__ void cholqr_lds(float* p, int n, int r, float* part, float* R,
-                                           unsigned* deadp) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // Gram P^T P on the matrix cores (f32 in, exact f32 FMA chain): for 16x16x4, lane l holds
-  // A[l & 15][k = l >> 4] = P[row k][col l & 15] and B[k = l >> 4][l & 15] -- the same value,
-  // so one LDS read feeds both operands; each wave takes every 4th block of 4 rows
-  {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int c = lane & 15, kr = lane >> 4;
-    for (int rb = 4 * w; rb < n; rb += 16) {
-      const int row = rb + kr;
-      const float v = (row < n && c < r) ? p[row * r + c] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v, v, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) part[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][i][c]
-  }
-  __syncthreads();
-  if (w == 0) {
-    // wave 0: lane i < r holds row i of the Gram (fixed-order combine of the 4 partials)
-    float a[LR_MAXR];
-#pragma unroll
-    for (int jj = 0; jj < LR_MAXR; ++jj) {
-      const int e = (lane & 15) * 16 + jj;
-      a[jj] = (lane < r && jj < r) ? part[e] + part[256 + e] + part[512 + e] + part[768 + e] : 0.f;
-    }
-    float dmax = 0.f;
-#pragma unroll
-    for (int jj = 0; jj < LR_MAXR; ++jj) dmax = fmaxf(dmax, __shfl(a[jj], jj, 64));
-    const float thr = fmaxf(1e-9f * dmax, 1e-30f);
-    unsigned dead = 0;
-    // right-looking Cholesky, upper R (R^T R = A): row k of R lives in lane k
-#pragma unroll
-    for (int k = 0; k < LR_MAXR; ++k) {
-      if (k < r) {
-        const float akk = __shfl(a[k], k, 64);
-        const bool dk = akk <= thr;  // vanished pivot: drop column k
-        const float inv = dk ? 0.f : 1.f / sqrtf(akk);
-        if (dk) dead |= 1u << k;
-        if (lane == k) {
-#pragma unroll
-          for (int jj = 0; jj < LR_MAXR; ++jj)
-            a[jj] = jj == k ? (dk ? 1.f : akk * inv) : (jj > k ? a[jj] * inv : 0.f);
-        }
-        float rk[LR_MAXR];
-#pragma unroll
-        for (int jj = 0; jj < LR_MAXR; ++jj) rk[jj] = __shfl(a[jj], k, 64);  // row k of R
-        float rki = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < LR_MAXR; ++jj) rki = lane == jj ? rk[jj] : rki;
-        if (lane > k && lane < r) {
-#pragma unroll
-          for (int jj = 0; jj < LR_MAXR; ++jj)
-            if (jj > k) a[jj] -= rki * rk[jj];
-        }
-      }
-    }
-    if (lane < r) {
-#pragma unroll
-      for (int jj = 0; jj < LR_MAXR; ++jj) R[lane * LR_MAXR + jj] = a[jj];
-    }
-    // R^{-1} (upper): lane j < r back-substitutes column j (compile-time indices, predicated);
-    // a dropped column j stays zero
-    float col[LR_MAXR];
-#pragma unroll
-    for (int i = LR_MAXR - 1; i >= 0; --i) {
-      float v = 0.f;
-      if (i <= lane && lane < r) {
-        v = i == lane ? 1.f : 0.f;
-#pragma unroll
-        for (int k = i + 1; k < LR_MAXR; ++k)
-          if (k <= lane) v -= R[i * LR_MAXR + k] * col[k];
-        v /= R[i * LR_MAXR + i];
-      }
-      col[i] = (dead >> lane & 1u) ? 0.f : v;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): R reads done before it is overwritten
-    if (lane < LR_MAXR) {
-#pragma unroll
-      for (int i = 0; i < LR_MAXR; ++i) R[i * LR_MAXR + lane] = lane < r ? col[i] : 0.f;
-    }
-    if (lane == 0) *deadp = dead;
-  }
-  __syncthreads();
-  // P <- P R^{-1} on the matrix cores: 16-row blocks, K = 16 in four 16x16x4 steps; lane l
-  // feeds A[l & 15][k = l >> 4] = P[row][4 s + k] and B[k][l & 15] = R^{-1}[4 s + k][l & 15]
-  {
-    const int c = lane & 15, kr = lane >> 4;
-    for (int b0 = 16 * w; b0 < n; b0 += 64) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int row = b0 + c;
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int k = 4 * st + kr;
-        const float av = (row < n && k < r) ? p[row * r + k] : 0.f;
-        const float bv = R[k * LR_MAXR + c];
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int orow = b0 + 4 * kr + j;
-        if (orow < n && c < r) p[orow * r + c] = acc[j];
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// grid = nl, block 256
-__global__ void __launch_bounds__(256)
-lr_orth_kernel(const LrLayer* __restrict__ Ls, int it) {
-  __shared__ float ps[LR_PLDS];
-  __shared__ float part[4 * 256];
-  __shared__ float R[LR_MAXR * LR_MAXR];
-  __shared__ unsigned dead;
-  const LrLayer& X = Ls[blockIdx.x];
-  if (it > 0 && !*X.active) return;
-  const int tid = threadIdx.x, n = X.out, r = X.r;
-  if (((n * r) & 3) == 0) {  // 16-B loads, several in flight (a scalar loop here is latency-bound)
-    const f32x4* src = reinterpret_cast<const f32x4*>(X.P);
-#pragma unroll 8
-    for (int i = tid; i < n * r / 4; i += 256) reinterpret_cast<f32x4*>(ps)[i] = src[i];
-  } else {
-    for (int i = tid; i < n * r; i += 256) ps[i] = X.P[i];
-  }
-  __syncthreads();
-  cholqr_lds(ps, n, r, part, R, &dead);  // Cholesky QR ...
-  cholqr_lds(ps, n, r, part, R, &dead);  // ... twice (CholeskyQR2)
-  for (int i = tid; i < n * r; i += 256) X.Psend[i] = ps[i];
-}
-
 // grid = sum of n3, block 256: 16 columns of one layer per block, all rows.  Q[16 cols] =
 // G[:, 16 cols]^T Pn on the matrix cores: lane l feeds A[l & 15][k] = G[r0 + k][16 cb + (l & 15)]
 // (coalesced along the row) and B[k][l & 15] = Pn[r0 + k][l & 15], k = l >> 4; the 4 waves
@@ -331,6 +229,10 @@ __global__ void __launch_bounds__(256)
 lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
   __shared__ float ps[LR_PLDS];
   __shared__ float red[4 * 256];
+  __shared__ double gm[256];
+  __shared__ double gpart[4 * 256];
+  __shared__ double rdiag[LR_MAXR];
+  __shared__ float Ri[LR_MAXR * LR_MAXR];
   __shared__ float nrm[2][4];
   int l = 0;
   while (l + 1 < nl && (int)blockIdx.x >= Ls[l + 1].b3) ++l;
@@ -338,26 +240,143 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
   if (it > 0 && !*X.active) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = X.r, n = X.out;
   const int cb = blockIdx.x - X.b3;
+  const int c = lane & 15, kr = lane >> 4;
   if (((n * r) & 3) == 0) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(X.Psend);
+    const f32x4* src = reinterpret_cast<const f32x4*>(X.P);
 #pragma unroll 8
     for (int i = tid; i < n * r / 4; i += 256) reinterpret_cast<f32x4*>(ps)[i] = src[i];
   } else {
-    for (int i = tid; i < n * r; i += 256) ps[i] = X.Psend[i];
+    for (int i = tid; i < n * r; i += 256) ps[i] = X.P[i];
   }
   __syncthreads();
-  const int c = lane & 15, kr = lane >> 4;
+  {  // Gram P^T P on the fp64 matrix cores (fp32 values, exact products): for 16x16x4 f64 lane l
+     // holds A[l & 15][k = l >> 4] = P[row k][col l & 15] and B[k][l & 15] -- the same value
+     // (C: row (l >> 4) + 4 reg, col l & 15 -- the f64 map, not the f32 one);
+     // wave w takes every 4th block of 4 rows, the four partials meet in LDS in a fixed order
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int c = lane & 15, kr = lane >> 4;
+    for (int rb = 4 * w; rb < n; rb += 16) {
+      const int row = rb + kr;
+      const double v = (row < n && c < r) ? (double)ps[row * r + c] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gpart[w * 256 + (kr + 4 * j) * 16 + c] = acc[j];  // f64 C map
+  }
+  __syncthreads();
+  gm[tid] = (gpart[tid] + gpart[256 + tid]) + (gpart[512 + tid] + gpart[768 + tid]);
+  __syncthreads();
+  if (w == 0) {
+    // wave 0: lane i < r holds row i of the Gram; right-looking Cholesky, upper R (R^T R = A),
+    // row k of R in lane k; then R^{-1} by back substitution, lane j = column j
+    double a[LR_MAXR];
+#pragma unroll
+    for (int jj = 0; jj < LR_MAXR; ++jj) a[jj] = (lane < r && jj < r) ? gm[(lane & 15) * 16 + jj] : 0.0;
+    double dmax = 0.0;
+#pragma unroll
+    for (int jj = 0; jj < LR_MAXR; ++jj) dmax = fmax(dmax, jj < r ? gm[jj * 17] : 0.0);
+    const double thr = fmax(1e-13 * dmax, 1e-280);
+    unsigned dead = 0;
+#pragma unroll
+    for (int k = 0; k < LR_MAXR; ++k) {
+      if (k < r) {
+        const double akk = shfl_d(a[k], k);
+        const bool dk = akk <= thr;  // vanished pivot: drop column k
+        const double inv = dk ? 0.0 : 1.0 / sqrt(akk);
+        if (dk) dead |= 1u << k;
+        if (lane == k) {
+#pragma unroll
+          for (int jj = 0; jj < LR_MAXR; ++jj)
+            a[jj] = jj == k ? (dk ? 1.0 : akk * inv) : (jj > k ? a[jj] * inv : 0.0);
+          rdiag[k] = inv;
+        }
+        double rk[LR_MAXR];
+#pragma unroll
+        for (int jj = 0; jj < LR_MAXR; ++jj) rk[jj] = (jj > k && jj < r) ? shfl_d(a[jj], k) : 0.0;
+        double rki = 0.0;
+#pragma unroll
+        for (int jj = 0; jj < LR_MAXR; ++jj) rki = lane == jj ? rk[jj] : rki;
+        if (lane > k && lane < r) {
+#pragma unroll
+          for (int jj = 0; jj < LR_MAXR; ++jj)
+            if (jj > k) a[jj] -= rki * rk[jj];
+        }
+      }
+    }
+    // R row-major through LDS (gm is free now: every lane has read its Gram row)
+    if (lane < r) {
+#pragma unroll
+      for (int jj = 0; jj < LR_MAXR; ++jj) gm[lane * LR_MAXR + jj] = a[jj];
+    }
+
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    double col[LR_MAXR];
+#pragma unroll
+    for (int i = LR_MAXR - 1; i >= 0; --i) {
+      double v = 0.0;
+      if (i < r && i <= lane && lane < r) {
+        v = i == lane ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = i + 1; k < LR_MAXR; ++k)
+          if (k <= lane) v -= gm[i * LR_MAXR + k] * col[k];
+        v *= rdiag[i];  // 1 / R_ii (0 for a dropped column)
+      }
+      col[i] = (dead >> lane & 1u) ? 0.0 : v;
+    }
+    if (lane < LR_MAXR) {
+#pragma unroll
+      for (int i = 0; i < LR_MAXR; ++i) Ri[i * LR_MAXR + lane] = lane < r ? (float)col[i] : 0.f;
+    }
+  }
+  __syncthreads();
+  // Pn = P R^{-1} in place, f32 MFMA: 16-row blocks, K = 16 in four 16x16x4 steps; lane l feeds
+  // A[l & 15][k = l >> 4] = P[row][4 s + k] and B[k][l & 15] = R^{-1}[4 s + k][l & 15]
+  for (int b0 = 16 * w; b0 < n; b0 += 64) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int row = b0 + c;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int k = 4 * st + kr;
+      const float av = (row < n && k < r) ? ps[row * r + k] : 0.f;
+      const float bv = Ri[k * LR_MAXR + c];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+    // a block's 16 rows are read only by the wave that rewrites them
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int orow = b0 + 4 * kr + j;
+      if (orow < n && c < r) ps[orow * r + c] = acc[j];
+    }
+  }
+  __syncthreads();
+  if (cb == 0) {
+    if (((n * r) & 3) == 0) {
+      f32x4* dst = reinterpret_cast<f32x4*>(X.Psend);
+      for (int i = tid; i < n * r / 4; i += 256) dst[i] = reinterpret_cast<const f32x4*>(ps)[i];
+    } else {
+      for (int i = tid; i < n * r; i += 256) X.Psend[i] = ps[i];
+    }
+  }
   const int col = 16 * cb + c;
   const bool cv = col < X.in;
   const float* gcol = X.G + (cv ? col : 16 * cb);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int r0 = 4 * w; r0 < n; r0 += 16) {
-    const int row = r0 + kr;
-    const bool rv = row < n;
-    const float av = (rv && cv) ? gcol[(long)row * X.in] : 0.f;
-    const float bv = (rv && c < r) ? ps[row * r + c] : 0.f;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+  constexpr int U = 16;  // as in lr_gq: a round's G loads all in flight before its MFMAs
+  for (int rb = 4 * w; rb < n; rb += 16 * U) {
+    float av[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = rb + 16 * u + kr;
+      av[u] = (row < n && cv) ? gcol[(long)row * X.in] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = rb + 16 * u + kr;
+      const float bv = (row < n && c < r) ? ps[row * r + c] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv, acc, 0, 0, 0);
+    }
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][k][c]
@@ -440,8 +459,7 @@ DN_API int dn_lr_limits(int* maxr, int* plds, int* qlds) {
 
 // One power iteration / PowerSGD half-round over every layer of the table.
 //   stage 0: lr_gq (P = G Q; it == 0 re-activates every layer, it > 0 applies dad_tol first)
-//   stage 1: lr_orth + lr_gtp (Pn = CholQR2(P); Q = G^T Pn committed to Qsend)
-//   (stages 2 / 3: lr_orth / lr_gtp alone, for tools/lowrank_bench.py)
+//   stage 1: lr_gtp (Pn = P R^{-1} from the fp64 Gram; Q = G^T Pn committed to Qsend)
 DN_API int dn_lr_stage(const void* layers, int nl, int blocks1, int blocks3, int stage, int it,
                        float tol, hipStream_t st) {
   if (nl <= 0) return DN_OK;
@@ -449,9 +467,7 @@ DN_API int dn_lr_stage(const void* layers, int nl, int blocks1, int blocks3, int
   const LrLayer* L = (const LrLayer*)layers;
   if (stage == 0)
     hipLaunchKernelGGL(lr_gq_kernel, dim3(blocks1), dim3(256), 0, st, L, nl, it, tol);
-  if (stage == 1 || stage == 2) hipLaunchKernelGGL(lr_orth_kernel, dim3(nl), dim3(256), 0, st, L, it);
-  if (stage == 1 || stage == 3)
-    hipLaunchKernelGGL(lr_gtp_kernel, dim3(blocks3), dim3(256), 0, st, L, nl, it);
+  if (stage == 1) hipLaunchKernelGGL(lr_gtp_kernel, dim3(blocks3), dim3(256), 0, st, L, nl, it);
   return dn_launch_status();
 }
 

@@ -725,9 +725,9 @@ static inline int pick_br(int B) {
     const int v = atoi(e);
     if (v == 4 || v == 8 || v == 16) return v;
   }
-  if (B <= 128) return 4;
-  if (B <= 512) return 8;
-  return 16;
+  // measured per step (bench.py, MI355X): B = 512: 4 rows 1.059 ms vs 8 rows 1.292;
+  // B = 2048: 8 rows 3.79 vs 4 rows 3.88 vs 16 rows 3.98
+  return B <= 1024 ? 4 : 8;
 }
 
 // unit groups per wave for (HD, BR) = (192, 4): 1 (12 waves, 3 per SIMD) unless

@@ -376,7 +376,7 @@ class RankDADEngine(Engine):
 
     def pre_reduce(self):
         """Local rank-r factors of every large Linear's gradient into the send buffer: two
-        launches per power iteration for all layers (``G Q``; CholeskyQR2 + ``G^T P``), the
+        launches per power iteration for all layers (``G Q``; fp64-Gram Cholesky QR + ``G^T P``), the
         ``dad_tol`` stop decided on the device: no host sync, HIP-graph capturable."""
         if not self.fast or not self.fast_layers:
             return
@@ -548,7 +548,7 @@ class PowerSGDEngine(Engine):
         gen = torch.Generator(device="cpu").manual_seed(int(self.cfg.get("seed", 0)) + 12345)
         dev = flat.data.device
         # GPU: every matrix of the model per launch (csrc/kernels/lowrank.hip): P = M Q with
-        # M = G + err formed in the same pass, CholeskyQR2 + Q = M^T P, then G = P Q^T and the
+        # M = G + err formed in the same pass, Cholesky QR (fp64 Gram) + Q = M^T P, then G = P Q^T and the
         # error feedback -- three launches and two all-reduces per step, no host sync
         self.fast = bool(flat.data.is_cuda and self.warm and _lib.native_available()
                          and self.cfg.get("powersgd_device", True) and self.mats)

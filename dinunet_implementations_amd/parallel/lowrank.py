@@ -91,8 +91,8 @@ class LowRankTable:
     ``layers``: ``[(G view [out, in], err [out, in] or None, P [out, r], Psend [out, r],
     Qsend [in, r])]`` (fp32 CUDA tensors, contiguous).  ``Qsend`` holds the committed Q: the
     input of every iteration and the next step's warm start (initialise it).  The
-    change norms and an ``active`` flag per layer are allocated here.  One power iteration =
-    :meth:`gq` (1 launch) + :meth:`orth_gtp` (2 launches), all layers each."""
+    change norms and an ``active`` flag per layer are allocated here.  One
+    power iteration = :meth:`gq` + :meth:`orth_gtp`, one launch each, all layers per launch."""
 
     def __init__(self, layers, device):
         import ctypes
@@ -152,7 +152,8 @@ class LowRankTable:
         self._stage(0, it, tol)
 
     def orth_gtp(self, it: int):
-        """Pn = CholeskyQR2(P) -> Psend, Q = G^T Pn -> Qsend (2 launches, all layers)."""
+        """Pn = P R^{-1} (Cholesky of the fp64 Gram P^T P) -> Psend,
+        Q = G^T Pn -> Qsend (one launch, all layers)."""
         self._stage(1, it)
 
     def recon_ef(self):

@@ -176,6 +176,49 @@ def report_markdown(out_dir: str) -> str:
     return "\n".join(parts) + "\n"
 
 
+def plot_boxes(experiments: Dict[str, List[Dict[str, Any]]], perf_png: str, epoch_png: str,
+               scores=("Accuracy", "F1")) -> None:
+    """The reference notebook's two figures (``NB.ipynb:131-189`` -> ``assets/perf_box.png`` /
+    ``assets/pretrain_box.png``) from per-fold tables (``fold_report(...)["folds"]``), one entry
+    per experiment label (e.g. ``{"scratch": ..., "pretrain": ...}``): test scores per
+    experiment as box plots with means, and the stopping (best-validation) epoch per experiment.
+    matplotlib only (the notebook used seaborn)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    labels = list(experiments)
+    fig, ax = plt.subplots(figsize=(10, 6))
+    width = 0.8 / max(len(scores), 1)
+    for si, sc in enumerate(scores):
+        data = [[f[sc] for f in experiments[e] if f.get(sc) is not None] for e in labels]
+        pos = [i + (si - (len(scores) - 1) / 2) * width for i in range(len(labels))]
+        bp = ax.boxplot(data, positions=pos, widths=width * 0.8, showmeans=True,
+                        patch_artist=True)
+        for b in bp["boxes"]:
+            b.set_facecolor(f"C{si}")
+            b.set_alpha(0.6)
+        ax.plot([], [], color=f"C{si}", linewidth=8, alpha=0.6, label=sc)
+    ax.set_xticks(range(len(labels)))
+    ax.set_xticklabels(labels)
+    ax.set_ylabel("Value")
+    ax.legend()
+    ax.set_title("Test performance, scratch vs with pre-training, per-fold box plot (higher is better)")
+    fig.tight_layout()
+    fig.savefig(perf_png)
+    plt.close(fig)
+    fig, ax = plt.subplots(figsize=(8, 6))
+    data = [[f["best_val_epoch"] for f in experiments[e] if f.get("best_val_epoch") is not None]
+            for e in labels]
+    ax.boxplot(data, widths=0.3, showmeans=True)
+    ax.set_xticks(range(1, len(labels) + 1))
+    ax.set_xticklabels(labels)
+    ax.set_ylabel("Stopped on epoch")
+    ax.set_title("Train from scratch vs with pre-training, per-fold box plot (lower is better)")
+    fig.tight_layout()
+    fig.savefig(epoch_png)
+    plt.close(fig)
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv:

@@ -296,7 +296,7 @@ def test_accumulated_graph_step_matches_eager():
 
 
 def test_powersgd_device_matches_reference_math():
-    """Device PowerSGD (csrc/kernels/lowrank.hip: P = M Q with M = G + err, CholeskyQR2,
+    """Device PowerSGD (csrc/kernels/lowrank.hip: P = M Q with M = G + err, Cholesky QR,
     Q = M^T P, G = P Q^T, err = M - G) == the same algorithm in torch ops (MGS), over 3
     steps of error feedback and warm-started Q."""
     from dinunet_implementations_amd.ops import FlatParams
