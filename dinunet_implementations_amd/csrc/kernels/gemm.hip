@@ -210,6 +210,8 @@ struct Epi {
   int relu;
   int out_bf16;
   int ncol;  // > 0: only output columns < ncol are stored (e.g. a ones-operand column sum)
+  const bf16* mask;  // optional [M][ldm] bf16: outputs where mask <= 0 are zeroed (ReLU backward)
+  long ldm;
 };
 
 constexpr int GMAX = 12;  // problems per grouped launch (kernarg: ~1.6 KB)
@@ -240,6 +242,7 @@ __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int
   v *= epi.alpha;
   if (epi.bias) v += epi.bias[col];
   if (epi.relu) v = fmaxf(v, 0.f);
+  if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col] > 0.f)) v = 0.f;
   const long orow = epi.row_map ? epi.row_map[row] : row;
   if (orow < 0) return;  // dropped row (e.g. zero-padded LSTM units)
   if (epi.out_bf16) {
@@ -598,6 +601,11 @@ gemm_dma_kernel(GemmGroup g) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(E + lr * ES + lc + 4);
         bf16x8* cp = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(P.C) + (long)row * P.ldc + col);
         float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        if (ep.mask) {
+          const bf16x8 m = *reinterpret_cast<const bf16x8*>(ep.mask + (long)row * ep.ldm + col);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (float)m[e] > 0.f ? v[e] : 0.f;
+        }
         if (ep.beta != 0.f) {
           const bf16x8 o = *cp;
 #pragma unroll
@@ -617,6 +625,11 @@ gemm_dma_kernel(GemmGroup g) {
         if (row >= M || col >= N) continue;
         f32x4 v = *reinterpret_cast<const f32x4*>(E + lr * ES + lc);
         f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + (long)row * P.ldc + col);
+        if (ep.mask) {
+          const bf16x4 m = *reinterpret_cast<const bf16x4*>(ep.mask + (long)row * ep.ldm + col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (float)m[e] > 0.f ? v[e] : 0.f;
+        }
         if (ep.beta != 0.f) {
           const f32x4 o = *cp;
 #pragma unroll
@@ -654,6 +667,7 @@ __device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, in
     v[e] *= epi.alpha;
     if (epi.bias) v[e] += epi.bias[col + e];
     if (epi.relu) v[e] = fmaxf(v[e], 0.f);
+    if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col + e] > 0.f)) v[e] = 0.f;
   }
   if (epi.out_bf16) {
     bf16x4* cp = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(C) + orow * ldc + col);
@@ -810,6 +824,7 @@ static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int t
     const int cv = P.epi.out_bf16 ? 8 : 4;
     if (P.slab || P.epi.row_map || P.epi.ncol > 0 || P.N % cv || P.ldc % cv || !aligned16(P.C))
       g.vepi = 0;
+    if (P.epi.mask && (P.epi.ldm % 8 || !aligned16(P.epi.mask))) g.vepi = 0;
   }
   if (tile == 1) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
   return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, g, st);
@@ -832,7 +847,7 @@ DN_API long dn_gemm_workspace(int M, int N, int K, int splits) {
 DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, int b_bf16, int tb,
                    long ldb, void* C, int c_bf16, long ldc, int M, int N, int K, float alpha,
                    float beta, const float* bias, int relu, const int* row_map, int tile,
-                   int splits, float* slab, hipStream_t st) {
+                   int splits, float* slab, const void* mask, long ldm, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
@@ -845,7 +860,7 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   P.kchunk = kchunk_for(K, g.splits);
   if (g.splits > 1) g.splits = (K + P.kchunk - 1) / P.kchunk;
   P.slab = g.splits > 1 ? slab : nullptr;
-  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0};
+  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0, (const bf16*)mask, ldm};
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }
 
@@ -877,7 +892,7 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
     P.slab = g.splits > 1 ? slab + soff : nullptr;
     soff += (long)g.splits * M[i] * N[i];
     P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16,
-                ncol ? ncol[i] : 0};
+                ncol ? ncol[i] : 0, nullptr, 0};
   }
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }

@@ -82,14 +82,15 @@ class LSTM(nn.Module):
         return pack_params(flat, self.input_size, device, side=side, casts=casts,
                            cast_out=cast_out)
 
-    def forward(self, x: torch.Tensor, h=None, reduce: str = "none", packed=None, xp=None):
+    def forward(self, x: torch.Tensor, h=None, reduce: str = "none", packed=None, xp=None,
+                relu_input: bool = False):
         """``reduce='none'`` returns ``(hidden_seq [B,S,H*dirs], (h, c))`` like the reference;
         ``reduce='mean'`` returns the temporal mean ``[B, H*dirs]`` instead of the sequence
         (what ``ICALstm`` consumes) so the fused kernel never materialises the sequence."""
         if h is None and self.fused_ok(x):
             params = [cell.params() for cell in self.lstms]
             return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms), packed=packed,
-                              xp=xp)
+                              xp=xp, relu_input=relu_input)
         if x.is_cuda and self.use_fused:
             _slow_lstm_gate(self.hidden_size, x.shape[0])
         x = x.to(self.lstms[0].i2h.weight.dtype)  # the fused encoder hands over bf16
@@ -214,7 +215,8 @@ class ICALstm(nn.Module):
     def body_loss(self, enc: torch.Tensor, y: torch.Tensor):
         """Second half of :meth:`forward_loss`: bi-LSTM, classifier, softmax-CE on ``enc``."""
         packed, self._packed = getattr(self, "_packed", None), None
-        o, _ = self.lstm(enc, reduce="mean", packed=packed)
+        # enc = ReLU(encoder), consumed only by the LSTM: its mask joins the LSTM's dX GEMM
+        o, _ = self.lstm(enc, reduce="mean", packed=packed, relu_input=True)
         o = o.flatten(1).to(self.classifier[1].weight.dtype)
         if self.use_fused and o.is_cuda:
             return ops.head_loss(o, self.head_spec(), y, log_out=False)

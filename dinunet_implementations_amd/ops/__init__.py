@@ -10,8 +10,10 @@ from .heads import softmax_ce, log_softmax_nll
 from .head import HeadSpec, head_loss
 
 
-def bilstm(x, params, reduce: str = "none", modules=None, packed=None, xp=None):
-    return _bilstm_fused(x, params, reduce=reduce, modules=modules, packed=packed, xp=xp)
+def bilstm(x, params, reduce: str = "none", modules=None, packed=None, xp=None,
+           relu_input: bool = False):
+    return _bilstm_fused(x, params, reduce=reduce, modules=modules, packed=packed, xp=xp,
+                         relu_input=relu_input)
 
 
 __all__ = [

@@ -22,7 +22,7 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_int, _lib.c_int, _lib.c_long, _lib.c_void_p, _lib.c_int,
                           _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_float,
                           _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
-                          _lib.c_int, _lib.c_void_p, _lib.c_void_p])
+                          _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p])
 
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
 _lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 14 + [_lib.c_int] * 8
@@ -89,7 +89,10 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
        out_dtype: torch.dtype = torch.float32, out: Optional[Tensor] = None,
        bias: Optional[Tensor] = None, relu: bool = False, alpha: float = 1.0, beta: float = 0.0,
        row_map: Optional[Tensor] = None, splits: Optional[int] = None,
-       tile: Optional[int] = None) -> Tensor:
+       tile: Optional[int] = None, mask: Optional[Tensor] = None) -> Tensor:
+    """``out (+)= alpha * op(a) @ op(b) (+ bias) (ReLU)``; ``mask`` (bf16 [M, N], row-contiguous):
+    outputs where ``mask <= 0`` are zeroed in the epilogue (a ReLU backward fused into the GEMM
+    producing its incoming gradient)."""
     A = a.t() if trans_a else a
     B = b.t() if trans_b else b
     M, K = A.shape
@@ -102,6 +105,8 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
             res = res + bias.float()
         if relu:
             res = torch.relu(res)
+        if mask is not None:
+            res = res * (mask.float() > 0)
         if out is None:
             out = torch.zeros(M if row_map is None else int(row_map.max()) + 1, N,
                               dtype=out_dtype) if row_map is not None else None
@@ -134,11 +139,14 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
         bias = bias.float().contiguous()
     if row_map is not None:
         row_map = row_map.to(device=a.device, dtype=torch.int32).contiguous()
+    if mask is not None:
+        if (mask.dtype != torch.bfloat16 or tuple(mask.shape) != (M, N) or mask.stride(1) != 1):
+            raise ValueError("mm mask must be a row-contiguous bf16 [M, N] tensor")
     _lib.call("dn_gemm", A.data_ptr(), int(A.dtype == torch.bfloat16), ta, lda, B.data_ptr(),
               int(B.dtype == torch.bfloat16), tb, ldb, out.data_ptr(),
               int(out.dtype == torch.bfloat16), out.stride(0), M, N, K, float(alpha), float(beta),
               _lib.ptr(bias), int(relu), _lib.ptr(row_map), tile, sp, _lib.ptr(slab),
-              _lib.stream())
+              _lib.ptr(mask), mask.stride(0) if mask is not None else 0, _lib.stream())
     return out
 
 

@@ -26,6 +26,28 @@ _lib.register("dn_relu_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.
                               _lib.c_void_p])
 _RB_SLABS = 64
 
+# The one gradient tensor whose ReLU mask was already applied by the GEMM that produced it (the
+# fused LSTM's input-gradient GEMM, ``ops.lstm``): a weak reference, so a freed tensor can never
+# match a later one that reuses its memory.  Masking is idempotent, so a miss only costs the
+# mask launch.
+_PREMASKED = None
+
+
+def mark_premasked(t: torch.Tensor) -> None:
+    global _PREMASKED
+    import weakref
+    _PREMASKED = weakref.ref(t)
+
+
+def _take_premasked(dy: torch.Tensor) -> bool:
+    global _PREMASKED
+    r = _PREMASKED() if _PREMASKED is not None else None
+    hit = (r is not None and r.data_ptr() == dy.data_ptr() and r.numel() == dy.numel()
+           and r.dtype == dy.dtype and dy.is_contiguous())
+    if hit:
+        _PREMASKED = None
+    return hit
+
 
 class _LinearBiasReLU(torch.autograd.Function):
     @staticmethod
@@ -53,13 +75,17 @@ def _relu_linear_backward(ctx, dy):
     x2d, y = ctx.saved_tensors
     weight, bias = ctx.weight, ctx.bias
     N, O = y.shape
+    premasked = _take_premasked(dy)
     dy = dy.to(torch.bfloat16).contiguous()
-    dym = torch.empty_like(dy)
     if (N * O) % 8 == 0:
         # mask only; dW += dym^T x and db += dym^T 1 are deferred into the end-of-backward
         # grouped launch with the LSTM's weight gradients (ops._grad.defer)
-        _lib.call("dn_relu_bwd", dy.data_ptr(), y.data_ptr(), dym.data_ptr(), N * O,
-                  _lib.stream())
+        if premasked:
+            dym = dy.view(N, O)  # masked in the epilogue of the GEMM that produced it
+        else:
+            dym = torch.empty_like(dy)
+            _lib.call("dn_relu_bwd", dy.data_ptr(), y.data_ptr(), dym.data_ptr(), N * O,
+                      _lib.stream())
         probs = [dict(a=dym, b=x2d, out=_grad.grad_buffer(weight), beta=1.0)]
         if bias is not None:
             from .lstm import _ones
@@ -67,6 +93,7 @@ def _relu_linear_backward(ctx, dy):
                               beta=1.0, ncol=1))
         _grad.defer(probs, [weight] + ([bias] if bias is not None else []))
     else:
+        dym = torch.empty_like(dy)
         ws = torch.empty(_RB_SLABS * O, dtype=torch.float32, device=dy.device)
         db = _grad.grad_buffer(bias) if bias is not None else \
             torch.empty(O, dtype=torch.float32, device=dy.device)

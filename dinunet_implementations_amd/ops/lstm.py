@@ -34,7 +34,7 @@ from . import _grad
 from . import _lib
 from . import _streams
 from . import capture as _cap
-from .gemm import mm, mm_grouped, mm_plain
+from .gemm import PLAIN_BLAS, mm, mm_grouped, mm_plain
 
 Tensor = torch.Tensor
 
@@ -97,7 +97,8 @@ def _ones(n: int, device) -> Tensor:
 
 class _BiLSTMFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, enc: Tensor, mode: str, modules, packed, xp_pre, *params: Tensor):
+    def forward(ctx, enc: Tensor, mode: str, modules, packed, xp_pre, relu_in: bool,
+                *params: Tensor):
         ctx.set_materialize_grads(False)  # unused hT / cT -> None (no zero tensors, no syncs)
         B, S, I = enc.shape
         ndir = len(params) // 4
@@ -142,6 +143,7 @@ class _BiLSTMFn(torch.autograd.Function):
             out = hseq.view(Bp, S, ndir, HD)[:B, :, :, :Hd].reshape(B, S, ndir * Hd)
         ctx.save_for_backward(x2d, wih_p, whh_p, whhT_p, bias_p, xp, c_save, hprev)
         ctx.params = params
+        ctx.relu_in = bool(relu_in)
         ctx.meta = (B, S, I, Hd, HD, ndir, mode, enc.dtype)
         ctx.modules = modules
         return out, hT, cT
@@ -181,7 +183,16 @@ class _BiLSTMFn(torch.autograd.Function):
         # (7) input grad
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = mm_plain(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
+            if ctx.relu_in and not PLAIN_BLAS:
+                # the input is a ReLU output consumed only here: the ReLU backward's mask rides
+                # in this GEMM's epilogue (d input where input <= 0 cannot reach anything), and
+                # the encoder backward skips its own mask launch for exactly this tensor
+                dx = mm(dpre_v, wih_p, out_dtype=torch.bfloat16, mask=x2d)
+                from .linear import mark_premasked
+                mark_premasked(dx)
+                dx = dx.view(B, S, I)
+            else:
+                dx = mm_plain(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
             if enc_dtype != torch.bfloat16:
                 dx = dx.to(enc_dtype)
         if capturing:
@@ -189,7 +200,7 @@ class _BiLSTMFn(torch.autograd.Function):
             for d, cell in enumerate(ctx.modules):
                 _cap.record(cell.i2h, x2d, dref[:, d])
                 _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
-        return (dx, None, None, None, None) + (None,) * len(params)
+        return (dx, None, None, None, None, None) + (None,) * len(params)
 
 
 def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = False,
@@ -317,13 +328,17 @@ def _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
 
 
 def bilstm(x: Tensor, params: Sequence[Tuple[Tensor, Tensor, Tensor, Tensor]],
-           reduce: str = "none", modules=None, packed=None, xp: Optional[Tensor] = None):
-    """Fused bi-LSTM: returns ``(hmean [B, ndir*Hd] | hseq [B, S, ndir*Hd], (hT, cT))``."""
+           reduce: str = "none", modules=None, packed=None, xp: Optional[Tensor] = None,
+           relu_input: bool = False):
+    """Fused bi-LSTM: returns ``(hmean [B, ndir*Hd] | hseq [B, S, ndir*Hd], (hT, cT))``.
+
+    ``relu_input``: ``x`` is a ReLU output whose only consumer is this LSTM (the ICA encoder);
+    the backward then fuses the ReLU mask into its input-gradient GEMM."""
     if not _lib.native_available():
         raise RuntimeError("fused LSTM requested but the gfx950 kernel library is not built")
     flat: List[Tensor] = []
     for p in params:
         flat.extend(p)
     out, hT, cT = _BiLSTMFn.apply(x, "mean" if reduce == "mean" else "seq", modules, packed, xp,
-                                  *flat)
+                                  bool(relu_input), *flat)
     return out, (hT, cT)

@@ -94,6 +94,23 @@ def test_gemm_lds_dma_vector_epilogue(tile, M, N, K):
     assert rel(c, c0 + 0.5 * (a.float() @ w.float().t())) < 2e-3
 
 
+@pytest.mark.parametrize("bf16_ops", [True, False])
+def test_gemm_relu_mask_epilogue(bf16_ops):
+    """mm(..., mask=y): outputs where y <= 0 are zeroed in the epilogue (the ICA encoder's ReLU
+    backward fused into the LSTM input-gradient GEMM), LDS-DMA and register-staged kernels."""
+    from dinunet_implementations_amd.ops import mm
+    M, N, K = 3136, 256, 1536
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV)
+    if bf16_ops:
+        a, b = a.to(torch.bfloat16), b.to(torch.bfloat16)
+    y = torch.relu(torch.randn(M, N, device=DEV)).to(torch.bfloat16)
+    out = mm(a, b, out_dtype=torch.bfloat16, mask=y)
+    ref = (bf(a) @ bf(b)) * (y.float() > 0)
+    assert rel(out, ref) < 1e-2
+    assert bool(((out.float() != 0) <= (y.float() > 0)).all())
+
+
 def test_gemm_epilogue_bias_relu_bf16_out_and_beta():
     from dinunet_implementations_amd.ops import mm
     M, N, K = 300, 200, 128
