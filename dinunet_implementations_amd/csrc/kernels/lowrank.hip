@@ -151,8 +151,12 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
   } else {
     if (!*X.active) return;  // stopped at an earlier iteration
     if (tol > 0.f) {
+      // every wave reduces the per-block norms the same way (lane-strided partials, butterfly):
+      // one bit-identical decision in every wave and block, no serial L2 round-trip chain
       float D = 0.f, Qn = 0.f;
-      for (int b = 0; b < X.n3; ++b) { D += X.norms[2 * b]; Qn += X.norms[2 * b + 1]; }
+      for (int b = lane; b < X.n3; b += 64) { D += X.norms[2 * b]; Qn += X.norms[2 * b + 1]; }
+      D = wave_sum(D);
+      Qn = wave_sum(Qn);
       if (sqrtf(D) / (sqrtf(Qn) + 1e-8f) < tol) {
         if (lead) *X.active = 0;
         return;
@@ -426,23 +430,47 @@ struct PiRecon {
   long start;      // first output element (prefix over layers)
 };
 
-// rank-dAD: one thread per output element of every layer:
-// G[row][k] = sum_s sum_c P_s[row][c] Q_s[k][c] / W
+// rank-dAD: G = sum over the W sites of P_s Q_s^T / W for every layer, one 16 x 16 output tile
+// per wave on the f32 matrix cores (16x16x4, K = r in chunks of 4 per site: lane l feeds
+// A[l & 15][k] = P_s[r0 + (l & 15)][c + k] and B[k][l & 15] = Q_s[k0 + (l & 15)][c + k],
+// k = l >> 4).  The tile list is every layer's tiles in order; the per-thread-element loop it
+// replaced was latency-bound (17 us for the ICA layers).
 __global__ void __launch_bounds__(256)
 pi_reconstruct_kernel(const PiRecon* __restrict__ R, int n, long total, long stride, int W, float inv_w) {
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c16 = lane & 15, kq = lane >> 4;
+  long ntiles = 0;
+  for (int l = 0; l < n; ++l) ntiles += (long)((R[l].out + 15) / 16) * ((R[l].in + 15) / 16);
+  for (long tile = blockIdx.x * 4L + w; tile < ntiles; tile += (long)gridDim.x * 4) {
     int l = 0;
-    while (l + 1 < n && e >= R[l + 1].start) ++l;
-    const PiRecon& X = R[l];
-    const long i = e - X.start;
-    const int row = (int)(i / X.in), k = (int)(i - (long)row * X.in);
-    float s = 0.f;
-    for (int w = 0; w < W; ++w) {
-      const float* p = X.P + (long)w * stride + (long)row * X.r;
-      const float* q = X.Q + (long)w * stride + (long)k * X.r;
-      for (int c = 0; c < X.r; ++c) s += p[c] * q[c];
+    long t0 = 0;
+    for (;; ++l) {
+      const long nt = (long)((R[l].out + 15) / 16) * ((R[l].in + 15) / 16);
+      if (tile < t0 + nt || l + 1 == n) break;
+      t0 += nt;
     }
-    X.G[i] = s * inv_w;
+    const PiRecon& X = R[l];
+    const int tn = (X.in + 15) / 16;
+    const int ti = (int)(tile - t0);
+    const int r0 = 16 * (ti / tn), k0 = 16 * (ti % tn);
+    const int prow = r0 + c16, qrow = k0 + c16;
+    const bool pv = prow < X.out, qv = qrow < X.in;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < W; ++s) {
+      const float* p = X.P + (long)s * stride + (long)(pv ? prow : 0) * X.r;
+      const float* q = X.Q + (long)s * stride + (long)(qv ? qrow : 0) * X.r;
+      for (int c = 0; c < X.r; c += 4) {
+        const int cc = c + kq;
+        const float av = (pv && cc < X.r) ? p[cc] : 0.f;
+        const float bv = (qv && cc < X.r) ? q[cc] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = r0 + 4 * kq + j, col = k0 + c16;
+      if (row < X.out && col < X.in) X.G[(long)row * X.in + col] = acc[j] * inv_w;
+    }
   }
 }
 
@@ -486,7 +514,8 @@ DN_API int dn_lr_recon_ef(const void* layers, const long* starts, int nl, long t
 DN_API int dn_pi_reconstruct(const void* recon, int n, long total, long stride, int W,
                              hipStream_t st) {
   if (n <= 0 || total <= 0) return DN_OK;
-  long blocks = (total + 255) / 256;
+  long blocks = (total / 256 + 3) / 4;  // ~one 16 x 16 tile per wave
+  if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(pi_reconstruct_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
                      (const PiRecon*)recon, n, total, stride, W, 1.f / (float)W);
