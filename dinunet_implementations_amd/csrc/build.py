@@ -35,6 +35,12 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contr
              "-munsafe-fp-atomics", "-fno-slp-vectorize", "-Wno-unused-result"]
 
 
+# per-file code-generation flags: the low-rank kernels' fp64 / f32 MFMA accumulators stay in
+# VGPRs (the AGPR form made hipcc copy every loop-carried accumulator AGPR <-> VGPR each
+# iteration of the Gram loop: 19k -> see profiles/r2_lowrank_stamps.txt)
+FILE_FLAGS = {"lowrank.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def _sources(kind: str):
     if kind == "hip":
         return sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip")))
@@ -68,7 +74,7 @@ def _run(cmd):
 def build_kernels(force: bool = False, jobs: int = 4, verbose: bool = True) -> str:
     srcs = _sources("hip")
     os.makedirs(OUT_DIR, exist_ok=True)
-    digest = _digest(srcs, " ".join(HIP_FLAGS) + ARCH)
+    digest = _digest(srcs, " ".join(HIP_FLAGS) + ARCH + repr(sorted(FILE_FLAGS.items())))
     if not force and _stamp_ok(KERNEL_LIB, digest):
         return KERNEL_LIB
     objdir = os.path.join(OUT_DIR, "obj")
@@ -76,7 +82,8 @@ def build_kernels(force: bool = False, jobs: int = 4, verbose: bool = True) -> s
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
-        _run([HIPCC, *HIP_FLAGS, "-I", os.path.join(HERE, "kernels"), "-c", src, "-o", obj])
+        _run([HIPCC, *HIP_FLAGS, *FILE_FLAGS.get(os.path.basename(src), []),
+              "-I", os.path.join(HERE, "kernels"), "-c", src, "-o", obj])
         if verbose:
             print(f"[build] {os.path.relpath(src, PKG)}", flush=True)
         return obj

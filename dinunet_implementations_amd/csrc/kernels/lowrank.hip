@@ -118,6 +118,16 @@ struct LrLayer {
   int b3, n3;      // lr_gtp: first block, blocks (16 columns each)
 };
 
+// LR_STAMPS (diagnostic builds only): lr_gtp phase timestamps (s_memtime) of the last column
+// block of every layer, [layer][8], via dn_lr_set_stamps
+#ifdef LR_STAMPS
+__device__ unsigned long long* lr_stamp_buf;
+#define LR_STAMP(i) do { if (threadIdx.x == 0 && lr_stamp_buf && blockIdx.x == (unsigned)(X.b3 + X.n3 - 1)) { \
+  unsigned long long v_; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v_) :: "memory"); \
+  lr_stamp_buf[(long)l * 8 + (i)] = v_; } } while (0)
+#else
+#define LR_STAMP(i) do { } while (0)
+#endif
 constexpr int LR_QLDS = 16384;  // floats of Q staged by lr_gq (in * r)
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -127,6 +137,9 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ float rlane(float v, int k) {  // k: compile-time lane index
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
 __device__ __forceinline__ double shfl_d(double v, int src) {
   const long long b = __double_as_longlong(v);
   const int lo = __shfl((int)(b & 0xffffffffLL), src, 64);
@@ -134,9 +147,132 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+typedef const __attribute__((address_space(1))) float gfloat;  // global loads, not flat
+typedef const __attribute__((address_space(1))) f32x4 gfloat4;
+
+// LDS staging of a small fp32 matrix through registers: every thread issues all of its (clamped)
+// loads up front, the caller issues its own long loads, then the stores wait only for these.
+constexpr int LR_STV = 16;  // f32x4 per thread: 256 * 16 * 4 = 16384 floats
+__device__ __forceinline__ void stage_load(f32x4 (&v)[LR_STV], const float* src, int nf, int tid) {
+  const int n4 = nf >> 2;
+#pragma unroll
+  for (int j = 0; j < LR_STV; ++j) {
+    const int i = tid + 256 * j;
+    v[j] = ((gfloat4*)src)[i < n4 ? i : n4 - 1];
+  }
+}
+__device__ __forceinline__ void stage_store(const f32x4 (&v)[LR_STV], float* dst, int nf, int tid) {
+  const int n4 = nf >> 2;
+#pragma unroll
+  for (int j = 0; j < LR_STV; ++j) {
+    const int i = tid + 256 * j;
+    if (i < n4) reinterpret_cast<f32x4*>(dst)[i] = v[j];
+  }
+}
+
+// lr_gq body for one layer kind: VEC = 16-byte row runs (in % 4 == 0, every ICA layer), ERR =
+// PowerSGD error feedback (M = G + err formed on the fly and written back to the gradient buffer),
+// QL = Q staged in LDS (in * r <= LR_QLDS; a generic pointer would make every B read a flat load)
+template <bool VEC, bool ERR, bool QL>
+__device__ __forceinline__ void gq_main(const LrLayer& X, float* qs, float* red, int tid, int w) {
+  const int lane = tid & 63, r = X.r, in = X.in;
+  const int nq = in * r;
+  constexpr bool lds = QL;
+  const bool qvec = lds && (nq & 3) == 0;
+  f32x4 qv[LR_STV];
+  if (qvec) stage_load(qv, X.Qsend, nq, tid);
+  const int row0 = 16 * (blockIdx.x - X.b1);
+  const int c = lane & 15, kr = lane >> 4;
+  const int row = row0 + c;
+  const bool rv = row < X.out;
+  const long roff = (long)(rv ? row : row0) * in;
+  float* gw = X.G + roff;
+  gfloat* grow = (gfloat*)(X.G + roff);
+  gfloat* erow = (gfloat*)(X.err + (ERR ? roff : 0));
+  constexpr int U = 8;
+  const int nch = (in + 15) >> 4;
+  // chunk j of this wave = global chunk w + 4 j; its lane run starts at column 16 ch + 4 kr
+  auto load = [&](f32x4 (&v)[U], int j0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k0 = 16 * (w + 4 * (j0 + u)) + 4 * kr;
+      f32x4 g;
+      if (VEC) {
+        const bool ok = rv && k0 < in;
+        g = ((gfloat4*)grow)[(ok ? k0 : 0) >> 2];
+        if (ERR) {
+          g += ((gfloat4*)erow)[(ok ? k0 : 0) >> 2];
+          if (ok) reinterpret_cast<f32x4*>(gw)[k0 >> 2] = g;
+        }
+        g *= ok ? 1.f : 0.f;  // a multiply, not a select: keeps the load unconditional
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int k = k0 + s2;
+          const bool ok = rv && k < in;
+          float x = grow[ok ? k : 0];
+          if (ERR) {
+            x += erow[ok ? k : 0];
+            if (ok) gw[k] = x;
+          }
+          g[s2] = x * (ok ? 1.f : 0.f);
+        }
+      }
+      v[u] = g;
+    }
+  };
+  const float cmask = c < r ? 1.f : 0.f;
+  const int cc = c < r ? c : 0;
+  auto mma = [&](const f32x4 (&v)[U], int j0, f32x4& acc) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k0 = 16 * (w + 4 * (j0 + u)) + 4 * kr;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int k = k0 + s2;
+        // columns past `in` meet a zero A entry; the clamp keeps the read in bounds
+        const int qi = (k < in ? k : 0) * r + cc;
+        const float bq = (QL ? qs[qi] : ((gfloat*)X.Qsend)[qi]) * cmask;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v[u][s2], bq, acc, 0, 0, 0);
+      }
+    }
+  };
+  const int nj = (nch - w + 3) >> 2;  // this wave's chunk count (scalar)
+  f32x4 g0[U], g1[U];
+  load(g0, 0);
+  if (U < nj) load(g1, U);
+  if (qvec) {
+    stage_store(qv, qs, nq, tid);
+  } else if (lds) {
+    for (int i = tid; i < nq; i += 256) qs[i] = X.Qsend[i];
+  }
+  __syncthreads();
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < nj; j += 2 * U) {
+    mma(g0, j, acc);
+    if (j + 2 * U < nj) load(g0, j + 2 * U);
+    if (j + U >= nj) break;
+    mma(g1, j + U, acc);
+    if (j + 3 * U < nj) load(g1, j + 3 * U);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][i][c]
+  __syncthreads();
+  {
+    const int i = tid >> 4, c2 = tid & 15, e = i * 16 + c2;
+    if (row0 + i < X.out && c2 < r)
+      X.P[(long)(row0 + i) * r + c2] = red[e] + red[256 + e] + red[512 + e] + red[768 + e];
+  }
+}
+
 // grid = sum of n1, block 256: 16 rows of one layer per block.  At it > 0 the layer's dad_tol
 // decision is taken here from the last commit's per-block norms (every block of the layer sums
 // them in the same order: one decision everywhere); block 0 records it for the later launches.
+// P[16 rows] = G[16 rows][:] Q on the matrix cores (f32 16x16x4): the K axis is cut in 16-column
+// chunks, wave w taking chunks w, w + 4, ...; in a chunk lane l loads the 16-byte run
+// G[row0 + (l & 15)][16 ch + 4 (l >> 4) .. + 3] and MFMA step s uses its element s with
+// B[k][l & 15] = Q[16 ch + 4 (l >> 4) + s][l & 15].  Two rounds of U chunks are in flight at
+// once, issued before Q is staged: one HBM round trip for a 1000-column layer instead of four.
 __global__ void __launch_bounds__(256)
 lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
   __shared__ float qs[LR_QLDS];
@@ -144,7 +280,8 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
   int l = 0;
   while (l + 1 < nl && (int)blockIdx.x >= Ls[l + 1].b1) ++l;
   const LrLayer& X = Ls[l];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = X.r, in = X.in;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform loops, no exec masks
   const bool lead = blockIdx.x == (unsigned)X.b1 && tid == 0;
   if (it == 0) {
     if (lead) *X.active = 1;
@@ -163,88 +300,93 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
       }
     }
   }
-  const int nq = in * r;
-  const bool lds = nq <= LR_QLDS;
-  if (lds) {
-    if ((nq & 3) == 0) {
-      const f32x4* src = reinterpret_cast<const f32x4*>(X.Qsend);
-#pragma unroll 4
-      for (int i = tid; i < nq / 4; i += 256) reinterpret_cast<f32x4*>(qs)[i] = src[i];
-    } else {
-      for (int i = tid; i < nq; i += 256) qs[i] = X.Qsend[i];
-    }
+  const bool vec = (X.in & 3) == 0, ql = X.in * X.r <= LR_QLDS;  // uniform per layer
+#define LR_GQ(V, E) (ql ? gq_main<V, E, true>(X, qs, red, tid, w) : gq_main<V, E, false>(X, qs, red, tid, w))
+  if (X.err) {
+    if (vec) LR_GQ(true, true); else LR_GQ(false, true);
+  } else {
+    if (vec) LR_GQ(true, false); else LR_GQ(false, false);
   }
-  __syncthreads();
-  const float* q = lds ? qs : X.Qsend;
-  // P[16 rows] = G[16 rows][:] Q on the matrix cores (f32 16x16x4): lane l feeds
-  // A[l & 15][k] = G[row0 + (l & 15)][k0 + k] and B[k][l & 15] = Q[k0 + k][l & 15], k = l >> 4;
-  // the 4 waves take interleaved 4-column chunks of K and meet in LDS
-  const int row0 = 16 * (blockIdx.x - X.b1);
-  const int c = lane & 15, kr = lane >> 4;
-  const int row = row0 + c;
-  const bool rv = row < X.out;
-  const float* grow = X.G + (long)(rv ? row : row0) * in;
-  float* gw = X.G + (long)(rv ? row : row0) * in;
-  const float* erow = X.err ? X.err + (long)(rv ? row : row0) * in : nullptr;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  // 16 chunks per round: all their G loads are issued before the first MFMA (a K loop with a
-  // few loads in flight was latency-bound: ~1 us per round trip)
-  constexpr int U = 16;
-  for (int kb = 4 * w; kb < in; kb += 16 * U) {
-    float av[U];
+#undef LR_GQ
+}
+
+// Forward substitution x <- x D^{-1/2} R_s^{-1} for one row held in registers: Rh[k][m] =
+// R_s[k][m] above the diagonal, Rh[k][k] = 1 / R_s[k][k] (0 for a dropped column), zeros below;
+// Sv = D^{-1/2}.  Uniform LDS reads (broadcast); right-looking so the chain per step is one FMA.
+__device__ __forceinline__ void lr_solve_row(float (&x)[LR_MAXR], const float* Rh,
+                                             const float* Sv) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = kb + 16 * u + kr;
-      av[u] = (rv && k < in) ? grow[k] : 0.f;
+  for (int j = 0; j < LR_MAXR; ++j) x[j] *= Sv[j];
+#pragma unroll
+  for (int j = 0; j < LR_MAXR; ++j) {
+    float rw[LR_MAXR];
+#pragma unroll
+    for (int q4 = 0; q4 < LR_MAXR / 4; ++q4) {
+      const f32x4 v = reinterpret_cast<const f32x4*>(Rh + j * LR_MAXR)[q4];
+      rw[4 * q4] = v[0]; rw[4 * q4 + 1] = v[1]; rw[4 * q4 + 2] = v[2]; rw[4 * q4 + 3] = v[3];
     }
-    if (erow) {  // PowerSGD: M = G + error feedback, kept in the gradient buffer
+    x[j] *= rw[j];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = kb + 16 * u + kr;
-        if (rv && k < in) {
-          av[u] += erow[k];
-          gw[k] = av[u];
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = kb + 16 * u + kr;
-      const float bv = (k < in && c < r) ? q[k * r + c] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv, acc, 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) red[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][i][c]
-  __syncthreads();
-  {
-    const int i = tid >> 4, cc = tid & 15, e = i * 16 + cc;
-    if (row0 + i < X.out && cc < r)
-      X.P[(long)(row0 + i) * r + cc] = red[e] + red[256 + e] + red[512 + e] + red[768 + e];
+    for (int m = j + 1; m < LR_MAXR; ++m) x[m] = __builtin_fmaf(-x[j], rw[m], x[m]);
   }
 }
 
 // grid = sum of n3, block 256: 16 columns of one layer per block, all rows.  Q[16 cols] =
-// G[:, 16 cols]^T Pn on the matrix cores: lane l feeds A[l & 15][k] = G[r0 + k][16 cb + (l & 15)]
-// (coalesced along the row) and B[k][l & 15] = Pn[r0 + k][l & 15], k = l >> 4; the 4 waves
-// take interleaved 4-row chunks and meet in LDS.  The commit rides here: the new Q slice
-// replaces Qsend, and the block's ||Q - Q_prev||^2, ||Q||^2 go to `norms` for the next lr_gq.
+// G[:, 16 cols]^T Pn with Pn = P R^{-1} is computed as (G^T P) R^{-1}: the G^T P product does not
+// wait for the factorisation, so its column loads are issued at the top of the kernel and land
+// while P is staged and the Gram formed; R^{-1} is then applied to the 16 x r result by forward
+// substitution (no explicit inverse, no n-row apply pass).  Column block 0 alone forms Pn (Psend)
+// by the same substitution over P's rows.  G^T P on the matrix cores: lane l feeds
+// A[l & 15][k] = G[r0 + k][16 cb + (l & 15)] (coalesced along the row) and B[k][l & 15] =
+// P[r0 + k][l & 15], k = l >> 4; the 4 waves take interleaved 4-row chunks and meet in LDS.  The
+// commit rides here: the new Q slice replaces Qsend, and the block's ||Q - Q_prev||^2, ||Q||^2
+// go to `norms` for the next lr_gq.
 __global__ void __launch_bounds__(256)
 lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
   __shared__ float ps[LR_PLDS];
   __shared__ float red[4 * 256];
   __shared__ double gm[256];
   __shared__ double gpart[4 * 256];
-  __shared__ double rdiag[LR_MAXR];
-  __shared__ float Ri[LR_MAXR * LR_MAXR];
-  __shared__ float nrm[2][4];
+  __shared__ __attribute__((aligned(16))) float Rh[LR_MAXR * LR_MAXR];
+  __shared__ float Sv[LR_MAXR];
   int l = 0;
   while (l + 1 < nl && (int)blockIdx.x >= Ls[l + 1].b3) ++l;
   const LrLayer& X = Ls[l];
   if (it > 0 && !*X.active) return;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = X.r, n = X.out;
+  LR_STAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, r = X.r, n = X.out;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform loops, no exec masks
   const int cb = blockIdx.x - X.b3;
   const int c = lane & 15, kr = lane >> 4;
+  const int col = 16 * cb + c;
+  const bool cv = col < X.in;
+  gfloat* gcol = (gfloat*)(X.G + (cv ? col : 16 * cb));
+  // the first two rounds of this wave's G^T P column loads: in flight from here on (double
+  // buffered below -- a load-then-MFMA loop exposed one HBM round trip per round)
+  constexpr int U = 16;
+  float g0[U], g1[U];
+  auto load = [&](float (&v)[U], int rb) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = rb + 16 * u + kr;
+      // clamped load, zeroed by a multiply: with a select hipcc sinks the load into an
+      // exec-mask branch (and the LDS reads below each into a serialised lgkmcnt(0) wait)
+      v[u] = gcol[(long)(row < n ? row : 0) * X.in] * ((row < n && cv) ? 1.f : 0.f);
+    }
+  };
+  const float cmask = c < r ? 1.f : 0.f;
+  auto mma = [&](const float (&v)[U], int rb, f32x4& acc) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = rb + 16 * u + kr;
+      // rows past n meet a zero A entry; columns past r give H columns the solve ignores
+      const float pv = ps[(row < n ? row : 0) * r + (c < r ? c : 0)] * cmask;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v[u], pv, acc, 0, 0, 0);
+    }
+  };
+  const int rb0 = 4 * w;
+  load(g0, rb0);
+  if (rb0 + 16 * U < n) load(g1, rb0 + 16 * U);
   if (((n * r) & 3) == 0) {
     const f32x4* src = reinterpret_cast<const f32x4*>(X.P);
 #pragma unroll 8
@@ -253,154 +395,149 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
     for (int i = tid; i < n * r; i += 256) ps[i] = X.P[i];
   }
   __syncthreads();
+  LR_STAMP(1);
   {  // Gram P^T P on the fp64 matrix cores (fp32 values, exact products): for 16x16x4 f64 lane l
      // holds A[l & 15][k = l >> 4] = P[row k][col l & 15] and B[k][l & 15] -- the same value
-     // (C: row (l >> 4) + 4 reg, col l & 15 -- the f64 map, not the f32 one);
-     // wave w takes every 4th block of 4 rows, the four partials meet in LDS in a fixed order
+     // (C: row (l >> 4) + 4 reg, col l & 15 -- the f64 map, not the f32 one).  Wave w takes
+     // every 4th block of 4 rows; the four wave partials are added in a fixed order.  The loop
+     // is uniform (scalar wave id and trip count) with unconditional clamped LDS reads: a
+     // divergent loop made hipcc shuttle the accumulators between AGPRs and VGPRs every
+     // iteration (19k cycles for 768 rows)
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    const int c = lane & 15, kr = lane >> 4;
-    for (int rb = 4 * w; rb < n; rb += 16) {
-      const int row = rb + kr;
-      const double v = (row < n && c < r) ? (double)ps[row * r + c] : 0.0;
+    const int iters = (n - 4 * w + 15) / 16;  // scalar trip count: a uniform loop
+    const int cc = c < r ? c : 0;
+    int it2 = 0;
+    for (; it2 + 4 <= iters; it2 += 4) {  // four rows' reads in flight per round
+      float x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 4 * w + 16 * (it2 + j) + kr;
+        x[j] = ps[(row < n ? row : 0) * r + cc];  // clamped, unconditional LDS reads
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 4 * w + 16 * (it2 + j) + kr;
+        const double v = (row < n && c < r) ? (double)x[j] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+      }
+    }
+    for (; it2 < iters; ++it2) {
+      const int row = 4 * w + 16 * it2 + kr;
+      const float x = ps[(row < n ? row : 0) * r + cc];
+      const double v = (row < n && c < r) ? (double)x : 0.0;
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) gpart[w * 256 + (kr + 4 * j) * 16 + c] = acc[j];  // f64 C map
   }
+  LR_STAMP(2);
+  {  // H = G[:, 16 cols]^T P, rounds of 16 chunks, two buffers in flight
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int rb = rb0; rb < n; rb += 32 * U) {
+      mma(g0, rb, acc);
+      if (rb + 32 * U < n) load(g0, rb + 32 * U);
+      if (rb + 16 * U >= n) break;
+      mma(g1, rb + 16 * U, acc);
+      if (rb + 48 * U < n) load(g1, rb + 48 * U);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][k][c]
+  }
   __syncthreads();
+  LR_STAMP(3);
   gm[tid] = (gpart[tid] + gpart[256 + tid]) + (gpart[512 + tid] + gpart[768 + tid]);
+  red[tid] = red[tid] + red[256 + tid] + red[512 + tid] + red[768 + tid];  // H[k][c], own entry
   __syncthreads();
+  LR_STAMP(4);
   if (w == 0) {
-    // wave 0: lane i < r holds row i of the Gram; right-looking Cholesky, upper R (R^T R = A),
-    // row k of R in lane k; then R^{-1} by back substitution, lane j = column j
-    double a[LR_MAXR];
+    // wave 0, lane i < r = row i.  Jacobi scaling in fp64: A_s = D^{-1/2} A D^{-1/2} has a unit
+    // diagonal (P's columns are ~sigma_i u_i: the scaling removes nearly all of cond(A)), so the
+    // Cholesky R_s^T R_s = A_s runs in fp32 on the hardware rsq / FMA units, and
+    // R^{-1} = D^{-1/2} R_s^{-1} is applied by substitution.  A column whose norm vanished
+    // (d_i <= 1e-13 max d) or that is numerically dependent (pivot <= 1e-6 after scaling) is
+    // dropped: its Pn and Q columns are zero.
+    const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
+    double dmax = di;
 #pragma unroll
-    for (int jj = 0; jj < LR_MAXR; ++jj) a[jj] = (lane < r && jj < r) ? gm[(lane & 15) * 16 + jj] : 0.0;
-    double dmax = 0.0;
+    for (int o = 1; o < 16; o <<= 1) dmax = fmax(dmax, shfl_d(dmax, lane ^ o));
+    const bool live = lane < r && di > fmax(1e-13 * dmax, 1e-280);
+    const double si = live ? 1.0 / sqrt(di) : 0.0;
+    float sv[LR_MAXR];  // s_j, uniform (read with v_readlane: no LDS round trip)
 #pragma unroll
-    for (int jj = 0; jj < LR_MAXR; ++jj) dmax = fmax(dmax, jj < r ? gm[jj * 17] : 0.0);
-    const double thr = fmax(1e-13 * dmax, 1e-280);
-    unsigned dead = 0;
+    for (int jj = 0; jj < LR_MAXR; ++jj) sv[jj] = rlane((float)si, jj);
+    float a[LR_MAXR];
+#pragma unroll
+    for (int jj = 0; jj < LR_MAXR; ++jj)
+      a[jj] = (lane < r && jj < r) ? (float)(gm[(lane & 15) * 16 + jj] * si) * sv[jj] : 0.f;
+    unsigned dead = ~(unsigned)__ballot(live) & ((1u << r) - 1u);
+    // right-looking Cholesky, straight line: lane i keeps row i of the (symmetric) trailing
+    // matrix, so R_s[k][i] = A[i][k] / sqrt(A[k][k]) is the lane's OWN a[k] -- no transposed
+    // access -- and row k reaches every lane through v_readlane (k is a compile-time index).
+    // Steps k >= r find a zero pivot and drop out, so there are no rank branches.  (Divergent
+    // `if (lane == k)` blocks and shuffles made this ~17k cycles.)
 #pragma unroll
     for (int k = 0; k < LR_MAXR; ++k) {
-      if (k < r) {
-        const double akk = shfl_d(a[k], k);
-        const bool dk = akk <= thr;  // vanished pivot: drop column k
-        const double inv = dk ? 0.0 : 1.0 / sqrt(akk);
-        if (dk) dead |= 1u << k;
-        if (lane == k) {
+      const float akk = rlane(a[k], k);
+      const bool dk = ((dead >> k) & 1u) || akk <= 1e-6f;
+      const float inv = dk ? 0.f : __builtin_amdgcn_rsqf(akk);
+      dead |= dk ? 1u << k : 0u;
+      const float rki = a[k] * inv;  // R_s[k][lane] for lane > k (symmetry)
+      if (lane < LR_MAXR) Rh[k * LR_MAXR + lane] = lane > k ? rki : (lane == k ? inv : 0.f);
+      const float sk = rki * inv;    // A[lane][k] / A[k][k]
 #pragma unroll
-          for (int jj = 0; jj < LR_MAXR; ++jj)
-            a[jj] = jj == k ? (dk ? 1.0 : akk * inv) : (jj > k ? a[jj] * inv : 0.0);
-          rdiag[k] = inv;
-        }
-        double rk[LR_MAXR];
-#pragma unroll
-        for (int jj = 0; jj < LR_MAXR; ++jj) rk[jj] = (jj > k && jj < r) ? shfl_d(a[jj], k) : 0.0;
-        double rki = 0.0;
-#pragma unroll
-        for (int jj = 0; jj < LR_MAXR; ++jj) rki = lane == jj ? rk[jj] : rki;
-        if (lane > k && lane < r) {
-#pragma unroll
-          for (int jj = 0; jj < LR_MAXR; ++jj)
-            if (jj > k) a[jj] -= rki * rk[jj];
-        }
-      }
+      for (int jj = k + 1; jj < LR_MAXR; ++jj)  // rows <= k are finished: garbage there is unread
+        a[jj] = __builtin_fmaf(-sk, rlane(a[jj], k), a[jj]);
     }
-    // R row-major through LDS (gm is free now: every lane has read its Gram row)
-    if (lane < r) {
-#pragma unroll
-      for (int jj = 0; jj < LR_MAXR; ++jj) gm[lane * LR_MAXR + jj] = a[jj];
-    }
-
+    if (lane < LR_MAXR) Sv[lane] = (float)si;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    double col[LR_MAXR];
+    LR_STAMP(5);
+    // Q rows: lane i < 16 takes column 16 cb + i of G: q = H[i][:] D^{-1/2} R_s^{-1}
+    const int k = 16 * cb + lane;
+    float dd = 0.f, qq = 0.f;
+    if (lane < 16) {
+      float x[LR_MAXR];
 #pragma unroll
-    for (int i = LR_MAXR - 1; i >= 0; --i) {
-      double v = 0.0;
-      if (i < r && i <= lane && lane < r) {
-        v = i == lane ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = i + 1; k < LR_MAXR; ++k)
-          if (k <= lane) v -= gm[i * LR_MAXR + k] * col[k];
-        v *= rdiag[i];  // 1 / R_ii (0 for a dropped column)
+      for (int q4 = 0; q4 < LR_MAXR / 4; ++q4) {
+        const f32x4 v = reinterpret_cast<const f32x4*>(red + lane * 16)[q4];
+        x[4 * q4] = v[0]; x[4 * q4 + 1] = v[1]; x[4 * q4 + 2] = v[2]; x[4 * q4 + 3] = v[3];
       }
-      col[i] = (dead >> lane & 1u) ? 0.0 : v;
-    }
-    if (lane < LR_MAXR) {
+      lr_solve_row(x, Rh, Sv);
+      if (k < X.in) {
+        float* qrow = X.Qsend + (long)k * r;
 #pragma unroll
-      for (int i = 0; i < LR_MAXR; ++i) Ri[i * LR_MAXR + lane] = lane < r ? (float)col[i] : 0.f;
+        for (int j = 0; j < LR_MAXR; ++j) {
+          if (j < r) {
+            const float old = qrow[j];
+            dd += (x[j] - old) * (x[j] - old);
+            qq += x[j] * x[j];
+            qrow[j] = x[j];
+          }
+        }
+      }
     }
+    dd = wave_sum(dd);
+    qq = wave_sum(qq);
+    LR_STAMP(6);
+    if (lane == 0) {
+      X.norms[2 * cb] = dd;
+      X.norms[2 * cb + 1] = qq;
+    }
+    LR_STAMP(7);
   }
-  __syncthreads();
-  // Pn = P R^{-1} in place, f32 MFMA: 16-row blocks, K = 16 in four 16x16x4 steps; lane l feeds
-  // A[l & 15][k = l >> 4] = P[row][4 s + k] and B[k][l & 15] = R^{-1}[4 s + k][l & 15]
-  for (int b0 = 16 * w; b0 < n; b0 += 64) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int row = b0 + c;
+  if (cb == 0) {  // Psend = P D^{-1/2} R_s^{-1}, one row per thread
+    __syncthreads();
+    for (int row = tid; row < n; row += 256) {
+      float x[LR_MAXR];
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int k = 4 * st + kr;
-      const float av = (row < n && k < r) ? ps[row * r + k] : 0.f;
-      const float bv = Ri[k * LR_MAXR + c];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-    }
-    // a block's 16 rows are read only by the wave that rewrites them
+      for (int j = 0; j < LR_MAXR; ++j) x[j] = j < r ? ps[row * r + j] : 0.f;
+      lr_solve_row(x, Rh, Sv);
+      float* prow = X.Psend + (long)row * r;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int orow = b0 + 4 * kr + j;
-      if (orow < n && c < r) ps[orow * r + c] = acc[j];
+      for (int j = 0; j < LR_MAXR; ++j)
+        if (j < r) prow[j] = x[j];
     }
-  }
-  __syncthreads();
-  if (cb == 0) {
-    if (((n * r) & 3) == 0) {
-      f32x4* dst = reinterpret_cast<f32x4*>(X.Psend);
-      for (int i = tid; i < n * r / 4; i += 256) dst[i] = reinterpret_cast<const f32x4*>(ps)[i];
-    } else {
-      for (int i = tid; i < n * r; i += 256) X.Psend[i] = ps[i];
-    }
-  }
-  const int col = 16 * cb + c;
-  const bool cv = col < X.in;
-  const float* gcol = X.G + (cv ? col : 16 * cb);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  constexpr int U = 16;  // as in lr_gq: a round's G loads all in flight before its MFMAs
-  for (int rb = 4 * w; rb < n; rb += 16 * U) {
-    float av[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int row = rb + 16 * u + kr;
-      av[u] = (row < n && cv) ? gcol[(long)row * X.in] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int row = rb + 16 * u + kr;
-      const float bv = (row < n && c < r) ? ps[row * r + c] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv, acc, 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) red[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][k][c]
-  __syncthreads();
-  const int i = tid >> 4, cc = tid & 15, e = i * 16 + cc, k = 16 * cb + i;
-  float dd = 0.f, qq = 0.f;
-  if (k < X.in && cc < r) {
-    const float v = red[e] + red[256 + e] + red[512 + e] + red[768 + e];
-    const float old = X.Qsend[(long)k * r + cc];
-    dd = (v - old) * (v - old);
-    qq = v * v;
-    X.Qsend[(long)k * r + cc] = v;
-  }
-  dd = wave_sum(dd);
-  qq = wave_sum(qq);
-  if (lane == 0) { nrm[0][w] = dd; nrm[1][w] = qq; }
-  __syncthreads();
-  if (tid == 0) {
-    X.norms[2 * cb] = nrm[0][0] + nrm[0][1] + nrm[0][2] + nrm[0][3];
-    X.norms[2 * cb + 1] = nrm[1][0] + nrm[1][1] + nrm[1][2] + nrm[1][3];
   }
 }
 
@@ -437,7 +574,7 @@ struct PiRecon {
 // replaced was latency-bound (17 us for the ICA layers).
 __global__ void __launch_bounds__(256)
 pi_reconstruct_kernel(const PiRecon* __restrict__ R, int n, long total, long stride, int W, float inv_w) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
   long ntiles = 0;
   for (int l = 0; l < n; ++l) ntiles += (long)((R[l].out + 15) / 16) * ((R[l].in + 15) / 16);
@@ -476,6 +613,11 @@ pi_reconstruct_kernel(const PiRecon* __restrict__ R, int n, long total, long str
 
 }  // namespace
 
+#ifdef LR_STAMPS
+DN_API int dn_lr_set_stamps(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(lr_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+#endif
 DN_API long dn_lr_layer_size() { return (long)sizeof(LrLayer); }
 DN_API long dn_pi_recon_size() { return (long)sizeof(PiRecon); }
 DN_API int dn_lr_limits(int* maxr, int* plds, int* qlds) {

@@ -19,8 +19,8 @@ def main():
 
     def one(src):
         obj = os.path.join(out, os.path.basename(src) + ".o")
-        B._run([B.HIPCC, *B.HIP_FLAGS, *flags, "-I", os.path.join(B.HERE, "kernels"), "-c", src,
-                "-o", obj])
+        B._run([B.HIPCC, *B.HIP_FLAGS, *B.FILE_FLAGS.get(os.path.basename(src), []), *flags,
+                "-I", os.path.join(B.HERE, "kernels"), "-c", src, "-o", obj])
         return obj
     with cf.ThreadPoolExecutor(4) as ex:
         objs = list(ex.map(one, B._sources("hip")))
