@@ -54,6 +54,13 @@ __device__ __forceinline__ typename Gate4Raw<XT>::type load_raw4(const XT* p, bo
   return z;
 }
 
+// 16-B weight fragment through a buffer descriptor: per-lane offset in one VGPR, the
+// fragment's constant part as the scalar offset -- no per-fragment 64-bit address held live
+// across the time loop (the streamed-weight variants re-read W every step)
+__device__ __forceinline__ bf16x8 load_wfrag(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
+}
+
 __device__ __forceinline__ void load_gate4(const float* p, bool ok, float (&v)[4]) {
   f32x4 x = load_raw4<float>(p, ok);
   v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
@@ -185,7 +192,10 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   // ds_read_b128 lane group land on 16 distinct bank quads (HD + 8 left rows 4 banks apart,
   // colliding with the k-quad offsets)
   constexpr int LDH = HD + 32;
-  constexpr int NLM = UG == 1 ? LdsSplit<HD, BR>::FWD_MT : 0, NRM = MT - NLM;
+  // HD > 192: W_hh (>= 512 KB per direction) exceeds the register file, so it is streamed from
+  // L2 every step (k-step ks+1's fragments requested before ks's MFMAs) instead of resident
+  constexpr bool STREAM = HD > 192;
+  constexpr int NLM = (UG == 1 && !STREAM) ? LdsSplit<HD, BR>::FWD_MT : 0, NRM = MT - NLM;
   constexpr int G16 = 16 / BR, NSL1 = BR / 4, NSL = UG * NSL1;
   __shared__ __attribute__((aligned(16))) bf16 hbuf[2][16][LDH];
   // hcnt[g] = h_t tiles published by producer group g (4 waves): 4 (t + 1) after step t
@@ -202,15 +212,18 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   const int bc = b < B ? b : B - 1;             // clamped row for loads
   const long rowX = (long)ndir * 4 * HD;
 
-  bf16x8 wf[NRM][KS];
-  {
-    const bf16* wd = whh + (long)dir * 4 * HD * HD;
+  // this direction's W_hh (streamed variant: re-read every step, L2-resident) and the lane's
+  // byte offset into it
+  const __amdgpu_buffer_rsrc_t w_rs = dn_rsrc(whh + (long)dir * 4 * HD * HD, (uint32_t)(4 * HD * HD * 2));
+  const uint32_t wvo = (uint32_t)(((16 * MT * w + n) * HD + 8 * q) * 2);
+  bf16x8 wf[STREAM ? 1 : NRM][STREAM ? 1 : KS];
+  if constexpr (!STREAM) {
+    const bf16* wlane = whh + (long)dir * 4 * HD * HD + (long)(16 * MT * w + n) * HD + 8 * q;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const int row = 16 * (MT * w + mt) + n;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(wd + (long)row * HD + 32 * ks + 8 * q);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(wlane + (long)16 * mt * HD + 32 * ks);
         if (mt < NRM) wf[mt < NRM ? mt : 0][ks] = v;
         else wlds[w][mt - NRM][ks][lane] = v;
       }
@@ -297,8 +310,28 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (STREAM) {
+      bf16x8 wa[MT], wb[MT];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+      for (int mt = 0; mt < MT; ++mt) wa[mt] = load_wfrag(w_rs, wvo, 16 * mt * HD * 2);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        // one k-step of loads in flight at a time: unbounded hoisting spills
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 (&wc)[MT] = (ks & 1) ? wb : wa;
+        bf16x8 (&wn)[MT] = (ks & 1) ? wa : wb;
+        if (ks + 1 < KS) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            wn[mt] = load_wfrag(w_rs, wvo, (16 * mt * HD + 32 * (ks + 1)) * 2);
+        }
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wc[mt], hb, acc[mt]);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < (STREAM ? 0 : KS); ++ks) {
       if constexpr (LSTM_FLAGS) {
         if (ks % (2 * UG) == 0) wait_count(&hcnt[ks / (2 * UG)], 4 * t);
       }
@@ -421,7 +454,8 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
                 bf16* __restrict__ dpre) {          // [Bp*S][ndir][4*HD] permuted, original time
   constexpr int KS = 4 * HD / 32;
   constexpr int LDD = 4 * HD + 32;  // 16 dwords mod 64 banks: see LDH in the forward
-  constexpr int NLK = UG == 1 ? LdsSplit<HD, BR>::BWD_KS : 0, NRK = KS - NLK;
+  constexpr bool STREAM = HD > 192;  // W_hh^T streamed from L2 every step (see the forward)
+  constexpr int NLK = (UG == 1 && !STREAM) ? LdsSplit<HD, BR>::BWD_KS : 0, NRK = KS - NLK;
   constexpr int NW = HD / (16 * UG);
   constexpr int NT = NW * 64;
   constexpr int G16 = 16 / BR, NSL1 = BR / 4, NSL = UG * NSL1;
@@ -437,15 +471,16 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   const int bc = vb ? b : B - 1;
   const long rowX = (long)ndir * 4 * HD;
 
-  bf16x8 af[UG][NRK];
-  {
-    const bf16* wt = whhT + (long)dir * HD * 4 * HD;
+  const __amdgpu_buffer_rsrc_t w_rs = dn_rsrc(whhT + (long)dir * HD * 4 * HD, (uint32_t)(4 * HD * HD * 2));
+  const uint32_t wvo = (uint32_t)(((16 * UG * w + n) * 4 * HD + 8 * q) * 2);
+  bf16x8 af[STREAM ? 1 : UG][STREAM ? 1 : NRK];
+  if constexpr (!STREAM) {
+    const bf16* wtl = whhT + (long)dir * HD * 4 * HD + (long)(16 * UG * w + n) * 4 * HD + 8 * q;
 #pragma unroll
     for (int g = 0; g < UG; ++g)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(
-            wt + (long)(16 * (UG * w + g) + n) * 4 * HD + 32 * ks + 8 * q);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(wtl + (long)16 * g * 4 * HD + 32 * ks);
         if (ks < NRK) af[g][ks < NRK ? ks : 0] = v;
         else wlds[w][ks - NRK][lane] = v;
       }
@@ -542,8 +577,27 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     for (int g = 0; g < UG; ++g)
 #pragma unroll
       for (int c = 0; c < NCH; ++c) accp[g][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (STREAM) {
+      bf16x8 wa[UG], wb[UG];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+      for (int g = 0; g < UG; ++g) wa[g] = load_wfrag(w_rs, wvo, 16 * g * 4 * HD * 2);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 (&wc)[UG] = (ks & 1) ? wb : wa;
+        bf16x8 (&wn)[UG] = (ks & 1) ? wa : wb;
+        if (ks + 1 < KS) {
+#pragma unroll
+          for (int g = 0; g < UG; ++g)
+            wn[g] = load_wfrag(w_rs, wvo, (16 * g * 4 * HD + 32 * (ks + 1)) * 2);
+        }
+        const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
+#pragma unroll
+        for (int g = 0; g < UG; ++g) accp[g][ks % NCH] = mfma16(wc[g], db, accp[g][ks % NCH]);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < (STREAM ? 0 : KS); ++ks) {
       // see the forward: padded columns read (broadcast) a valid row; never consumed
       const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
@@ -720,7 +774,11 @@ __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
 }
 
 // rows per workgroup: spread small batches over more CUs (the gate phase is VALU-bound per CU)
-static inline int pick_br(int B) {
+static inline int pick_br(int B, int HD) {
+  // streamed-weight variants (HD > 192): 4 rows per workgroup keeps them spill-free at every
+  // HD (8 / 16 rows spill above 256), and their step time is bound by the per-CU W stream,
+  // which more rows per workgroup would not shorten
+  if (HD > 192) return 4;
   if (const char* e = getenv("DN_LSTM_BR")) {
     const int v = atoi(e);
     if (v == 4 || v == 8 || v == 16) return v;
@@ -767,7 +825,10 @@ int launch_fwd_br(float* xp, const float* bias, const bf16* whh, int B, int S, i
       return launch_fwd_ug<HD, BR, 3>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
                                       mean_scale, hT, cT, store_pre, st);
   }
-  return launch_fwd_ug<HD, BR, 1>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
+  if constexpr (HD > 256)  // streamed weights: 2 unit groups per wave keep the block <= 16 waves
+    return launch_fwd_ug<HD, BR, 2>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
+                                    mean_scale, hT, cT, store_pre, st);
+  else return launch_fwd_ug<HD, BR, 1>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
                                   mean_scale, hT, cT, store_pre, st);
 }
 
@@ -776,8 +837,11 @@ int launch_fwd(int BR, float* xp, const float* bias, const bf16* whh, int B, int
                int ndir, float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale,
                float* hT, float* cT, int store_pre, hipStream_t st) {
   if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+  if constexpr (HD > 192) return DN_UNSUPPORTED;  // streamed variants: 4 rows only (pick_br)
+  else {
   if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
   return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+  }
 }
 
 template <int HD, int BR, int UG>
@@ -803,7 +867,10 @@ int launch_bwd_br(const float* pre, const float* c_save, const bf16* whhT, const
       return launch_bwd_ug<HD, BR, 3>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S,
                                       Hd, ndir, dpre, st);
   }
-  return launch_bwd_ug<HD, BR, 1>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd,
+  if constexpr (HD > 256)
+    return launch_bwd_ug<HD, BR, 2>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd,
+                                    ndir, dpre, st);
+  else return launch_bwd_ug<HD, BR, 1>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd,
                                   ndir, dpre, st);
 }
 
@@ -812,8 +879,11 @@ int launch_bwd(int BR, const float* pre, const float* c_save, const bf16* whhT, 
                long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
                int Hd, int ndir, bf16* dpre, hipStream_t st) {
   if (BR == 4) return launch_bwd_br<HD, 4>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
+  if constexpr (HD > 192) return DN_UNSUPPORTED;
+  else {
   if (BR == 8) return launch_bwd_br<HD, 8>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
   return launch_bwd_br<HD, 16>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
+  }
 }
 
 }  // namespace
@@ -824,6 +894,10 @@ DN_API int dn_lstm_padded_hidden(int Hd) {
   if (Hd <= 64) return 64;
   if (Hd <= 128) return 128;
   if (Hd <= 192) return 192;
+  // above 192 the recurrent weights no longer fit the register file: streamed variants
+  if (Hd <= 256) return 256;
+  if (Hd <= 384) return 384;
+  if (Hd <= 512) return 512;
   return 0;
 }
 
@@ -885,7 +959,13 @@ DN_API int dn_lstm_pack_prologue(const float* wih0, const float* bih0, const flo
 
 
 // rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
-DN_API int dn_lstm_rows_per_wg(int B) { return pick_br(B); }
+DN_API int dn_lstm_rows_per_wg(int B, int Hd) { return pick_br(B, dn_lstm_padded_hidden(Hd)); }
+
+// every per-step access of the recurrences is a 32-bit buffer offset
+static bool lstm_fits_32bit(int B, int S, int HD, int ndir, int BR) {
+  const long Bp = (B + BR - 1) / BR * (long)BR;
+  return (long)Bp * S * ndir * 4 * HD * 4 < (1L << 31);
+}
 
 // store_pre != 0: xp is overwritten in place by the gate pre-activations (+ bias) the
 // backward consumes
@@ -894,11 +974,15 @@ DN_API int dn_lstm_fwd(float* xp, const float* bias, const void* whh_p, int B, i
                        float mean_scale, float* hT, float* cT, int store_pre, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
-  const int BR = pick_br(B);
+  const int BR = pick_br(B, HD);
+  if (!lstm_fits_32bit(B, S, HD, ndir, BR)) return DN_BAD_SHAPE;
   switch (HD) {
     case 64: return launch_fwd<64>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
     case 128: return launch_fwd<128>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
     case 192: return launch_fwd<192>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+    case 256: return launch_fwd<256>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+    case 384: return launch_fwd<384>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+    case 512: return launch_fwd<512>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
   }
   return DN_UNSUPPORTED;
 }
@@ -909,11 +993,15 @@ DN_API int dn_lstm_bwd(const float* pre, const float* c_save, const void* whhT_p
                        void* dpre, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
-  const int BR = pick_br(B);
+  const int BR = pick_br(B, HD);
+  if (!lstm_fits_32bit(B, S, HD, ndir, BR)) return DN_BAD_SHAPE;
   switch (HD) {
     case 64: return launch_bwd<64>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
     case 128: return launch_bwd<128>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
     case 192: return launch_bwd<192>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 256: return launch_bwd<256>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 384: return launch_bwd<384>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 512: return launch_bwd<512>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
   }
   return DN_UNSUPPORTED;
 }

@@ -112,13 +112,13 @@ _SLOW_WARNED = False
 
 
 def _slow_lstm_gate(hidden: int, batch: int):
-    """A GPU LSTM the persistent kernels do not cover (per-direction hidden > 192: W_hh no longer
-    fits the register file of one CU) runs the reference's per-step loop of library ops, ~100x
-    slower.  That is never silent: it raises unless ``DINUNET_ALLOW_SLOW_LSTM=1`` opts in, and
+    """A GPU LSTM the persistent kernels do not cover (per-direction hidden > 512; up to 192
+    W_hh stays in the register file, up to 512 the kernels stream it from L2 every step) runs
+    the reference's per-step loop of library ops, ~100x slower.  That is never silent: it raises unless ``DINUNET_ALLOW_SLOW_LSTM=1`` opts in, and
     then warns once."""
     global _SLOW_WARNED
     msg = (f"LSTM hidden {hidden} (batch {batch}) is outside the fused gfx950 kernels "
-           f"(per-direction hidden <= 192); the step-by-step reference loop would run instead")
+           f"(per-direction hidden <= 512); the step-by-step reference loop would run instead")
     if os.environ.get("DINUNET_ALLOW_SLOW_LSTM", "0") != "1":
         raise NotImplementedError(msg + ": set DINUNET_ALLOW_SLOW_LSTM=1 to accept it")
     if not _SLOW_WARNED:

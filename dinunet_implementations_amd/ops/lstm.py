@@ -4,7 +4,7 @@ Per training step (both directions together):
 
 forward
   1. ``dn_lstm_pack``: fp32 reference-layout params -> bf16 kernel layouts (gate rows permuted to
-     ``m = 4u + g``, units zero-padded to HD in {64,128,192}), fused bias ``b_ih + b_hh``.
+     ``m = 4u + g``, units zero-padded to HD in {64,128,192,256,384,512}), fused bias ``b_ih + b_hh``.
   2. input projection of both directions as ONE GEMM ``[B*S, I] x [I, ndir*4*HD]`` (fp32 out).
   3. ``dn_lstm_fwd``: persistent recurrence (grid = batch-row chunks x directions), stores
      ``c_t`` and ``h_{t-1}`` per step and, when a backward will follow, the gate
@@ -52,7 +52,7 @@ _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.
                               _lib.c_long, _lib.c_long, _lib.c_float, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
                               _lib.c_void_p, _lib.c_void_p])
-_lib.register("dn_lstm_rows_per_wg", [_lib.c_int])
+_lib.register("dn_lstm_rows_per_wg", [_lib.c_int, _lib.c_int])
 
 _ROWMAP_CACHE: Dict[Tuple[int, int, str], Tensor] = {}
 
@@ -60,7 +60,8 @@ _ROWMAP_CACHE: Dict[Tuple[int, int, str], Tensor] = {}
 def padded_hidden(hd: int) -> int:
     if hd <= 0:
         return 0
-    for p in (64, 128, 192):
+    # <= 192: W_hh resident in registers; 256 / 384 / 512: streamed from L2 every step
+    for p in (64, 128, 192, 256, 384, 512):
         if hd <= p:
             return p
     return 0
@@ -105,7 +106,7 @@ class _BiLSTMFn(torch.autograd.Function):
         Hd = params[2].shape[1]
         HD = padded_hidden(Hd)
         GP = 4 * HD
-        BR = int(_lib.lib().dn_lstm_rows_per_wg(B))  # rows per workgroup the kernels use
+        BR = int(_lib.lib().dn_lstm_rows_per_wg(B, Hd))  # rows per workgroup the kernels use
         Bp = (B + BR - 1) // BR * BR
         dev = enc.device
         st = _lib.stream()

@@ -150,6 +150,10 @@ def _lstm_params(I, Hd, ndir, scale=0.1):
     (20, 17, 64, 174, 2, "mean"),
     (5, 9, 32, 64, 1, "seq"),
     (40, 12, 48, 100, 2, "seq"),
+    # per-direction hidden > 192: W_hh streamed from L2 (256 / 384 / 512 instantiations)
+    (16, 20, 64, 256, 2, "mean"),
+    (9, 13, 48, 300, 2, "seq"),
+    (6, 11, 32, 512, 1, "mean"),
 ])
 def test_lstm_fwd_bwd_matches_reference(B, S, I, Hd, ndir, mode):
     from dinunet_implementations_amd.ops import reference as ref
@@ -365,11 +369,11 @@ def test_gemm_grouped_matches_per_problem(splits):
 
 @pytest.mark.gpu
 def test_lstm_outside_fused_kernels_is_loud(monkeypatch):
-    """Per-direction hidden > 192 has no persistent kernel: the GPU refuses the ~100x slower
+    """Per-direction hidden > 512 has no persistent kernel: the GPU refuses the ~100x slower
     reference loop unless DINUNET_ALLOW_SLOW_LSTM=1 opts in (then it warns and runs)."""
     import warnings
     from dinunet_implementations_amd.models import ica as ica_mod
-    m = ica_mod.ICALstm(input_size=32, hidden_size=512, num_comps=4, window_size=5).cuda()
+    m = ica_mod.ICALstm(input_size=32, hidden_size=1200, num_comps=4, window_size=5).cuda()
     x = torch.randn(2, 6, 4, 5, device="cuda")
     monkeypatch.delenv("DINUNET_ALLOW_SLOW_LSTM", raising=False)
     with pytest.raises(NotImplementedError, match="DINUNET_ALLOW_SLOW_LSTM"):
@@ -380,3 +384,23 @@ def test_lstm_outside_fused_kernels_is_loud(monkeypatch):
         warnings.simplefilter("always")
         logits, _ = m(x)
     assert logits.shape == (2, 2) and any("outside the fused" in str(i.message) for i in w)
+
+
+@pytest.mark.gpu
+def test_ica_wide_hidden_runs_fused(monkeypatch):
+    """hidden_size 1024 (512 per direction, the widest streamed variant) trains through the
+    fused kernels (the slow-loop gate would raise otherwise) and matches the fp32 oracle model."""
+    from dinunet_implementations_amd.models import ica as ica_mod
+    monkeypatch.delenv("DINUNET_ALLOW_SLOW_LSTM", raising=False)
+    torch.manual_seed(0)
+    m = ica_mod.ICALstm(input_size=64, hidden_size=1024, num_comps=8, window_size=5).cuda().eval()
+    x = torch.randn(4, 7, 8, 5, device="cuda")
+    logits, _ = m(x)
+    for mod in m.modules():
+        if hasattr(mod, "use_fused"):
+            mod.use_fused = False
+    monkeypatch.setenv("DINUNET_ALLOW_SLOW_LSTM", "1")
+    with torch.no_grad():
+        ref_logits, _ = m(x)
+    assert logits.shape == (4, 2)
+    assert rel(logits, ref_logits) < 5e-2

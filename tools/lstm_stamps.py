@@ -43,7 +43,7 @@ def main():
     HD = padded_hidden(Hd)
     ndir = 2
     GP = 4 * HD
-    BR = int(_lib.lib().dn_lstm_rows_per_wg(B)); Bp = (B + BR - 1) // BR * BR
+    BR = int(_lib.lib().dn_lstm_rows_per_wg(B, Hd)); Bp = (B + BR - 1) // BR * BR
     torch.manual_seed(0)
     ps = []
     for _ in range(ndir):

@@ -25,13 +25,13 @@ def time_lib(path, B=32, S=98, I=256, H=384, reps=50):
     lib.dn_lstm_pack.argtypes = [V] * 8 + [I_] * 3 + [V] * 4 + [I_, V, V, V, V]
     lib.dn_lstm_fwd.argtypes = [V, V, V, I_, I_, I_, I_, V, V, V, V, F, V, V, I_, V]
     lib.dn_lstm_bwd.argtypes = [V, V, V, V, L, L, F, V, V, I_, I_, I_, I_, V, V]
-    lib.dn_lstm_rows_per_wg.argtypes = [I_]
+    lib.dn_lstm_rows_per_wg.argtypes = [I_, I_]
     lib.dn_lstm_padded_hidden.argtypes = [I_]
     dev = "cuda"
     Hd = H // 2
     HD = lib.dn_lstm_padded_hidden(Hd)
     ndir, GP = 2, 4 * HD
-    BR = lib.dn_lstm_rows_per_wg(B)
+    BR = lib.dn_lstm_rows_per_wg(B, Hd)
     Bp = (B + BR - 1) // BR * BR
     g = torch.Generator(device=dev).manual_seed(0)
     ps = []
