@@ -309,31 +309,42 @@ head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
     constexpr int R = 16;         // chunk loads per thread in flight
     const int nch = Mp * Kp / 4;  // 4-element chunks (Kp % 32 == 0: chunks never straddle rows)
     const bool vec = (K % 4) == 0 && (ldx % 4) == 0 && (((uintptr_t)x) & 15) == 0;
+    // chunk c -> (row m, element k) advanced incrementally (c grows by NT per unrolled slot): a
+    // runtime integer division per chunk made this loop VALU-issue bound (one wave per SIMD;
+    // 6.6 us at B=32, linear in B)
+    const int KC = Kp / 4, dm = NT / KC, dk = NT - (NT / KC) * KC;
+    int cm = tid / KC, ck = tid - (tid / KC) * KC;  // coordinates of chunk `base`
     for (int base = tid; base < nch; base += R * NT) {
       f32x4 v[R];
+      int ms[R], ks[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        ms[u] = cm;
+        ks[u] = 4 * ck;
+        ck += dk;
+        cm += dm;
+        if (ck >= KC) { ck -= KC; ++cm; }
+      }
       if (vec) {  // (uniform) all loads of the round first
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-          const int c = base + u * NT;
-          const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
-          const int idx = (c < nch && m < B && k < K) ? m * (int)ldx + k : 0;
+          const int m = ms[u], k = ks[u];
+          const int idx = (m < B && k < K) ? m * (int)ldx + k : 0;
           v[u] = *reinterpret_cast<const f32x4*>(x + idx);
         }
       } else {
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-          const int c = base + u * NT;
-          const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
+          const int m = ms[u], k = ks[u];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            v[u][e] = x[(c < nch && m < B && k + e < K) ? m * (int)ldx + k + e : 0];
+            v[u][e] = x[(m < B && k + e < K) ? m * (int)ldx + k + e : 0];
         }
       }
 #pragma unroll
       for (int u = 0; u < R; ++u) {
-        const int c = base + u * NT;
-        if (c >= nch) continue;  // (not break: keeps the loop unrolled and v[] in VGPRs)
-        const int m = (4 * c) / Kp, k = 4 * c - m * Kp;
+        const int m = ms[u], k = ks[u];
+        if (m >= Mp) continue;  // chunk past the image (not break: keeps v[] in VGPRs)
         bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
