@@ -399,13 +399,16 @@ head_fwd0_kernel(HArgs a, const float* __restrict__ x, long ldx,
 
 // ---------------------------------------------------------------------------------------------
 // fwd1: layers 1.. and the loss in one workgroup.
+// dzl_lds (fused fwd1+bwd1 only): d loss / d logits also parked in LDS for the backward chain.
+// Returns the dropout seed of this forward.
 template <int MT, bool VECW>
-__device__ __forceinline__ void fwd1_body(const HArgs& a, const long long* __restrict__ y,
-                                          float* __restrict__ out, float* __restrict__ loss,
-                                          long long* __restrict__ pred,
-                                          unsigned long long* __restrict__ rng,
-                                          char* __restrict__ ws,
-                                          unsigned long long* __restrict__ stamps, char* smem) {
+__device__ __forceinline__ uint64_t fwd1_body(const HArgs& a, const long long* __restrict__ y,
+                                              float* __restrict__ out, float* __restrict__ loss,
+                                              long long* __restrict__ pred,
+                                              unsigned long long* __restrict__ rng,
+                                              char* __restrict__ ws,
+                                              unsigned long long* __restrict__ stamps, char* smem,
+                                              float* dzl_lds = nullptr) {
   constexpr int Mp = 16 * MT, NT = HS_NT, NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int B = a.B;
@@ -504,7 +507,9 @@ __device__ __forceinline__ void fwd1_body(const HArgs& a, const long long* __res
         const float lp = logit[m * 16 + c] - lse;
         const float p = expf(lp);
         out[(long)m * C + c] = a.log_out ? lp : p;
-        if (train) dzl[m * 16 + c] = (p - (c == yc ? 1.f : 0.f)) / (float)B;
+        const float dl = (p - (c == yc ? 1.f : 0.f)) / (float)B;
+        if (train) dzl[m * 16 + c] = dl;
+        if (dzl_lds) dzl_lds[m * 16 + c] = dl;
       }
       ls = lse - logit[m * 16 + yc];
       pred[m] = am;
@@ -516,12 +521,16 @@ __device__ __forceinline__ void fwd1_body(const HArgs& a, const long long* __res
       if (train) {
         *reinterpret_cast<unsigned long long*>(ws) = seed;
         if (rng) *rng = seed + 1ull;
+        // no-return atomic: a read-modify-write here was one more global round trip
         for (int l = 0; l < a.nl; ++l)
-          if (a.L[l].bn == 2 && a.L[l].nbt) *a.L[l].nbt += 1;
+          if (a.L[l].bn == 2 && a.L[l].nbt)
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.L[l].nbt), 1ull,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     HSTAMP(12);
   }
+  return seed;
 }
 
 template <int MT, bool VECW>
@@ -538,11 +547,19 @@ head_fwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ o
 // bwd1: output-gradient chain down to dZ_0 (+ bias / BatchNorm parameter gradients).
 // stash = 1 (fused forward): the bias / BatchNorm gradients go to the workspace stash (not
 // accumulated: bwd0 adds them into .grad once the backward is known to use this d loss)
+// pre (fused fwd1+bwd1): d out / d loss, the forward's dropout seed and d loss / d logits in
+// LDS come from the forward half instead of global round trips
+struct Bwd1Pre {
+  float gs;
+  uint64_t seed;
+  const float* dzl_lds;
+};
+
 template <int MT>
 __device__ __forceinline__ void bwd1_body(const HArgs& a, char* __restrict__ ws,
                                           const float* __restrict__ dloss,
                                           unsigned long long* __restrict__ stamps, char* smem,
-                                          int stash) {
+                                          int stash, const Bwd1Pre* pre = nullptr) {
   constexpr int Mp = 16 * MT, NT = HS_NT, NW = NT / 64;
   constexpr int CB = 2;  // weight-column k-steps per load batch (x2 register sets: see pipe)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -550,9 +567,9 @@ __device__ __forceinline__ void bwd1_body(const HArgs& a, char* __restrict__ ws,
   bf16* dz = reinterpret_cast<bf16*>(smem);
   bf16* dzn = dz + a.buf_z;
   bf16* abuf = dzn + a.buf_z;
-  const float gs = *dloss;
-  const uint64_t seed = *reinterpret_cast<const unsigned long long*>(ws);
-  const float* dzl = reinterpret_cast<const float*>(ws + a.dzl_off);
+  const float gs = pre ? pre->gs : *dloss;
+  const uint64_t seed = pre ? pre->seed : *reinterpret_cast<const unsigned long long*>(ws);
+  const float* dzl = pre ? pre->dzl_lds : reinterpret_cast<const float*>(ws + a.dzl_off);
   HSTAMP(16);
   {  // gradient of the logits
     const HLayer& L = a.L[a.nl - 1];
@@ -747,12 +764,16 @@ __global__ void __launch_bounds__(HS_NT)
 head_fwd1_bwd1_kernel(HArgs a, const long long* __restrict__ y, float* __restrict__ out,
                       float* __restrict__ loss, long long* __restrict__ pred,
                       unsigned long long* __restrict__ rng, char* __restrict__ ws,
-                      const float* __restrict__ dloss, unsigned long long* __restrict__ stamps) {
+                      const float* __restrict__ dloss, unsigned long long* __restrict__ stamps,
+                      int dzl_lds_off) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  fwd1_body<MT, VECW>(a, y, out, loss, pred, rng, ws, stamps, smem);
+  const float gs = *dloss;  // requested now: used after the whole forward half
+  float* dzl_lds = reinterpret_cast<float*>(smem + dzl_lds_off);  // clear of both halves' LDS
+  const uint64_t seed = fwd1_body<MT, VECW>(a, y, out, loss, pred, rng, ws, stamps, smem, dzl_lds);
   __threadfence_block();
   __syncthreads();
-  bwd1_body<MT>(a, ws, dloss, stamps, smem, 1);
+  const Bwd1Pre pre{gs, seed, dzl_lds};
+  bwd1_body<MT>(a, ws, dloss, stamps, smem, 1, &pre);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -898,6 +919,7 @@ struct Plan {
   int Mp;
   int grid_fwd0, grid_bwd0_dw, grid_bwd0_dx;
   long lds_fwd0, lds_fwd1, lds_bwd1, lds_bwd0;
+  long lds_fused_base, lds_fused;  // fused fwd1+bwd1: both halves, then d loss / d logits
 };
 
 static long al256(long v) { return (v + 255) & ~255L; }
@@ -980,8 +1002,11 @@ static bool make_plan(int nl, const int* dims, const int* flags, const float* dr
   p.lds_bwd1 = 2L * (2 * a.buf_z + a.buf_a1);
   const long dwl = 2L * (a.buf_aall + Mp * 24);
   p.lds_bwd0 = dwl > red ? dwl : red;
+  p.lds_fused_base = ((p.lds_fwd1 > p.lds_bwd1 ? p.lds_fwd1 : p.lds_bwd1) + 15) & ~15L;
+  p.lds_fused = p.lds_fused_base + 4L * Mp * 16;
   const long lim = 160 * 1024;
-  return p.lds_fwd0 <= lim && p.lds_fwd1 <= lim && p.lds_bwd1 <= lim && p.lds_bwd0 <= lim;
+  return p.lds_fwd0 <= lim && p.lds_fwd1 <= lim && p.lds_bwd1 <= lim && p.lds_bwd0 <= lim &&
+         p.lds_fused <= lim;
 }
 
 template <typename K>
@@ -1020,9 +1045,9 @@ static void launch_fwd_t(const Plan& p, const float* x, long ldx, const long lon
   // (no fused variant for 64-row batches: the bwd1 phase spills at MT = 4)
   if constexpr (MT == 2) {
     if (dloss) {
-      const long lds = p.lds_fwd1 > p.lds_bwd1 ? p.lds_fwd1 : p.lds_bwd1;
-      hipLaunchKernelGGL((head_fwd1_bwd1_kernel<MT, V1>), dim3(1), dim3(HS_NT), lds, st, p.a, y,
-                         out, loss, pred, rng, (char*)ws, dloss, g_head_stamps);
+      hipLaunchKernelGGL((head_fwd1_bwd1_kernel<MT, V1>), dim3(1), dim3(HS_NT), p.lds_fused, st,
+                         p.a, y, out, loss, pred, rng, (char*)ws, dloss, g_head_stamps,
+                         (int)p.lds_fused_base);
       return;
     }
   }
