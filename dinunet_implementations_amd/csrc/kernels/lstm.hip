@@ -217,6 +217,19 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   const __amdgpu_buffer_rsrc_t w_rs = dn_rsrc(whh + (long)dir * 4 * HD * HD, (uint32_t)(4 * HD * HD * 2));
   const uint32_t wvo = (uint32_t)(((16 * MT * w + n) * HD + 8 * q) * 2);
   bf16x8 wf[STREAM ? 1 : NRM][STREAM ? 1 : KS];
+  // streamed variant: a ring of RS k-steps of fragments, PD = RS - 1 k-steps requested ahead of
+  // the MFMAs and continuing across time steps (W does not change), so the next step's first
+  // fragments fly during this step's gate math and hand-off.  RS divides KS, so a k-step's slot
+  // is the same every time step.
+  constexpr int RS = !STREAM ? 1 : (HD == 256 ? 4 : (HD == 384 ? 3 : 2));
+  static_assert(KS % RS == 0, "weight ring");
+  bf16x8 wring[RS][MT];
+  if constexpr (STREAM) {
+#pragma unroll
+    for (int ks = 0; ks + 1 < RS; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) wring[ks][mt] = load_wfrag(w_rs, wvo, (16 * mt * HD + 32 * ks) * 2);
+  }
   if constexpr (!STREAM) {
     const bf16* wlane = whh + (long)dir * 4 * HD * HD + (long)(16 * MT * w + n) * HD + 8 * q;
 #pragma unroll
@@ -311,23 +324,18 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (STREAM) {
-      bf16x8 wa[MT], wb[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) wa[mt] = load_wfrag(w_rs, wvo, 16 * mt * HD * 2);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        // one k-step of loads in flight at a time: unbounded hoisting spills
+        // bounded look-ahead: unbounded hoisting of the loads spills
         __builtin_amdgcn_sched_barrier(0);
-        bf16x8 (&wc)[MT] = (ks & 1) ? wb : wa;
-        bf16x8 (&wn)[MT] = (ks & 1) ? wa : wb;
-        if (ks + 1 < KS) {
+        constexpr int PD = RS - 1;
+        const int kl = (ks + PD) % KS;  // past the last k-step: the next time step's
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            wn[mt] = load_wfrag(w_rs, wvo, (16 * mt * HD + 32 * (ks + 1)) * 2);
-        }
+        for (int mt = 0; mt < MT; ++mt)
+          wring[(ks + PD) % RS][mt] = load_wfrag(w_rs, wvo, (16 * mt * HD + 32 * kl) * 2);
         const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wc[mt], hb, acc[mt]);
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wring[ks % RS][mt], hb, acc[mt]);
       }
     }
 #pragma unroll
@@ -474,6 +482,15 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   const __amdgpu_buffer_rsrc_t w_rs = dn_rsrc(whhT + (long)dir * HD * 4 * HD, (uint32_t)(4 * HD * HD * 2));
   const uint32_t wvo = (uint32_t)(((16 * UG * w + n) * 4 * HD + 8 * q) * 2);
   bf16x8 af[STREAM ? 1 : UG][STREAM ? 1 : NRK];
+  constexpr int RS = !STREAM ? 1 : (UG == 1 ? 8 : (HD == 512 ? 2 : 4));  // weight ring (see the forward)
+  static_assert(KS % RS == 0, "weight ring");
+  bf16x8 wring[RS][UG];
+  if constexpr (STREAM) {
+#pragma unroll
+    for (int ks = 0; ks + 1 < RS; ++ks)
+#pragma unroll
+      for (int g = 0; g < UG; ++g) wring[ks][g] = load_wfrag(w_rs, wvo, (16 * g * 4 * HD + 32 * ks) * 2);
+  }
   if constexpr (!STREAM) {
     const bf16* wtl = whhT + (long)dir * HD * 4 * HD + (long)(16 * UG * w + n) * 4 * HD + 8 * q;
 #pragma unroll
@@ -578,22 +595,17 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
 #pragma unroll
       for (int c = 0; c < NCH; ++c) accp[g][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (STREAM) {
-      bf16x8 wa[UG], wb[UG];
-#pragma unroll
-      for (int g = 0; g < UG; ++g) wa[g] = load_wfrag(w_rs, wvo, 16 * g * 4 * HD * 2);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         __builtin_amdgcn_sched_barrier(0);
-        bf16x8 (&wc)[UG] = (ks & 1) ? wb : wa;
-        bf16x8 (&wn)[UG] = (ks & 1) ? wa : wb;
-        if (ks + 1 < KS) {
+        constexpr int PD = RS - 1;
+        const int kl = (ks + PD) % KS;
 #pragma unroll
-          for (int g = 0; g < UG; ++g)
-            wn[g] = load_wfrag(w_rs, wvo, (16 * g * 4 * HD + 32 * (ks + 1)) * 2);
-        }
+        for (int g = 0; g < UG; ++g)
+          wring[(ks + PD) % RS][g] = load_wfrag(w_rs, wvo, (16 * g * 4 * HD + 32 * kl) * 2);
         const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
-        for (int g = 0; g < UG; ++g) accp[g][ks % NCH] = mfma16(wc[g], db, accp[g][ks % NCH]);
+        for (int g = 0; g < UG; ++g) accp[g][ks % NCH] = mfma16(wring[ks % RS][g], db, accp[g][ks % NCH]);
       }
     }
 #pragma unroll
