@@ -215,20 +215,21 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   // this direction's W_hh (streamed variant: re-read every step, L2-resident) and the lane's
   // byte offset into it
   const __amdgpu_buffer_rsrc_t w_rs = dn_rsrc(whh + (long)dir * 4 * HD * HD, (uint32_t)(4 * HD * HD * 2));
-  const uint32_t wvo = (uint32_t)(((16 * MT * w + n) * HD + 8 * q) * 2);
+  // fragment-linear image (lstm_pack_kernel): this wave's tiles start at tile MT*w, lane-linear
+  const uint32_t wvo = (uint32_t)((MT * w * KS * 64 + lane) * 16);
   bf16x8 wf[STREAM ? 1 : NRM][STREAM ? 1 : KS];
   // streamed variant: a ring of RS k-steps of fragments, PD = RS - 1 k-steps requested ahead of
   // the MFMAs and continuing across time steps (W does not change), so the next step's first
   // fragments fly during this step's gate math and hand-off.  RS divides KS, so a k-step's slot
   // is the same every time step.
-  constexpr int RS = !STREAM ? 1 : (HD == 256 ? 4 : (HD == 384 ? 3 : 2));
+  constexpr int RS = !STREAM ? 1 : (HD == 256 ? 4 : 2);  // 3 at HD = 384 spills (SEQ)
   static_assert(KS % RS == 0, "weight ring");
   bf16x8 wring[RS][MT];
   if constexpr (STREAM) {
 #pragma unroll
     for (int ks = 0; ks + 1 < RS; ++ks)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) wring[ks][mt] = load_wfrag(w_rs, wvo, (16 * mt * HD + 32 * ks) * 2);
+      for (int mt = 0; mt < MT; ++mt) wring[ks][mt] = load_wfrag(w_rs, wvo, (mt * KS + ks) * 1024);
   }
   if constexpr (!STREAM) {
     const bf16* wlane = whh + (long)dir * 4 * HD * HD + (long)(16 * MT * w + n) * HD + 8 * q;
@@ -332,7 +333,7 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
         const int kl = (ks + PD) % KS;  // past the last k-step: the next time step's
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-          wring[(ks + PD) % RS][mt] = load_wfrag(w_rs, wvo, (16 * mt * HD + 32 * kl) * 2);
+          wring[(ks + PD) % RS][mt] = load_wfrag(w_rs, wvo, (mt * KS + kl) * 1024);
         const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wring[ks % RS][mt], hb, acc[mt]);
@@ -480,7 +481,7 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   const long rowX = (long)ndir * 4 * HD;
 
   const __amdgpu_buffer_rsrc_t w_rs = dn_rsrc(whhT + (long)dir * HD * 4 * HD, (uint32_t)(4 * HD * HD * 2));
-  const uint32_t wvo = (uint32_t)(((16 * UG * w + n) * 4 * HD + 8 * q) * 2);
+  const uint32_t wvo = (uint32_t)((UG * w * KS * 64 + lane) * 16);  // fragment-linear
   bf16x8 af[STREAM ? 1 : UG][STREAM ? 1 : NRK];
   constexpr int RS = !STREAM ? 1 : (UG == 1 ? 8 : (HD == 512 ? 2 : 4));  // weight ring (see the forward)
   static_assert(KS % RS == 0, "weight ring");
@@ -489,7 +490,7 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
 #pragma unroll
     for (int ks = 0; ks + 1 < RS; ++ks)
 #pragma unroll
-      for (int g = 0; g < UG; ++g) wring[ks][g] = load_wfrag(w_rs, wvo, (16 * g * 4 * HD + 32 * ks) * 2);
+      for (int g = 0; g < UG; ++g) wring[ks][g] = load_wfrag(w_rs, wvo, (g * KS + ks) * 1024);
   }
   if constexpr (!STREAM) {
     const bf16* wtl = whhT + (long)dir * HD * 4 * HD + (long)(16 * UG * w + n) * 4 * HD + 8 * q;
@@ -602,7 +603,7 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
         const int kl = (ks + PD) % KS;
 #pragma unroll
         for (int g = 0; g < UG; ++g)
-          wring[(ks + PD) % RS][g] = load_wfrag(w_rs, wvo, (16 * g * 4 * HD + 32 * kl) * 2);
+          wring[(ks + PD) % RS][g] = load_wfrag(w_rs, wvo, (g * KS + kl) * 1024);
         const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
         for (int g = 0; g < UG; ++g) accp[g][ks % NCH] = mfma16(wring[ks % RS][g], db, accp[g][ks % NCH]);
@@ -719,6 +720,17 @@ struct StepPrologue {
   int* bump;  // Adam's device step counter (graph-captured update), advanced once; null: none
 };
 
+// Fragment-linear image of a row-major [rows][KS*32] bf16 matrix (the streamed-weight kernels,
+// HD > 192): element f sits at ((T*KS + ks)*64 + lane)*8 + e for MFMA A-fragment lane
+// (q = lane/16, n = lane%16) of 16-row tile T and k-step ks, i.e. row 16T + n, column
+// 32ks + 8q + e -- every wave-wide 16-B fragment load reads 1 KiB contiguous.
+__device__ __forceinline__ void frag_rc(int f, int KS, int& row, int& col) {
+  const int e = f & 7, lane = (f >> 3) & 63, rest = f >> 9;
+  const int ks = rest % KS, T = rest / KS;
+  row = 16 * T + (lane & 15);
+  col = 32 * ks + 8 * (lane >> 4) + e;
+}
+
 __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
                                  bf16* __restrict__ wih_p,    // [ndir*4HD][I]
                                  float* __restrict__ bias_p,  // [ndir*4HD]
@@ -772,14 +784,32 @@ __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
       }
       bias_p[r] = v;
     } else if (idx < n_wih + n_b + n_whh) {
-      const int r = idx - n_wih - n_b;  // [d][m][k]
-      const int dm = r / HD, k = r - dm * HD;
-      const int d = dm / GP, m = dm - d * GP, u = m >> 2, g = m & 3;
+      const int r = idx - n_wih - n_b;  // [d][m][k], or fragment-linear (see frag_rc)
+      int d, m, k;
+      if (HD > 192) {
+        d = r / (GP * HD);
+        frag_rc(r - d * GP * HD, HD / 32, m, k);
+      } else {
+        const int dm = r / HD;
+        k = r - dm * HD;
+        d = dm / GP;
+        m = dm - d * GP;
+      }
+      const int u = m >> 2, g = m & 3;
       whh_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][(g * Hd + u) * Hd + k] : 0.f);
     } else {
-      const int r = idx - n_wih - n_b - n_whh;  // [d][k][m]
-      const int dk = r / GP, m = r - dk * GP;
-      const int d = dk / HD, k = dk - d * HD, u = m >> 2, g = m & 3;
+      const int r = idx - n_wih - n_b - n_whh;  // [d][k][m], or fragment-linear
+      int d, m, k;
+      if (HD > 192) {
+        d = r / (GP * HD);
+        frag_rc(r - d * GP * HD, GP / 32, k, m);
+      } else {
+        const int dk = r / GP;
+        m = r - dk * GP;
+        d = dk / HD;
+        k = dk - d * HD;
+      }
+      const int u = m >> 2, g = m & 3;
       whhT_p[r] = (bf16)((u < Hd && k < Hd) ? p.whh[d][(g * Hd + u) * Hd + k] : 0.f);
     }
   }
