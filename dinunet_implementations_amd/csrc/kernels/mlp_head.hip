@@ -647,6 +647,7 @@ __device__ __forceinline__ void bwd1_body(const HArgs& a, char* __restrict__ ws,
     if (wid < ntl) prefetch(wid);
     ws_to_lds<NT>(abuf, ws + L.a_off, Mp * Sa, tid);  // relu mask of the layer below
     __syncthreads();
+    HSTAMP(26 + (a.nl - 1 - l));  // operands in (diagnostic stamps)
     for (int t = wid; t < ntl; t += NW) {
       if (t != wid) {
         if (pipe) {

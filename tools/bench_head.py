@@ -91,6 +91,22 @@ def stamps(spec, x, y, log_out):
         print(f"   {tag}: " + " ".join(f"{i}:{(v[i] - t0) / 100:.1f}" for i in idx) + " us")
     show("fwd (0-2 fwd0, 3-12 fwd1)", b[:16])
     show("bwd (16-21 bwd1, 24 bwd0 start)", b[16:32])
+    # the training step's path: fwd1 + bwd1 fused in one launch (d loss known at forward time)
+    from dinunet_implementations_amd.ops.head import loss_grad_hint
+    buf.zero_()
+    L.dn_head_set_stamps(buf.data_ptr())
+    xf = x.detach().clone().requires_grad_()
+    one = torch.ones((), device=x.device)
+    with loss_grad_hint(one):
+        _, loss, _ = head_loss(xf, spec, y, log_out=log_out)
+    torch.autograd.backward(loss, one)
+    torch.cuda.synchronize()
+    L.dn_head_set_stamps(None)
+    b = buf.cpu().tolist()
+    t0 = b[0]
+    idx = [i for i, t in enumerate(b) if t]
+    print("   fused (0-2 fwd0, 3-12 fwd1, 16-21 bwd1, 24 bwd0): "
+          + " ".join(f"{i}:{(b[i] - t0) / 100:.1f}" for i in idx) + " us")
 
 
 def kernel_us(spec, x, y, log_out, n=20):
