@@ -119,6 +119,10 @@ __device__ __forceinline__ void wait_count(int* ctr, int need) {
 #ifndef BWD_CHAINS
 #define BWD_CHAINS 2
 #endif
+// k-steps per group of exchange-tile reads in the backward's resident-weight K loop
+#ifndef BWD_RG
+#define BWD_RG 4
+#endif
 // LSTM_FLAGS: forward step hand-off through LDS counters (1) or a workgroup barrier (0);
 // LSTM_PRIO: wave priority raised over the gate phase (the step's critical path) when > 0
 #ifndef LSTM_FLAGS
@@ -339,6 +343,17 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
         for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wring[ks % RS][mt], hb, acc[mt]);
       }
     }
+    // every k-step's h fragment requested up front (4-row layout, resident weights, barrier
+    // hand-off): hipcc otherwise issued them two at a time right before their MFMAs and exposed
+    // the LDS latency three times per step
+    constexpr bool HB_ALL = !STREAM && !LSTM_FLAGS && BR == 4 && UG == 1 && NLM == 0;
+    bf16x8 hball[HB_ALL ? KS : 1];
+    if constexpr (HB_ALL) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        hball[ks] = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int ks = 0; ks < (STREAM ? 0 : KS); ++ks) {
       if constexpr (LSTM_FLAGS) {
@@ -346,7 +361,8 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
       }
       // unmasked (exec-masking made the compiler branch and drain lgkmcnt before every MFMA):
       // lanes of padded columns re-read a valid row, see above
-      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
+      const bf16x8 hb = HB_ALL ? hball[HB_ALL ? ks : 0]
+                               : *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
       for (int mt = 0; mt < NRM; ++mt) acc[mt] = mfma16(wf[mt][ks], hb, acc[mt]);
 #pragma unroll
@@ -609,15 +625,52 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
         for (int g = 0; g < UG; ++g) accp[g][ks % NCH] = mfma16(wring[ks % RS][g], db, accp[g][ks % NCH]);
       }
     }
+    // Resident weights: the exchange-tile (and LDS-resident weight) reads go in groups of RG
+    // k-steps, group g+1 requested before group g's MFMAs (scheduling barriers pin the order).
+    // Left to itself hipcc kept ONE read in flight -- ds_read, wait, MFMA for each of the 24
+    // k-steps -- so the LDS latency, not the MFMA pipe, paced the step.
+    // (4-row layout only: at 8 / 16 rows per workgroup the second register set spills; the
+    // per-step output-gradient variant takes groups of 2 for the same reason)
+    constexpr int RG = BR != 4 ? 1 : (DSEQ ? 2 : BWD_RG);
+    if constexpr (!STREAM && RG == 1) {
 #pragma unroll
-    for (int ks = 0; ks < (STREAM ? 0 : KS); ++ks) {
-      // see the forward: padded columns read (broadcast) a valid row; never consumed
-      const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
+      for (int ks = 0; ks < KS; ++ks) {
+        // see the forward: padded columns read (broadcast) a valid row; never consumed
+        const bf16x8 db = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
-      for (int g = 0; g < UG; ++g)
-        accp[g][ks % NCH] = mfma16(
-            ks < NRK ? af[g][ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db,
-            accp[g][ks % NCH]);
+        for (int g = 0; g < UG; ++g)
+          accp[g][ks % NCH] = mfma16(
+              ks < NRK ? af[g][ks < NRK ? ks : 0] : wlds[w][ks < NRK ? 0 : ks - NRK][lane], db,
+              accp[g][ks % NCH]);
+      }
+    }
+    if constexpr (!STREAM && RG > 1) {
+      static_assert(KS % RG == 0, "read groups");
+      bf16x8 dg[2][RG], wg[2][RG];
+      auto issue = [&](int k0, bf16x8 (&d)[RG], bf16x8 (&wv)[RG]) {
+#pragma unroll
+        for (int j = 0; j < RG; ++j) {
+          // see the forward: padded columns read (broadcast) a valid row; never consumed
+          d[j] = *reinterpret_cast<const bf16x8*>(&dbuf[cur][n % BR][32 * (k0 + j) + 8 * q]);
+          if (k0 + j >= NRK) wv[j] = wlds[w][k0 + j >= NRK ? k0 + j - NRK : 0][lane];
+        }
+      };
+      issue(0, dg[0], wg[0]);
+#pragma unroll
+      for (int k0 = 0; k0 < KS; k0 += RG) {
+        const int cb = (k0 / RG) & 1;
+        if (k0 + RG < KS) issue(k0 + RG, dg[cb ^ 1], wg[cb ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < RG; ++j) {
+          const int ks = k0 + j;
+#pragma unroll
+          for (int g = 0; g < UG; ++g)
+            accp[g][ks % NCH] = mfma16(ks < NRK ? af[g][ks < NRK ? ks : 0] : wg[cb][j], dg[cb][j],
+                                       accp[g][ks % NCH]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
 #pragma unroll
     for (int g = 0; g < UG; ++g) {
