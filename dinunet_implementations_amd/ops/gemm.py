@@ -68,16 +68,20 @@ def choose_tiling(M: int, N: int, K: int):
     return 0, _split_rule(t64, K)
 
 
-def _split_rule(t64: int, K: int) -> int:
+_LONG_K = 16384
+
+
+def _split_rule(t64: int, K: int, per_cu: int = 8) -> int:
     """Split-K count for ``t64`` 64x64 tiles of depth K.  A tile's K loop is latency-bound (one
     workgroup keeps ~32 KB in flight), so long-K problems cut K until ~3 workgroups share each
     CU; medium K only splits when few tiles exist (a second ~5 us reduce launch otherwise eats
     the gain).  Measured on MI355X (bench.py, merged ICA weight-gradient launch: 284 tiles of
     K = 3136): 1 split 0.4156 ms/step, 2: 0.4045, 3: 0.4010, 4: 0.4024."""
-    if K >= 16384:
+    if K >= _LONG_K:
         # very long K (large-batch weight gradients, K = B*S): ~8 workgroups per CU, each still
-        # >= 2048 deep (B = 2048 ICA step, grouped dW: 3 splits 1556 us, see profiles/r2_*)
-        return max(1, min(32, -(-8 * _NCU // max(t64, 1)), K // 2048))
+        # >= 2048 deep (B = 2048 ICA step, grouped dW: 3 splits 1556 us, see profiles/r2_*);
+        # `t64` counts the launch's tiles of whatever size it uses
+        return max(1, min(32, -(-per_cu * _NCU // max(t64, 1)), K // 2048))
     if K >= 2048:
         return max(1, min(8, round(3 * _NCU / max(t64, 1)), K // 512))
     if K >= 768 and t64 < _NCU // 2:
@@ -184,7 +188,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
     ta = tb = None
     a_bf = b_bf = c_bf = None
     maxk = 0
-    t64 = 0
+    t64 = t128 = 0
     for q in probs:
         A = q["a"].t() if trans_a else q["a"]
         B = q["b"].t() if trans_b else q["b"]
@@ -216,12 +220,18 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
             arrs[k].append(v)
         maxk = max(maxk, K)
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
+        t128 += ((M + 127) // 128) * ((N + 127) // 128)
     if splits is None and _GROUP_SPLITS:
         splits = _GROUP_SPLITS
     if tile is None and _GROUP_TILE >= 0:
         tile = _GROUP_TILE
+    if tile is None and maxk >= _LONG_K:
+        # very long K (large-batch weight gradients, K = B*S): 128x128 tiles double the MFMA
+        # work per staged byte.  B = 2048 ICA step on MI355X (tools/_gpu_group_ab.sh): 64x64
+        # 3.88 ms/step, 128x128 3.45 ms at ~8 workgroups per CU (24 splits)
+        tile = 1
     if splits is None:
-        splits = _split_rule(t64, maxk)
+        splits = _split_rule(t128, maxk, per_cu=8) if tile == 1 else _split_rule(t64, maxk)
     sp = max(1, int(splits))
     dev = probs[0]["out"].device
     slab = None
