@@ -177,8 +177,7 @@ template <> struct LdsSplit<192, 16> { static constexpr int FWD_MT = 1, BWD_KS =
 // tile is read once per k-step for 12 MFMAs instead of 4.
 template <int HD, int BR, bool SEQ, int UG>
 __global__ void __launch_bounds__(HD / (16 * UG) * 64)
-lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted cols, no bias;
-                                                 // store_pre: overwritten by the gate pre-activations
+lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, no bias (bf16)
                 const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
                 const bf16* __restrict__ whh,    // [ndir][4*HD][HD] permuted rows, zero padded
                 int B, int S, int Hd, int ndir,
@@ -187,7 +186,7 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
                 float* __restrict__ hseq,        // SEQ: [Bp][S][ndir*HD] (processing order)
                 float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
                 float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
-                int store_pre) {
+                float* __restrict__ pre) {  // [B*S][ndir][4*HD] fp32 gate pre-activations (+ bias), or null
   constexpr int NW = HD / (16 * UG);
   constexpr int NT = NW * 64;
   constexpr int MT = 4 * UG;   // m-tiles per wave
@@ -261,21 +260,23 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   // (b >= B) get an out-of-range offset and are dropped (no branch, see common.h); without a
   // backward the descriptor has no records and every such store is dropped.
   const int rowXi = ndir * 4 * HD;
-  const __amdgpu_buffer_rsrc_t x_rs = dn_rsrc(xp, (uint32_t)(B * S * rowXi * 4));
-  const __amdgpu_buffer_rsrc_t pre_rs = dn_rsrc(xp, store_pre ? (uint32_t)(B * S * rowXi * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t x_rs = dn_rsrc(xp, (uint32_t)(B * S * rowXi * 2));
+  const __amdgpu_buffer_rsrc_t pre_rs = dn_rsrc(pre, pre ? (uint32_t)(B * S * rowXi * 4) : 0u);
   const __amdgpu_buffer_rsrc_t c_rs = dn_rsrc(c_save, (uint32_t)(ndir * Bp * S * HD * 4));
   const __amdgpu_buffer_rsrc_t hp_rs = dn_rsrc(hprev, (uint32_t)(ndir * Bp * S * HD * 2));
   uint32_t xo[NSL], po[NSL], co[NSL], ho[NSL];  // per-lane byte offsets at time index 0
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
-    xo[s] = (uint32_t)((bc * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 4);
+    xo[s] = (uint32_t)((bc * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 2);
     po[s] = b < B ? (uint32_t)((b * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 4) : DN_OOB;
     co[s] = (uint32_t)((((dir * Bp + b) * S) * HD + uu[s]) * 4);
     ho[s] = (uint32_t)((((dir * Bp + b) * S) * HD + uu[s]) * 2);
   }
-  const uint32_t xstep = (uint32_t)(rowXi * 4);  // bytes per time index
+  const uint32_t xstep = (uint32_t)(rowXi * 2);  // bytes per time index (bf16 projection)
+  const uint32_t pstep = (uint32_t)(rowXi * 4);  // (fp32 pre-activations)
+  // the 4 gate inputs of a slot stay packed (2 VGPRs, unconverted) while the load is in flight
   auto load_x = [&](int s, int tau) {  // time index -1 / S wraps out of range: reads 0
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+    return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
         x_rs, (int)(xo[s] + (uint32_t)tau * xstep), 0, 0));
   };
   // h_{t-1} for the weight-gradient GEMMs: each lane stores the h it produces into step t+1's
@@ -292,7 +293,8 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   // xa / xb: the input projection of the current / next step, ping-ponged over a 2-step
   // unrolled loop so that no register copy (and no vmcnt wait) sits between a prefetch and its
   // use one step later
-  f32x4 xa[NSL], xb[NSL], bbr[NSL];
+  bf16x4 xa[NSL], xb[NSL];
+  f32x4 bbr[NSL];
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
     c[s] = hs[s] = hl[s] = 0.f;
@@ -310,7 +312,7 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
   // step t+1's projection is requested before this step's MFMAs (one gate slot per lane only:
   // at BR >= 8 the second register set spills; those lanes re-load in place after the use)
   constexpr bool EARLY = NSL == 1;
-  auto step = [&](const int t, f32x4 (&xn)[NSL], f32x4 (&xnn)[NSL]) {
+  auto step = [&](const int t, bf16x4 (&xn)[NSL], bf16x4 (&xnn)[NSL]) {
     __builtin_amdgcn_sched_barrier(0);  // step boundary for the scheduler (see the backward)
 #ifdef DN_STAMPS
     STAMP(ts0);
@@ -396,13 +398,13 @@ lstm_fwd_kernel(float* xp,                       // [B*S][ndir][4*HD] permuted c
     for (int s = 0; s < NSL; ++s) {
       const int u = uu[s];
       const f32x4 bb = EARLY ? bbr[s] : *reinterpret_cast<const f32x4*>(&bias_s[4 * u]);
-      const float p0 = pa[s][0] + xn[s][0] + bb[0];
-      const float p1 = pa[s][1] + xn[s][1] + bb[1];
-      const float p2 = pa[s][2] + xn[s][2] + bb[2];
-      const float p3 = pa[s][3] + xn[s][3] + bb[3];
+      const float p0 = pa[s][0] + (float)xn[s][0] + bb[0];
+      const float p1 = pa[s][1] + (float)xn[s][1] + bb[1];
+      const float p2 = pa[s][2] + (float)xn[s][2] + bb[2];
+      const float p3 = pa[s][3] + (float)xn[s][3] + bb[3];
       // the gate pre-activations x W_ih^T + h W_hh^T + b, in place of the projection they were
       // built from: the backward reads them instead of re-running a time-parallel GEMM
-      dn_store_f32x4(pre_rs, po[s] + (uint32_t)tau * xstep, f32x4{p0, p1, p2, p3});
+      dn_store_f32x4(pre_rs, po[s] + (uint32_t)tau * pstep, f32x4{p0, p1, p2, p3});
       if constexpr (!EARLY) xn[s] = load_x(s, tau1);
       const float gi = sigmoid_unit(dn_sigmoid(p0));
       const float gf = sigmoid_unit(dn_sigmoid(p1));
@@ -898,44 +900,44 @@ static int lstm_ug() {
 }
 
 template <int HD, int BR, int UG>
-int launch_fwd_ug(float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
+int launch_fwd_ug(const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
-                  float* cT, int store_pre, hipStream_t st) {
+                  float* cT, float* pre, hipStream_t st) {
   dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
   if (hseq)
     hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, true, UG>), grid, block, 0, st, xp, bias, whh, B, S,
-                       Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
+                       Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre);
   else
     hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false, UG>), grid, block, 0, st, xp, bias, whh, B,
-                       S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre);
+                       S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre);
   return dn_launch_status();
 }
 
 template <int HD, int BR>
-int launch_fwd_br(float* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
+int launch_fwd_br(const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
-                  float* cT, int store_pre, hipStream_t st) {
+                  float* cT, float* pre, hipStream_t st) {
   if constexpr (HD == 192 && BR == 4) {
     if (lstm_ug() == 3)
       return launch_fwd_ug<HD, BR, 3>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
-                                      mean_scale, hT, cT, store_pre, st);
+                                      mean_scale, hT, cT, pre, st);
   }
   if constexpr (HD > 256)  // streamed weights: 2 unit groups per wave keep the block <= 16 waves
     return launch_fwd_ug<HD, BR, 2>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
-                                    mean_scale, hT, cT, store_pre, st);
+                                    mean_scale, hT, cT, pre, st);
   else return launch_fwd_ug<HD, BR, 1>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
-                                  mean_scale, hT, cT, store_pre, st);
+                                  mean_scale, hT, cT, pre, st);
 }
 
 template <int HD>
-int launch_fwd(int BR, float* xp, const float* bias, const bf16* whh, int B, int S, int Hd,
+int launch_fwd(int BR, const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd,
                int ndir, float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale,
-               float* hT, float* cT, int store_pre, hipStream_t st) {
-  if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+               float* hT, float* cT, float* pre, hipStream_t st) {
+  if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
   if constexpr (HD > 192) return DN_UNSUPPORTED;  // streamed variants: 4 rows only (pick_br)
   else {
-  if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
-  return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+  if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+  return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
   }
 }
 
@@ -1062,22 +1064,22 @@ static bool lstm_fits_32bit(int B, int S, int HD, int ndir, int BR) {
   return (long)Bp * S * ndir * 4 * HD * 4 < (1L << 31);
 }
 
-// store_pre != 0: xp is overwritten in place by the gate pre-activations (+ bias) the
-// backward consumes
-DN_API int dn_lstm_fwd(float* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
+// xp: the bf16 input projection [B*S][ndir][4*HD]; pre (fp32, same layout, or null when no
+// backward follows) receives the gate pre-activations (+ bias) the backward consumes
+DN_API int dn_lstm_fwd(const void* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
                        int ndir, float* c_save, void* hprev, float* hseq, float* hmean,
-                       float mean_scale, float* hT, float* cT, int store_pre, hipStream_t st) {
+                       float mean_scale, float* hT, float* cT, float* pre, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
   const int BR = pick_br(B, HD);
   if (!lstm_fits_32bit(B, S, HD, ndir, BR)) return DN_BAD_SHAPE;
   switch (HD) {
-    case 64: return launch_fwd<64>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
-    case 128: return launch_fwd<128>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
-    case 192: return launch_fwd<192>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
-    case 256: return launch_fwd<256>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
-    case 384: return launch_fwd<384>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
-    case 512: return launch_fwd<512>(BR, xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, store_pre, st);
+    case 64: return launch_fwd<64>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+    case 128: return launch_fwd<128>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+    case 192: return launch_fwd<192>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+    case 256: return launch_fwd<256>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+    case 384: return launch_fwd<384>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+    case 512: return launch_fwd<512>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
   }
   return DN_UNSUPPORTED;
 }

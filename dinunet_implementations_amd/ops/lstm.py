@@ -5,13 +5,13 @@ Per training step (both directions together):
 forward
   1. ``dn_lstm_pack``: fp32 reference-layout params -> bf16 kernel layouts (gate rows permuted to
      ``m = 4u + g``, units zero-padded to HD in {64,128,192,256,384,512}), fused bias ``b_ih + b_hh``.
-  2. input projection of both directions as ONE GEMM ``[B*S, I] x [I, ndir*4*HD]`` (fp32 out).
+  2. input projection of both directions as ONE GEMM ``[B*S, I] x [I, ndir*4*HD]`` (bf16 out).
   3. ``dn_lstm_fwd``: persistent recurrence (grid = batch-row chunks x directions), stores
      ``c_t`` and ``h_{t-1}`` per step and, when a backward will follow, the gate
-     pre-activations ``x W_ih^T + h_{t-1} W_hh^T + b`` in place of the projection it read
-     (one 16-B store per lane and step, no extra GEMM).
+     pre-activations ``x W_ih^T + h_{t-1} W_hh^T + b`` (fp32, one 16-B store per lane and
+     step, no extra GEMM).
 backward
-  4. (nothing to recompute: the projection buffer holds the pre-activations).
+  4. (nothing to recompute: the forward stored the pre-activations).
   5. ``dn_lstm_bwd``: reverse-time recurrence -> gate grads ``dpre`` (bf16, original time order).
   6. parameter grads ACCUMULATED straight into ``.grad`` (flat buffer) by GEMM epilogues with a
      row map back to the reference ``[i|f|o|g]`` layout: ``dW_ih += dpre^T x``,
@@ -47,7 +47,7 @@ _lib.register("dn_lstm_pack_prologue", [_lib.c_void_p] * 8 + [_lib.c_int] * 3
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
-                              _lib.c_int, _lib.c_void_p])
+                              _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_long, _lib.c_long, _lib.c_float, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
@@ -120,11 +120,13 @@ class _BiLSTMFn(torch.autograd.Function):
             x2d = x2d.to(torch.bfloat16)
         x2d = x2d.contiguous()
         if xp_pre is not None:  # the caller's own input projection (same layout as below)
-            if xp_pre.shape != (B * S, ndir * GP) or xp_pre.dtype != torch.float32:
+            if xp_pre.shape != (B * S, ndir * GP) or xp_pre.dtype != torch.bfloat16:
                 raise ValueError("precomputed LSTM input projection has the wrong shape/dtype")
             xp = xp_pre
         else:
-            xp = mm_plain(x2d, wih_p, trans_b=True, out_dtype=torch.float32)  # [B*S, ndir*GP]
+            # bf16 projection: half the bytes the recurrence streams per step (large batches
+            # are HBM-bound there); the sum with the recurrent part stays fp32
+            xp = mm_plain(x2d, wih_p, trans_b=True, out_dtype=torch.bfloat16)  # [B*S, ndir*GP]
         c_save = torch.empty(ndir, Bp, S, HD, dtype=torch.float32, device=dev)
         hprev = torch.empty(ndir, Bp, S, HD, dtype=torch.bfloat16, device=dev)
         hT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
@@ -135,14 +137,16 @@ class _BiLSTMFn(torch.autograd.Function):
         else:
             hseq = torch.empty(Bp, S, ndir * HD, dtype=torch.float32, device=dev)
         need_bwd = any(ctx.needs_input_grad)
+        # fp32 gate pre-activations (x W_ih^T + h W_hh^T + b) for the backward
+        pre = torch.empty(B * S, ndir * GP, dtype=torch.float32, device=dev) if need_bwd else None
         _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
                   ndir, c_save.data_ptr(), hprev.data_ptr(), _lib.ptr(hseq), _lib.ptr(hmean),
-                  1.0 / S, hT.data_ptr(), cT.data_ptr(), int(need_bwd), st)
+                  1.0 / S, hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), st)
         if mode == "mean":
             out = hmean
         else:
             out = hseq.view(Bp, S, ndir, HD)[:B, :, :, :Hd].reshape(B, S, ndir * Hd)
-        ctx.save_for_backward(x2d, wih_p, whh_p, whhT_p, bias_p, xp, c_save, hprev)
+        ctx.save_for_backward(x2d, wih_p, whh_p, whhT_p, bias_p, pre, c_save, hprev)
         ctx.params = params
         ctx.relu_in = bool(relu_in)
         ctx.meta = (B, S, I, Hd, HD, ndir, mode, enc.dtype)
@@ -151,7 +155,7 @@ class _BiLSTMFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout: Optional[Tensor], dhT: Optional[Tensor], dcT: Optional[Tensor]):
-        x2d, wih_p, whh_p, whhT_p, bias_p, xp, c_save, hprev = ctx.saved_tensors
+        x2d, wih_p, whh_p, whhT_p, bias_p, pre, c_save, hprev = ctx.saved_tensors
         params = ctx.params
         B, S, I, Hd, HD, ndir, mode, enc_dtype = ctx.meta
         GP = 4 * HD
@@ -159,7 +163,7 @@ class _BiLSTMFn(torch.autograd.Function):
         Bp = c_save.shape[1]
         dev = x2d.device
         st = _lib.stream()
-        # (4) xp already holds the gate pre-activations (stored in place by the forward kernel)
+        # (4) the forward kernel stored the gate pre-activations
         # (5) reverse-time recurrence
         if dout is None:
             dout = torch.zeros((B, ndir * Hd) if mode == "mean" else (B, S, ndir * Hd),
@@ -172,7 +176,7 @@ class _BiLSTMFn(torch.autograd.Function):
         dhT = None if dhT is None else dhT.float().contiguous()
         dcT = None if dcT is None else dcT.float().contiguous()
         dpre = torch.empty(Bp * S, ndir * GP, dtype=torch.bfloat16, device=dev)
-        _lib.call("dn_lstm_bwd", xp.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
+        _lib.call("dn_lstm_bwd", pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
                   dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir,
                   dpre.data_ptr(), st)
         dpre_v = dpre[:N]

@@ -23,7 +23,7 @@ def time_lib(path, B=32, S=98, I=256, H=384, reps=50):
     lib = ctypes.CDLL(path)
     V, I_, F, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
     lib.dn_lstm_pack.argtypes = [V] * 8 + [I_] * 3 + [V] * 4 + [I_, V, V, V, V]
-    lib.dn_lstm_fwd.argtypes = [V, V, V, I_, I_, I_, I_, V, V, V, V, F, V, V, I_, V]
+    lib.dn_lstm_fwd.argtypes = [V, V, V, I_, I_, I_, I_, V, V, V, V, F, V, V, V, V]
     lib.dn_lstm_bwd.argtypes = [V, V, V, V, L, L, F, V, V, I_, I_, I_, I_, V, V]
     lib.dn_lstm_rows_per_wg.argtypes = [I_, I_]
     lib.dn_lstm_padded_hidden.argtypes = [I_]
@@ -50,8 +50,8 @@ def time_lib(path, B=32, S=98, I=256, H=384, reps=50):
                           None, st)
     assert rc == 0, rc
     x = torch.randn(B * S, I, device=dev, generator=g).to(torch.bfloat16)
-    xp0 = mm(x, wih_p, trans_b=True)
-    xp = xp0.clone()
+    xp = mm(x, wih_p, trans_b=True, out_dtype=torch.bfloat16)  # bf16 projection
+    pre = torch.empty(xp.shape, dtype=torch.float32, device=dev)
     c_save = torch.empty(ndir, Bp, S, HD, device=dev)
     hprev = torch.empty(ndir, Bp, S, HD, dtype=torch.bfloat16, device=dev)
     hmean = torch.empty(B, ndir * Hd, device=dev)
@@ -62,15 +62,14 @@ def time_lib(path, B=32, S=98, I=256, H=384, reps=50):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     tf, tb = [], []
     for it in range(reps + 5):
-        xp.copy_(xp0)  # the forward overwrites the projection with the pre-activations
         ev[0].record()
         rc = lib.dn_lstm_fwd(xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd, ndir,
                              c_save.data_ptr(), hprev.data_ptr(), None, hmean.data_ptr(), 1.0 / S,
-                             hT.data_ptr(), cT.data_ptr(), 1, st)
+                             hT.data_ptr(), cT.data_ptr(), pre.data_ptr(), st)
         ev[1].record()
         assert rc == 0, rc
         ev[2].record()
-        rc = lib.dn_lstm_bwd(xp.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(), dout.data_ptr(),
+        rc = lib.dn_lstm_bwd(pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(), dout.data_ptr(),
                              ndir * Hd, 0, 1.0 / S, None, None, B, S, Hd, ndir, dpre.data_ptr(), st)
         ev[3].record()
         assert rc == 0, rc
