@@ -33,10 +33,7 @@ _SIGS = {
     "dn_lstm_padded_hidden": [c_int],
     "dn_lstm_pack": [c_void_p] * 8 + [c_int, c_int, c_int] + [c_void_p] * 4
                     + [c_int, c_void_p, c_void_p, c_void_p] + [c_void_p],
-    "dn_lstm_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
-                    c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
-    "dn_lstm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_float, c_void_p,
-                    c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    # (the LSTM launchers are registered with their signatures by ops.lstm)
 }
 
 
