@@ -298,7 +298,7 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
     c[s] = hs[s] = hl[s] = 0.f;
-    if constexpr (NSL == 1) bbr[s] = *reinterpret_cast<const f32x4*>(&bias_s[4 * uu[s]]);
+    if constexpr (NSL == 1 || (NSL == 2 && HD != 512)) bbr[s] = *reinterpret_cast<const f32x4*>(&bias_s[4 * uu[s]]);
     xa[s] = load_x(s, dir == 0 ? 0 : S - 1);
   }
   int cur = 0;
@@ -309,9 +309,10 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
 #ifdef DN_STAMPS
   unsigned long long st_a = 0, st_b = 0, st_c = 0, ts0, ts1, ts2, ts3;
 #endif
-  // step t+1's projection is requested before this step's MFMAs (one gate slot per lane only:
-  // at BR >= 8 the second register set spills; those lanes re-load in place after the use)
-  constexpr bool EARLY = NSL == 1;
+  // step t+1's projection is requested before this step's MFMAs (up to two gate slots per lane:
+  // the bf16 projection keeps a slot's prefetch in 2 VGPRs; 4 slots, and 2 at HD = 512, spill
+  // and re-load in place after the use instead).  The bias registers bbr follow the same rule.
+  constexpr bool EARLY = NSL == 1 || (NSL == 2 && HD != 512);
   auto step = [&](const int t, bf16x4 (&xn)[NSL], bf16x4 (&xnn)[NSL]) {
     __builtin_amdgcn_sched_barrier(0);  // step boundary for the scheduler (see the backward)
 #ifdef DN_STAMPS
