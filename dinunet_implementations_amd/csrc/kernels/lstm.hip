@@ -150,7 +150,16 @@ __device__ __forceinline__ float sigmoid_unit(float s) {
   }
 }
 template <int HD, int BR> struct LdsSplit { static constexpr int FWD_MT = 0, BWD_KS = 0; };
-template <> struct LdsSplit<192, 4> { static constexpr int FWD_MT = 0, BWD_KS = 4; };
+// (192, 4): all of W_hh^T in VGPRs, exchange-tile reads in groups of 2 k-steps (BWD_RG_192):
+// 111.3 vs 117.0 us with 4 k-steps of W^T in LDS and groups of 4 (tools/lstm_time.py) -- the
+// LDS-resident weights cost 48 extra wave-wide LDS reads per step on an LDS-bound loop
+#ifndef LSTM_BWD_KS_192_4
+#define LSTM_BWD_KS_192_4 0
+#endif
+#ifndef BWD_RG_192
+#define BWD_RG_192 2
+#endif
+template <> struct LdsSplit<192, 4> { static constexpr int FWD_MT = 0, BWD_KS = LSTM_BWD_KS_192_4; };
 template <> struct LdsSplit<192, 8> { static constexpr int FWD_MT = 0, BWD_KS = 6; };
 template <> struct LdsSplit<192, 16> { static constexpr int FWD_MT = 1, BWD_KS = 9; };
 
@@ -634,7 +643,7 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     // k-steps -- so the LDS latency, not the MFMA pipe, paced the step.
     // (4-row layout only: at 8 / 16 rows per workgroup the second register set spills; the
     // per-step output-gradient variant takes groups of 2 for the same reason)
-    constexpr int RG = BR != 4 ? 1 : (DSEQ ? 2 : BWD_RG);
+    constexpr int RG = BR != 4 ? 1 : ((DSEQ || HD == 192) ? (HD == 192 ? BWD_RG_192 : 2) : BWD_RG);
     if constexpr (!STREAM && RG == 1) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
