@@ -617,7 +617,10 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     }
     // K = 4*HD runs as BWD_CHAINS independent accumulator chains per unit group (summed after
     // the loop): one chain of 24 dependent MFMAs left the SIMD waiting on its own results
-    constexpr int NCH = BWD_CHAINS;
+    constexpr int RG = BR != 4 ? 1 : ((DSEQ || HD == 192) ? (HD == 192 ? BWD_RG_192 : 2) : BWD_RG);
+    // with the exchange-tile reads grouped ahead (RG > 1) one chain is fastest (192 / 4 rows:
+    // 109.3 us vs 111.0 at 2 chains, 112.9 at 3, 114.8 at 4; tools/lstm_time.py)
+    constexpr int NCH = (RG > 1 && !STREAM) ? 1 : BWD_CHAINS;
     f32x4 acc[UG], accp[UG][NCH];
 #pragma unroll
     for (int g = 0; g < UG; ++g)
@@ -643,7 +646,6 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
     // k-steps -- so the LDS latency, not the MFMA pipe, paced the step.
     // (4-row layout only: at 8 / 16 rows per workgroup the second register set spills; the
     // per-step output-gradient variant takes groups of 2 for the same reason)
-    constexpr int RG = BR != 4 ? 1 : ((DSEQ || HD == 192) ? (HD == 192 ? BWD_RG_192 : 2) : BWD_RG);
     if constexpr (!STREAM && RG == 1) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
