@@ -91,7 +91,9 @@ class LSTM(nn.Module):
             params = [cell.params() for cell in self.lstms]
             return ops.bilstm(x, params, reduce=reduce, modules=list(self.lstms), packed=packed,
                               xp=xp, relu_input=relu_input)
-        if x.is_cuda and self.use_fused:
+        if x.is_cuda and self.use_fused and h is None and self.bias:
+            # only the hidden size can push a default (zero-state, biased) LSTM off the fused
+            # kernels; an explicit initial state or bias=False takes the reference loop by choice
             _slow_lstm_gate(self.hidden_size, x.shape[0])
         x = x.to(self.lstms[0].i2h.weight.dtype)  # the fused encoder hands over bf16
         if h is not None:

@@ -15,6 +15,7 @@ import argparse
 import json
 import os
 import sys
+import traceback
 from typing import Any, Dict, List
 
 
@@ -68,6 +69,8 @@ def main(argv=None):
     except Exception as e:  # a peer site died / timed out, or this site failed
         # report and leave without tearing the process group down: a destroy that waits on a
         # dead peer would hang this survivor too
+        # the traceback tells a local bug (shape error, kernel status) from a dead peer
+        traceback.print_exc(file=sys.stderr)
         print(f"[local{grp.rank}] site failure ({type(e).__name__}): {e}", file=sys.stderr,
               flush=True)
         sys.stdout.flush()

@@ -168,10 +168,13 @@ class FederatedSite:
         tl = logs.setdefault(f"{tag}train_log", [])
         vl = logs.setdefault(f"{tag}validation_log", [])
         lvl = logs.setdefault(f"{tag}local_validation_log", [])
-        comp = logs.setdefault("time_spent_on_computation", [])
-        cum = logs.setdefault("cumulative_total_duration", [])
-        itd = logs.setdefault("local_iter_duration", [])
-        t_run = time.time() - (cum[-1] if cum else 0.0)  # a resumed run continues the clock
+        # duration lists per phase (the pretraining pass logs under its own tag, so the
+        # federated clock of the pretrain site starts at 0 like every other site's)
+        comp = logs.setdefault(f"{tag}time_spent_on_computation", [])
+        cum = logs.setdefault(f"{tag}cumulative_total_duration", [])
+        itd = logs.setdefault(f"{tag}local_iter_duration", [])
+        # only a resumed run continues its clock from the checkpointed total
+        t_run = time.time() - (cum[-1] if (resume and cum) else 0.0)
         trainer.train()
         for epoch in range(start_epoch, epochs + 1):
             t0 = time.time()

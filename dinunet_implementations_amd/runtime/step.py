@@ -78,7 +78,12 @@ class TrainStep:
         # factorisation joins the captured region via pre_reduce)
         self.use_graph = (use_graph and flat.data.is_cuda
                           and (engine.name == "dSGD" or getattr(engine, "fast", False)))
-        self._pre_reduce = getattr(engine, "pre_reduce", None) if engine.name != "dSGD" else None
+        # the local factorisation (rank-dAD / PowerSGD pre_reduce) is captured only when every
+        # replay is a whole step: with accumulation it must run once, after the LAST micro-batch
+        # (PowerSGD's error feedback and rank-dAD's warm start would otherwise be applied to
+        # every partial gradient), so it then runs eagerly inside engine.reduce()
+        pre = getattr(engine, "pre_reduce", None) if engine.name != "dSGD" else None
+        self._pre_reduce = pre if self.accum == 1 else None
         self.eager_warmup = eager_warmup
         self.calls = 0
         self.graph = None

@@ -295,6 +295,24 @@ def test_accumulated_graph_step_matches_eager():
     assert torch.allclose(fe.data, fg.data, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("engine", ["powerSGD", "rankDAD"])
+def test_accumulated_lowrank_graph_matches_eager(engine):
+    """local_iterations = 2 with a low-rank engine on the graph path: the local factorisation
+    (PowerSGD error feedback, rank-dAD warm start) runs once per step, after the second
+    micro-batch, exactly as in the eager accumulation (it used to be captured and so
+    replayed with every micro-batch)."""
+    xs, ys = _batches(n=8)
+    _, fe, se = _trainer(0, engine=engine, use_graph=False, accum=2)
+    _, fg, sg = _trainer(0, engine=engine, use_graph=True, accum=2)
+    for st in (se, sg):
+        for i in range(xs.shape[0]):
+            st(xs[i], ys[i], first=i % 2 == 0, last=i % 2 == 1)
+    torch.cuda.synchronize()
+    assert sg.graph is not None and sg._pre_reduce is None
+    assert se.opt.step_count == sg.opt.step_count == 4
+    assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5), (fe.data - fg.data).abs().max()
+
+
 def test_powersgd_device_matches_reference_math():
     """Device PowerSGD (csrc/kernels/lowrank.hip: P = M Q with M = G + err, Cholesky QR,
     Q = M^T P, G = P Q^T, err = M - G) == the same algorithm in torch ops (MGS), over 3
