@@ -43,6 +43,13 @@ def parse():
     ap.add_argument("--precision-bits", default="32", choices=["16", "32"])
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+bwd(+opt) in a HIP graph")
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic batches resident in HBM")
+    ap.add_argument("--feed", default="device", choices=["device", "host"],
+                    help="device: the site dataset lives in HBM as bf16 and every step gathers its "
+                         "batch on the device (K whole steps per HIP graph); host: each step is fed "
+                         "a batch tensor by the host loop")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps per HIP graph in device-feed mode (0: the largest divisor of "
+                         "--steps up to 10)")
     return ap.parse_args()
 
 
@@ -73,17 +80,37 @@ def main():
     xs = torch.randn(args.pool, args.batch, S, args.comps, args.window, device=dev, generator=g)
     ys = torch.randint(0, 2, (args.pool, args.batch), device=dev, generator=g)
 
-    for i in range(args.warmup):
-        step(xs[i % args.pool], ys[i % args.pool])
-    torch.cuda.synchronize()
-    grp.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(xs[i % args.pool], ys[i % args.pool])
-    torch.cuda.synchronize()
-    grp.barrier()
-    torch.cuda.synchronize()
+    if args.feed == "device":
+        # the site's (synthetic) dataset resident in HBM as bf16, batches gathered on the device
+        # by the step's first launch; the timed steps run as replays of K-step graphs
+        from dinunet_implementations_amd.ops import DeviceSource
+        src = DeviceSource(xs.view(args.pool * args.batch, S, args.comps, args.window)
+                           .to(torch.bfloat16), ys.view(-1), args.batch)
+        del xs
+        K = args.graph_steps or max(d for d in range(1, 11) if args.steps % d == 0)
+        step.bind(src, steps_per_graph=K)
+        step.run(args.warmup)
+        step.prepare(args.steps)
+        torch.cuda.synchronize()
+        grp.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step.run(args.steps)
+        torch.cuda.synchronize()
+        grp.barrier()
+        torch.cuda.synchronize()
+    else:
+        for i in range(args.warmup):
+            step(xs[i % args.pool], ys[i % args.pool])
+        torch.cuda.synchronize()
+        grp.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(xs[i % args.pool], ys[i % args.pool])
+        torch.cuda.synchronize()
+        grp.barrier()
+        torch.cuda.synchronize()
     dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
     grp.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
     dt = float(dt.item())
@@ -110,7 +137,8 @@ def main():
                                 f"I={args.input_size}, H={args.hidden}, bi-dir)",
                        "global_batch": args.batch * n, "seq_len": S,
                        "parallelism": f"dp{n}", "engine": args.engine,
-                       "precision_bits": args.precision_bits, "hip_graph": bool(args.graph)},
+                       "precision_bits": args.precision_bits, "hip_graph": bool(args.graph),
+                       "feed": args.feed},
             "per_site": round(total / n, 2),
             "vs_baseline_per_site": round((total / n) / BASELINE_SAMPLES_PER_SEC_PER_SITE, 2),
             "baseline_note": "vs_baseline = value / 172.7 samples/s (BASELINE.md: the reference "

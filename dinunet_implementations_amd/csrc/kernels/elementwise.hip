@@ -1,5 +1,6 @@
 // Small fused memory-bound kernels (vectorised 16 B per lane, deterministic reductions).
 #include "common.h"
+#include "prologue.h"
 
 namespace {
 
@@ -82,32 +83,26 @@ __global__ void colsum_slabs_kernel(const float* __restrict__ part, int slabs, i
   out[c] = accumulate ? out[c] + v : v;
 }
 
-// Training-step prologue in ONE launch (it replaces three: two copies into the HIP graph's static
-// inputs and the gradient zeroing): x fp32 -> bf16 static input (the GEMMs round their operands
-// to bf16 while staging anyway, so this is bit-identical and halves their reads), the int64
-// labels, and zeros into the flat gradient buffer.  Grid-stride over 8-element x units, 4-element
-// gradient units and single labels; n_x % 8 == 0 and n_g % 4 == 0 (host-checked).
+// Training-step prologue in ONE launch (prologue.h; it replaces three: two copies into the HIP
+// graph's static inputs and the gradient zeroing).  Grid-stride over 8-element batch units,
+// 4-element gradient units and single labels.
 __global__ void __launch_bounds__(256)
-step_prologue_kernel(const float* __restrict__ x, long ux, bf16* __restrict__ xb,
-                     const long long* __restrict__ y, long ny, long long* __restrict__ yd,
-                     float* __restrict__ g, long ug, int* __restrict__ bump) {
-  if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;  // Adam's device step counter
-  const long total = ux + ug + ny;
+step_prologue_kernel(StepPrologue sp) {
+  if (sp.bump && blockIdx.x == 0 && threadIdx.x == 0) *sp.bump += 1;  // Adam's device step counter
+  const long total = sp.ux + sp.ug + sp.ny;
+  const long cur = prologue_cursor(sp);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    if (i < ux) {
-      const f32x4 a = reinterpret_cast<const f32x4*>(x)[2 * i];
-      const f32x4 b = reinterpret_cast<const f32x4*>(x)[2 * i + 1];
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { o[e] = (bf16)a[e]; o[4 + e] = (bf16)b[e]; }
-      reinterpret_cast<bf16x8*>(xb)[i] = o;
-    } else if (i < ux + ug) {
-      reinterpret_cast<f32x4*>(g)[i - ux] = f32x4{0.f, 0.f, 0.f, 0.f};
-    } else {
-      yd[i - ux - ug] = y[i - ux - ug];
-    }
-  }
+       i += (long)gridDim.x * blockDim.x)
+    prologue_item(sp, i, cur);
+}
+
+static int prologue_launch(const StepPrologue& sp, hipStream_t st) {
+  const long total = sp.ux + sp.ug + sp.ny;
+  if (total <= 0) return DN_OK;
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st, sp);
+  return dn_launch_status();
 }
 
 }  // namespace
@@ -116,13 +111,28 @@ step_prologue_kernel(const float* __restrict__ x, long ux, bf16* __restrict__ xb
 DN_API int dn_step_prologue(const float* x, long nx, void* xb, const long long* y, long ny,
                             long long* yd, float* g, long ng, int* bump, hipStream_t st) {
   if (nx % 8 || ng % 4 || (((uintptr_t)x | (uintptr_t)xb | (uintptr_t)g) & 15)) return DN_BAD_SHAPE;
-  const long total = nx / 8 + ng / 4 + ny;
-  if (total <= 0) return DN_OK;
-  long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, nx / 8,
-                     (bf16*)xb, y, ny, yd, g, ng / 4, bump);
-  return dn_launch_status();
+  StepPrologue sp{};
+  sp.x = x;
+  sp.xb = (bf16*)xb;
+  sp.y = y;
+  sp.yd = yd;
+  sp.g = g;
+  sp.ux = nx / 8;
+  sp.ug = ng / 4;
+  sp.ny = ny;
+  sp.bump = bump;
+  return prologue_launch(sp, st);
+}
+
+// the device-fed prologue as a launch of its own (models whose first launch is not the LSTM pack)
+DN_API int dn_step_gather(const void* gx, int gx_bf16, long row_elems, const long long* gy,
+                          const long long* order, long nb, const long long* cursor, int B, void* xb,
+                          long long* yd, float* g, long ng, int* bump, hipStream_t st) {
+  StepPrologue sp;
+  const int rc = prologue_gather(sp, gx, gx_bf16, row_elems, gy, order, nb, cursor, B, xb, yd, g,
+                                 ng, bump);
+  if (rc != DN_OK) return rc;
+  return prologue_launch(sp, st);
 }
 
 DN_API int dn_relu_bwd(const void* dy, const void* y, void* dym, long n, hipStream_t st) {

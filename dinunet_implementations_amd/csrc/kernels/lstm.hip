@@ -25,6 +25,7 @@
 // pre-activations, and writes dpre (bf16, original time order) for the weight-gradient GEMMs
 // dW_ih = dpre^T x, dW_hh = dpre^T h_{t-1} that run after it on the full chip.
 #include "common.h"
+#include "prologue.h"
 #include <stdlib.h>
 
 #ifdef DN_STAMPS
@@ -774,19 +775,6 @@ struct CastJobs {
   int cnt;
 };
 
-// The training step's prologue riding in the same launch (runtime.step.TrainStep before a graph
-// replay): batch -> bf16 static input (8 per item), labels copy, gradient buffer zeroing (4 per
-// item).  ux = ug = ny = 0 when unused.
-struct StepPrologue {
-  const float* x;
-  bf16* xb;
-  const long long* y;
-  long long* yd;
-  float* g;
-  long ux, ug, ny;
-  int* bump;  // Adam's device step counter (graph-captured update), advanced once; null: none
-};
-
 // Fragment-linear image of a row-major [rows][KS*32] bf16 matrix (the streamed-weight kernels,
 // HD > 192): element f sits at ((T*KS + ks)*64 + lane)*8 + e for MFMA A-fragment lane
 // (q = lane/16, n = lane%16) of 16-row tile T and k-step ks, i.e. row 16T + n, column
@@ -813,23 +801,11 @@ __global__ void lstm_pack_kernel(LstmParams p, int I, int Hd, int HD, int ndir,
   int n_pc = n_pack;
   for (int j = 0; j < cj.cnt; ++j) n_pc += cj.n[j];
   const long total = n_pc + sp.ux + sp.ug + sp.ny;
+  const long cur = prologue_cursor(sp);
   for (long li = blockIdx.x * (long)blockDim.x + threadIdx.x; li < total;
        li += (long)gridDim.x * blockDim.x) {
     if (li >= n_pc) {  // step prologue
-      long i = li - n_pc;
-      if (i < sp.ux) {
-        const f32x4 a = reinterpret_cast<const f32x4*>(sp.x)[2 * i];
-        const f32x4 b = reinterpret_cast<const f32x4*>(sp.x)[2 * i + 1];
-        bf16x8 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { o[e] = (bf16)a[e]; o[4 + e] = (bf16)b[e]; }
-        reinterpret_cast<bf16x8*>(sp.xb)[i] = o;
-      } else if ((i -= sp.ux) < sp.ug) {
-        reinterpret_cast<f32x4*>(sp.g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        i -= sp.ug;
-        sp.yd[i] = sp.y[i];
-      }
+      prologue_item(sp, li - n_pc, cur);
       continue;
     }
     const int idx = (int)li;
@@ -1061,7 +1037,36 @@ DN_API int dn_lstm_pack_prologue(const float* wih0, const float* bih0, const flo
                                  const long long* y, long ny, long long* yd, float* g, long ng,
                                  int* bump, hipStream_t st) {
   if (nx % 8 || ng % 4 || (((uintptr_t)x | (uintptr_t)xb | (uintptr_t)g) & 15)) return DN_BAD_SHAPE;
-  const StepPrologue sp{x, (bf16*)xb, y, yd, g, nx / 8, ng / 4, ny, bump};
+  StepPrologue sp{};
+  sp.x = x;
+  sp.xb = (bf16*)xb;
+  sp.y = y;
+  sp.yd = yd;
+  sp.g = g;
+  sp.ux = nx / 8;
+  sp.ug = ng / 4;
+  sp.ny = ny;
+  sp.bump = bump;
+  return lstm_pack_launch(wih0, bih0, whh0, bhh0, wih1, bih1, whh1, bhh1, I, Hd, ndir, wih_p,
+                          bias_p, whh_p, whhT_p, ncast, cast_src, cast_dst, cast_n, sp, st);
+}
+
+// dn_lstm_pack + the DEVICE-FED step prologue (prologue.h) in one launch: batch rows gathered
+// from the HBM-resident dataset gx ([N][row_elems], bf16 if gx_bf16 else fp32) at the device
+// cursor, labels from gy, gradient zeroed, Adam's counter advanced
+DN_API int dn_lstm_pack_gather(const float* wih0, const float* bih0, const float* whh0,
+                               const float* bhh0, const float* wih1, const float* bih1,
+                               const float* whh1, const float* bhh1, int I, int Hd, int ndir,
+                               void* wih_p, float* bias_p, void* whh_p, void* whhT_p, int ncast,
+                               const float* const* cast_src, void* const* cast_dst,
+                               const int* cast_n, const void* gx, int gx_bf16, long row_elems,
+                               const long long* gy, const long long* order, long nb,
+                               const long long* cursor, int B, void* xb, long long* yd, float* g,
+                               long ng, int* bump, hipStream_t st) {
+  StepPrologue sp;
+  const int rc = prologue_gather(sp, gx, gx_bf16, row_elems, gy, order, nb, cursor, B, xb, yd, g,
+                                 ng, bump);
+  if (rc != DN_OK) return rc;
   return lstm_pack_launch(wih0, bih0, whh0, bhh0, wih1, bih1, whh1, bhh1, I, Hd, ndir, wih_p,
                           bias_p, whh_p, whhT_p, ncast, cast_src, cast_dst, cast_n, sp, st);
 }

@@ -12,7 +12,10 @@ __global__ void __launch_bounds__(256)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
             float bc1, float inv_sqrt_bc2, float grad_scale, const int* __restrict__ tdev,
-            double b1d, double b2d, int tofs) {
+            double b1d, double b2d, int tofs, long long* __restrict__ cursor) {
+  // the device-fed batch cursor (prologue.h) advances once per update; no workgroup of this
+  // launch reads it
+  if (cursor && blockIdx.x == 0 && threadIdx.x == 0) *cursor += 1;
   if (tdev) {  // graph-replayable form: the step number lives on the device (adam_bump_kernel);
                // double math as on the host, so both forms round to the same fp32 corrections
     const double t = (double)(*tdev + tofs);  // tofs 0: the step prologue advanced it
@@ -86,11 +89,11 @@ int grid_for(long n) {
 
 DN_API int dn_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1,
                    float b2, float eps, float wd, float bc1, float inv_sqrt_bc2, float grad_scale,
-                   hipStream_t st) {
+                   long long* cursor, hipStream_t st) {
   if (n <= 0) return DN_OK;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, n, lr,
-                     b1, b2, eps, wd, bc1, inv_sqrt_bc2, grad_scale, (const int*)nullptr, 0.0, 0.0, 1);
+                     b1, b2, eps, wd, bc1, inv_sqrt_bc2, grad_scale, (const int*)nullptr, 0.0, 0.0, 1, cursor);
   return dn_launch_status();
 }
 
@@ -98,11 +101,12 @@ DN_API int dn_adam(float* p, const float* g, float* m, float* v, long n, float l
 // HIP graph and replayed every step with the right bias corrections.  *tdev = completed steps.
 DN_API int dn_adam_dev(float* p, const float* g, float* m, float* v, long n, float lr, double b1,
                        double b2, float eps, float wd, float grad_scale, int* tdev, int prebumped,
-                       hipStream_t st) {
+                       long long* cursor, hipStream_t st) {
   if (n <= 0) return DN_OK;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, n, lr,
-                     (float)b1, (float)b2, eps, wd, 0.f, 0.f, grad_scale, (const int*)tdev, b1, b2, prebumped ? 0 : 1);
+                     (float)b1, (float)b2, eps, wd, 0.f, 0.f, grad_scale, (const int*)tdev, b1, b2, prebumped ? 0 : 1,
+                     cursor);
   if (!prebumped) hipLaunchKernelGGL(adam_bump_kernel, dim3(1), dim3(1), 0, st, tdev);
   return dn_launch_status();
 }

@@ -211,6 +211,12 @@ class ICALstm(nn.Module):
                 return enc.view(B, S, -1)
         return self.encode(x)
 
+    def prologue_rides_pack(self, x: torch.Tensor) -> bool:
+        """Will :meth:`stem` on ``x`` start with the LSTM weight-pack launch (which can also run
+        a device-fed step prologue, ``ops.lstm.ride_pack``)?  Same test as in :meth:`stem`."""
+        return bool(self.use_fused and x.is_cuda and self.lstm.fused_ok(x)
+                    and ops.capture.active() is None)
+
     def stem_parameters(self):
         return self.encoder.parameters()
 

@@ -56,6 +56,10 @@ _lib.register("dn_head_fwd_train", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_l
                                     _P, _P, _P, _P, _P, _P, _lib.c_int, _P, _P])
 _lib.register("dn_head_bwd0", [_lib.c_int, _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long,
                                _P])
+_lib.register("dn_head_step_layout", [_lib.c_int, _P, _P, _lib.c_int, _P])
+_lib.register("dn_head_step_sync_bytes", [])
+_lib.register("dn_head_step", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int, _P, _P,
+                               _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
 
 # d(loss) tensor of the running training step, when the step will backpropagate exactly that
 # tensor (runtime.step.TrainStep's persistent 1): the forward then runs the head's output-gradient
@@ -63,6 +67,9 @@ _lib.register("dn_head_bwd0", [_lib.c_int, _P, _P, _P, _P, _P, _lib.c_int, _P, _
 _HINT: Optional[torch.Tensor] = None
 import os as _os
 _FUSED_HEAD = _os.environ.get("DINUNET_FUSED_HEAD", "1") == "1"
+# the whole training step of the head in ONE launch (csrc/kernels/head_step.hip) when the d loss
+# is known at forward time; DINUNET_HEAD_STEP=0 keeps the three-launch path
+_HEAD_STEP = _os.environ.get("DINUNET_HEAD_STEP", "1") == "1"
 
 
 class loss_grad_hint:
@@ -143,7 +150,9 @@ class HeadSpec:
             bnp += [L.bn.eps, L.bn.momentum or 0.0] if L.bn is not None else [1e-5, 0.1]
         self._bnp = (ctypes.c_float * (2 * n))(*bnp)
         self._layout = {}
+        self._step_layout = {}
         self._rng: Optional[Tensor] = None
+        self._sync: Optional[Tensor] = None
 
     @staticmethod
     def _bn_mode(L: _Layer) -> int:
@@ -189,6 +198,25 @@ class HeadSpec:
         if any(p.dtype != torch.float32 or not p.is_contiguous() for p in self.params()):
             return False
         return self.layout(B) is not None
+
+    def step_ws(self, B: int) -> Optional[int]:
+        """Workspace bytes of the one-launch head step at batch B (None: outside its envelope)."""
+        if B not in self._step_layout:
+            buf = (ctypes.c_long * 1)()
+            rc = _lib.lib().dn_head_step_layout(self.nl, self._dims, self._flags, B, buf)
+            self._step_layout[B] = int(buf[0]) if rc == 0 else None
+        return self._step_layout[B]
+
+    def sync(self, device) -> Tensor:
+        """The one-launch kernel's persistent hand-off counters (zeroed once; the kernel keeps
+        them consistent across launches with a monotonic epoch)."""
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if self._sync is None or self._sync.device != device:
+            n = int(_lib.lib().dn_head_step_sync_bytes())
+            self._sync = torch.zeros(n // 4, dtype=torch.int32, device=device)
+        return self._sync
 
     def rng(self, device) -> Tensor:
         if self._rng is None or self._rng.device != device:
@@ -244,6 +272,29 @@ class _HeadFn(torch.autograd.Function):
         pred = torch.empty(B, dtype=torch.long, device=x.device)
         rng = spec.rng(x.device)
         ctx.hint_ptr = None
+        ctx.step_dx = None
+        ctx.one_launch = False
+        if train and hint is not None and _HEAD_STEP and _cap.active() is None:
+            sw = spec.step_ws(B)
+            if sw is not None:
+                sws = torch.empty(max(sw, 16), dtype=torch.uint8, device=x.device)
+                dx = (torch.empty(B, x.shape[1], dtype=torch.float32, device=x.device)
+                      if ctx.needs_input_grad[0] else None)
+                rc = _lib.lib().dn_head_step(
+                    spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True),
+                    x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(), loss.data_ptr(),
+                    pred.data_ptr(), rng.data_ptr(), sws.data_ptr(), spec.sync(x.device).data_ptr(),
+                    int(log_out), hint.data_ptr(), _lib.ptr(dx), x.shape[1], _lib.stream())
+                if rc == 0:
+                    ctx.one_launch = True
+                    ctx.hint_ptr = hint.data_ptr()
+                    ctx.step_dx = dx
+                    ctx.spec, ctx.B, ctx.D0, ctx.train = spec, B, x.shape[1], train
+                    ctx.ws = None
+                    ctx.mark_non_differentiable(out, pred)
+                    return out, loss, pred
+                if rc != 3:
+                    raise RuntimeError(f"dn_head_step failed with status {rc}")
         if train and hint is not None:
             rc = _lib.lib().dn_head_fwd_train(
                 spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True),
@@ -272,6 +323,14 @@ class _HeadFn(torch.autograd.Function):
         if not ctx.train:
             raise RuntimeError("fused head: backward needs a training-mode forward")
         spec, B = ctx.spec, ctx.B
+        if ctx.one_launch:
+            # the forward launch already ran the whole backward for d loss == the hint tensor
+            # and accumulated every head gradient; any other d loss cannot be honoured
+            if dloss.data_ptr() != ctx.hint_ptr:
+                raise RuntimeError("fused head step: backward must pass the loss_grad_hint tensor")
+            _grad.notify(spec.params())
+            dx, ctx.step_dx = ctx.step_dx, None
+            return (dx,) + (None,) * (n_in - 1)
         dloss = dloss.float().contiguous()
         dx = torch.empty(B, ctx.D0, dtype=torch.float32, device=dloss.device) \
             if ctx.needs_input_grad[0] else None

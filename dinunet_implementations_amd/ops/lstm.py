@@ -44,6 +44,11 @@ _lib.register("dn_lstm_pack_prologue", [_lib.c_void_p] * 8 + [_lib.c_int] * 3
               + [_lib.c_void_p] * 4 + [_lib.c_int] + [_lib.c_void_p] * 3
               + [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                  _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_lstm_pack_gather", [_lib.c_void_p] * 8 + [_lib.c_int] * 3
+              + [_lib.c_void_p] * 4 + [_lib.c_int] + [_lib.c_void_p] * 3
+              + [_lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                 _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                 _lib.c_long, _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
@@ -241,7 +246,13 @@ def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = 
                 (P * max(nc, 1))(*[c.data_ptr() for c in srcs]),
                 (P * max(nc, 1))(*[d.data_ptr() for d in dsts]),
                 (I_ * max(nc, 1))(*[c.numel() for c in srcs])])
-        if _DEFERRED is not None and not side:
+        rp = _RIDE
+        if rp is not None and not rp.consumed and not side and _DEFERRED is None:
+            # the step's device-fed prologue (batch gather, labels, gradient zeroing, Adam's
+            # counter) rides in this launch: the step's first kernel
+            _lib.call("dn_lstm_pack_gather", *args, *rp.tail, _lib.stream())
+            rp.consumed = True
+        elif _DEFERRED is not None and not side:
             # recorded, launched before each replay (run_deferred_pack); the record keeps every
             # operand alive so the graph pool never hands the packed buffers to another tensor
             _DEFERRED.append((args, (ps, srcs, dsts, wih_p, bias_p, whh_p, whhT_p)))
@@ -270,6 +281,27 @@ class _nullctx:
 
 
 _DEFERRED: Optional[list] = None
+_RIDE = None
+
+
+class ride_pack:
+    """While active, the next in-stream ``pack_params`` launch also runs the device-fed step
+    prologue (``dn_lstm_pack_gather``; ``tail`` = ``ops.DeviceSource.prologue_args``), so the
+    batch gather costs no launch of its own.  ``consumed`` tells the caller it happened."""
+
+    def __init__(self, tail):
+        self.tail = tail
+        self.consumed = False
+
+    def __enter__(self):
+        global _RIDE
+        self._prev, _RIDE = _RIDE, self
+        return self
+
+    def __exit__(self, *a):
+        global _RIDE
+        _RIDE = self._prev
+        return False
 
 
 class defer_pack:

@@ -20,11 +20,15 @@ import torch.nn as nn
 from . import _lib
 
 _lib.register("dn_adam", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
-                          _lib.c_long] + [_lib.c_float] * 8 + [_lib.c_void_p])
+                          _lib.c_long] + [_lib.c_float] * 8 + [_lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_adam_dev", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_long, _lib.c_float, _lib.c_double, _lib.c_double,
                               _lib.c_float, _lib.c_float, _lib.c_float, _lib.c_void_p,
-                              _lib.c_int, _lib.c_void_p])
+                              _lib.c_int, _lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_step_gather", [_lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_void_p,
+                                 _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int,
+                                 _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                                 _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_step_prologue", [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p,
                                    _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                                    _lib.c_void_p, _lib.c_void_p])
@@ -93,6 +97,8 @@ class FusedAdam:
         self.exp_avg_sq = torch.zeros_like(flat.data)
         self.step_count = 0
         self._tdev: Optional[torch.Tensor] = None  # device step counter (graph-captured steps)
+        # device-fed batches (ops.DeviceSource): the update advances the source's cursor
+        self.cursor: Optional[torch.Tensor] = None
 
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
@@ -106,7 +112,8 @@ class FusedAdam:
         if d.is_cuda:
             _lib.call("dn_adam", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
                       self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
-                      self.weight_decay, bc1, 1.0 / math.sqrt(bc2), grad_scale, _lib.stream())
+                      self.weight_decay, bc1, 1.0 / math.sqrt(bc2), grad_scale,
+                      _lib.ptr(self.cursor), _lib.stream())
             return
         g = self.flat.grad * grad_scale
         if self.weight_decay:
@@ -137,7 +144,7 @@ class FusedAdam:
         _lib.call("dn_adam_dev", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
                   self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
                   self.weight_decay, grad_scale, self._tdev.data_ptr(), int(prebumped),
-                  _lib.stream())
+                  _lib.ptr(self.cursor), _lib.stream())
 
     def device_step(self) -> torch.Tensor:
         """The device step counter (int32[1]) the graph-captured update reads; a step prologue
@@ -189,3 +196,69 @@ def cast_bf16_to_f32(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
                   _lib.stream())
     else:
         dst.copy_(src.float() * scale)
+
+
+class DeviceSource:
+    """Training batches resident in HBM (BASELINE config 5 sizing: a site's whole dataset fits one
+    MI355X): ``X [N, *sample]`` (bf16, or fp32), labels ``Y [N]`` int64, an optional per-pass order
+    ``[nb * B]`` of row indices, and a device batch cursor.  Step ``c`` trains on rows
+    ``order[(c mod nb) * B : ... + B]``; the gather runs in the step's first launch and the cursor
+    advances in its Adam launch, so a HIP graph can hold several whole steps
+    (``runtime.step.TrainStep.run``)."""
+
+    def __init__(self, X: torch.Tensor, Y: torch.Tensor, batch: int,
+                 order: Optional[torch.Tensor] = None):
+        if not X.is_cuda or X.dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("DeviceSource: X must be a bf16 / fp32 GPU tensor")
+        self.X = X.contiguous()
+        self.Y = Y.to(device=X.device, dtype=torch.int64).contiguous()
+        self.B = int(batch)
+        self.row = self.X[0].numel()
+        if self.row % 8:
+            raise ValueError("DeviceSource: sample size must be a multiple of 8 elements")
+        self.order = None
+        self.set_order(order)
+        self.cursor = torch.zeros(1, dtype=torch.int64, device=X.device)
+
+    def set_order(self, order: Optional[torch.Tensor]):
+        """A new pass order (e.g. the next epoch's shuffle) in place: captured graphs keep
+        reading the same buffer."""
+        n = self.X.shape[0] if order is None else order.numel()
+        nb = n // self.B
+        if nb < 1:
+            raise ValueError("DeviceSource: fewer samples than one batch")
+        if order is None:
+            self.order = None
+        else:
+            o = order.to(device=self.X.device, dtype=torch.int64).reshape(-1)[:nb * self.B]
+            if self.order is not None and self.order.numel() == o.numel():
+                self.order.copy_(o)
+            else:
+                self.order = o.clone()
+        self.nb = nb
+
+    @property
+    def sample_shape(self):
+        return tuple(self.X.shape[1:])
+
+    def batch(self, c: int):
+        """Host-side view of batch ``c`` (tests / eager fallbacks): ``(x, y)``."""
+        j = (c % self.nb) * self.B
+        rows = (self.order[j:j + self.B] if self.order is not None
+                else torch.arange(j, j + self.B, device=self.X.device))
+        return self.X[rows], self.Y[rows]
+
+    def gather(self, xb: torch.Tensor, yd: torch.Tensor, grad: torch.Tensor,
+               bump: Optional[torch.Tensor] = None):
+        """The standalone device-fed prologue launch (``dn_step_gather``)."""
+        _lib.call("dn_step_gather", self.X.data_ptr(), int(self.X.dtype == torch.bfloat16),
+                  self.row, self.Y.data_ptr(), _lib.ptr(self.order), self.nb,
+                  self.cursor.data_ptr(), self.B, xb.data_ptr(), yd.data_ptr(), grad.data_ptr(),
+                  grad.numel(), _lib.ptr(bump), _lib.stream())
+
+    def prologue_args(self, xb, yd, grad, bump=None):
+        """Argument tail of ``dn_lstm_pack_gather`` (the prologue riding in the weight pack)."""
+        return [self.X.data_ptr(), int(self.X.dtype == torch.bfloat16), self.row,
+                self.Y.data_ptr(), _lib.ptr(self.order), self.nb, self.cursor.data_ptr(),
+                self.B, xb.data_ptr(), yd.data_ptr(), grad.data_ptr(), grad.numel(),
+                _lib.ptr(bump)]

@@ -25,7 +25,7 @@ from typing import Callable, Optional
 import torch
 
 from .. import ops
-from ..ops.lstm import defer_pack, run_deferred_pack
+from ..ops.lstm import defer_pack, ride_pack, run_deferred_pack
 from .timers import NULL, PhaseTimer, enabled_by_env
 
 
@@ -108,6 +108,7 @@ class TrainStep:
         self._cap_lr = None
         self._bf16_in = False
         self._packs: list = []  # LSTM repacks deferred out of the captured graph
+        self.src = None  # device-fed batches (bind)
 
     def _grad_one(self, device, dtype=torch.float32):
         # a persistent d(loss)/d(loss) = 1: loss.backward() would launch a fill kernel for it
@@ -297,3 +298,188 @@ class TrainStep:
                 self.opt.step(grad_scale=scale)
         self.last_out, self.last_loss, self.last_pred = out, loss, pred
         return loss
+
+    # ---- device-fed steps ---------------------------------------------------------------------
+    def bind(self, src, steps_per_graph: int = 8):
+        """Train from an ``ops.DeviceSource`` (batches resident in HBM, gathered on the device).
+
+        Every step is then device-only: its first launch gathers the batch at the source's cursor
+        into the static input (riding in the LSTM weight pack when the model allows,
+        ``ops.lstm.ride_pack``), zeroes the gradient and advances Adam's counter; its Adam
+        launch advances the cursor.  With one site (the update inside the graph) ``run``
+        replays graphs holding ``steps_per_graph`` whole steps, so there is no host work and no
+        graph boundary between them."""
+        if self.accum != 1:
+            raise ValueError("TrainStep.bind: device-fed steps need local_iterations == 1")
+        if not getattr(self.model, "accepts_bf16_input", False):
+            raise ValueError("TrainStep.bind: the model must take a bf16 batch")
+        if not isinstance(self.opt, ops.FusedAdam):
+            raise ValueError("TrainStep.bind: device-fed steps need the fused Adam")
+        self.src = src
+        self.opt.cursor = src.cursor
+        dev = src.X.device
+        self._dsx = torch.empty((src.B,) + src.sample_shape, dtype=torch.bfloat16, device=dev)
+        self._dsy = torch.empty(src.B, dtype=torch.int64, device=dev)
+        self._dK = max(1, int(steps_per_graph)) if (self.use_graph and self._graph_opt_ok()) else 1
+        self._dgraphs = {}
+        self._dcalls = 0
+
+    def _rides(self) -> bool:
+        fn = getattr(self.model, "prologue_rides_pack", None)
+        return bool(fn is not None and fn(self._dsx))
+
+    def _dev_prologue(self, bump):
+        """The device-fed prologue of one step: riding in the model's first launch when it can
+        (returns the context to run the forward in), else as a launch of its own."""
+        if self._rides():
+            tail = self.src.prologue_args(self._dsx, self._dsy, self.flat.grad, bump)
+            return ride_pack(tail)
+        self.src.gather(self._dsx, self._dsy, self.flat.grad, bump)
+        return _NoDefer()
+
+    def _dev_body(self, graph_opt: bool):
+        """One whole device-fed step as issued into the current stream (eager or captured)."""
+        bump = self.opt.device_step() if graph_opt else None
+        sx, sy = self._dsx, self._dsy
+        with self._dev_prologue(bump) as rp:
+            out, loss, pred = self._fwd_bwd(sx, sy)
+        if isinstance(rp, ride_pack) and not rp.consumed:
+            raise RuntimeError("device-fed prologue was not absorbed by the model's weight pack")
+        if self._pre_reduce is not None and graph_opt:
+            self._pre_reduce()
+        if graph_opt:
+            scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
+                     else self.engine.reduce())
+            self.opt.step_graphable(grad_scale=scale, prebumped=True)
+        return out, loss, pred
+
+    def _dev_capture(self, k: int):
+        g = torch.cuda.CUDAGraph()
+        prev = getattr(self.engine, "sync_enabled", None)
+        if prev is not None:
+            self.engine.sync_enabled = False
+        graph_opt = self._dK > 1 or self._graph_opt_ok()
+        if graph_opt:
+            self.opt.sync_device_step()
+            self._cap_lr = self.opt.lr
+        try:
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+                for _ in range(k):
+                    res = self._dev_body(graph_opt)
+        finally:
+            if prev is not None:
+                self.engine.sync_enabled = prev
+        self._dgraphs[k] = (g, res, graph_opt)
+
+    def _dev_capture_split(self):
+        """Device-fed form of :meth:`_capture_split`: graph A = prologue + forward + backward
+        down to the stem output, graph B = the stem's backward (the all-reduce of every other
+        gradient runs between the two replays)."""
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        sx, sy = self._dsx, self._dsy
+        self.engine.sync_enabled = False
+        try:
+            with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
+                with self._dev_prologue(None) as rp:
+                    with self.engine.step_context():
+                        h = self.model.stem(sx)
+                        hd = h.detach().requires_grad_(h.requires_grad)
+                        with ops.head.loss_grad_hint(self._grad_one(sx.device)):
+                            out, loss, pred = self.model.body_loss(hd, sy)
+                        self._backward(loss)
+                if isinstance(rp, ride_pack) and not rp.consumed:
+                    raise RuntimeError("device-fed prologue was not absorbed by the weight pack")
+            with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):
+                if h.requires_grad:
+                    torch.autograd.backward(h, hd.grad)
+        finally:
+            self.engine.sync_enabled = True
+        self._dgraphs["split"] = (ga, gb, (out, loss, pred), (h, hd))
+
+    def _dev_eager(self):
+        T = self.timers
+        sync = getattr(self.engine, "sync_enabled", None)
+        with T.phase("fwd_bwd"):
+            if sync is not None:
+                self.engine.sync_enabled = True
+            out, loss, pred = self._dev_body(False)
+        with T.phase("reduce"):
+            scale = self.engine.reduce()
+        with T.phase("optim"):
+            self.opt.step(grad_scale=scale)  # advances the source cursor too
+        self.last_out, self.last_loss, self.last_pred = out.detach(), loss.detach(), pred
+        return loss
+
+    def run(self, n: int):
+        """``n`` device-fed training steps (``bind`` first); returns the last step's loss."""
+        if self.src is None:
+            raise RuntimeError("TrainStep.run: bind a DeviceSource first")
+        loss = self.last_loss
+        done = 0
+        while done < n:
+            self._dcalls += 1
+            if not self.use_graph or self._dcalls <= self.eager_warmup:
+                if self.use_graph:  # warm-up off the capture stream, like __call__
+                    s = torch.cuda.Stream()
+                    s.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s):
+                        loss = self._dev_eager()
+                    torch.cuda.current_stream().wait_stream(s)
+                else:
+                    loss = self._dev_eager()
+                done += 1
+                continue
+            if self._dgraphs and self.opt.lr != self._cap_lr and any(
+                    v[2] is True for v in self._dgraphs.values()):
+                self._dgraphs = {}  # the learning rate is baked into the captured update
+            if self.split:
+                if "split" not in self._dgraphs:
+                    self._dev_capture_split()
+                ga, gb, (out, loss, pred), _ = self._dgraphs["split"]
+                with self.timers.phase("fwd_bwd"):
+                    ga.replay()
+                    for b in self._first_buckets:  # all-reduce under the stem backward
+                        self.engine.launch_bucket(b)
+                    gb.replay()
+                self.engine.sync_enabled = True
+                with self.timers.phase("reduce"):
+                    scale = self._reduce_after_replay()
+                with self.timers.phase("optim"):
+                    self.opt.step(grad_scale=scale)
+                self.last_out, self.last_loss, self.last_pred = out, loss, pred
+                done += 1
+                continue
+            k = self._dK if n - done >= self._dK else 1
+            if k not in self._dgraphs:
+                self._dev_capture(k)
+            g, (out, loss, pred), graph_opt = self._dgraphs[k]
+            with self.timers.phase("fwd_bwd"):
+                g.replay()
+            if graph_opt:
+                self.opt.step_count += k
+            else:
+                with self.timers.phase("reduce"):
+                    scale = self._reduce_after_replay()
+                with self.timers.phase("optim"):
+                    self.opt.step(grad_scale=scale)
+            self.last_out, self.last_loss, self.last_pred = out, loss, pred
+            done += k
+        return loss
+
+    def prepare(self, n: int = 0):
+        """Capture (without running) every graph a following ``run(n)`` will replay, so a timed
+        region never includes a capture.  Call after the eager warm-up steps."""
+        if self.src is None or not self.use_graph or self._dcalls < self.eager_warmup:
+            return
+        if self.split:
+            if "split" not in self._dgraphs:
+                self._dev_capture_split()
+            return
+        for k in ({self._dK, 1} if n <= 0 else ({self._dK} if n % self._dK == 0 else {self._dK, 1})):
+            if k not in self._dgraphs and (k == 1 or n <= 0 or n >= k):
+                self._dev_capture(k)
+
+    @property
+    def last_labels(self):
+        """Labels of the last device-fed step (the static label buffer)."""
+        return self._dsy

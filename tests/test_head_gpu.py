@@ -253,27 +253,27 @@ def test_fs_backward_exact_given_forward_state(B):
         assert rel(kd, dz.to(torch.bfloat16).float()) < 1e-3, l
 
 
-@pytest.mark.parametrize("scale", [1.0, 2.5])
-def test_fused_forward_backward_chain_matches_two_phase(scale):
-    """With a d(loss) hint the forward also runs the output-gradient chain (one launch) and
-    the backward only dW / dX + the stashed bias / BatchNorm grads: bitwise the unfused result
-    when the backward uses the hinted tensor; a backward with another tensor (scale 2.5) falls
-    back to the full chain and stays exact."""
-    from dinunet_implementations_amd.ops.head import HeadSpec, head_loss, loss_grad_hint
+@pytest.mark.parametrize("one_launch", [True, False])
+def test_fused_forward_backward_chain_matches_two_phase(one_launch, monkeypatch):
+    """With a d(loss) hint the forward runs the backward too: either the WHOLE head step in one
+    launch (csrc/kernels/head_step.hip) or the output-gradient chain with dW / dX left to the
+    backward launch.  Both are bitwise the unfused three-phase result (same reduction orders,
+    same bf16 rounding points)."""
+    from dinunet_implementations_amd.ops import head as H
+    monkeypatch.setattr(H, "_HEAD_STEP", one_launch)
     torch.manual_seed(0)
     mods = _ica_head(p=0.0).to(DEV).train()
     ref_mods = copy.deepcopy(mods)
     x = torch.randn(32, 384, device=DEV)
     y = torch.randint(0, 2, (32,), device=DEV)
     one = torch.ones((), device=DEV)
-    g = one if scale == 1.0 else torch.full((), scale, device=DEV)
     res = []
     for fused, m in ((True, mods), (False, ref_mods)):
         xi = x.clone().requires_grad_()
-        spec = HeadSpec(list(m))
-        with loss_grad_hint(one if fused else None):
-            out, loss, _ = head_loss(xi, spec, y, log_out=False)
-        torch.autograd.backward(loss, g)
+        spec = H.HeadSpec(list(m))
+        with H.loss_grad_hint(one if fused else None):
+            out, loss, _ = H.head_loss(xi, spec, y, log_out=False)
+        torch.autograd.backward(loss, one)
         torch.cuda.synchronize()
         res.append((out.clone(), xi.grad.clone(), [p.grad.clone() for p in m.parameters()],
                     [b.clone() for b in m.buffers()]))
@@ -283,3 +283,121 @@ def test_fused_forward_backward_chain_matches_two_phase(scale):
         assert torch.equal(a, b)
     for a, b in zip(b1, b2):
         assert torch.equal(a, b)
+
+
+def test_hinted_backward_with_other_dloss():
+    """The two-phase fused path stays exact for a backward with another d loss tensor; the
+    one-launch step (which already accumulated the gradients) refuses it loudly."""
+    from dinunet_implementations_amd.ops import head as H
+    torch.manual_seed(0)
+    mods = _ica_head(p=0.0).to(DEV).train()
+    x = torch.randn(32, 384, device=DEV, requires_grad=True)
+    y = torch.randint(0, 2, (32,), device=DEV)
+    one = torch.ones((), device=DEV)
+    spec = H.HeadSpec(list(mods))
+    with H.loss_grad_hint(one):
+        _, loss, _ = H.head_loss(x, spec, y, log_out=False)
+    with pytest.raises(RuntimeError, match="loss_grad_hint"):
+        torch.autograd.backward(loss, torch.full((), 2.5, device=DEV))
+
+
+def _step_vs_classic(mods, x, y, log_out, reps=1):
+    """Run the head with the one-launch step and the three-launch path from identical state;
+    return both results (outputs, dx, grads, buffers)."""
+    from dinunet_implementations_amd.ops import head as H
+    ref_mods = [copy.deepcopy(m) for m in mods]
+    one = torch.ones((), device=DEV)
+    res = []
+    seed0 = None
+    for flag, ms in ((True, mods), (False, ref_mods)):
+        old = H._HEAD_STEP
+        H._HEAD_STEP = flag
+        try:
+            spec = H.HeadSpec(ms)
+            r = spec.rng(x.device)  # both paths draw the same dropout masks
+            if seed0 is None:
+                seed0 = r.clone()
+            else:
+                r.copy_(seed0)
+            for _ in range(reps):
+                xi = x.clone().requires_grad_()
+                with H.loss_grad_hint(one):
+                    out, loss, pred = H.head_loss(xi, spec, y, log_out=log_out)
+                torch.autograd.backward(loss, one)
+            torch.cuda.synchronize()
+            params = [p for m in ms for p in m.parameters()]
+            bufs = [b for m in ms for b in m.buffers()]
+            res.append((out.clone(), loss.clone(), pred.clone(), xi.grad.clone(),
+                        [p.grad.clone() for p in params], [b.clone() for b in bufs], spec))
+        finally:
+            H._HEAD_STEP = old
+    return res
+
+
+@pytest.mark.parametrize("B,p", [(32, 0.0), (17, 0.0), (32, 0.25), (2, 0.0)])
+def test_head_step_one_launch_ica_bitwise(B, p):
+    torch.manual_seed(11)
+    mods = list(_ica_head(p=p).to(DEV).train())
+    x = torch.randn(B, 384, device=DEV)
+    y = torch.randint(0, 2, (B,), device=DEV)
+    a, b = _step_vs_classic(mods, x, y, log_out=False, reps=3)
+    assert int(a[-1].sync(torch.device(DEV))[160].item()) == 0  # no hand-off timed out
+    for u, v in zip(a[:4], b[:4]):
+        assert torch.equal(u, v)
+    for u, v in zip(a[4], b[4]):
+        assert torch.equal(u, v)
+    for u, v in zip(a[5], b[5]):  # running stats: FMA contraction may differ by an ulp
+        assert torch.allclose(u.double(), v.double(), rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("B,dropout_in", [(16, ()), (32, ()), (9, (1,))])
+def test_head_step_one_launch_fs_bitwise(B, dropout_in):
+    torch.manual_seed(12)
+    net = _fs_head(dropout_in=dropout_in).to(DEV).train()
+    mods = [m for blk in net.layers for m in blk] + [net.fc_out]
+    x = torch.rand(B, 66, device=DEV)
+    y = torch.randint(0, 2, (B,), device=DEV)
+    a, b = _step_vs_classic(mods, x, y, log_out=True, reps=2)
+    assert int(a[-1].sync(torch.device(DEV))[160].item()) == 0
+    for u, v in zip(a[:4], b[:4]):
+        assert torch.equal(u, v)
+    for u, v in zip(a[4], b[4]):
+        assert torch.equal(u, v)
+
+
+def test_head_step_one_launch_graph_replay_and_epochs():
+    """Captured in a HIP graph and replayed 200 times (with eager launches in between): the
+    monotonic-epoch hand-offs stay consistent (no timeout, epoch == launches) and the replayed
+    result equals the eager one from the same state."""
+    from dinunet_implementations_amd.ops import head as H
+    torch.manual_seed(13)
+    mods = list(_ica_head(p=0.25).to(DEV).train())
+    spec = H.HeadSpec(mods)
+    x = torch.randn(32, 384, device=DEV, requires_grad=True)
+    y = torch.randint(0, 2, (32,), device=DEV)
+    one = torch.ones((), device=DEV)
+
+    def run():
+        with H.loss_grad_hint(one):
+            _, loss, _ = H.head_loss(x, spec, y, log_out=False)
+        torch.autograd.backward(loss, one)
+        return loss
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            run()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        sl = run()
+    for i in range(200):
+        g.replay()
+        if i % 50 == 0:
+            run()
+    torch.cuda.synchronize()
+    sync = spec.sync(torch.device(DEV))
+    assert int(sync[160].item()) == 0
+    assert int(sync[0].item()) == 3 + 200 + 4  # one epoch per launch
+    assert torch.isfinite(sl).all() and torch.isfinite(x.grad).all()

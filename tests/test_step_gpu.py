@@ -350,3 +350,33 @@ def test_powersgd_step_graph_matches_eager():
     _run(sg, xs, ys)
     assert sg.graph is not None and sg.graph_opt
     assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_device_fed_multistep_graph_matches_host_fed(shuffle):
+    """Batches resident in HBM (bf16) gathered by the step's first launch at a device cursor the
+    Adam launch advances, 4 whole steps per HIP graph: the same trajectory as feeding the same
+    batches from the host loop one step per replay."""
+    from dinunet_implementations_amd.ops import DeviceSource
+    xs, ys = _batches(n=8)
+    B = xs.shape[1]
+    X = xs.reshape(-1, *xs.shape[2:]).to(torch.bfloat16)
+    Y = ys.reshape(-1)
+    order = torch.randperm(X.shape[0], device="cuda") if shuffle else None
+    _, fh, sh = _trainer(0, use_graph=True)
+    _, fd, sd = _trainer(0, use_graph=True)
+    src = DeviceSource(X, Y, B, order=order)
+    sd.bind(src, steps_per_graph=4)
+    n = 16
+    for c in range(n):
+        xb, yb = src.batch(c)
+        sh(xb.float(), yb)
+    sd.run(3)
+    sd.prepare(n - 3)
+    assert set(sd._dgraphs) == {4, 1}
+    sd.run(n - 3)
+    torch.cuda.synchronize()
+    assert int(src.cursor.item()) == n and sd.opt.step_count == sh.opt.step_count == n
+    assert torch.equal(sd.last_labels, src.batch(n - 1)[1])
+    assert torch.allclose(fh.data, fd.data, rtol=1e-6, atol=1e-7), (fh.data - fd.data).abs().max()
+    assert abs(float(sh.last_loss) - float(sd.last_loss)) < 1e-5
