@@ -53,7 +53,9 @@ class LocalNode:
     def __init__(self, device: Optional[str] = None, **code_defaults):
         self.code_defaults = code_defaults
         self.cfg: Optional[Dict[str, Any]] = None
-        self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        # explicit device, else the site input's `gpus` (resolved in _setup)
+        self._device_arg = device
+        self.device = torch.device(device) if device else torch.device("cpu")
         self.trainer = None
         self.engine = None
         self.it = None
@@ -62,6 +64,9 @@ class LocalNode:
     def _setup(self, inp: Dict[str, Any], state: Dict[str, Any]):
         self.state = state
         self.cfg = build_config(site_input=inp, **self.code_defaults)
+        if not self._device_arg:
+            from ..parallel.group import resolve_device
+            self.device = resolve_device(self.cfg.get("gpus"))
         self.site = state.get("clientId", "local0")
         T, D, H = get_task(self.cfg["task_id"])
         self.Trainer, self.Dataset = T, D

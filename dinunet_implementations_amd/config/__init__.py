@@ -62,7 +62,9 @@ FRAMEWORK_DEFAULTS: Dict[str, Any] = {
     "metric_direction": "maximize",
     "log_header": "loss|auc",
     "seed": 0,
-    "gpus": [],
+    # GPU ids of a site (inputspec "gpus"): None = this process's GPU, [] = CPU, [k] = GPU k
+    # (parallel.group.resolve_device)
+    "gpus": None,
     # rank-dAD / PowerSGD knobs (compspec.json:236-238, 268-270)
     "dad_reduction_rank": 10,
     "dad_num_pow_iters": 5,

@@ -12,8 +12,9 @@
 //   register shuffle.
 // * Small/skinny problems (the ICA shapes: M = B*S = 3136, N <= 1536) use 64x64 tiles to put
 //   >= 200 workgroups on the 256 CUs; long-K weight-gradient GEMMs (K = B*S) split K across
-//   workgroups into fp32 slabs reduced by a second, deterministic kernel (no float atomics, so
-//   every site computes bit-identical gradients for identical inputs).
+//   workgroups into fp32 slabs, combined in a fixed split order (no float atomics, so every site
+//   computes bit-identical gradients for identical inputs) either inside the launch by each
+//   tile's last-arriving split (GemmGroup::cnt) or by a second reduce kernel.
 // * Epilogue: bias add, ReLU, accumulate (beta), fp32 or bf16 store, optional row permutation
 //   (used to emit LSTM gate-permuted rows straight into the reference [i|f|o|g] layout).
 #include "common.h"
@@ -236,7 +237,89 @@ struct GemmGroup {
   int n, splits;
   int vec;  // every operand satisfies stage_load_vec's alignment contract
   int vepi;  // every problem can take the LDS-staged vector epilogue (see gemm_dma_kernel)
+  // split-K arrival tickets, one per output tile of the launch (zero between launches: each
+  // tile's combining workgroup resets its own); null -> gemm_splitk_reduce combines
+  int* cnt;
 };
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+// Split-K epilogue of one workgroup (cdna_hip_programming §5, in-launch split-K reduction, sc1
+// form): its fp32 partial goes to the slab with write-through (sc1) stores; every wave drains;
+// one lane draws an arrival ticket; the workgroup drawing splits-1 is the tile's combiner: it
+// resets the ticket, reads the other splits' partials with sc1 loads and sums all of them in
+// split order 0..S-1 (its own from registers), so the result does not depend on arrival order.
+// `flag`: one int of the kernel's (single) LDS array, free after the K loop.
+template <int FM, int FN, int WM, int WN>
+__device__ __forceinline__ void splitk_epilogue(const GemmGroup& g, const GemmProb& P,
+                                                const f32x4 (&acc)[FM][FN], int gtile, int row0,
+                                                int col0, int wm, int wn, int lane, int* flag) {
+  const int M = P.M, N = P.N, z = blockIdx.z;
+  float* slab = P.slab;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = col0 + wn * WN + 16 * j + (lane & 15);
+      if (col >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= M) continue;
+        __hip_atomic_store((gu32*)(slab + ((long)z * M + row) * N + col),
+                           __builtin_bit_cast(unsigned, acc[i][j][r]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add((gu32*)(g.cnt + gtile), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == (unsigned)(g.splits - 1);
+    if (last) __hip_atomic_store((gu32*)(g.cnt + gtile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nst = P.epi.ncol > 0 ? min(N, P.epi.ncol) : N;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = col0 + wn * WN + 16 * j + (lane & 15);
+      float part[4][8];  // the other splits' partials, all loads issued before any use
+      const int ns = g.splits < 8 ? g.splits : 8;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
+        const bool ok = row < M && col < nst;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+          part[r][s] = (ok && s < ns && s != z)
+                           ? __builtin_bit_cast(float, __hip_atomic_load(
+                                 (gu32*)(slab + ((long)s * M + row) * N + col), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT))
+                           : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= M || col >= nst) continue;
+        float v = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+          if (s < ns) v += s == z ? acc[i][j][r] : part[r][s];
+        for (int s = 8; s < g.splits; ++s)
+          v += s == z ? acc[i][j][r]
+                      : __builtin_bit_cast(float, __hip_atomic_load(
+                            (gu32*)(slab + ((long)s * M + row) * N + col), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT));
+        epi_store(P.epi, P.C, P.ldc, row, col, v);
+      }
+    }
+}
 
 __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int row, int col, float v) {
   v *= epi.alpha;
@@ -359,6 +442,12 @@ gemm_kernel(GemmGroup g) {
 #undef Bs
   // epilogue
   float* slab = P.slab;
+  if (slab && g.cnt) {
+    asm volatile("s_barrier" ::: "memory");  // the last tile's LDS reads are done: reuse smem
+    splitk_epilogue<T::FM, T::FN, T::WM, T::WN>(g, P, acc, gtile, row0, col0, wm, wn, lane,
+                                                reinterpret_cast<int*>(smem));
+    return;
+  }
   const int nst = (slab || P.epi.ncol <= 0) ? N : min(N, P.epi.ncol);
 #pragma unroll
   for (int i = 0; i < T::FM; ++i)
@@ -641,6 +730,11 @@ gemm_dma_kernel(GemmGroup g) {
     return;
   }
   float* slab = P.slab;
+  if (slab && g.cnt) {
+    splitk_epilogue<FM, FN, WM, WN>(g, P, acc, gtile, row0, col0, wm, wn, lane,
+                                    reinterpret_cast<int*>(smem));
+    return;
+  }
   const int nst = (slab || P.epi.ncol <= 0) ? N : min(N, P.epi.ncol);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -782,7 +876,7 @@ int launch(GemmGroup& g, hipStream_t st) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, true>), grid, dim3(256), 0, st, g);
   else
     hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, false>), grid, dim3(256), 0, st, g);
-  if (g.splits > 1) {
+  if (g.splits > 1 && !g.cnt) {
     const long t4 = elems / 4;
     const int blocks = (int)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g);
@@ -838,6 +932,15 @@ DN_API int dn_gemm_set_dma(int on) {
   return DN_OK;
 }
 
+// Output tiles of a launch (the split-K ticket count `counters` must provide): 64x64 tiles
+// (tile 0) or 128x128 (tile 1) summed over the problems.
+DN_API long dn_gemm_tiles(int n, const int* M, const int* N, int tile) {
+  const int b = tile == 1 ? 128 : 64;
+  long t = 0;
+  for (int i = 0; i < n; ++i) t += (long)((M[i] + b - 1) / b) * ((N[i] + b - 1) / b);
+  return t;
+}
+
 // Returns the fp32 slab elements the caller must provide for a split-K launch (0 if none).
 DN_API long dn_gemm_workspace(int M, int N, int K, int splits) {
   return splits > 1 ? (long)splits * M * N : 0;
@@ -847,10 +950,12 @@ DN_API long dn_gemm_workspace(int M, int N, int K, int splits) {
 DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, int b_bf16, int tb,
                    long ldb, void* C, int c_bf16, long ldc, int M, int N, int K, float alpha,
                    float beta, const float* bias, int relu, const int* row_map, int tile,
-                   int splits, float* slab, const void* mask, long ldm, hipStream_t st) {
+                   int splits, float* slab, const void* mask, long ldm, int* counters,
+                   hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
+  g.cnt = splits > 1 ? counters : nullptr;
   g.n = 1;
   g.splits = splits > 1 ? splits : 1;
   GemmProb& P = g.p[0];
@@ -874,10 +979,11 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
                            const void* const* bias, const void* const* row_map,
                            const int* ncol, int relu,
                            int a_bf16, int b_bf16, int ta, int tb, int c_bf16, int tile,
-                           int splits, float* slab, hipStream_t st) {
+                           int splits, float* slab, int* counters, hipStream_t st) {
   if (n < 1 || n > GMAX) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
+  g.cnt = splits > 1 ? counters : nullptr;
   g.n = n;
   g.splits = splits > 1 ? splits : 1;
   long soff = 0;

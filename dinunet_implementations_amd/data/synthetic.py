@@ -138,7 +138,7 @@ def make_ica_sites(root: str, sites: int = 2, subjects: Sequence[int] = (64, 64)
             w.writerow(["data_index", "label"])
             w.writerows([[i, int(v)] for i, v in enumerate(y)])
         specs.append({"task_id": {"value": "ICA-Classification"}, "mode": {"value": "train"},
-                      "gpus": {"value": [0]}, "num_class": {"value": 2},
+                      "gpus": {"value": [s]}, "num_class": {"value": 2},
                       "learning_rate": {"value": 0.001}, "data_file": {"value": "ica_data.npy"},
                       "labels_file": {"value": "labels.csv"}, "input_size": {"value": input_size},
                       "hidden_size": {"value": hidden_size}, "window_size": {"value": window_size},

@@ -22,11 +22,32 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_int, _lib.c_int, _lib.c_long, _lib.c_void_p, _lib.c_int,
                           _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_float,
                           _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
-                          _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p])
+                          _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p,
+                          _lib.c_void_p])
 
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
 _lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 14 + [_lib.c_int] * 8
-              + [_lib.c_void_p, _lib.c_void_p])
+              + [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p])
+
+# Split-K partials are combined inside the GEMM launch by each tile's last-arriving workgroup
+# (csrc/kernels/gemm.hip splitk_epilogue); DINUNET_SPLITK_REDUCE=1 keeps the separate reduce
+# kernel instead.  The arrival tickets live in one persistent zeroed buffer per device (each
+# combiner resets its ticket, so the buffer is all-zero between launches); launches that use it
+# must not overlap in time, which holds for the one-stream training step.
+_SPLITK_INLAUNCH = __import__("os").environ.get("DINUNET_SPLITK_REDUCE", "0") != "1"
+_TICKETS = {}
+
+
+def _tickets(device, tiles: int) -> Optional[Tensor]:
+    if not _SPLITK_INLAUNCH:
+        return None
+    t = _TICKETS.get(device)
+    if t is None or t.numel() < tiles:
+        if torch.cuda.is_current_stream_capturing():
+            return None  # cannot allocate a zeroed buffer inside a capture: reduce kernel
+        t = torch.zeros(max(tiles, 4096), dtype=torch.int32, device=device)
+        _TICKETS[device] = t
+    return t
 
 _NCU = 256
 GMAX = 12  # problems per grouped launch (csrc/kernels/gemm.hip)
@@ -136,9 +157,11 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
     auto_tile, auto_splits = choose_tiling(M, N, K)
     tile = auto_tile if tile is None else int(tile)
     sp = auto_splits if splits is None else max(1, int(splits))
-    slab = None
+    slab = cnt = None
     if sp > 1:
         slab = torch.empty(sp * M * N, dtype=torch.float32, device=a.device)
+        b_ = 128 if tile == 1 else 64
+        cnt = _tickets(a.device, -(-M // b_) * -(-N // b_))
     if bias is not None:
         bias = bias.float().contiguous()
     if row_map is not None:
@@ -150,7 +173,8 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
               int(B.dtype == torch.bfloat16), tb, ldb, out.data_ptr(),
               int(out.dtype == torch.bfloat16), out.stride(0), M, N, K, float(alpha), float(beta),
               _lib.ptr(bias), int(relu), _lib.ptr(row_map), tile, sp, _lib.ptr(slab),
-              _lib.ptr(mask), mask.stride(0) if mask is not None else 0, _lib.stream())
+              _lib.ptr(mask), mask.stride(0) if mask is not None else 0, _lib.ptr(cnt),
+              _lib.stream())
     return out
 
 
@@ -234,10 +258,12 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         splits = _split_rule(t128, maxk, per_cu=8) if tile == 1 else _split_rule(t64, maxk)
     sp = max(1, int(splits))
     dev = probs[0]["out"].device
-    slab = None
+    slab = cnt = None
     if sp > 1:
         slab = torch.empty(sp * sum(m * nn for m, nn in zip(arrs["M"], arrs["N"])),
                            dtype=torch.float32, device=dev)
+        b_ = 128 if tile == 1 else 64
+        cnt = _tickets(dev, sum(-(-m // b_) * -(-nn // b_) for m, nn in zip(arrs["M"], arrs["N"])))
     P = ctypes.c_void_p
     L = ctypes.c_long
     I = ctypes.c_int
@@ -248,7 +274,8 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               (I * n)(*arrs["K"]), (F * n)(*arrs["alpha"]), (F * n)(*arrs["beta"]),
               (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), (I * n)(*arrs["ncol"]), 0,
               int(a_bf), int(b_bf), ta, tb,
-              int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.stream())
+              int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.ptr(cnt),
+              _lib.stream())
 
 
 # Plain GEMMs (bf16 operands, no row map) run on csrc/kernels/gemm.hip's LDS-DMA kernel, which

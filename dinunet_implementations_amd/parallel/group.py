@@ -105,8 +105,47 @@ class SiteGroup:
 _GROUP: Optional[SiteGroup] = None
 
 
+def resolve_device(gpus=None, local_rank: int = 0, world: int = 1, backend: Optional[str] = None,
+                   n_devices: Optional[int] = None) -> torch.device:
+    """The device of a site from its ``gpus`` input (the reference's "GPU IDs to use",
+    ``datasets/icalstm/inputspec.json:6-10``: site 0 -> ``[0]``, site 1 -> ``[1]``;
+    ``datasets/test_fsl/inputspec.json:15-17``: ``[]`` = CPU-only FreeSurfer sites).
+
+    * ``None`` (not given): this rank's GPU (``LOCAL_RANK``) when one exists, else the CPU;
+    * ``[]``: the CPU, as the reference;
+    * ``[k, ...]``: GPU ``k`` (one site = one MI355X: further ids are not used).  With RCCL every
+      site needs its own GPU, so ``k`` must equal ``LOCAL_RANK`` (one process per GPU); a site
+      listing another GPU is a configuration conflict and raises."""
+    if n_devices is None:
+        n_devices = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if gpus is None:
+        return torch.device("cuda", local_rank % n_devices) if n_devices else torch.device("cpu")
+    if isinstance(gpus, int):
+        gpus = [gpus]
+    ids = [int(g) for g in gpus]
+    if not ids:
+        return torch.device("cpu")
+    k = ids[0]
+    if not n_devices:
+        import warnings
+        warnings.warn(f"gpus={ids} but no GPU is visible: the site runs on the CPU", RuntimeWarning)
+        return torch.device("cpu")
+    if not 0 <= k < n_devices:
+        if backend == "nccl":
+            raise ValueError(f"gpus={ids}: GPU {k} does not exist ({n_devices} visible)")
+        # several sites rehearsed on fewer GPUs (gloo, the in-process simulator): wrap around
+        import warnings
+        warnings.warn(f"gpus={ids}: GPU {k} does not exist ({n_devices} visible); using GPU "
+                      f"{k % n_devices}", RuntimeWarning)
+        k %= n_devices
+    if world > 1 and backend == "nccl" and k != local_rank:
+        raise ValueError(f"gpus={ids} conflicts with LOCAL_RANK={local_rank}: with RCCL each "
+                         f"site's process owns GPU LOCAL_RANK (site r -> gpus [r])")
+    return torch.device("cuda", k)
+
+
 def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
-               timeout_s: Optional[int] = None) -> SiteGroup:
+               timeout_s: Optional[int] = None, gpus=None) -> SiteGroup:
     """Initialise from torchrun-style env vars; world 1 when they are absent.
 
     ``timeout_s`` (default ``DINUNET_PG_TIMEOUT``, else 1800 s) bounds every collective: a site
@@ -119,12 +158,17 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    want_gpu = device != "cpu" and torch.cuda.is_available()
-    if want_gpu:
-        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
-        dev = torch.device("cuda", torch.cuda.current_device())
-    else:
+    if device == "cpu":
         dev = torch.device("cpu")
+    elif device not in (None, "", "auto", "cuda"):
+        dev = torch.device(device)  # an explicit device wins over the site input
+    else:
+        # the site input's `gpus` picks the device (None: this rank's GPU); with RCCL it must
+        # be GPU LOCAL_RANK
+        be0 = backend or os.environ.get("DINUNET_BACKEND") or "nccl"
+        dev = resolve_device(gpus, local, world, be0)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
     # DINUNET_BACKEND=gloo rehearses the multi-site GPU path with several ranks on ONE GPU
     # (RCCL needs one device per rank); production multi-GPU runs use nccl (= RCCL)
     be = backend or os.environ.get("DINUNET_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")

@@ -57,7 +57,8 @@ def main(argv=None):
     site_in = specs[rank % len(specs)]
     cfg = build_config(site_input=site_in, overrides=parse_sets(a.set))
     apply_collective_plan(cfg)  # before the communicator exists
-    grp = init_sites(device=a.device, timeout_s=cfg.get("collective_timeout_s"))
+    grp = init_sites(device=a.device, timeout_s=cfg.get("collective_timeout_s"),
+                     gpus=cfg.get("gpus"))
     base = os.path.join(a.data_path, "input", f"local{grp.rank}", "simulatorRun")
     if not os.path.isdir(base):
         base = os.path.join(a.data_path, "input", f"local{grp.rank % len(specs)}", "simulatorRun")

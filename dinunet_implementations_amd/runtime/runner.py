@@ -57,8 +57,9 @@ class SiteRunner:
     def run(self, trainer_cls, dataset_cls, datahandle_cls):
         import torch
         cfg = self.config(trainer_cls)
-        dev = self.device or ("cuda" if torch.cuda.is_available() and cfg.get("gpus", []) != [] else "cpu")
-        group = SiteGroup(device=torch.device(dev))
+        from ..parallel.group import resolve_device
+        dev = torch.device(self.device) if self.device else resolve_device(cfg.get("gpus"))
+        group = SiteGroup(device=dev)
         site = FederatedSite(cfg, group, trainer_cls, dataset_cls, datahandle_cls, self.state(),
                              self.out_dir, site_name=f"local{self.site_index}")
         return site.run()

@@ -404,3 +404,26 @@ def test_ica_wide_hidden_runs_fused(monkeypatch):
         ref_logits, _ = m(x)
     assert logits.shape == (4, 2)
     assert rel(logits, ref_logits) < 5e-2
+
+
+@pytest.mark.parametrize("splits", [2, 3, 4, 11])
+def test_gemm_splitk_in_launch_combine_matches_reduce_kernel(splits, monkeypatch):
+    """Split-K partials combined inside the launch by each tile's last-arriving workgroup equal
+    the separate reduce kernel's result (same split order; bitwise up to 4 splits) and leave the
+    arrival tickets all zero for the next launch."""
+    from dinunet_implementations_amd.ops import gemm as G
+    torch.manual_seed(5)
+    a = torch.randn(3136, 384, device="cuda").to(torch.bfloat16)
+    b = torch.randn(3136, 520, device="cuda").to(torch.bfloat16)
+    monkeypatch.setattr(G, "_SPLITK_INLAUNCH", True)
+    r1 = G.mm(a, b, trans_a=True, splits=splits)
+    r1b = G.mm(a, b, trans_a=True, splits=splits)
+    torch.cuda.synchronize()
+    assert int(G._TICKETS[a.device].abs().sum()) == 0
+    monkeypatch.setattr(G, "_SPLITK_INLAUNCH", False)
+    r2 = G.mm(a, b, trans_a=True, splits=splits)
+    ref = a.float().t() @ b.float()
+    assert torch.equal(r1, r1b)
+    if splits <= 4:
+        assert torch.equal(r1, r2)
+    assert (r1 - ref).abs().max() < 1e-2 * ref.abs().max()

@@ -8,7 +8,17 @@ identical; any divergence means two ranks applied different updates.
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
         tools/multirank_check.py --engine dSGD --precision 16 --ragged --accum 2
 
-Prints one JSON line (rank 0); exit status 0 iff all ranks are bit-identical.
+Prints one JSON line (rank 0); exit status 0 iff all ranks are bit-identical (and, with
+``--oracle``, the N-rank result matches the single-process oracle).
+
+``--oracle``: rank 0 also replays the whole run in-process as the reference semantics of dSGD
+(SURVEY.md E10): for every step it computes EACH site's gradient on that site's batches (the same
+generators, the same ragged batch), averages them in fp64 in site order, and applies the same
+fused Adam.  Agreement is judged on the parameter UPDATE (final - initial): the relative L2 error
+of the N-rank update against the oracle's is reported (``update_rel_err``) and, at
+``--precision 32``, must stay below ``--oracle-tol``; at 16 bits it measures what the payload
+precision costs.  (Bit-identical replicas alone would also pass if every rank applied the same
+WRONG update.)
 """
 import argparse
 import json
@@ -34,6 +44,8 @@ def main():
     ap.add_argument("--overlap", type=int, default=1, help="dSGD all-reduce under the backward")
     ap.add_argument("--diag", action="store_true", help="report dSGD gradient-ready counts")
     ap.add_argument("--split", type=int, default=-1, help="-1: TrainStep's default")
+    ap.add_argument("--oracle", action="store_true", help="compare with the fp64-mean oracle")
+    ap.add_argument("--oracle-tol", type=float, default=1e-3)
     a = ap.parse_args()
 
     import torch
@@ -48,6 +60,7 @@ def main():
     m = ICALstm(input_size=128, hidden_size=384, num_comps=50, window_size=10).to(dev).train()
     m.classifier[0].p = 0.0
     flat = FlatParams(m.parameters())
+    init = flat.data.detach().clone()
     opt = FusedAdam(flat, lr=1e-3)
     cfg = {"precision_bits": a.precision, "dad_reduction_rank": 8, "powersgd_rank": 4, "seed": 5,
            "dsgd_overlap": bool(a.overlap)}
@@ -70,13 +83,19 @@ def main():
         eng._hooks = [p.register_post_accumulate_grad_hook(spy) for p in m.parameters()]
     step = TrainStep(m, flat, opt, eng, task="ica", use_graph=bool(a.graph), accum=a.accum,
                      split=None if a.split < 0 else bool(a.split))
-    g = torch.Generator(device=dev).manual_seed(100 + grp.rank)  # site-specific data
     n_micro = a.steps * a.accum
     ragged_at = (n_micro // 2) // a.accum * a.accum + a.accum - 1  # a last micro-batch
-    for i in range(n_micro):
-        B = a.batch - 5 if (a.ragged and grp.rank == 1 and i == ragged_at) else a.batch
-        x = torch.randn(B, a.seq, 50, 10, device=dev, generator=g)
-        y = torch.randint(0, 2, (B,), device=dev, generator=g)
+
+    def site_batches(rank):
+        """The micro-batches site ``rank`` trains on, in order (its own generator)."""
+        g = torch.Generator(device=dev).manual_seed(100 + rank)  # site-specific data
+        for i in range(n_micro):
+            B = a.batch - 5 if (a.ragged and rank == 1 and i == ragged_at) else a.batch
+            x = torch.randn(B, a.seq, 50, 10, device=dev, generator=g)
+            y = torch.randint(0, 2, (B,), device=dev, generator=g)
+            yield i, x, y
+
+    for i, x, y in site_batches(grp.rank):
         step(x, y, first=i % a.accum == 0, last=i % a.accum == a.accum - 1)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -88,6 +107,38 @@ def main():
            "accum": a.accum, "ragged": a.ragged, "graph": step.graph is not None,
            "split": bool(step.split), "steps": opt.step_count, "max_abs_diff": maxdiff,
            "param_sum": float(mine.double().sum())}
+    if a.oracle:
+        ok_o = torch.zeros(1, dtype=torch.float64, device=dev)
+        if grp.rank == 0:
+            torch.manual_seed(1234)
+            mo = ICALstm(input_size=128, hidden_size=384, num_comps=50, window_size=10).to(dev).train()
+            mo.classifier[0].p = 0.0
+            fo = FlatParams(mo.parameters())
+            oo = FusedAdam(fo, lr=1e-3)
+            assert torch.equal(fo.data, init)
+            sites = [site_batches(r) for r in range(grp.world)]
+            for _ in range(a.steps):
+                gsum = torch.zeros(fo.numel, dtype=torch.float64, device=dev)
+                for r in range(grp.world):
+                    fo.zero_grad()
+                    for _k in range(a.accum):
+                        _, x, y = next(sites[r])
+                        _, loss, _ = mo.forward_loss(x, y)
+                        (loss / a.accum).backward()
+                    gsum += fo.grad.double()
+                fo.grad.copy_((gsum / grp.world).float())
+                oo.step()
+            d_n = (flat.data - init).double()
+            d_o = (fo.data - init).double()
+            err = float((d_n - d_o).norm() / d_o.norm().clamp_min(1e-30))
+            res["update_rel_err"] = err
+            res["update_max_abs_err"] = float((d_n - d_o).abs().max())
+            res["update_norm"] = float(d_o.norm())
+            good = err <= a.oracle_tol if (a.precision == "32" and a.engine == "dSGD") else True
+            res["oracle_ok"] = bool(good)
+            ok_o.fill_(1.0 if good else 0.0)
+        grp.broadcast(ok_o, 0)
+        same = same and bool(ok_o.item() > 0.5)
     if a.diag:
         res["notify_counts_per_param"] = {k: v / n_micro for k, v in counts.items() if v != n_micro}
         res["params_never_notified"] = [n for n, _ in m.named_parameters() if n not in counts]
