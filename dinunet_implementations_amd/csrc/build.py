@@ -54,7 +54,9 @@ def _digest(paths, extra: str) -> str:
         deps.update(glob.glob(os.path.join(HERE, d, "*.h")))
     for p in sorted(deps):
         with open(p, "rb") as f:
-            h.update(p.encode())
+            # relative names: the digest must not depend on where the tree lives (the GPU box
+            # runs a copy at another path and checks the library against its sources)
+            h.update(os.path.relpath(p, HERE).encode())
             h.update(f.read())
     return h.hexdigest()
 
@@ -71,10 +73,22 @@ def _run(cmd):
     return r
 
 
+def _kernel_digest() -> str:
+    return _digest(_sources("hip"), " ".join(HIP_FLAGS) + ARCH + repr(sorted(FILE_FLAGS.items())))
+
+
+def kernels_stale() -> bool:
+    """True when the built kernel library does not match the kernel sources next to it (a build
+    that failed after a source edit leaves the previous library in place)."""
+    if not _sources("hip"):
+        return False  # sources stripped: nothing to compare against
+    return not _stamp_ok(KERNEL_LIB, _kernel_digest())
+
+
 def build_kernels(force: bool = False, jobs: int = 4, verbose: bool = True) -> str:
     srcs = _sources("hip")
     os.makedirs(OUT_DIR, exist_ok=True)
-    digest = _digest(srcs, " ".join(HIP_FLAGS) + ARCH + repr(sorted(FILE_FLAGS.items())))
+    digest = _kernel_digest()
     if not force and _stamp_ok(KERNEL_LIB, digest):
         return KERNEL_LIB
     objdir = os.path.join(OUT_DIR, "obj")

@@ -244,6 +244,24 @@ struct GemmGroup {
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 
+__device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int row, int col, float v) {
+  v *= epi.alpha;
+  if (epi.bias) v += epi.bias[col];
+  if (epi.relu) v = fmaxf(v, 0.f);
+  if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col] > 0.f)) v = 0.f;
+  const long orow = epi.row_map ? epi.row_map[row] : row;
+  if (orow < 0) return;  // dropped row (e.g. zero-padded LSTM units)
+  if (epi.out_bf16) {
+    bf16* cp = reinterpret_cast<bf16*>(C) + orow * ldc + col;
+    if (epi.beta != 0.f) v += epi.beta * (float)*cp;
+    *cp = (bf16)v;
+  } else {
+    float* cp = reinterpret_cast<float*>(C) + orow * ldc + col;
+    if (epi.beta != 0.f) v += epi.beta * *cp;
+    *cp = v;
+  }
+}
+
 // Split-K epilogue of one workgroup (cdna_hip_programming §5, in-launch split-K reduction, sc1
 // form): its fp32 partial goes to the slab with write-through (sc1) stores; every wave drains;
 // one lane draws an arrival ticket; the workgroup drawing splits-1 is the tile's combiner: it
@@ -256,6 +274,9 @@ __device__ __forceinline__ void splitk_epilogue(const GemmGroup& g, const GemmPr
                                                 int col0, int wm, int wn, int lane, int* flag) {
   const int M = P.M, N = P.N, z = blockIdx.z;
   float* slab = P.slab;
+  // write-through (sc1 = aux bit 4) buffer stores / L1-bypassing loads of the slab; the launcher
+  // guarantees splits * M * N * 4 < 2^31 (32-bit offsets)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -266,9 +287,10 @@ __device__ __forceinline__ void splitk_epilogue(const GemmGroup& g, const GemmPr
       for (int r = 0; r < 4; ++r) {
         const int row = row0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
         if (row >= M) continue;
-        __hip_atomic_store((gu32*)(slab + ((long)z * M + row) * N + col),
-                           __builtin_bit_cast(unsigned, acc[i][j][r]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        const float val = acc[i][j][r];  // (bit_cast of the vector-element lvalue itself
+                                         //  read element 0 for every r: clang, ROCm 7.2)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs,
+                                              4 * ((z * M + row) * N + col), 0, 16);
       }
     }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -298,9 +320,8 @@ __device__ __forceinline__ void splitk_epilogue(const GemmGroup& g, const GemmPr
 #pragma unroll
         for (int s = 0; s < 8; ++s)
           part[r][s] = (ok && s < ns && s != z)
-                           ? __builtin_bit_cast(float, __hip_atomic_load(
-                                 (gu32*)(slab + ((long)s * M + row) * N + col), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT))
+                           ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                 rs, 4 * ((s * M + row) * N + col), 0, 16))
                            : 0.f;
       }
 #pragma unroll
@@ -313,31 +334,13 @@ __device__ __forceinline__ void splitk_epilogue(const GemmGroup& g, const GemmPr
           if (s < ns) v += s == z ? acc[i][j][r] : part[r][s];
         for (int s = 8; s < g.splits; ++s)
           v += s == z ? acc[i][j][r]
-                      : __builtin_bit_cast(float, __hip_atomic_load(
-                            (gu32*)(slab + ((long)s * M + row) * N + col), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT));
+                      : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                            rs, 4 * ((s * M + row) * N + col), 0, 16));
         epi_store(P.epi, P.C, P.ldc, row, col, v);
       }
     }
 }
 
-__device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int row, int col, float v) {
-  v *= epi.alpha;
-  if (epi.bias) v += epi.bias[col];
-  if (epi.relu) v = fmaxf(v, 0.f);
-  if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col] > 0.f)) v = 0.f;
-  const long orow = epi.row_map ? epi.row_map[row] : row;
-  if (orow < 0) return;  // dropped row (e.g. zero-padded LSTM units)
-  if (epi.out_bf16) {
-    bf16* cp = reinterpret_cast<bf16*>(C) + orow * ldc + col;
-    if (epi.beta != 0.f) v += epi.beta * (float)*cp;
-    *cp = (bf16)v;
-  } else {
-    float* cp = reinterpret_cast<float*>(C) + orow * ldc + col;
-    if (epi.beta != 0.f) v += epi.beta * *cp;
-    *cp = v;
-  }
-}
 
 template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe, bool VEC>
 __global__ void __launch_bounds__(256)
@@ -955,7 +958,7 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   if (M <= 0 || N <= 0 || K <= 0) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
-  g.cnt = splits > 1 ? counters : nullptr;
+  g.cnt = splits > 1 && (long)splits * M * N < (1L << 29) ? counters : nullptr;
   g.n = 1;
   g.splits = splits > 1 ? splits : 1;
   GemmProb& P = g.p[0];
@@ -997,6 +1000,7 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
     P.kchunk = kchunk_for(K[i], sp);
     P.slab = g.splits > 1 ? slab + soff : nullptr;
     soff += (long)g.splits * M[i] * N[i];
+    if ((long)g.splits * M[i] * N[i] >= (1L << 29)) g.cnt = nullptr;  // 32-bit slab offsets
     P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16,
                 ncol ? ncol[i] : 0, nullptr, 0};
   }

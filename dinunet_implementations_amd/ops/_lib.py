@@ -61,6 +61,18 @@ def _load() -> Optional[ctypes.CDLL]:
         if not os.path.exists(LIB_PATH):
             _load_error = _load_error or f"{LIB_PATH} not built (python -m dinunet_implementations_amd.csrc.build)"
             return None
+        if os.environ.get("DINUNET_ALLOW_STALE", "0") != "1":
+            # a library older than its sources has an older C ABI: calling it through the
+            # current signatures passes arguments in the wrong slots (e.g. a null stream)
+            try:
+                from ..csrc import build
+                stale = build.kernels_stale()
+            except Exception:  # pragma: no cover
+                stale = False
+            if stale:
+                _load_error = (f"{LIB_PATH} is stale: the kernel sources changed since it was built "
+                               "(python -m dinunet_implementations_amd.csrc.build)")
+                return None
         try:
             lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         except OSError as e:
