@@ -265,22 +265,29 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
   for (int s = 0; s < NSL; ++s)
     uu[s] = 16 * (UG * w + s / NSL1) + 4 * (r + (s % NSL1) * G16) + q;
   // Every per-step global access goes through a buffer descriptor with a 32-bit per-lane byte
-  // offset (host guarantees every buffer < 2 GiB): the step part of an address is one scalar
-  // multiply, no 64-bit address math per access.  Gate pre-activation stores of padded rows
-  // (b >= B) get an out-of-range offset and are dropped (no branch, see common.h); without a
-  // backward the descriptor has no records and every such store is dropped.
+  // offset: the step part of an address is one scalar multiply, no 64-bit address math per
+  // access.  The descriptors are based at THIS workgroup's first batch row (64-bit base), so an
+  // offset spans only its BR rows -- any batch size fits (a global base capped the recurrence
+  // at B * S * ndir * 4 * HD * 4 < 2 GiB, B ~ 3,500 at the headline geometry).  Gate
+  // pre-activation stores of padded rows (b >= B) get an out-of-range offset and are dropped (no
+  // branch, see common.h); without a backward the descriptor has no records and every such store
+  // is dropped.
   const int rowXi = ndir * 4 * HD;
-  const __amdgpu_buffer_rsrc_t x_rs = dn_rsrc(xp, (uint32_t)(B * S * rowXi * 2));
-  const __amdgpu_buffer_rsrc_t pre_rs = dn_rsrc(pre, pre ? (uint32_t)(B * S * rowXi * 4) : 0u);
-  const __amdgpu_buffer_rsrc_t c_rs = dn_rsrc(c_save, (uint32_t)(ndir * Bp * S * HD * 4));
-  const __amdgpu_buffer_rsrc_t hp_rs = dn_rsrc(hprev, (uint32_t)(ndir * Bp * S * HD * 2));
+  const int b0 = blockIdx.x * BR;                 // first batch row of this workgroup (< B)
+  const int nrow = B - b0 < BR ? B - b0 : BR;     // its valid rows
+  const __amdgpu_buffer_rsrc_t x_rs = dn_rsrc(xp + (long)b0 * S * rowXi, (uint32_t)(nrow * S * rowXi * 2));
+  const __amdgpu_buffer_rsrc_t pre_rs =
+      dn_rsrc(pre ? pre + (long)b0 * S * rowXi : pre, pre ? (uint32_t)(nrow * S * rowXi * 4) : 0u);
+  const long cb0 = ((long)dir * Bp + b0) * S * HD;  // [ndir][Bp][S][HD] images
+  const __amdgpu_buffer_rsrc_t c_rs = dn_rsrc(c_save + cb0, (uint32_t)(BR * S * HD * 4));
+  const __amdgpu_buffer_rsrc_t hp_rs = dn_rsrc(hprev + cb0, (uint32_t)(BR * S * HD * 2));
   uint32_t xo[NSL], po[NSL], co[NSL], ho[NSL];  // per-lane byte offsets at time index 0
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
-    xo[s] = (uint32_t)((bc * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 2);
-    po[s] = b < B ? (uint32_t)((b * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 4) : DN_OOB;
-    co[s] = (uint32_t)((((dir * Bp + b) * S) * HD + uu[s]) * 4);
-    ho[s] = (uint32_t)((((dir * Bp + b) * S) * HD + uu[s]) * 2);
+    xo[s] = (uint32_t)(((bc - b0) * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 2);
+    po[s] = b < B ? (uint32_t)(((b - b0) * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 4) : DN_OOB;
+    co[s] = (uint32_t)((((b - b0) * S) * HD + uu[s]) * 4);
+    ho[s] = (uint32_t)((((b - b0) * S) * HD + uu[s]) * 2);
   }
   const uint32_t xstep = (uint32_t)(rowXi * 2);  // bytes per time index (bf16 projection)
   const uint32_t pstep = (uint32_t)(rowXi * 4);  // (fp32 pre-activations)
@@ -1075,10 +1082,12 @@ DN_API int dn_lstm_pack_gather(const float* wih0, const float* bih0, const float
 // rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
 DN_API int dn_lstm_rows_per_wg(int B, int Hd) { return pick_br(B, dn_lstm_padded_hidden(Hd)); }
 
-// every per-step access of the recurrences is a 32-bit buffer offset
+// the forward's per-workgroup buffer descriptors span BR rows (32-bit offsets); the backward
+// addresses with 64-bit pointers.  Only a single sequence longer than the descriptors can hold
+// (BR * S * ndir * 4 * HD * 4 >= 2 GiB, S in the millions) is refused.
 static bool lstm_fits_32bit(int B, int S, int HD, int ndir, int BR) {
-  const long Bp = (B + BR - 1) / BR * (long)BR;
-  return (long)Bp * S * ndir * 4 * HD * 4 < (1L << 31);
+  (void)B;
+  return (long)BR * S * ndir * 4 * HD * 4 < (1L << 31);
 }
 
 // xp: the bf16 input projection [B*S][ndir][4*HD]; pre (fp32, same layout, or null when no

@@ -72,7 +72,7 @@ class LSTM(nn.Module):
     def fused_ok(self, x: torch.Tensor) -> bool:
         return (self.use_fused and x.is_cuda and self.bias
                 and ops.lstm_supported(x.shape[0], self.input_size, self.hidden_size,
-                                       self.num_direction))
+                                       self.num_direction, seq=x.shape[1]))
 
     def prepack(self, device, side: bool = True, casts=(), cast_out=None):
         """Pack the LSTM weights into the kernel layouts ahead of the forward (on the side

@@ -72,8 +72,16 @@ def padded_hidden(hd: int) -> int:
     return 0
 
 
-def lstm_supported(batch: int, input_size: int, hidden: int, ndir: int) -> bool:
-    return padded_hidden(hidden) > 0 and ndir in (1, 2) and batch > 0 and input_size > 0
+def lstm_supported(batch: int, input_size: int, hidden: int, ndir: int,
+                   seq: Optional[int] = None) -> bool:
+    """Shapes the persistent kernels take: per-direction hidden <= 512, any batch (the forward's
+    buffer descriptors are based per workgroup), and a sequence whose per-workgroup span fits the
+    descriptors' 32-bit offsets (<= 16 rows x S x ndir x 4 HD fp32 < 2 GiB: S < 8,192 at
+    HD = 512, < 21,845 at HD = 192)."""
+    HD = padded_hidden(hidden)
+    if not (HD > 0 and ndir in (1, 2) and batch > 0 and input_size > 0):
+        return False
+    return seq is None or 16 * seq * ndir * 4 * HD * 4 < (1 << 31)
 
 
 def _row_map(Hd: int, HD: int, device) -> Tensor:

@@ -136,6 +136,16 @@ def test_gemm_splitk_deterministic():
     assert rel(r1, bf(a).t() @ bf(b)) < 2e-3
 
 
+def _record_errs(kind, case, errs):
+    """Observed relative errors -> $DINUNET_ERR_LOG (jsonl) when set (profiles/r3_lstm_errors)."""
+    import json
+    import os
+    path = os.environ.get("DINUNET_ERR_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"kind": kind, **case, **{k: round(v, 6) for k, v in errs.items()}}) + "\n")
+
+
 def _lstm_params(I, Hd, ndir, scale=0.1):
     ps = []
     for _ in range(ndir):
@@ -154,6 +164,10 @@ def _lstm_params(I, Hd, ndir, scale=0.1):
     (16, 20, 64, 256, 2, "mean"),
     (9, 13, 48, 300, 2, "seq"),
     (6, 11, 32, 512, 1, "mean"),
+    # batches past the former 2 GiB single-descriptor ceiling (B ~ 3,566 at S = 98, Hd = 192):
+    # the forward's buffer descriptors are based per workgroup
+    (4096, 98, 64, 192, 2, "mean"),
+    (8192, 6, 32, 192, 2, "mean"),
 ])
 def test_lstm_fwd_bwd_matches_reference(B, S, I, Hd, ndir, mode):
     from dinunet_implementations_amd.ops import reference as ref
@@ -167,15 +181,21 @@ def test_lstm_fwd_bwd_matches_reference(B, S, I, Hd, ndir, mode):
     hs, (rh, rc) = ref.bilstm(xr, ps_r, bidirectional=ndir == 2)
     ro = hs.mean(1) if mode == "mean" else hs
     assert out.shape == ro.shape
-    assert rel(out, ro) < 2e-2
-    assert rel(hT, rh) < 3e-2 and rel(cT, rc) < 3e-2
+    errs = {"out": rel(out, ro), "hT": rel(hT, rh), "cT": rel(cT, rc)}
+    assert errs["out"] < 2e-2
+    assert errs["hT"] < 3e-2 and errs["cT"] < 3e-2
     g = torch.randn_like(out)
     (out * g).sum().backward()
     (ro * g).sum().backward()
-    assert rel(x.grad, xr.grad) < 5e-2
-    for p, pr in zip(ps, ps_r):
-        for t, tr in zip(p, pr):
-            assert rel(t.grad, tr.grad) < 5e-2, (t.shape, rel(t.grad, tr.grad))
+    errs["dx"] = rel(x.grad, xr.grad)
+    for d, (p, pr) in enumerate(zip(ps, ps_r)):
+        for name, t, tr in zip(("w_ih", "b_ih", "w_hh", "b_hh"), p, pr):
+            errs[f"d{name}{d}"] = rel(t.grad, tr.grad)
+    _record_errs("lstm", dict(B=B, S=S, I=I, Hd=Hd, ndir=ndir, mode=mode), errs)
+    assert errs["dx"] < 5e-2
+    for k, v in errs.items():
+        if k.startswith("d"):
+            assert v < 5e-2, (k, v)
 
 
 def test_linear_bias_relu_grad():
