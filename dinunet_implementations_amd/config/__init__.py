@@ -77,6 +77,9 @@ FRAMEWORK_DEFAULTS: Dict[str, Any] = {
     "rccl_algo": None,
     "rccl_proto": None,
     "collective_timeout_s": 1800,
+    # the non-pretraining sites' wait for the pretraining site (not a collective: see
+    # runtime.site.FederatedSite._await_pretrain)
+    "pretrain_timeout_s": 7 * 86400,
     # "fused": gfx950 kernels (bf16 MFMA operands, fp32 accumulation / state);
     # "reference": the fp32 oracle math of ops/reference.py on the same device (fidelity baseline)
     "compute_path": "fused",

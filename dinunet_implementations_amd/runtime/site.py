@@ -278,6 +278,9 @@ class FederatedSite:
         logs["pretrain_site"] = f"local{src}"
         pa = dict(self.cfg.get("pretrain_args") or {})
         if self.group.rank == src and int(pa.get("epochs", 0)) > 0:
+            delay = float(os.environ.get("DINUNET_PRETRAIN_DELAY_S", "0") or 0)
+            if delay > 0:  # tests: a pretraining phase longer than the collective timeout
+                time.sleep(delay)
             pcfg = copy.deepcopy(self.cfg)
             pcfg.update(pa)
             from ..parallel import DSGDEngine
@@ -290,9 +293,32 @@ class FederatedSite:
             b = self._train_epochs(trainer, eng, data, pcfg, solo, fold_dir, seed, logs, tag="pretrain_")
             trainer.load_checkpoint(os.path.join(fold_dir, "pretrain_checkpoint_best.pt"))
             logs["pretrain_best_val_epoch"] = b["epoch"]
+        self._await_pretrain(src, fold_dir)
         self._broadcast_model(trainer, src)
         # fresh optimizer state for the federated phase
         trainer._init_optimizer()
+
+    def _await_pretrain(self, src: int, tag: str):
+        """The other sites wait for the pretraining site OUTSIDE the collectives: a wait inside
+        the weight broadcast would be bounded by ``collective_timeout_s`` (the failure detector's
+        clock), so a long pretraining phase would make every idle site time out.  They block on a
+        key the pretraining site sets in the process group's store, bounded by its own deadline
+        (``pretrain_timeout_s``); a dead pretraining site ends the wait with an error too (its
+        store connection drops, or the deadline passes)."""
+        g = self.group
+        if not g.distributed or g.pg is None:
+            return
+        if os.environ.get("DINUNET_PRETRAIN_STORE_WAIT", "1") == "0":
+            return  # negative control of tests/test_failure.py: wait inside the broadcast
+        import datetime
+        import torch.distributed as dist
+        store = dist.distributed_c10d._get_default_store()
+        key = "dinunet/pretrain_done/" + os.path.basename(os.path.normpath(tag))
+        if g.rank == src:
+            store.set(key, "1")
+        else:
+            timeout = float(self.cfg.get("pretrain_timeout_s") or 7 * 86400)
+            store.wait([key], datetime.timedelta(seconds=timeout))
 
     # ---- folds ------------------------------------------------------------------------------
     def run_fold(self, fold: int, split: Dict[str, List[Any]]) -> Dict[str, Any]:

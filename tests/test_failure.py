@@ -40,3 +40,37 @@ def test_dead_site_makes_survivor_exit_nonzero(fs_data_root, tmp_path):
     assert procs[0].returncode == 3, (procs[0].returncode, outs[0][1][-3000:])
     assert "site failure" in outs[0][1]
     assert elapsed < 90
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("store_wait", [True, False])
+def test_pretrain_longer_than_collective_timeout(fs_data_root, tmp_path, store_wait):
+    """The sites that do not pretrain wait for the pretraining site on the process group's store
+    (its own deadline), not inside the weight broadcast: a pretraining phase much longer than
+    ``collective_timeout_s`` (2 s here, pretraining held 8 s) must not make them time out."""
+    port = free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT,
+                   OMP_NUM_THREADS="1", DINUNET_PRETRAIN_DELAY_S="8",
+                   DINUNET_PRETRAIN_STORE_WAIT="1" if store_wait else "0")
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "dinunet_implementations_amd.run", "--data-path", fs_data_root,
+             "--out", str(tmp_path / "out"), "--device", "cpu", "--set", "epochs=2",
+             "--set", "pretrain=true", "--set", 'pretrain_args={"epochs": 1}',
+             "--set", "collective_timeout_s=2"],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        outs = [p.communicate(timeout=150) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    if not store_wait:  # negative control: the idle site's broadcast times out
+        assert procs[1].returncode == 3, (procs[1].returncode, outs[1][1][-3000:])
+        return
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, (r, p.returncode, outs[r][1][-3000:])
