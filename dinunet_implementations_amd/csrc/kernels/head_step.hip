@@ -40,6 +40,7 @@ constexpr int DXT_MAX = 2;   // dX 16-column tiles per column workgroup
 constexpr int DXN_MAX = 2;   // dX reduction steps (32 layer-0 outputs) per wave: outputs <= 256
 constexpr int DW0_MAX = 8;   // dW0 16x16 tiles per wave: layer-0 inputs <= 512
 constexpr int W1S_MAX = 8;   // dA1 reduction steps over layer-1 outputs: <= 256
+constexpr int W1T_MAX = 4;   // dW1 16-row tiles per wave (layer-1 outputs <= 256)
 constexpr int SPIN_MAX = 1 << 22;  // ~0.2 s of polling before a hand-off gives up
 
 // sync block (u32 words, one 128-B line each)
@@ -76,8 +77,8 @@ struct StepArgs {
   int nl, B, G0, ndx;      // ndx = 16-column tiles of dX
   long a1_off, dz1_off, dz0_off;  // workspace: published images (bf16)
   int SA1, SZ1, SZ0;       // their row strides (elements)
-  // column-workgroup LDS: input image, cross-wave reduction, dZ0 slice
-  int c_img, c_red, c_dzs;
+  // column-workgroup LDS: input image, cross-wave reduction, dZ0 slice, A1 slice, dZ1 image
+  int c_img, c_red, c_dzs, c_a1s, c_z1s;
   // tail LDS: logits + dlogits fp32 [SMP][16] each, labels [SMP]
   int t_logit, t_dlogit, t_y;
   int log_out;
@@ -142,6 +143,16 @@ __device__ __forceinline__ bf16x8 wcol_cvt(const float (&r)[8], int N, int K, in
   return f;
 }
 
+// LDS-only workgroup barrier: orders the waves and their LDS traffic WITHOUT waiting for the
+// wave's outstanding global stores (a __syncthreads is also a device-scope fence: every phase
+// that ended in a global store then waited a memory round trip at the barrier).  Global data
+// shared between waves of a workgroup goes through explicit waits / hand-offs instead.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ============================================================================================
 // column workgroup c: layer 0 for output columns 16c .. 16c+15
 // ============================================================================================
@@ -160,65 +171,18 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
   bf16* img = reinterpret_cast<bf16*>(smem + a.c_img);
   float* red = reinterpret_cast<float*>(smem + a.c_red);
   bf16* dzs = reinterpret_cast<bf16*>(smem + a.c_dzs);  // [SMP][24] dZ0 slice
+  bf16* a1s = reinterpret_cast<bf16*>(smem + a.c_a1s);  // [SMP][24] A1 slice (dW1)
+  bf16* z1s = reinterpret_cast<bf16*>(smem + a.c_z1s);  // [SMP][SZ1] dZ1 (dW1)
   const bool st = c == 0 && stamps;
   if (st) YSTAMP(0);
 
-  // ---- every global operand of the launch requested up front --------------------------------
   const int n = 16 * c + (lane & 15);  // this lane's layer-0 column (wave 0 epilogue)
   const bool cv = n < N;
   const int ni = cv ? n : 0;
   const int nks = Kp / 32;
   const bool vec0 = (K % 8) == 0;
-  f32x4 wr[KS0_MAX][2];
-#pragma unroll
-  for (int u = 0; u < KS0_MAX; ++u) {
-    const int ks = wid + 4 * u;
-    wrow_raw(L0.W, N, K, n, 32 * (ks < nks ? ks : 0) + 8 * (lane >> 4), vec0, wr[u]);
-  }
-  float bias = 0.f, ga = 1.f, be = 0.f, rm = 0.f, rv = 1.f, gbo = 0.f, ggo = 0.f, gbeo = 0.f;
-  if (wid == 0) {
-    if (L0.b) { bias = L0.b[ni]; gbo = L0.gb[ni]; }
-    if (L0.bn) {
-      ga = L0.gamma[ni]; be = L0.beta[ni];
-      ggo = L0.ggamma[ni]; gbeo = L0.gbeta[ni];
-      if (L0.bn == 2) { rm = L0.rmean[ni]; rv = L0.rvar[ni]; }
-    }
-  }
-  // W1 columns of this workgroup (dA1 = dZ1 W1[:, cols]), wave 0
-  const int n1s = L1.Np / 32;
-  float w1c[W1S_MAX][8];
-  if (wid == 0) {
-#pragma unroll
-    for (int s = 0; s < W1S_MAX; ++s)
-      if (s < n1s) wcol_raw(L1.W, L1.out, L1.in, 32 * s + 8 * (lane >> 4), n, w1c[s]);
-  }
-  // W0 columns of this workgroup's dX tiles (dX[:, t] = dZ0 W0[:, t])
-  const int nns = L0.Np / 32;
-  float w0c[DXT_MAX][DXN_MAX][8];
-#pragma unroll
-  for (int i = 0; i < DXT_MAX; ++i) {
-    const int t = c + a.G0 * i;
-#pragma unroll
-    for (int j = 0; j < DXN_MAX; ++j) {
-      const int s = wid + 4 * j;
-      if (t < a.ndx && s < nns) wcol_raw(L0.W, N, K, 32 * s + 8 * (lane >> 4), 16 * t + (lane & 15), w0c[i][j]);
-    }
-  }
-  // old dW0 values of this wave's tiles: rows 16c + 4(lane>>4) + r, columns 16 tk + (lane & 15)
-  const int ntk = (K + 15) / 16;
-  float gold[DW0_MAX][4];
-#pragma unroll
-  for (int i = 0; i < DW0_MAX; ++i) {
-    const int tk = wid + 4 * i;
-    const int k = 16 * tk + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int nr = 16 * c + 4 * (lane >> 4) + r;
-      gold[i][r] = L0.gW[(tk < ntk && nr < N && k < K) ? (long)nr * K + k : 0];
-    }
-  }
 
-  // ---- the input image (layer-0 dropout applied), bf16 in LDS ----------------------------------
+  // ---- 1. the input image (layer-0 dropout applied), bf16 in LDS: its loads lead the queue --
   {
     const float p0 = L0.drop;
     const float inv = p0 > 0.f ? 1.f / (1.f - p0) : 1.f;
@@ -266,7 +230,70 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
       }
     }
   }
-  __syncthreads();
+
+  if (st) YSTAMP(7);
+  // ---- 2. W0 rows of this wave's k-steps (the layer-0 GEMM) and the epilogue parameters -----
+  f32x4 wr[KS0_MAX][2];
+#pragma unroll
+  for (int u = 0; u < KS0_MAX; ++u) {
+    const int ks = wid + 4 * u;
+    wrow_raw(L0.W, N, K, n, 32 * (ks < nks ? ks : 0) + 8 * (lane >> 4), vec0, wr[u]);
+  }
+  float bias = 0.f, ga = 1.f, be = 0.f, rm = 0.f, rv = 1.f, gbo = 0.f, ggo = 0.f, gbeo = 0.f;
+  if (wid == 0) {
+    if (L0.b) { bias = L0.b[ni]; gbo = L0.gb[ni]; }
+    if (L0.bn) {
+      ga = L0.gamma[ni]; be = L0.beta[ni];
+      ggo = L0.ggamma[ni]; gbeo = L0.gbeta[ni];
+      if (L0.bn == 2) { rm = L0.rmean[ni]; rv = L0.rvar[ni]; }
+    }
+  }
+  const int n1s = L1.Np / 32, nn1 = L1.Np / 16;
+  const int nns = L0.Np / 32;
+  const int ntk = (K + 15) / 16;
+  float w1c[W1S_MAX][8];           // W1 columns of this workgroup (dA1 = dZ1 W1[:, cols]), wave 0
+  float w0c[DXT_MAX][DXN_MAX][8];  // W0 columns of this workgroup's dX tiles
+  float gold[DW0_MAX][4];          // old dW0 of this wave's tiles: rows 16c + 4(lane>>4) + r
+  float g1o[W1T_MAX][4];           // old dW1 of this workgroup's input columns: n1-tiles wid + 4i
+  // operands needed only after the dZ1 hand-off: requested once this wave's part of the
+  // forward is out (issuing ~100 loads per lane before the layer-0 GEMM delayed it by ~4.7 us)
+  auto prefetch_late = [&]() {
+    if (wid == 0) {
+#pragma unroll
+      for (int s = 0; s < W1S_MAX; ++s)
+        if (s < n1s) wcol_raw(L1.W, L1.out, L1.in, 32 * s + 8 * (lane >> 4), n, w1c[s]);
+    }
+#pragma unroll
+    for (int i = 0; i < DXT_MAX; ++i) {
+      const int t = c + a.G0 * i;
+#pragma unroll
+      for (int j = 0; j < DXN_MAX; ++j) {
+        const int s = wid + 4 * j;
+        if (t < a.ndx && s < nns) wcol_raw(L0.W, N, K, 32 * s + 8 * (lane >> 4), 16 * t + (lane & 15), w0c[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < DW0_MAX; ++i) {
+      const int tk = wid + 4 * i;
+      const int k = 16 * tk + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nr = 16 * c + 4 * (lane >> 4) + r;
+        gold[i][r] = L0.gW[(tk < ntk && nr < N && k < K) ? (long)nr * K + k : 0];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < W1T_MAX; ++i) {
+      const int tn = wid + 4 * i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n1 = 16 * tn + 4 * (lane >> 4) + r;
+        g1o[i][r] = L1.gW[(tn < nn1 && n1 < L1.out && n < N) ? (long)n1 * L1.in + n : 0];
+      }
+    }
+  };
+  if (st) YSTAMP(15);
+  lds_barrier();  // the input image
   if (st) YSTAMP(1);
 
   // ---- layer 0: K split over the four waves -------------------------------------------------
@@ -291,15 +318,16 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[((wid - 1) * SMT * 4 + mt * 4 + r) * 64 + lane] = acc[mt][r];
   }
-  __syncthreads();
+  lds_barrier();
+  if (wid > 0) prefetch_late();
 
   // wave 0: epilogue + publish; keeps xhat / rstd / the ReLU mask for the backward
-  float xh[SMT][4];
-  float rstd = 0.f;
-  unsigned relu_ok = 0xffu;  // bit 4 mt + r: post-ReLU output > 0
   const float p1 = L1.drop;
   const float inv1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
   if (wid == 0) {
+    float xh[SMT][4];
+    float rstd = 0.f;
+    unsigned relu_ok = 0xffu;  // bit 4 mt + r: post-ReLU output > 0
 #pragma unroll
     for (int w = 0; w < 3; ++w)
 #pragma unroll
@@ -342,8 +370,12 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
           xh[mt][r] = (row < B && cv) ? (z[mt][r] - mean) * rstd : 0.f;
           z[mt][r] = g * xh[mt][r] + bb;
         }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < SMT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xh[mt][r] = 0.f;
     }
-    bf16* stg = dzs;  // the A1 slice is staged where the dZ0 slice goes later
 #pragma unroll
     for (int mt = 0; mt < SMT; ++mt)
 #pragma unroll
@@ -356,15 +388,16 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
         }
         v = (row < B && cv) ? v : 0.f;
         if (p1 > 0.f && v != 0.f) v = hkeep(seed, 1, row, n, N, p1) ? v * inv1 : 0.f;
-        stg[row * 24 + (lane & 15)] = (bf16)v;
+        a1s[row * 24 + (lane & 15)] = (bf16)v;
       }
     // publish: lane -> (row, 8-column half), one 16-B write-through store each
     const int row = lane >> 1, h = lane & 1;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + row * 24 + 8 * h);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(a1s + row * 24 + 8 * h);
     st_sc1(rw, a.a1_off + 2L * (row * a.SA1 + 16 * c + 8 * h), v);
     drain();
     if (lane == 0) arrive(sync, Y_A1);
     if (st) YSTAMP(2);
+    prefetch_late();
 
     // ---- wait for dZ1, then dA1 = dZ1 W1[:, cols] and the layer-0 backward -----------------
     if (lane == 0) poll_ge(sync, Y_DZ1, E1, 1u);
@@ -386,7 +419,11 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
       if (s < n1s) {
         const bf16x8 bq = wcol_cvt(w1c[s], L1.out, L1.in, 32 * s + 8 * (lane >> 4), n);
 #pragma unroll
-        for (int mt = 0; mt < SMT; ++mt) da[mt] = mfma16(zf[s][mt], bq, da[mt]);
+        for (int mt = 0; mt < SMT; ++mt) {
+          da[mt] = mfma16(zf[s][mt], bq, da[mt]);
+          // dZ1 also to LDS: the dW1 tiles of this workgroup's columns read it transposed
+          *reinterpret_cast<bf16x8*>(z1s + (16 * mt + (lane & 15)) * a.SZ1 + 32 * s + 8 * (lane >> 4)) = zf[s][mt];
+        }
       }
     float d[SMT][4];
 #pragma unroll
@@ -443,9 +480,9 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
     if (lane == 0) arrive(sync, Y_DZ0);
     if (st) YSTAMP(4);
   }
-  __syncthreads();  // dZ0 slice in LDS
+  lds_barrier();  // dZ0 slice, dZ1 and the A1 slice in LDS
 
-  // ---- dW0[cols, :] += dZ0_slice^T A0 (local input image) -----------------------------------
+  // ---- dW0[cols, :] += dZ0_slice^T A0 ; dW1[:, cols] += dZ1^T A1_slice ------------------------
   {
     f32x4 dw[DW0_MAX];
 #pragma unroll
@@ -453,6 +490,13 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
       const int tk = wid + 4 * i;
       dw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (tk < ntk) dw[i] = mfma16(tr_frag(dzs, 24, 0, 0, lane), tr_frag(img, S0, 16 * tk, 0, lane), dw[i]);
+    }
+    f32x4 d1[W1T_MAX];
+#pragma unroll
+    for (int i = 0; i < W1T_MAX; ++i) {
+      const int tn = wid + 4 * i;
+      d1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (tn < nn1) d1[i] = mfma16(tr_frag(z1s, a.SZ1, 16 * tn, 0, lane), tr_frag(a1s, 24, 0, 0, lane), d1[i]);
     }
 #pragma unroll
     for (int i = 0; i < DW0_MAX; ++i) {
@@ -464,12 +508,21 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
         if (tk < ntk && nr < N && k < K) L0.gW[(long)nr * K + k] = gold[i][r] + dw[i][r];
       }
     }
+#pragma unroll
+    for (int i = 0; i < W1T_MAX; ++i) {
+      const int tn = wid + 4 * i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n1 = 16 * tn + 4 * (lane >> 4) + r;
+        if (tn < nn1 && n1 < L1.out && n < N) L1.gW[(long)n1 * L1.in + n] = g1o[i][r] + d1[i][r];
+      }
+    }
   }
 
   // ---- dX tiles: dX[:, t] = dZ0 W0[:, t] (+ the layer-0 dropout) ---------------------------
   if (dx) {
     if (tid == 0) poll_ge(sync, Y_DZ0, E1 * (unsigned)a.G0, 2u);
-    __syncthreads();
+    lds_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (st) YSTAMP(5);
     bf16x8 zf[DXN_MAX][SMT];
@@ -508,7 +561,7 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
           for (int r = 0; r < 4; ++r)
             red[(((wid - 1) * DXT_MAX + i) * SMT * 4 + mt * 4 + r) * 64 + lane] = ax[i][mt][r];
     }
-    __syncthreads();
+    lds_barrier();
     if (wid == 0) {
       const float p0 = L0.drop;
       const float inv0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f;
@@ -638,7 +691,7 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
   }
   // ---- A1 from the column workgroups --------------------------------------------------------
   if (tid == 0) poll_ge(sync, Y_A1, E1 * (unsigned)a.G0, 3u);
-  __syncthreads();
+  lds_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (st) YSTAMP(9);
   {
@@ -663,7 +716,7 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (st) YSTAMP(10);
 
   // ---- forward of layers 1 .. nl-1 ---------------------------------------------------------
@@ -749,37 +802,52 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
           }
         }
     }
-    __syncthreads();
+    lds_barrier();
   }
   if (st) YSTAMP(11);
 
   // ---- loss: softmax / log-softmax + CE / NLL, argmax (wave 0, lane = row) -------------------
+  // (d loss / d logits stays in registers: the dZ image and the bias gradient come from them
+  // without another pass through LDS)
   const SLayer& LL = a.L[nl - 1];
-  const int C = LL.out, Cp = LL.Np;
+  const int C = LL.out;
   if (wid == 0) {
     const int m = lane;
-    float ls = 0.f;
-    if (m < B) {
-      float mx = -INFINITY;
-      int am = 0;
-      for (int cc = 0; cc < C; ++cc) {
-        const float v = logit[m * 16 + cc];
-        if (v > mx) { mx = v; am = cc; }
-      }
-      float se = 0.f;
-      for (int cc = 0; cc < C; ++cc) se += expf(logit[m * 16 + cc] - mx);
-      const float lse = mx + logf(se);
-      int yc = ylds[m];
-      yc = yc < 0 ? 0 : (yc >= C ? C - 1 : yc);
-      for (int cc = 0; cc < C; ++cc) {
-        const float lp = logit[m * 16 + cc] - lse;
-        const float p = expf(lp);
-        out[(long)m * C + cc] = a.log_out ? lp : p;
-        dlogit[m * 16 + cc] = (p - (cc == yc ? 1.f : 0.f)) / (float)B;
-      }
-      ls = lse - logit[m * 16 + yc];
-      pred[m] = am;
+    const bool mv = m < B;
+    // (C is uniform: `if (cc < C)` are scalar branches, so only the live classes cost VALU)
+    float lg[16], dl[16];
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      lg[cc] = -INFINITY;
+      dl[cc] = 0.f;
+      if (cc < C) lg[cc] = mv ? logit[m * 16 + cc] : 0.f;
     }
+    float mx = -INFINITY;
+    int am = 0;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc)
+      if (cc < C && lg[cc] > mx) { mx = lg[cc]; am = cc; }
+    float se = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc)
+      if (cc < C) se += expf(lg[cc] - mx);
+    const float lse = mx + logf(se);
+    if (st) YSTAMP(19);
+    int yc = mv ? ylds[m] : 0;
+    yc = yc < 0 ? 0 : (yc >= C ? C - 1 : yc);
+    float ly = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      if (cc < C) {
+        const float lp = lg[cc] - lse;
+        const float p = expf(lp);
+        dl[cc] = mv ? (p - (cc == yc ? 1.f : 0.f)) / (float)B : 0.f;
+        if (mv) out[(long)m * C + cc] = a.log_out ? lp : p;
+        if (cc == yc) ly = lg[cc];
+      }
+    }
+    float ls = mv ? lse - ly : 0.f;
+    if (mv) pred[m] = am;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) ls += __shfl_xor(ls, off);
     if (lane == 0) {
@@ -790,22 +858,45 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
           __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.L[l].nbt), 1ull,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // dZ of the logits layer (scaled by d out / d loss), its bias gradient
+    if (st) YSTAMP(16);
+    // dZ of the logits layer (scaled by d out / d loss): lanes 0-31 row m's 16 leading columns,
+    // lanes 32-63 the zero pad columns 16..31 of row m - 32 (C <= 16)
     bf16* dz = reinterpret_cast<bf16*>(smem + LL.z_lds);
-    for (int i = lane; i < SMP * Cp; i += 64) {
-      const int mm = i / Cp, cc = i - mm * Cp;
-      dz[mm * LL.SZ + cc] = (bf16)((mm < B && cc < C) ? gs * dlogit[mm * 16 + cc] : 0.f);
+    bf16x8 z0, z1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      z0[j] = (bf16)(lane < 32 ? gs * dl[j] : 0.f);
+      z1[j] = (bf16)(lane < 32 ? gs * dl[8 + j] : 0.f);
     }
-    if (LL.b && lane < C) {
-      float s = 0.f;
-      for (int mm = 0; mm < B; ++mm) s += dlogit[mm * 16 + lane];
-      LL.gb[lane] = reinterpret_cast<const float*>(smem + LL.p_lds)[5 * LL.Np + lane] + gs * s;
+    bf16* zr = dz + (lane & 31) * LL.SZ + (lane < 32 ? 0 : 16);
+    *reinterpret_cast<bf16x8*>(zr) = z0;
+    *reinterpret_cast<bf16x8*>(zr + 8) = z1;
+    if (st) YSTAMP(17);
+    // bias gradient: column sums of d loss / d logits over the batch, summed in row order
+    // (shuffles; the same order as the three-launch path, so both agree bitwise)
+    if (LL.b) {
+      const float* pb = reinterpret_cast<const float*>(smem + LL.p_lds) + 5 * LL.Np;
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) {
+        if (cc >= C) break;
+        // row values to scalar registers (independent readlanes), then the ordered sum
+        const int bits = __float_as_int(dl[cc]);
+        float v = 0.f;
+        for (int mm = 0; mm < B; ++mm) v += __int_as_float(__builtin_amdgcn_readlane(bits, mm));
+        if (lane == 0) LL.gb[cc] = pb[cc] + gs * v;
+      }
     }
+    if (st) YSTAMP(18);
   }
-  __syncthreads();
+  lds_barrier();
   if (st) YSTAMP(12);
 
   // ---- output-gradient chain: dZ_l -> dZ_{l-1} for l = nl-1 .. 2 ----------------------------
+  // (the BatchNorm xhat / rstd of the narrow layers went to the workspace; each wave reads back
+  // the columns it wrote itself, so its own stores only need to have completed)
+  bool tail_bn = false;
+  for (int l = 1; l < nl - 1; ++l) tail_bn = tail_bn || a.L[l].bn != 0;
+  if (tail_bn) drain();
   for (int l = nl - 1; l >= 2; --l) {
     const SLayer& L = a.L[l];
     const SLayer& P = a.L[l - 1];
@@ -891,7 +982,7 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
 #pragma unroll
         for (int r = 0; r < 4; ++r) dzn[(16 * mt + 4 * (lane >> 4) + r) * P.SZ + kk] = (bf16)d[mt][r];
     }
-    __syncthreads();
+    lds_barrier();
   }
   // dZ1 -> the column workgroups
   {
@@ -903,12 +994,12 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
       st_sc1(rw, a.dz1_off + 2L * (m * a.SZ1 + kk), *reinterpret_cast<const bf16x8*>(dz1 + m * L1.SZ + kk));
     }
     drain();
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) __hip_atomic_store((gu32*)(sync + Y_DZ1), E1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (st) YSTAMP(13);
-  // ---- dW of layers 1 .. nl-1 (off the column workgroups' critical path) --------------------
-  for (int l = 1; l < nl; ++l) {
+  // ---- dW of layers 2 .. nl-1 (layer 1's dW runs in the column workgroups) -----------------
+  for (int l = 2; l < nl; ++l) {
     const SLayer& L = a.L[l];
     tail_dw(L, reinterpret_cast<const bf16*>(smem + L.z_lds), L.SZ,
             reinterpret_cast<const bf16*>(smem + L.a_lds), lane, wid);
@@ -929,7 +1020,7 @@ head_step_kernel(StepArgs a, const float* __restrict__ x, long ldx, const long l
   } else {
     tail_wg(a, y, out, loss, pred, rng, dloss, ws, sync, smem, stamps);
   }
-  __syncthreads();
+  lds_barrier();
   // every wait of this workgroup is behind it: the last one to finish advances the epoch
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add((gu32*)(sync + Y_DONE), 1u, __ATOMIC_RELAXED,
@@ -1027,6 +1118,10 @@ static bool step_plan(int nl, const int* dims, const int* flags, const float* dr
   c = al16s(c + 4 * 3 * DXT_MAX * SMT * 4 * 64);
   a.c_dzs = c;
   c = al16s(c + 2 * SMP * 24);
+  a.c_a1s = c;
+  c = al16s(c + 2 * SMP * 24);
+  a.c_z1s = c;
+  c = al16s(c + 2 * SMP * (a.L[1].Np + 8));
   // tail LDS
   int t = 0;
   for (int l = 1; l < nl; ++l) {
