@@ -268,6 +268,9 @@ __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int
 // resets the ticket, reads the other splits' partials with sc1 loads and sums all of them in
 // split order 0..S-1 (its own from registers), so the result does not depend on arrival order.
 // `flag`: one int of the kernel's (single) LDS array, free after the K loop.
+// accumulator fragments (16x16) per wave up to which a tile carries the in-launch combine
+constexpr int SPLITK_INLAUNCH_FRAGS = 4;
+
 template <int FM, int FN, int WM, int WN>
 __device__ __forceinline__ void splitk_epilogue(const GemmGroup& g, const GemmProb& P,
                                                 const f32x4 (&acc)[FM][FN], int gtile, int row0,
@@ -445,11 +448,13 @@ gemm_kernel(GemmGroup g) {
 #undef Bs
   // epilogue
   float* slab = P.slab;
-  if (slab && g.cnt) {
-    asm volatile("s_barrier" ::: "memory");  // the last tile's LDS reads are done: reuse smem
-    splitk_epilogue<T::FM, T::FN, T::WM, T::WN>(g, P, acc, gtile, row0, col0, wm, wn, lane,
-                                                reinterpret_cast<int*>(smem));
-    return;
+  if constexpr (T::FM * T::FN <= SPLITK_INLAUNCH_FRAGS) {
+    if (slab && g.cnt) {
+      asm volatile("s_barrier" ::: "memory");  // the last tile's LDS reads are done: reuse smem
+      splitk_epilogue<T::FM, T::FN, T::WM, T::WN>(g, P, acc, gtile, row0, col0, wm, wn, lane,
+                                                  reinterpret_cast<int*>(smem));
+      return;
+    }
   }
   const int nst = (slab || P.epi.ncol <= 0) ? N : min(N, P.epi.ncol);
 #pragma unroll
@@ -733,10 +738,12 @@ gemm_dma_kernel(GemmGroup g) {
     return;
   }
   float* slab = P.slab;
-  if (slab && g.cnt) {
-    splitk_epilogue<FM, FN, WM, WN>(g, P, acc, gtile, row0, col0, wm, wn, lane,
-                                    reinterpret_cast<int*>(smem));
-    return;
+  if constexpr (FM * FN <= SPLITK_INLAUNCH_FRAGS) {
+    if (slab && g.cnt) {
+      splitk_epilogue<FM, FN, WM, WN>(g, P, acc, gtile, row0, col0, wm, wn, lane,
+                                      reinterpret_cast<int*>(smem));
+      return;
+    }
   }
   const int nst = (slab || P.epi.ncol <= 0) ? N : min(N, P.epi.ncol);
 #pragma unroll
@@ -852,6 +859,9 @@ static int kchunk_for(int K, int& splits) {
 
 template <int BM, int BN, bool TA, bool TB, typename TAe, typename TBe>
 int launch(GemmGroup& g, hipStream_t st) {
+  // the combiner's partial loads do not fit beside a 128x128 tile's accumulators (they spilled
+  // to scratch): those tiles always reduce in the second kernel
+  if constexpr ((BM / 32) * (BN / 32) > SPLITK_INLAUNCH_FRAGS) g.cnt = nullptr;  // 2x2 waves
   int tiles = 0;
   long elems = 0;
   for (int i = 0; i < g.n; ++i) {

@@ -1007,6 +1007,19 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
   if (st) YSTAMP(14);
 }
 
+// Touch every 64-B line of the kernel arguments with independent scalar loads, so the argument
+// lines are in this CU's scalar cache before the phases that read them one dependent field at a
+// time (a per-layer loop over StepArgs serialises one cold scalar miss per line it reaches).
+__device__ __forceinline__ void warm_kernargs() {
+  constexpr int LINES = (int)((sizeof(StepArgs) + 160 + 63) / 64);
+  typedef const __attribute__((address_space(4))) unsigned cu32;
+  cu32* kp = (cu32*)__builtin_amdgcn_kernarg_segment_ptr();
+  unsigned acc = 0;
+#pragma unroll
+  for (int i = 0; i < LINES; ++i) acc += kp[16 * i];
+  asm volatile("" ::"s"(acc));
+}
+
 __global__ void __launch_bounds__(SNT)
 head_step_kernel(StepArgs a, const float* __restrict__ x, long ldx, const long long* __restrict__ y,
                  float* __restrict__ out, float* __restrict__ loss, long long* __restrict__ pred,
@@ -1014,6 +1027,7 @@ head_step_kernel(StepArgs a, const float* __restrict__ x, long ldx, const long l
                  float* __restrict__ dx, long lddx, char* __restrict__ ws,
                  unsigned* __restrict__ sync, unsigned long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  warm_kernargs();
   const unsigned E1 = sync[Y_EPOCH] + 1u;
   if ((int)blockIdx.x < a.G0) {
     column_wg(a, blockIdx.x, x, ldx, rng, dx, lddx, ws, sync, smem, stamps);

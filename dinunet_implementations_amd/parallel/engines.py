@@ -31,7 +31,9 @@ import torch.nn as nn
 from ..ops import _grad as _gradreg
 from ..ops import _lib
 from ..ops import capture as _cap
-from ..ops.optim import FlatParams, cast_bf16_to_f32, cast_f32_to_bf16
+from ..ops.optim import FlatParams
+from .collective import (HDR, PAYLOAD_TYPES, DirectMean, from_payload, launch_on, payload_name,
+                         to_payload)
 from .group import SiteGroup
 from .lowrank import EPS as EPS_MGS
 from .lowrank import LowRankTable, _mgs_torch_, dad_factors, orthonormalize_
@@ -47,8 +49,12 @@ class Engine:
         self.flat = flat
         self.group = group
         self.cfg = dict(cfg or {})
-        self.half = str(self.cfg.get("precision_bits", "32")) == "16"
+        # wire type of every site-mean (collective.payload_name): fp16 at precision_bits=16 like
+        # the reference, or the explicit ``payload_dtype``; always accumulated in fp32
+        self.wire = payload_name(self.cfg)
+        self.half = self.wire != "fp32"
         self.comm_bytes = 0  # payload bytes this site sent in the last reduce (observability)
+        self._means: Dict[Tuple[int, int], DirectMean] = {}
 
     # collective path -------------------------------------------------------------------------
     def step_context(self):
@@ -78,17 +84,20 @@ class Engine:
         raise NotImplementedError
 
     # helpers ---------------------------------------------------------------------------------
+    def _direct(self, key, n: int, device) -> DirectMean:
+        dm = self._means.get(key)
+        if dm is None or dm.n != n:
+            dm = self._means[key] = DirectMean(self.group, n, self.wire, device)
+        return dm
+
     def _allreduce_mean_(self, buf: Tensor):
-        """In-place mean over sites, honouring ``precision_bits``."""
+        """In-place mean over sites, honouring ``precision_bits`` / ``payload_dtype``: a 16-bit
+        payload goes through the direct exchange (fp32 accumulation, collective.DirectMean)."""
         g = self.group
         if not g.distributed:
             return
         if self.half:
-            tmp = torch.empty(buf.numel(), dtype=torch.bfloat16, device=buf.device)
-            cast_f32_to_bf16(buf.reshape(-1), tmp)
-            g.all_reduce(tmp)
-            cast_bf16_to_f32(tmp, buf.reshape(-1), 1.0 / g.world)
-            self.comm_bytes += tmp.numel() * 2
+            self.comm_bytes += self._direct(("mean", buf.numel()), buf.numel(), buf.device).run_(buf)
         else:
             g.all_reduce(buf)
             buf.mul_(1.0 / g.world)
@@ -138,6 +147,15 @@ class DSGDEngine(Engine):
             self._expected[self._param_bucket[id(p)]] += 1
         self._handles: Dict[int, object] = {}
         self._half_bufs: Dict[int, Tensor] = {}
+        # ``dsgd_collective``: "direct" = all_to_all + fp32 sum + all_gather (collective.py) on a
+        # comm stream of its own; "allreduce" = one RCCL all-reduce per bucket (a 16-bit payload
+        # is then SUMMED in 16 bits inside RCCL); "auto" = direct for 16-bit payloads
+        coll = str(self.cfg.get("dsgd_collective", "auto"))
+        if coll not in ("auto", "direct", "allreduce"):
+            raise ValueError(f"dsgd_collective {coll!r}: expected auto, direct or allreduce")
+        self.direct = coll == "direct" or (coll == "auto" and self.half)
+        self._comm_stream = (torch.cuda.Stream(device=flat.grad.device)
+                             if self.direct and group.distributed and flat.grad.is_cuda else None)
         self._hooks = []
         self._delivered = set()
         if self.overlap:
@@ -218,13 +236,19 @@ class DSGDEngine(Engine):
             self.comm_bytes = 0
         s, e = self.buckets[b]
         view = self.flat.grad[s:e]
-        if self.half:
+        if self.direct:
+            dm = self._direct((s, e), e - s, view.device)
+            self._handles[b] = launch_on(self._comm_stream, lambda: dm.run_(view))
+            self.comm_bytes += dm.n * dm.send.element_size()
+        elif self.half:
             buf = self._half_bufs.get(b)
             if buf is None:
-                buf = self._half_bufs[b] = torch.empty(e - s, dtype=torch.bfloat16, device=view.device)
-            cast_f32_to_bf16(view, buf)
+                dt = PAYLOAD_TYPES[self.wire][1]  # one unscaled block: headers sum to 0
+                buf = self._half_bufs[b] = torch.zeros(HDR + -(-(e - s) // 8) * 8, dtype=dt,
+                                                       device=view.device)
+            to_payload(view, buf, 1, buf.numel() - HDR)
             self._handles[b] = self.group.all_reduce(buf, async_op=True)
-            self.comm_bytes += buf.numel() * 2
+            self.comm_bytes += (e - s) * buf.element_size()
         else:
             self._handles[b] = self.group.all_reduce(view, async_op=True)
             self.comm_bytes += view.numel() * 4
@@ -250,11 +274,13 @@ class DSGDEngine(Engine):
         self._drain()
         for b, h in self._handles.items():
             h.wait()
-            if self.half:
+            if self.half and not self.direct:
                 s, e = self.buckets[b]
-                cast_bf16_to_f32(self._half_bufs[b], self.flat.grad[s:e])
+                buf = self._half_bufs[b]
+                from_payload(buf, self.flat.grad[s:e], 1, buf.numel() - HDR)
         self._reset()
-        return 1.0 / g.world
+        self.last_scale = 1.0 if self.direct else 1.0 / g.world  # the direct exchange leaves the mean
+        return self.last_scale
 
     def close(self):
         for h in self._hooks:
@@ -265,7 +291,7 @@ class DSGDEngine(Engine):
     # file transport
     def payload(self):
         g = self.flat.grad
-        return {"grad": g.to(torch.bfloat16) if self.half else g.clone()}
+        return {"grad": g.to(PAYLOAD_TYPES[self.wire][1]) if self.half else g.clone()}
 
     @classmethod
     def aggregate(cls, payloads, cfg=None):
@@ -326,13 +352,32 @@ class RankDADEngine(Engine):
             off += (out_f + in_f) * r
         low = {id(l[0].weight) for l in self.fast_layers}
         self.fast_dense = [(o, n) for p, o, n in self.flat.segments() if id(p) not in low]
-        self._send = torch.zeros(max(off, 1), dtype=torch.float32, device=dev)
+        # the dense (dSGD-mean) part: adjacent segments merged; one index gather / scatter when
+        # they are not one range (no per-segment copies)
+        merged: List[List[int]] = []
+        for o, n in sorted(self.fast_dense):
+            if merged and merged[-1][1] == o:
+                merged[-1][1] = o + n
+            else:
+                merged.append([o, o + n])
+        self._dense_ranges = [(a, b) for a, b in merged]
+        self._dense_idx = (torch.cat([torch.arange(a, b) for a, b in self._dense_ranges]).to(dev)
+                           if len(self._dense_ranges) > 1 else None)
+        self._dense_buf = (torch.empty(self._dense_idx.numel(), dtype=torch.float32, device=dev)
+                           if self._dense_idx is not None else None)
+        # 16-byte multiple: the send slot is also the per-rank stride of the 16-bit gather
+        self._send = torch.zeros(-(-max(off, 1) // 8) * 8, dtype=torch.float32, device=dev)
         n = len(self.fast_layers)
         if not n:
             return
         W = self.group.world
         self._gathered = (torch.zeros(W * self._send.numel(), dtype=torch.float32, device=dev)
                           if self.group.distributed else self._send)
+        if self.half and self.group.distributed:
+            dt = PAYLOAD_TYPES[self.wire][1]
+            self._send16 = torch.zeros(HDR + self._send.numel(), dtype=dt, device=dev)
+            self._gathered16 = torch.zeros(W * (HDR + self._send.numel()), dtype=dt, device=dev)
+            self._amax = torch.zeros(1, dtype=torch.int32, device=dev)  # fp16 block scale
         layers = []
         self._praw = []
         for _, o, out_f, in_f, rr, po, qo in self.fast_layers:
@@ -388,18 +433,27 @@ class RankDADEngine(Engine):
         g = self.group
         W = g.world
         self.comm_bytes = 0
-        if g.distributed and self.fast_dense:
-            dense = torch.cat([self.flat.grad[o:o + n] for o, n in self.fast_dense])
-            self._allreduce_mean_(dense)
-            off = 0
-            for o, n in self.fast_dense:
-                self.flat.grad[o:o + n].copy_(dense[off:off + n])
-                off += n
+        if g.distributed and self._dense_ranges:
+            grad = self.flat.grad
+            if self._dense_idx is None:
+                a, b = self._dense_ranges[0]
+                self._allreduce_mean_(grad[a:b])
+            else:
+                torch.index_select(grad, 0, self._dense_idx, out=self._dense_buf)
+                self._allreduce_mean_(self._dense_buf)
+                grad.index_copy_(0, self._dense_idx, self._dense_buf)
         if not self.fast_layers:
             return 1.0
         if g.distributed:
-            g.all_gather_into(self._gathered, self._send)
-            self.comm_bytes += self._send.numel() * 4
+            if self.half:  # factors on the wire in the payload type, reconstructed in fp32
+                n = self._send.numel()
+                to_payload(self._send, self._send16, 1, n, amax=self._amax)
+                g.all_gather_into(self._gathered16, self._send16)
+                from_payload(self._gathered16, self._gathered, W, n, amax=self._amax)
+                self.comm_bytes += self._send16.numel() * self._send16.element_size()
+            else:
+                g.all_gather_into(self._gathered, self._send)
+                self.comm_bytes += self._send.numel() * 4
         # every layer's G = [P_1..P_W][Q_1..Q_W]^T / W in one launch
         _lib.call("dn_pi_reconstruct", self._rec.data_ptr(), len(self.fast_layers),
                   self._recon_total, self._send.numel(), W if g.distributed else 1, _lib.stream())
@@ -467,10 +521,12 @@ class RankDADEngine(Engine):
         low = [(m, X, Y) for m, mode, X, Y in facs if mode == "lowrank"]
         if low:
             flat = torch.cat([torch.cat([X.reshape(-1), Y.reshape(-1)]) for _, X, Y in low])
+            if self.half:
+                flat = flat.to(PAYLOAD_TYPES[self.wire][1])
             gathered = torch.empty(W * flat.numel(), dtype=flat.dtype, device=flat.device)
             g.all_gather_into(gathered, flat)
-            self.comm_bytes += flat.numel() * 4
-            gathered = gathered.view(W, -1)
+            self.comm_bytes += flat.numel() * flat.element_size()
+            gathered = gathered.view(W, -1).float()
             off = 0
             for m, X, Y in low:
                 nx, ny = X.numel(), Y.numel()

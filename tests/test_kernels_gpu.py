@@ -447,3 +447,40 @@ def test_gemm_splitk_in_launch_combine_matches_reduce_kernel(splits, monkeypatch
     if splits <= 4:
         assert torch.equal(r1, r2)
     assert (r1 - ref).abs().max() < 1e-2 * ref.abs().max()
+
+
+@pytest.mark.parametrize("payload", ["fp16", "bf16", "fp32"])
+@pytest.mark.parametrize("n,W", [(4099, 3), (4 << 20, 8), (37, 2)])
+def test_payload_kernels_match_torch_layout(payload, n, W):
+    """collective.py kernels vs its torch (CPU) implementation of the same block layout: pack
+    (block scale from amax, header, zero pad), fp32-accumulating row sum, unpack (scalar tail);
+    fp16 site values spanning 1e-5..1e2 keep 11-bit precision through the block scale."""
+    from dinunet_implementations_amd.parallel import collective as C
+    dt = C.PAYLOAD_TYPES[payload][1]
+    chunk = -(-n // (8 * W)) * 8
+    # |x| over 7 decades (fp16's normal range spans 2^29 ~ 5e8 once scaled to the block max)
+    x = ((torch.rand(n, device=DEV) + 0.5) * torch.randn(n, device=DEV).sign()
+         * torch.logspace(-5, 2, n, device=DEV))
+    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    send = torch.full((C.blocks_numel(W, chunk),), 7.0, dtype=dt, device=DEV)
+    C.to_payload(x, send, W, chunk, scale=0.5, amax=amax)
+    ref = torch.empty(send.numel(), dtype=dt)
+    C.to_payload(x.cpu(), ref, W, chunk, scale=0.5, amax=amax.cpu())
+    assert torch.equal(send.cpu(), ref)
+    blocks = torch.randn(W, C.HDR + chunk, device=DEV)
+    blocks[:, :C.HDR] = 0
+    blocks[:, 0] = torch.arange(W) - 1.0 if payload == "fp16" else 0.0
+    blocks = blocks.to(dt).reshape(-1)
+    mine = torch.empty(C.HDR + chunk, dtype=dt, device=DEV)
+    C.rowsum(blocks, mine, W, chunk, 1.0 / W)
+    ref_m = torch.empty(C.HDR + chunk, dtype=dt)
+    C.rowsum(blocks.cpu(), ref_m, W, chunk, 1.0 / W)
+    assert torch.equal(mine.cpu(), ref_m)
+    out = torch.empty(n, device=DEV)
+    C.from_payload(send, out, W, chunk, scale=2.0, amax=amax)
+    assert int(amax.item()) == 0  # reset for the next exchange
+    if payload == "fp32":
+        assert torch.equal(out, x)
+    else:
+        r = ((out - x).abs() / x.abs()).max().item()
+        assert r <= (2.0 ** -11 if payload == "fp16" else 2.0 ** -8) * 1.01, r

@@ -22,11 +22,17 @@ CASES = [
     (2, ["--engine", "powerSGD", "--precision", "16", "--accum", "2"]),
     (4, ["--engine", "dSGD", "--precision", "16", "--accum", "2", "--ragged"]),
     (4, ["--engine", "rankDAD", "--precision", "16"]),
+    # against the fp64-mean oracle (tools/multirank_check.py --oracle): fp32 wire, the reference's
+    # fp16 wire through the direct exchange, bf16 wire, and the 16-bit all-reduce it replaces
+    (2, ["--engine", "dSGD", "--precision", "32", "--oracle"]),
+    (3, ["--engine", "dSGD", "--precision", "16", "--oracle", "--ragged"]),
+    (2, ["--engine", "dSGD", "--precision", "16", "--payload", "bf16", "--oracle"]),
+    (2, ["--engine", "dSGD", "--precision", "16", "--collective", "allreduce", "--oracle"]),
 ]
 
 
-@pytest.mark.parametrize("world,args", CASES, ids=[f"w{w}-" + "-".join(a[1::2]) +
-                                                   ("-ragged" if "--ragged" in a else "")
+@pytest.mark.parametrize("world,args", CASES, ids=[f"w{w}-" + "-".join(x for x in a if not x.startswith("--")) +
+                                                   ("-ragged" if "--ragged" in a else "") + ("-oracle" if "--oracle" in a else "")
                                                    for w, a in CASES])
 def test_replicas_bit_identical(world, args):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -39,6 +45,10 @@ def test_replicas_bit_identical(world, args):
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert lines, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
     res = json.loads(lines[-1])
+    log = os.environ.get("DINUNET_ERR_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"test": "multirank", "args": args, **res}) + "\n")
     assert res["ok"], res
     assert res["graph"] and res["world"] == world
     assert r.returncode == 0, r.stderr[-3000:]

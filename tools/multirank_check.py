@@ -17,7 +17,9 @@ generators, the same ragged batch), averages them in fp64 in site order, and app
 fused Adam.  Agreement is judged on the parameter UPDATE (final - initial): the relative L2 error
 of the N-rank update against the oracle's is reported (``update_rel_err``) and, at
 ``--precision 32``, must stay below ``--oracle-tol``; at 16 bits it measures what the payload
-precision costs.  (Bit-identical replicas alone would also pass if every rank applied the same
+precision costs after Adam (which turns the sign of every near-zero mean gradient into a full
+``lr`` step, so it amplifies payload rounding).  For dSGD the first step's reduced gradient is
+also compared with the fp64 mean (``grad_rel_err``): the payload's own error.  (Bit-identical replicas alone would also pass if every rank applied the same
 WRONG update.)
 """
 import argparse
@@ -46,6 +48,8 @@ def main():
     ap.add_argument("--split", type=int, default=-1, help="-1: TrainStep's default")
     ap.add_argument("--oracle", action="store_true", help="compare with the fp64-mean oracle")
     ap.add_argument("--oracle-tol", type=float, default=1e-3)
+    ap.add_argument("--payload", default=None, help="payload_dtype (fp16 | bf16 | fp32)")
+    ap.add_argument("--collective", default="auto", help="dsgd_collective (auto | direct | allreduce)")
     a = ap.parse_args()
 
     import torch
@@ -63,7 +67,9 @@ def main():
     init = flat.data.detach().clone()
     opt = FusedAdam(flat, lr=1e-3)
     cfg = {"precision_bits": a.precision, "dad_reduction_rank": 8, "powersgd_rank": 4, "seed": 5,
-           "dsgd_overlap": bool(a.overlap)}
+           "dsgd_overlap": bool(a.overlap), "dsgd_collective": a.collective}
+    if a.payload:
+        cfg["payload_dtype"] = a.payload
     eng = make_engine(a.engine, m, flat, grp, cfg)
     counts = {}
     if a.diag and hasattr(eng, "_on_grad"):
@@ -95,8 +101,11 @@ def main():
             y = torch.randint(0, 2, (B,), device=dev, generator=g)
             yield i, x, y
 
+    g_first = None
     for i, x, y in site_batches(grp.rank):
         step(x, y, first=i % a.accum == 0, last=i % a.accum == a.accum - 1)
+        if i == a.accum - 1:  # the first step's reduced gradient (the payload's own error)
+            g_first = (flat.grad.double() * getattr(eng, "last_scale", 1.0)).clone()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     mine = flat.data.detach().cpu()
@@ -104,6 +113,7 @@ def main():
     same = all(torch.equal(p, allp[0]) for p in allp)
     maxdiff = max(float((p - allp[0]).abs().max()) for p in allp)
     res = {"ok": bool(same), "world": grp.world, "engine": a.engine, "precision": a.precision,
+           "payload": eng.wire, "collective": a.collective,
            "accum": a.accum, "ragged": a.ragged, "graph": step.graph is not None,
            "split": bool(step.split), "steps": opt.step_count, "max_abs_diff": maxdiff,
            "param_sum": float(mine.double().sum())}
@@ -117,7 +127,7 @@ def main():
             oo = FusedAdam(fo, lr=1e-3)
             assert torch.equal(fo.data, init)
             sites = [site_batches(r) for r in range(grp.world)]
-            for _ in range(a.steps):
+            for s_i in range(a.steps):
                 gsum = torch.zeros(fo.numel, dtype=torch.float64, device=dev)
                 for r in range(grp.world):
                     fo.zero_grad()
@@ -126,6 +136,10 @@ def main():
                         _, loss, _ = mo.forward_loss(x, y)
                         (loss / a.accum).backward()
                     gsum += fo.grad.double()
+                if s_i == 0 and a.engine == "dSGD":
+                    gm = gsum / grp.world
+                    res["grad_rel_err"] = float((g_first - gm).norm() / gm.norm().clamp_min(1e-30))
+                    res["grad_max_abs_err"] = float((g_first - gm).abs().max())
                 fo.grad.copy_((gsum / grp.world).float())
                 oo.step()
             d_n = (flat.data - init).double()
