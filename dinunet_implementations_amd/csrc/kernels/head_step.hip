@@ -807,86 +807,51 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
   if (st) YSTAMP(11);
 
   // ---- loss: softmax / log-softmax + CE / NLL, argmax (wave 0, lane = row) -------------------
-  // (d loss / d logits stays in registers: the dZ image and the bias gradient come from them
-  // without another pass through LDS)
+  // Only d loss / d logits is on the critical path (-> dZ image -> chain -> dZ1 publish); the
+  // outputs, the loss reduction, the counters and the last layer's bias gradient are written
+  // after the publish (deferred block below).  Rolled loops over the C live classes: an
+  // unrolled 16-class register form was if-converted into 16 precise expf per row.
   const SLayer& LL = a.L[nl - 1];
   const int C = LL.out;
+  const int m = lane;
+  const bool mv = m < B;
+  const float* lr = logit + m * 16;
+  float* dr = dlogit + m * 16;
+  float lse = 0.f, ly = 0.f;
+  int am = 0;
   if (wid == 0) {
-    const int m = lane;
-    const bool mv = m < B;
-    // (C is uniform: `if (cc < C)` are scalar branches, so only the live classes cost VALU)
-    float lg[16], dl[16];
-#pragma unroll
-    for (int cc = 0; cc < 16; ++cc) {
-      lg[cc] = -INFINITY;
-      dl[cc] = 0.f;
-      if (cc < C) lg[cc] = mv ? logit[m * 16 + cc] : 0.f;
-    }
     float mx = -INFINITY;
-    int am = 0;
-#pragma unroll
-    for (int cc = 0; cc < 16; ++cc)
-      if (cc < C && lg[cc] > mx) { mx = lg[cc]; am = cc; }
+    for (int cc = 0; cc < C; ++cc) {
+      const float v = mv ? lr[cc] : 0.f;
+      if (v > mx) { mx = v; am = cc; }
+    }
     float se = 0.f;
-#pragma unroll
-    for (int cc = 0; cc < 16; ++cc)
-      if (cc < C) se += expf(lg[cc] - mx);
-    const float lse = mx + logf(se);
+    for (int cc = 0; cc < C; ++cc) se += expf((mv ? lr[cc] : 0.f) - mx);
+    lse = mx + logf(se);
     if (st) YSTAMP(19);
     int yc = mv ? ylds[m] : 0;
     yc = yc < 0 ? 0 : (yc >= C ? C - 1 : yc);
-    float ly = 0.f;
-#pragma unroll
-    for (int cc = 0; cc < 16; ++cc) {
-      if (cc < C) {
-        const float lp = lg[cc] - lse;
-        const float p = expf(lp);
-        dl[cc] = mv ? (p - (cc == yc ? 1.f : 0.f)) / (float)B : 0.f;
-        if (mv) out[(long)m * C + cc] = a.log_out ? lp : p;
-        if (cc == yc) ly = lg[cc];
-      }
-    }
-    float ls = mv ? lse - ly : 0.f;
-    if (mv) pred[m] = am;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) ls += __shfl_xor(ls, off);
-    if (lane == 0) {
-      *loss = ls / (float)B;
-      *rng = seed + 1ull;
-      for (int l = 0; l < nl; ++l)
-        if (a.L[l].bn == 2 && a.L[l].nbt)
-          __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.L[l].nbt), 1ull,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int cc = 0; cc < C; ++cc) {
+      const float lg = mv ? lr[cc] : 0.f;
+      const float p = expf(lg - lse);
+      dr[cc] = mv ? (p - (cc == yc ? 1.f : 0.f)) / (float)B : 0.f;
+      if (cc == yc) ly = lg;
     }
     if (st) YSTAMP(16);
     // dZ of the logits layer (scaled by d out / d loss): lanes 0-31 row m's 16 leading columns,
-    // lanes 32-63 the zero pad columns 16..31 of row m - 32 (C <= 16)
+    // lanes 32-63 the zero pad columns 16..31 of row m - 32 (C <= 16); each lane reads back only
+    // the d loss / d logits row it wrote
     bf16* dz = reinterpret_cast<bf16*>(smem + LL.z_lds);
     bf16x8 z0, z1;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      z0[j] = (bf16)(lane < 32 ? gs * dl[j] : 0.f);
-      z1[j] = (bf16)(lane < 32 ? gs * dl[8 + j] : 0.f);
+      z0[j] = (bf16)(lane < 32 && j < C ? gs * dr[j] : 0.f);
+      z1[j] = (bf16)(lane < 32 && 8 + j < C ? gs * dr[8 + j] : 0.f);
     }
     bf16* zr = dz + (lane & 31) * LL.SZ + (lane < 32 ? 0 : 16);
     *reinterpret_cast<bf16x8*>(zr) = z0;
     *reinterpret_cast<bf16x8*>(zr + 8) = z1;
     if (st) YSTAMP(17);
-    // bias gradient: column sums of d loss / d logits over the batch, summed in row order
-    // (shuffles; the same order as the three-launch path, so both agree bitwise)
-    if (LL.b) {
-      const float* pb = reinterpret_cast<const float*>(smem + LL.p_lds) + 5 * LL.Np;
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc) {
-        if (cc >= C) break;
-        // row values to scalar registers (independent readlanes), then the ordered sum
-        const int bits = __float_as_int(dl[cc]);
-        float v = 0.f;
-        for (int mm = 0; mm < B; ++mm) v += __int_as_float(__builtin_amdgcn_readlane(bits, mm));
-        if (lane == 0) LL.gb[cc] = pb[cc] + gs * v;
-      }
-    }
-    if (st) YSTAMP(18);
   }
   lds_barrier();
   if (st) YSTAMP(12);
@@ -998,6 +963,37 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
     if (tid == 0) __hip_atomic_store((gu32*)(sync + Y_DZ1), E1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (st) YSTAMP(13);
+  // ---- deferred loss outputs (wave 0, off the critical path) -------------------------------
+  if (wid == 0) {
+    for (int cc = 0; cc < C; ++cc) {
+      const float lp = (mv ? lr[cc] : 0.f) - lse;
+      if (mv) out[(long)m * C + cc] = a.log_out ? lp : expf(lp);
+    }
+    float ls = mv ? lse - ly : 0.f;
+    if (mv) pred[m] = am;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ls += __shfl_xor(ls, off);
+    if (lane == 0) {
+      *loss = ls / (float)B;
+      *rng = seed + 1ull;
+      for (int l = 0; l < nl; ++l)
+        if (a.L[l].bn == 2 && a.L[l].nbt)
+          __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.L[l].nbt), 1ull,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // bias gradient: column sums of d loss / d logits over the batch, summed in row order
+    // (readlanes; the same order as the three-launch path, so both agree bitwise)
+    if (LL.b) {
+      const float* pb = reinterpret_cast<const float*>(smem + LL.p_lds) + 5 * LL.Np;
+      for (int cc = 0; cc < C; ++cc) {
+        const int bits = __float_as_int(dr[cc]);
+        float v = 0.f;
+        for (int mm = 0; mm < B; ++mm) v += __int_as_float(__builtin_amdgcn_readlane(bits, mm));
+        if (lane == 0) LL.gb[cc] = pb[cc] + gs * v;
+      }
+    }
+    if (st) YSTAMP(18);
+  }
   // ---- dW of layers 2 .. nl-1 (layer 1's dW runs in the column workgroups) -----------------
   for (int l = 2; l < nl; ++l) {
     const SLayer& L = a.L[l];

@@ -113,7 +113,8 @@ def linear_bias_relu(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[tor
                      module: Optional[nn.Module] = None,
                      bf16_params: Optional[tuple] = None) -> torch.Tensor:
     """``relu(x W^T + b)`` -> bf16.  ``bf16_params = (W_bf16, b_bf16)``: rounded copies of the
-    parameters made for this step; with a bf16 input the forward then runs on hipBLASLt."""
+    parameters made for this step; with a bf16 input the forward then runs on the LDS-DMA MFMA
+    GEMM (ops.gemm, bias + ReLU in its epilogue; hipBLASLt only under the PLAIN_BLAS A/B switch)."""
     if not x2d.is_cuda:
         return torch.relu(torch.nn.functional.linear(x2d, weight, bias))
     if not _lib.native_available():
