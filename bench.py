@@ -145,6 +145,11 @@ def main():
                              "model's step, B=32, H=384, measured on CPU; the reference publishes "
                              "no throughput); per-site rate in per_site",
             "final_loss": round(loss, 5),
+            # HBM high-water mark of the run (allocator view: model, optimizer state, activations,
+            # graph pools and the resident synthetic dataset of --pool batches)
+            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
+            "dataset_hbm_gib": round(args.pool * args.batch * S * args.comps * args.window
+                                     * (2 if args.feed == "device" else 4) / 2**30, 3),
         }
         print(json.dumps(rec), flush=True)
     from dinunet_implementations_amd.parallel import shutdown

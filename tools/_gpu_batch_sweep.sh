@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && export TMPDIR=/tmp && mkdir -p gpurun_out
 : > gpurun_out/batch_sweep.jsonl
 for B in ${BATCHES:-32 128 512 2048}; do
-  timeout -k 10 240 python bench.py --steps 30 --warmup 10 --batch $B > gpurun_out/bench_b$B.log 2>&1 || { tail -20 gpurun_out/bench_b$B.log; exit 3; }
+  timeout -k 10 ${BLIMIT:-240} python bench.py --steps ${BSTEPS:-30} --warmup 10 --batch $B --pool ${POOL:-8} > gpurun_out/bench_b$B.log 2>&1 || { tail -20 gpurun_out/bench_b$B.log; exit 3; }
   grep '"metric"' gpurun_out/bench_b$B.log >> gpurun_out/batch_sweep.jsonl
   grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_b$B.log
 done
