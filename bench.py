@@ -80,6 +80,7 @@ def main():
     xs = torch.randn(args.pool, args.batch, S, args.comps, args.window, device=dev, generator=g)
     ys = torch.randint(0, 2, (args.pool, args.batch), device=dev, generator=g)
 
+    pi, it0 = getattr(engine, "power_iterations", None), None
     if args.feed == "device":
         # the site's (synthetic) dataset resident in HBM as bf16, batches gathered on the device
         # by the step's first launch; the timed steps run as replays of K-step graphs
@@ -91,6 +92,7 @@ def main():
         step.bind(src, steps_per_graph=K)
         step.run(args.warmup)
         step.prepare(args.steps)
+        it0 = pi() if pi else None
         torch.cuda.synchronize()
         grp.barrier()
         torch.cuda.synchronize()
@@ -112,6 +114,12 @@ def main():
         grp.barrier()
         torch.cuda.synchronize()
     dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    iters = None
+    if it0 is not None:
+        # rank-dAD: power iterations actually run per timed step (mean over the factorised
+        # layers; dad_tol may stop a layer before dad_num_pow_iters)
+        it1 = pi()
+        iters = round(sum(b - a for a, b in zip(it0, it1)) / max(1, len(it0)) / args.steps, 3)
     grp.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
     dt = float(dt.item())
     loss = float(step.last_loss.detach())
@@ -145,6 +153,7 @@ def main():
                              "model's step, B=32, H=384, measured on CPU; the reference publishes "
                              "no throughput); per-site rate in per_site",
             "final_loss": round(loss, 5),
+            **({"dad_iters_per_step": iters} if iters is not None else {}),
             # HBM high-water mark of the run (allocator view: model, optimizer state, activations,
             # graph pools and the resident synthetic dataset of --pool batches)
             "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),

@@ -240,7 +240,19 @@ struct GemmGroup {
   // split-K arrival tickets, one per output tile of the launch (zero between launches: each
   // tile's combining workgroup resets its own); null -> gemm_splitk_reduce combines
   int* cnt;
+  // step counters advanced once by workgroup 0 (dn_gemm_arm_bump: the training step whose fused
+  // Adam also packs the next step's weights and batch, optim.hip adam_pack_kernel)
+  int* bump_t;
+  long long* bump_c;
 };
+
+// the armed bump rides in the next launch of one group only
+__device__ __forceinline__ void group_bump(const GemmGroup& g) {
+  if (g.bump_t && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+    *g.bump_t += 1;
+    if (g.bump_c) *g.bump_c += 1;
+  }
+}
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 
@@ -364,6 +376,7 @@ gemm_kernel(GemmGroup g) {
   const int bid = (int)blockIdx.x;
   const int gtile = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
   if (gtile >= ntiles) return;
+  group_bump(g);
   int pi = 0;
   while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
   const GemmProb& P = g.p[pi];
@@ -593,6 +606,7 @@ gemm_dma_kernel(GemmGroup g) {
   const int bid = (int)blockIdx.x;
   const int gtile = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);  // XCD-contiguous tiles
   if (gtile >= ntiles) return;
+  group_bump(g);
   int pi = 0;
   while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
   const GemmProb& P = g.p[pi];
@@ -921,7 +935,14 @@ static bool vec_ok(const void* base, int kcontig, int rows, int K, long ld) {
   return aligned16(base) && ld % 8 == 0 && (kcontig ? K % 8 == 0 : rows % 8 == 0);
 }
 
+int* g_bump_t = nullptr;
+long long* g_bump_c = nullptr;
+
 static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int tile, hipStream_t st) {
+  g.bump_t = g_bump_t;
+  g.bump_c = g_bump_c;
+  g_bump_t = nullptr;
+  g_bump_c = nullptr;
   g.vec = 1;
   g.vepi = 1;
   for (int i = 0; i < g.n; ++i) {
@@ -938,6 +959,18 @@ static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int t
 }
 
 }  // namespace
+
+// Arm a one-shot step-counter bump: the NEXT GEMM launch of this process advances *t (and *c when
+// given) once, from workgroup 0, before any other kernel of the step reads them.  Issued at
+// capture time, the pointers are baked into the captured launch.  dn_gemm_bump_armed reports a
+// bump no launch consumed.
+DN_API int dn_gemm_arm_bump(int* t, long long* c) {
+  g_bump_t = t;  // null: disarm
+  g_bump_c = t ? c : nullptr;
+  return DN_OK;
+}
+
+DN_API int dn_gemm_bump_armed() { return g_bump_t != nullptr; }
 
 // 1: bf16 x bf16 GEMMs use the LDS-DMA kernel (default); 0: the register-staged kernel.
 DN_API int dn_gemm_set_dma(int on) {

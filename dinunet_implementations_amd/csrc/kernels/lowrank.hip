@@ -113,6 +113,7 @@ struct LrLayer {
   float* Qsend;    // [in][r]  committed Q: input of every iteration, output, warm start
   float* norms;    // [n3][2] per-block ||Q - Q_prev||^2, ||Q||^2 of the last lr_gtp
   int* active;     // power iteration still running
+  int* iters;      // iterations run (cumulative, counted by lr_gq; rank-dAD dad_tol reporting)
   int out, in, r;
   int b1, n1;      // lr_gq: first block, blocks (16 rows each)
   int b3, n3;      // lr_gtp: first block, blocks (16 columns each)
@@ -300,6 +301,7 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
       }
     }
   }
+  if (lead) *X.iters += 1;  // one writer per layer (its first block's thread 0)
   const bool vec = (X.in & 3) == 0, ql = X.in * X.r <= LR_QLDS;  // uniform per layer
 #define LR_GQ(V, E) (ql ? gq_main<V, E, true>(X, qs, red, tid, w) : gq_main<V, E, false>(X, qs, red, tid, w))
   if (X.err) {

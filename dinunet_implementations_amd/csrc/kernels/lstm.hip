@@ -196,7 +196,8 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
                 float* __restrict__ hseq,        // SEQ: [Bp][S][ndir*HD] (processing order)
                 float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
                 float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
-                float* __restrict__ pre) {  // [B*S][ndir][4*HD] fp32 gate pre-activations (+ bias), or null
+                float* __restrict__ pre,  // [B*S][ndir][4*HD] fp32 gate pre-activations (+ bias), or null
+                int bsplit) {  // > 0: bias holds b_ih at [0] and b_hh at [bsplit], summed here
   constexpr int NW = HD / (16 * UG);
   constexpr int NT = NW * 64;
   constexpr int MT = 4 * UG;   // m-tiles per wave
@@ -255,7 +256,9 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
         else wlds[w][mt - NRM][ks][lane] = v;
       }
   }
-  for (int i = tid; i < 4 * HD; i += NT) bias_s[i] = bias[dir * 4 * HD + i];
+  for (int i = tid; i < 4 * HD; i += NT)
+    bias_s[i] = bsplit ? bias[dir * 4 * HD + i] + bias[bsplit + dir * 4 * HD + i]
+                       : bias[dir * 4 * HD + i];
   for (int i = tid; i < 2 * 16 * LDH; i += NT) (&hbuf[0][0][0])[i] = (bf16)0.f;
   if (tid < NW / 4) hcnt[tid] = 0;
   __syncthreads();
@@ -894,6 +897,10 @@ static int lstm_ug() {
   return ug;
 }
 
+// bias layout of the current dn_lstm_fwd call (0: fused b_ih + b_hh; > 0: split, see the kernel),
+// set by dn_lstm_fwd for the launchers below (host launches are issued from one thread)
+int g_bias_split = 0;
+
 template <int HD, int BR, int UG>
 int launch_fwd_ug(const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
@@ -901,10 +908,11 @@ int launch_fwd_ug(const bf16* xp, const float* bias, const bf16* whh, int B, int
   dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
   if (hseq)
     hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, true, UG>), grid, block, 0, st, xp, bias, whh, B, S,
-                       Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre);
+                       Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, g_bias_split);
   else
     hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false, UG>), grid, block, 0, st, xp, bias, whh, B,
-                       S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre);
+                       S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre,
+                       g_bias_split);
   return dn_launch_status();
 }
 
@@ -1092,11 +1100,16 @@ static bool lstm_fits_32bit(int B, int S, int HD, int ndir, int BR) {
 
 // xp: the bf16 input projection [B*S][ndir][4*HD]; pre (fp32, same layout, or null when no
 // backward follows) receives the gate pre-activations (+ bias) the backward consumes
+// bias_split > 0: `bias` is [2][ndir*4HD] (b_ih image, then b_hh image at offset bias_split, the
+// form the fused Adam keeps packed: optim.hip adam_pack_kernel); 0: the fused sum of dn_lstm_pack
 DN_API int dn_lstm_fwd(const void* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
                        int ndir, float* c_save, void* hprev, float* hseq, float* hmean,
-                       float mean_scale, float* hT, float* cT, float* pre, hipStream_t st) {
+                       float mean_scale, float* hT, float* cT, float* pre, int bias_split,
+                       hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
+  if (bias_split != 0 && bias_split != ndir * 4 * HD) return DN_BAD_SHAPE;
+  g_bias_split = bias_split;
   const int BR = pick_br(B, HD);
   if (!lstm_fits_32bit(B, S, HD, ndir, BR)) return DN_BAD_SHAPE;
   switch (HD) {

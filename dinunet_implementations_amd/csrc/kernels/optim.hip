@@ -1,6 +1,7 @@
 // Fused optimizer kernels over ONE flat fp32 parameter buffer (all of a model's tensors are views
 // into it), so a whole optimizer step is a single launch regardless of the parameter count.
 #include "common.h"
+#include "prologue.h"
 
 namespace {
 
@@ -47,6 +48,127 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
     m[t] = b1 * m[t] + (1.f - b1) * gr;
     v[t] = b2 * v[t] + (1.f - b2) * gr * gr;
     p[t] -= step * m[t] / (sqrtf(v[t]) * inv_sqrt_bc2 + eps);
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Fused Adam that also emits the NEXT step's operands: every updated
+// parameter element is written, rounded to bf16, straight into the packed images the step's
+// kernels read (the LSTM W_ih / W_hh / W_hh^T kernel layouts, the encoder's bf16 weight copy) and
+// the split LSTM bias images (b_ih, b_hh: dn_lstm_fwd bias_split); the gradient is zeroed as it is
+// consumed; and the next step's batch is gathered from the HBM-resident dataset at cursor + gofs
+// (prologue.h).  The step then starts at its encoder GEMM, which advances the step counter and the
+// cursor (gemm.hip group_bump): this launch READS both, so it cannot advance them itself.
+// update = 0: pack + gather only (priming the persistent images before the first such step).
+enum PackKind { PK_NONE = 0, PK_CAST = 1, PK_WIH = 2, PK_WHH = 3, PK_BIAS = 4 };
+constexpr int PACK_SEGS = 16;
+struct PackSeg {
+  long off;    // flat offset, multiple of 4
+  int n;       // elements (reference layout)
+  int kind, d; // PackKind, LSTM direction
+  void* dst;   // bf16 image (CAST / WIH / WHH), fp32 image (BIAS)
+  void* dst2;  // WHH: the W_hh^T image
+};
+struct PackPlan {
+  PackSeg s[PACK_SEGS];
+  int cnt;
+  int I, Hd, HD;  // LSTM input size, hidden, padded hidden
+};
+
+// fragment-linear position of (row, col) in a [rows][KS*32] image (lstm.hip frag_rc inverse)
+__device__ __forceinline__ int frag_index(int row, int col, int KS) {
+  const int T = row >> 4, n = row & 15, ks = col >> 5, q = (col >> 3) & 3, e = col & 7;
+  return ((T * KS + ks) * 64 + q * 16 + n) * 8 + e;
+}
+
+__device__ __forceinline__ void pack_store(const PackPlan& pl, const PackSeg& sg, int j, float v) {
+  const int GP = 4 * pl.HD;
+  switch (sg.kind) {
+    case PK_CAST:
+      reinterpret_cast<bf16*>(sg.dst)[j] = (bf16)v;
+      break;
+    case PK_WIH: {
+      const int row = j / pl.I, k = j - row * pl.I;
+      const int g = row / pl.Hd, u = row - g * pl.Hd;
+      reinterpret_cast<bf16*>(sg.dst)[(sg.d * GP + 4 * u + g) * pl.I + k] = (bf16)v;
+      break;
+    }
+    case PK_WHH: {
+      const int row = j / pl.Hd, k = j - row * pl.Hd;
+      const int g = row / pl.Hd, u = row - g * pl.Hd, m = 4 * u + g;
+      const int base = sg.d * GP * pl.HD;
+      int a, b;
+      if (pl.HD > 192) {
+        a = frag_index(m, k, pl.HD / 32);
+        b = frag_index(k, m, GP / 32);
+      } else {
+        a = m * pl.HD + k;
+        b = k * GP + m;
+      }
+      reinterpret_cast<bf16*>(sg.dst)[base + a] = (bf16)v;
+      reinterpret_cast<bf16*>(sg.dst2)[base + b] = (bf16)v;
+      break;
+    }
+    case PK_BIAS: {
+      const int g = j / pl.Hd, u = j - g * pl.Hd;
+      reinterpret_cast<float*>(sg.dst)[sg.d * GP + 4 * u + g] = v;
+      break;
+    }
+    default: break;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+adam_pack_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                 float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
+                 float grad_scale, const int* __restrict__ tdev, double b1d, double b2d, int update,
+                 int zero_grad, PackPlan pl, StepPrologue sp, int gofs, int ublocks) {
+  // blocks [0, ublocks) update the parameters (one float4 per thread and round), the rest gather
+  // the next batch: no divergent work mix inside a wave, every load of a round issued at once
+  if ((int)blockIdx.x >= ublocks) {
+    const long c = (*sp.cursor + gofs) % sp.nb;
+    const long ng = sp.ux + sp.ny, stride = (long)(gridDim.x - ublocks) * blockDim.x;
+    for (long i = (blockIdx.x - ublocks) * (long)blockDim.x + threadIdx.x; i < ng; i += stride)
+      prologue_item(sp, i, c);  // sp.ug == 0: the zeroing rides in the update below
+    return;
+  }
+  float bc1 = 1.f, inv_sqrt_bc2 = 1.f;
+  if (update) {  // the encoder GEMM of this step advanced *tdev (prebumped form)
+    const double t = (double)(*tdev);
+    bc1 = (float)(1.0 - pow(b1d, t));
+    inv_sqrt_bc2 = (float)(1.0 / sqrt(1.0 - pow(b2d, t)));
+  }
+  const float step = lr / bc1;
+  const long n4 = n >> 2, stride = (long)ublocks * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+    if (update) {
+      const f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
+      f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
+      f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gr = gg[e] * grad_scale + wd * pp[e];
+        mm[e] = b1 * mm[e] + (1.f - b1) * gr;
+        vv[e] = b2 * vv[e] + (1.f - b2) * gr * gr;
+        pp[e] -= step * mm[e] / (sqrtf(vv[e]) * inv_sqrt_bc2 + eps);
+      }
+      reinterpret_cast<f32x4*>(p)[i] = pp;
+      reinterpret_cast<f32x4*>(m)[i] = mm;
+      reinterpret_cast<f32x4*>(v)[i] = vv;
+    }
+    if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const long e0 = i << 2;
+    int s = 0;
+    while (s < pl.cnt && e0 >= pl.s[s].off + pl.s[s].n) ++s;
+    if (s < pl.cnt && e0 >= pl.s[s].off) {
+      const PackSeg& sg = pl.s[s];
+      const int j0 = (int)(e0 - sg.off);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j0 + e < sg.n) pack_store(pl, sg, j0 + e, pp[e]);
+    }
   }
 }
 
@@ -108,6 +230,49 @@ DN_API int dn_adam_dev(float* p, const float* g, float* m, float* v, long n, flo
                      (float)b1, (float)b2, eps, wd, 0.f, 0.f, grad_scale, (const int*)tdev, b1, b2, prebumped ? 0 : 1,
                      cursor);
   if (!prebumped) hipLaunchKernelGGL(adam_bump_kernel, dim3(1), dim3(1), 0, st, tdev);
+  return dn_launch_status();
+}
+
+// adam_pack_kernel launch.  segs: host PackSeg-compatible rows {off, n, kind, d, dst, dst2} sorted
+// by offset (cnt <= 16); the device-fed gather (gx ... yd) is optional (gx null: none).
+DN_API long dn_pack_seg_size() { return (long)sizeof(PackSeg); }
+DN_API int dn_adam_pack(float* p, float* g, float* m, float* v, long n, float lr, double b1,
+                        double b2, float eps, float wd, float grad_scale, const int* tdev,
+                        int update, int zero_grad, const void* segs, int cnt, int I, int Hd,
+                        int HD, const void* gx, int gx_bf16, long row_elems, const long long* gy,
+                        const long long* order, long nb, const long long* cursor, int B,
+                        void* xb, long long* yd, int gofs, hipStream_t st) {
+  if (n <= 0 || n % 4 || cnt < 0 || cnt > PACK_SEGS) return DN_BAD_SHAPE;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
+  if (update && !tdev) return DN_BAD_SHAPE;
+  PackPlan pl{};
+  pl.cnt = cnt;
+  pl.I = I;
+  pl.Hd = Hd;
+  pl.HD = HD;
+  const PackSeg* hs = reinterpret_cast<const PackSeg*>(segs);
+  for (int k = 0; k < cnt; ++k) {
+    pl.s[k] = hs[k];
+    const PackSeg& s = pl.s[k];
+    if (s.off % 4 || s.n <= 0 || s.off + s.n > n || !s.dst) return DN_BAD_SHAPE;
+    if (k && s.off < pl.s[k - 1].off + pl.s[k - 1].n) return DN_BAD_SHAPE;  // sorted, disjoint
+    if ((s.kind == PK_WIH || s.kind == PK_WHH || s.kind == PK_BIAS) && (Hd <= 0 || HD < Hd || I <= 0))
+      return DN_BAD_SHAPE;
+    if (s.kind == PK_WHH && !s.dst2) return DN_BAD_SHAPE;
+  }
+  StepPrologue sp{};
+  if (gx) {
+    const int rc = prologue_gather(sp, gx, gx_bf16, row_elems, gy, order, nb, cursor, B, xb, yd,
+                                   g, 0, nullptr);
+    if (rc != DN_OK) return rc;
+  }
+  // one item per thread up to 4096 workgroups per part (the chip holds ~2048 at a time; the
+  // rest start as the first retire)
+  auto parts = [](long items) { return (int)((items + 255) / 256 < 4096 ? (items + 255) / 256 : 4096); };
+  const int ub = parts(n / 4), gb = sp.gx ? parts(sp.ux + sp.ny) : 0;
+  hipLaunchKernelGGL(adam_pack_kernel, dim3(ub + gb), dim3(256), 0, st, p, g, m, v, n, lr,
+                     (float)b1, (float)b2, eps, wd, grad_scale, tdev, b1, b2, update, zero_grad,
+                     pl, sp, gofs, ub);
   return dn_launch_status();
 }
 

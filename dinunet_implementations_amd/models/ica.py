@@ -220,6 +220,17 @@ class ICALstm(nn.Module):
     def stem_parameters(self):
         return self.encoder.parameters()
 
+    def persistent_pack(self, device) -> Optional["ops.lstm.PersistentPack"]:
+        """Step-persistent packed operands for a fused Adam that keeps them current
+        (``runtime.step.TrainStep`` device-fed steps): the LSTM weight images and the encoder's
+        bf16 weight / bias, i.e. exactly what :meth:`stem`'s pack launch would produce."""
+        lin = self.encoder[0]
+        if not (self.use_fused and lin.bias is not None and self.lstm.bias):
+            return None
+        from ..ops.lstm import PersistentPack
+        flat = [t for cell in self.lstm.lstms for t in cell.params()]
+        return PersistentPack(flat, self.lstm.input_size, device, casts=(lin.weight, lin.bias))
+
     def body_loss(self, enc: torch.Tensor, y: torch.Tensor):
         """Second half of :meth:`forward_loss`: bi-LSTM, classifier, softmax-CE on ``enc``."""
         packed, self._packed = getattr(self, "_packed", None), None

@@ -26,6 +26,8 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_void_p])
 
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
+_lib.register("dn_gemm_arm_bump", [_lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_gemm_bump_armed", [])
 _lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 14 + [_lib.c_int] * 8
               + [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p])
 

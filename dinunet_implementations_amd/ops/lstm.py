@@ -52,7 +52,7 @@ _lib.register("dn_lstm_pack_gather", [_lib.c_void_p] * 8 + [_lib.c_int] * 3
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
-                              _lib.c_void_p, _lib.c_void_p])
+                              _lib.c_void_p, _lib.c_int, _lib.c_void_p])
 _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_long, _lib.c_long, _lib.c_float, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
@@ -152,9 +152,11 @@ class _BiLSTMFn(torch.autograd.Function):
         need_bwd = any(ctx.needs_input_grad)
         # fp32 gate pre-activations (x W_ih^T + h W_hh^T + b) for the backward
         pre = torch.empty(B * S, ndir * GP, dtype=torch.float32, device=dev) if need_bwd else None
+        # a persistent pack (PersistentPack) keeps b_ih and b_hh as two images: summed in-kernel
+        bsplit = ndir * GP if bias_p.numel() == 2 * ndir * GP else 0
         _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
                   ndir, c_save.data_ptr(), hprev.data_ptr(), _lib.ptr(hseq), _lib.ptr(hmean),
-                  1.0 / S, hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), st)
+                  1.0 / S, hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), bsplit, st)
         if mode == "mean":
             out = hmean
         else:
@@ -230,6 +232,13 @@ def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = 
     ``casts`` (<= 4 fp32 tensors) are rounded to bf16 by the same launch; the copies are
     appended to ``cast_out``.
     """
+    pp = _PERSIST
+    if pp is not None and not side and pp.matches(params, casts):
+        # the fused Adam keeps these images current (optim.hip adam_pack_kernel): no launch
+        if cast_out is not None:
+            cast_out.extend(pp.casts)
+        pp.used = True
+        return pp.wih_p, pp.bias_p, pp.whh_p, pp.whhT_p, None
     ndir = len(params) // 4
     Hd = params[2].shape[1]
     HD = padded_hidden(Hd)
@@ -290,6 +299,81 @@ class _nullctx:
 
 _DEFERRED: Optional[list] = None
 _RIDE = None
+_PERSIST = None
+
+# PackKind of csrc/kernels/optim.hip
+PK_CAST, PK_WIH, PK_WHH, PK_BIAS = 1, 2, 3, 4
+
+
+class PersistentPack:
+    """Packed LSTM operand images (and bf16 copies of ``casts``, e.g. the encoder weights) that
+    live across steps and are rewritten by the fused Adam as it updates each parameter
+    (``FusedAdam.step_pack``), so the training step needs no repack launch.  Same layouts as
+    :func:`pack_params` except the bias: ``[2][ndir*4HD]`` (the ``b_ih`` image, then ``b_hh``),
+    which ``dn_lstm_fwd`` sums as it loads (``bias_split``) -- the same fp32 sum the pack forms.
+    Padded units / columns are zero from allocation and never written.  While
+    :class:`use_persistent` is active, :func:`pack_params` on the same parameters returns these
+    buffers without a launch."""
+
+    def __init__(self, params: Sequence[Tensor], input_size: int, device,
+                 casts: Sequence[Tensor] = ()):
+        self.params = list(params)
+        if len(self.params) % 4 or any(p is None for p in self.params):
+            raise ValueError("PersistentPack: every direction needs W_ih, b_ih, W_hh, b_hh")
+        self.ndir = len(self.params) // 4
+        self.Hd = self.params[2].shape[1]
+        self.HD = padded_hidden(self.Hd)
+        self.I = int(input_size)
+        GP = 4 * self.HD
+        z = dict(device=device)
+        self.wih_p = torch.zeros(self.ndir * GP, self.I, dtype=torch.bfloat16, **z)
+        self.bias_p = torch.zeros(2 * self.ndir * GP, dtype=torch.float32, **z)
+        self.whh_p = torch.zeros(self.ndir, GP, self.HD, dtype=torch.bfloat16, **z)
+        self.whhT_p = torch.zeros(self.ndir, self.HD, GP, dtype=torch.bfloat16, **z)
+        self.cast_src = list(casts)
+        self.casts = [torch.zeros(c.shape, dtype=torch.bfloat16, **z) for c in casts]
+        self.used = False
+
+    def matches(self, params, casts) -> bool:
+        return (len(params) == len(self.params)
+                and all(a is b for a, b in zip(params, self.params))
+                and len(casts) == len(self.cast_src)
+                and all(a is b for a, b in zip(casts, self.cast_src)))
+
+    def rows(self, flat) -> list:
+        """``(flat offset, numel, kind, direction, dst ptr, dst2 ptr)`` per packed parameter of
+        the flat buffer ``flat`` (``ops.FlatParams``), sorted by offset."""
+        offs = {id(p): o for p, o, _ in flat.segments()}
+        GP = 4 * self.HD
+        out = []
+        for d in range(self.ndir):
+            w_ih, b_ih, w_hh, b_hh = self.params[4 * d:4 * d + 4]
+            out.append((offs[id(w_ih)], w_ih.numel(), PK_WIH, d, self.wih_p.data_ptr(), 0))
+            out.append((offs[id(w_hh)], w_hh.numel(), PK_WHH, d, self.whh_p.data_ptr(),
+                        self.whhT_p.data_ptr()))
+            out.append((offs[id(b_ih)], b_ih.numel(), PK_BIAS, d, self.bias_p.data_ptr(), 0))
+            out.append((offs[id(b_hh)], b_hh.numel(), PK_BIAS, d,
+                        self.bias_p.data_ptr() + 4 * self.ndir * GP, 0))
+        for src, dst in zip(self.cast_src, self.casts):
+            out.append((offs[id(src)], src.numel(), PK_CAST, 0, dst.data_ptr(), 0))
+        return sorted(out)
+
+
+class use_persistent:
+    """While active, :func:`pack_params` on ``pp``'s parameters returns ``pp``'s buffers."""
+
+    def __init__(self, pp: Optional[PersistentPack]):
+        self.pp = pp
+
+    def __enter__(self):
+        global _PERSIST
+        self._prev, _PERSIST = _PERSIST, self.pp
+        return self.pp
+
+    def __exit__(self, *a):
+        global _PERSIST
+        _PERSIST = self._prev
+        return False
 
 
 class ride_pack:

@@ -40,6 +40,20 @@ _lib.register("dn_cast_f32_bf16", [_lib.c_void_p, _lib.c_void_p, _lib.c_long, _l
 _lib.register("dn_cast_bf16_f32", [_lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_float,
                                    _lib.c_void_p])
 
+_lib.register("dn_adam_pack", [_lib.c_void_p] * 4 + [_lib.c_long, _lib.c_float, _lib.c_double,
+                               _lib.c_double, _lib.c_float, _lib.c_float, _lib.c_float,
+                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int,
+                               _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int,
+                               _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                               _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
+                               _lib.c_int, _lib.c_void_p])
+
+
+def ctypes_addr(obj) -> int:
+    import ctypes
+    return ctypes.addressof(obj)
+
+
 ALIGN = 4  # elements (16 bytes)
 
 
@@ -145,6 +159,47 @@ class FusedAdam:
                   self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
                   self.weight_decay, grad_scale, self._tdev.data_ptr(), int(prebumped),
                   _lib.ptr(self.cursor), _lib.stream())
+
+    # Adam that also emits the next step's operands (optim.hip adam_pack_kernel) ------------------
+    def attach_pack(self, pack, src=None, xb: Optional[torch.Tensor] = None,
+                    yd: Optional[torch.Tensor] = None):
+        """Keep ``pack`` (``ops.lstm.PersistentPack``) current from every :meth:`step_pack`, and
+        gather the next batch of ``src`` (``DeviceSource``) into ``xb`` / ``yd`` there too."""
+        import ctypes
+        rows = pack.rows(self.flat)
+
+        class _Seg(ctypes.Structure):
+            _fields_ = [("off", ctypes.c_long), ("n", ctypes.c_int), ("kind", ctypes.c_int),
+                        ("d", ctypes.c_int), ("dst", ctypes.c_void_p), ("dst2", ctypes.c_void_p)]
+        L = _lib.lib()
+        L.dn_pack_seg_size.restype = ctypes.c_long
+        if ctypes.sizeof(_Seg) != L.dn_pack_seg_size():
+            raise RuntimeError("pack segment layout mismatch with the kernel library")
+        tab = (_Seg * max(1, len(rows)))()
+        for i, (off, n, kind, d, dst, dst2) in enumerate(rows):
+            tab[i] = _Seg(off, n, kind, d, dst, dst2 or None)
+        self._pack = (pack, tab, len(rows), src, xb, yd)
+
+    def step_pack(self, grad_scale: float = 1.0, update: bool = True, gofs: int = 1):
+        """ONE launch: the graph-capturable Adam step (bias corrections from the device counter,
+        which the step's first GEMM advanced: ``dn_gemm_arm_bump``), the attached packed images
+        rewritten from the updated parameters, the gradient zeroed, and the batch at
+        ``cursor + gofs`` gathered.  ``update=False``: images + gather + zeroing only (priming)."""
+        pack, tab, cnt, src, xb, yd = self._pack
+        d = self.flat.data
+        if self._tdev is None:
+            self.sync_device_step()
+        b1, b2 = self.betas
+        if src is not None:
+            gx = [src.X.data_ptr(), int(src.X.dtype == torch.bfloat16), src.row,
+                  src.Y.data_ptr(), _lib.ptr(src.order), src.nb, src.cursor.data_ptr(), src.B,
+                  xb.data_ptr(), yd.data_ptr()]
+        else:
+            gx = [None, 0, 0, None, None, 1, None, 0, None, None]
+        _lib.call("dn_adam_pack", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
+                  self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
+                  self.weight_decay, grad_scale, self._tdev.data_ptr(), int(update), 1,
+                  ctypes_addr(tab), cnt, pack.I, pack.Hd, pack.HD, *gx, int(gofs), _lib.stream())
 
     def device_step(self) -> torch.Tensor:
         """The device step counter (int32[1]) the graph-captured update reads; a step prologue

@@ -429,6 +429,13 @@ class RankDADEngine(Engine):
             self._table.gq(it, self.tol)
             self._table.orth_gtp(it)
 
+    def power_iterations(self) -> Optional[List[int]]:
+        """Cumulative power iterations each factorised layer ran on the device (``dad_tol``
+        stops a layer early; ``dad_num_pow_iters`` bounds it), or None off the device path."""
+        if not (self.fast and getattr(self, "fast_layers", None)):
+            return None
+        return self._table.iterations()
+
     def _fast_reduce(self) -> float:
         g = self.group
         W = g.world

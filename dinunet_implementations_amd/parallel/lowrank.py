@@ -103,7 +103,7 @@ class LowRankTable:
 
         class LrLayer(ctypes.Structure):
             _fields_ = [(k, ctypes.c_void_p) for k in ("G", "err", "P", "Psend", "Qsend", "norms",
-                                                     "active")] + \
+                                                     "active", "iters")] + \
                        [(k, ctypes.c_int) for k in ("out", "in_", "r", "b1", "n1", "b3", "n3")]
         if ctypes.sizeof(LrLayer) != L.dn_lr_layer_size():
             raise RuntimeError("low-rank table layout mismatch with the kernel library")
@@ -113,6 +113,8 @@ class LowRankTable:
         self.n = n
         self._keep = []
         self.active = torch.ones(max(n, 1), dtype=torch.int32, device=device)
+        # power iterations each layer actually ran (lr_gq counts them; dad_tol stops early)
+        self.iters = torch.zeros(max(n, 1), dtype=torch.int32, device=device)
         tab = (LrLayer * max(n, 1))()
         b1 = b3 = 0
         starts = []
@@ -132,6 +134,7 @@ class LowRankTable:
             t.P, t.Psend, t.Qsend = P.data_ptr(), ps.data_ptr(), qs.data_ptr()
             t.norms = norms.data_ptr()
             t.active = self.active.data_ptr() + 4 * i
+            t.iters = self.iters.data_ptr() + 4 * i
             t.out, t.in_, t.r, t.b1, t.n1, t.b3, t.n3 = out_f, in_f, r, b1, n1, b3, n3
             b1 += n1
             b3 += n3
@@ -140,6 +143,10 @@ class LowRankTable:
         self.blocks1, self.blocks3, self.total = b1, b3, total
         self.table = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
         self.starts = torch.tensor(starts or [0], dtype=torch.int64).to(device)
+
+    def iterations(self) -> list:
+        """Cumulative power iterations run per layer (host sync)."""
+        return [int(v) for v in self.iters[:self.n].tolist()]
 
     def _stage(self, stage: int, it: int, tol: float = 0.0):
         if self.n:

@@ -25,7 +25,8 @@ from typing import Callable, Optional
 import torch
 
 from .. import ops
-from ..ops.lstm import defer_pack, ride_pack, run_deferred_pack
+from ..ops import _lib
+from ..ops.lstm import defer_pack, ride_pack, run_deferred_pack, use_persistent
 from .timers import NULL, PhaseTimer, enabled_by_env
 
 
@@ -48,6 +49,11 @@ CAPTURE_MODE = "thread_local"
 # The LSTM weight repack leaves the graph and rides in the step prologue's launch
 # (DINUNET_DEFER_PACK=0 keeps it captured)
 DEFER_PACK = os.environ.get("DINUNET_DEFER_PACK", "1") != "0"
+
+# Device-fed single-site steps: the fused Adam rewrites the packed LSTM / encoder operand images
+# from the parameters it updates, zeroes the gradient and gathers the next batch (one launch
+# instead of Adam + a pack/gather launch per step); DINUNET_ADAM_PACK=0 keeps the pack launch
+ADAM_PACK = os.environ.get("DINUNET_ADAM_PACK", "1") != "0"
 
 
 class _NoDefer:
@@ -323,6 +329,17 @@ class TrainStep:
         self._dK = max(1, int(steps_per_graph)) if (self.use_graph and self._graph_opt_ok()) else 1
         self._dgraphs = {}
         self._dcalls = 0
+        # the Adam-emitted operand pack (ADAM_PACK): every replayed step then runs encoder GEMM
+        # (which advances Adam's step counter and the cursor) ... Adam (update + images + zeroed
+        # gradient + NEXT batch); the eager warm-up steps keep the pack launch
+        self._apack = None
+        from ..ops.gemm import PLAIN_BLAS
+        if (ADAM_PACK and self.use_graph and self._graph_opt_ok() and not PLAIN_BLAS
+                and self._rides() and hasattr(self.model, "persistent_pack")):
+            pp = self.model.persistent_pack(dev)
+            if pp is not None:
+                self.opt.attach_pack(pp, src, self._dsx, self._dsy)
+                self._apack = pp
 
     def _rides(self) -> bool:
         fn = getattr(self.model, "prologue_rides_pack", None)
@@ -337,8 +354,44 @@ class TrainStep:
         self.src.gather(self._dsx, self._dsy, self.flat.grad, bump)
         return _NoDefer()
 
+    def _dev_body_apack(self):
+        """One device-fed step whose operands the previous step's Adam (or :meth:`_apack_prime`)
+        already packed and gathered: the encoder GEMM advances Adam's counter and the cursor."""
+        sx, sy = self._dsx, self._dsy
+        _lib.call("dn_gemm_arm_bump", self.opt.device_step().data_ptr(), self.src.cursor.data_ptr())
+        self._apack.used = False
+        try:
+            with use_persistent(self._apack):
+                out, loss, pred = self._fwd_bwd(sx, sy)
+        finally:
+            armed = int(_lib.lib().dn_gemm_bump_armed())
+            _lib.call("dn_gemm_arm_bump", None, None)  # never leaks into a later launch
+        if armed or not self._apack.used:
+            raise RuntimeError("Adam-emitted pack: the forward did not start with the encoder GEMM "
+                               "on the persistent operand images")
+        if self._pre_reduce is not None:
+            self._pre_reduce()
+        scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
+                 else self.engine.reduce())
+        self.opt.step_pack(grad_scale=scale)
+        return out, loss, pred
+
+    def _apack_prime(self):
+        """Before the first replay of a run: the persistent images from the current parameters,
+        the gradient zeroed and the batch at the cursor gathered (one launch); the cursor steps
+        back one, so the first step's encoder GEMM brings it back (see :meth:`_apack_unprime`)."""
+        self.opt.sync_device_step()
+        self.opt.step_pack(update=False, gofs=0)
+        self.src.cursor.sub_(1)
+
+    def _apack_unprime(self):
+        # after the last replay: the cursor names the NEXT batch again (the eager convention)
+        self.src.cursor.add_(1)
+
     def _dev_body(self, graph_opt: bool):
         """One whole device-fed step as issued into the current stream (eager or captured)."""
+        if self._apack is not None and graph_opt:
+            return self._dev_body_apack()
         bump = self.opt.device_step() if graph_opt else None
         sx, sy = self._dsx, self._dsy
         with self._dev_prologue(bump) as rp:
@@ -416,55 +469,69 @@ class TrainStep:
             raise RuntimeError("TrainStep.run: bind a DeviceSource first")
         loss = self.last_loss
         done = 0
-        while done < n:
-            self._dcalls += 1
-            if not self.use_graph or self._dcalls <= self.eager_warmup:
-                if self.use_graph:  # warm-up off the capture stream, like __call__
-                    s = torch.cuda.Stream()
-                    s.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.stream(s):
-                        loss = self._dev_eager()
-                    torch.cuda.current_stream().wait_stream(s)
-                else:
-                    loss = self._dev_eager()
-                done += 1
-                continue
-            if self._dgraphs and self.opt.lr != self._cap_lr and any(
-                    v[2] is True for v in self._dgraphs.values()):
-                self._dgraphs = {}  # the learning rate is baked into the captured update
-            if self.split:
-                if "split" not in self._dgraphs:
-                    self._dev_capture_split()
-                ga, gb, (out, loss, pred), _ = self._dgraphs["split"]
-                with self.timers.phase("fwd_bwd"):
-                    ga.replay()
-                    for b in self._first_buckets:  # all-reduce under the stem backward
-                        self.engine.launch_bucket(b)
-                    gb.replay()
-                self.engine.sync_enabled = True
-                with self.timers.phase("reduce"):
-                    scale = self._reduce_after_replay()
-                with self.timers.phase("optim"):
-                    self.opt.step(grad_scale=scale)
-                self.last_out, self.last_loss, self.last_pred = out, loss, pred
-                done += 1
-                continue
-            k = self._dK if n - done >= self._dK else 1
-            if k not in self._dgraphs:
-                self._dev_capture(k)
-            g, (out, loss, pred), graph_opt = self._dgraphs[k]
-            with self.timers.phase("fwd_bwd"):
-                g.replay()
-            if graph_opt:
-                self.opt.step_count += k
-            else:
-                with self.timers.phase("reduce"):
-                    scale = self._reduce_after_replay()
-                with self.timers.phase("optim"):
-                    self.opt.step(grad_scale=scale)
-            self.last_out, self.last_loss, self.last_pred = out, loss, pred
-            done += k
+        primed = False
+        try:
+            while done < n:
+                loss, done, primed = self._run_one(n, done, loss, primed)
+        finally:
+            if primed:
+                self._apack_unprime()
         return loss
+
+    def _run_one(self, n: int, done: int, loss, primed: bool):
+        """One eager step, one split-graph step or one K-step replay of :meth:`run`; returns
+        ``(loss, done, primed)``."""
+        self._dcalls += 1
+        if not self.use_graph or self._dcalls <= self.eager_warmup:
+            if primed:  # (never: warm-up steps precede every replay)
+                self._apack_unprime()
+                primed = False
+            if self.use_graph:  # warm-up off the capture stream, like __call__
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    loss = self._dev_eager()
+                torch.cuda.current_stream().wait_stream(s)
+            else:
+                loss = self._dev_eager()
+            return loss, done + 1, primed
+        if self._dgraphs and self.opt.lr != self._cap_lr and any(
+                v[2] is True for v in self._dgraphs.values()):
+            self._dgraphs = {}  # the learning rate is baked into the captured update
+        if self.split:
+            if "split" not in self._dgraphs:
+                self._dev_capture_split()
+            ga, gb, (out, loss, pred), _ = self._dgraphs["split"]
+            with self.timers.phase("fwd_bwd"):
+                ga.replay()
+                for b in self._first_buckets:  # all-reduce under the stem backward
+                    self.engine.launch_bucket(b)
+                gb.replay()
+            self.engine.sync_enabled = True
+            with self.timers.phase("reduce"):
+                scale = self._reduce_after_replay()
+            with self.timers.phase("optim"):
+                self.opt.step(grad_scale=scale)
+            self.last_out, self.last_loss, self.last_pred = out, loss, pred
+            return loss, done + 1, primed
+        k = self._dK if n - done >= self._dK else 1
+        if k not in self._dgraphs:
+            self._dev_capture(k)
+        g, (out, loss, pred), graph_opt = self._dgraphs[k]
+        if self._apack is not None and graph_opt and not primed:
+            self._apack_prime()
+            primed = True
+        with self.timers.phase("fwd_bwd"):
+            g.replay()
+        if graph_opt:
+            self.opt.step_count += k
+        else:
+            with self.timers.phase("reduce"):
+                scale = self._reduce_after_replay()
+            with self.timers.phase("optim"):
+                self.opt.step(grad_scale=scale)
+        self.last_out, self.last_loss, self.last_pred = out, loss, pred
+        return loss, done + k, primed
 
     def prepare(self, n: int = 0):
         """Capture (without running) every graph a following ``run(n)`` will replay, so a timed
@@ -481,5 +548,8 @@ class TrainStep:
 
     @property
     def last_labels(self):
-        """Labels of the last device-fed step (the static label buffer)."""
+        """Labels of the last device-fed step.  With the Adam-emitted pack the static label
+        buffer already holds the NEXT batch's labels, so they are looked up at the cursor."""
+        if self._apack is not None and self._dgraphs:
+            return self.src.batch(int(self.src.cursor.item()) - 1)[1]
         return self._dsy

@@ -182,8 +182,10 @@ def test_lstm_fwd_bwd_matches_reference(B, S, I, Hd, ndir, mode):
     ro = hs.mean(1) if mode == "mean" else hs
     assert out.shape == ro.shape
     errs = {"out": rel(out, ro), "hT": rel(hT, rh), "cT": rel(cT, rc)}
-    assert errs["out"] < 2e-2
-    assert errs["hT"] < 3e-2 and errs["cT"] < 3e-2
+    # tolerances ~2x the largest observed error over these cases on MI355X (r3,
+    # profiles/r3_lstm_errors.jsonl: forward <= 2.5e-3, gradients <= 3.3e-3)
+    assert errs["out"] < 4e-3
+    assert errs["hT"] < 5e-3 and errs["cT"] < 5e-3
     g = torch.randn_like(out)
     (out * g).sum().backward()
     (ro * g).sum().backward()
@@ -192,10 +194,10 @@ def test_lstm_fwd_bwd_matches_reference(B, S, I, Hd, ndir, mode):
         for name, t, tr in zip(("w_ih", "b_ih", "w_hh", "b_hh"), p, pr):
             errs[f"d{name}{d}"] = rel(t.grad, tr.grad)
     _record_errs("lstm", dict(B=B, S=S, I=I, Hd=Hd, ndir=ndir, mode=mode), errs)
-    assert errs["dx"] < 5e-2
+    assert errs["dx"] < 7e-3
     for k, v in errs.items():
         if k.startswith("d"):
-            assert v < 5e-2, (k, v)
+            assert v < 7e-3, (k, v)
 
 
 def test_linear_bias_relu_grad():

@@ -11,10 +11,10 @@ import torch.distributed as dist
 pytestmark = pytest.mark.gpu
 
 
-def _model(seed):
+def _model(seed, hidden=128):
     from dinunet_implementations_amd.models import ICALstm
     torch.manual_seed(seed)
-    m = ICALstm(input_size=64, hidden_size=128, num_comps=20, window_size=10).cuda().train()
+    m = ICALstm(input_size=64, hidden_size=hidden, num_comps=20, window_size=10).cuda().train()
     m.classifier[0].p = 0.0  # no dropout: runs must be comparable step for step
     return m
 
@@ -24,7 +24,7 @@ def _trainer(seed, engine="dSGD", group=None, **kw):
     from dinunet_implementations_amd.parallel import make_engine
     from dinunet_implementations_amd.parallel.group import SiteGroup
     from dinunet_implementations_amd.runtime.step import TrainStep
-    m = _model(seed)
+    m = _model(seed, kw.pop("hidden", 128))
     flat = FlatParams(m.parameters())
     opt = FusedAdam(flat, lr=1e-3)
     grp = group or SiteGroup(device=torch.device("cuda"))
@@ -352,12 +352,16 @@ def test_powersgd_step_graph_matches_eager():
     assert torch.allclose(fe.data, fg.data, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("shuffle", [False, True])
-def test_device_fed_multistep_graph_matches_host_fed(shuffle):
-    """Batches resident in HBM (bf16) gathered by the step's first launch at a device cursor the
-    Adam launch advances, 4 whole steps per HIP graph: the same trajectory as feeding the same
-    batches from the host loop one step per replay."""
+@pytest.mark.parametrize("shuffle,apack", [(False, False), (True, False), (False, True),
+                                           (True, True)])
+def test_device_fed_multistep_graph_matches_host_fed(shuffle, apack, monkeypatch):
+    """Batches resident in HBM (bf16) gathered on the device at a cursor, 4 whole steps per HIP
+    graph: the same trajectory as feeding the same batches from the host loop one step per
+    replay.  apack: the fused Adam also rewrites the packed LSTM / encoder operand images, zeroes
+    the gradient and gathers the next batch (no pack launch in the replayed steps)."""
     from dinunet_implementations_amd.ops import DeviceSource
+    from dinunet_implementations_amd.runtime import step as step_mod
+    monkeypatch.setattr(step_mod, "ADAM_PACK", apack)
     xs, ys = _batches(n=8)
     B = xs.shape[1]
     X = xs.reshape(-1, *xs.shape[2:]).to(torch.bfloat16)
@@ -367,6 +371,7 @@ def test_device_fed_multistep_graph_matches_host_fed(shuffle):
     _, fd, sd = _trainer(0, use_graph=True)
     src = DeviceSource(X, Y, B, order=order)
     sd.bind(src, steps_per_graph=4)
+    assert (sd._apack is not None) == apack
     n = 16
     for c in range(n):
         xb, yb = src.batch(c)
@@ -380,3 +385,33 @@ def test_device_fed_multistep_graph_matches_host_fed(shuffle):
     assert torch.equal(sd.last_labels, src.batch(n - 1)[1])
     assert torch.allclose(fh.data, fd.data, rtol=1e-6, atol=1e-7), (fh.data - fd.data).abs().max()
     assert abs(float(sh.last_loss) - float(sd.last_loss)) < 1e-5
+
+
+@pytest.mark.parametrize("hidden", [128, 348, 384, 600])
+def test_adam_pack_images_match_pack_kernel(hidden):
+    """The persistent images the fused Adam writes (update=False: from the current parameters)
+    equal dn_lstm_pack's layouts: W_ih / W_hh / W_hh^T bf16 images and the encoder copies
+    bit for bit, the split bias images summing to the fused bias."""
+    from dinunet_implementations_amd.ops.lstm import pack_params
+    model, flat, step = _trainer(0, use_graph=True, hidden=hidden)
+    opt = step.opt
+    pp = model.persistent_pack(flat.data.device)
+    opt.attach_pack(pp)
+    flat.grad.fill_(1.0)
+    opt.step_pack(update=False, gofs=0)
+    torch.cuda.synchronize()
+    assert float(flat.grad.abs().max()) == 0.0  # zeroed as consumed
+    lin = model.encoder[0]
+    casts = []
+    params = [t for cell in model.lstm.lstms for t in cell.params()]
+    wih_p, bias_p, whh_p, whhT_p, _ = pack_params(params, model.lstm.input_size, flat.data.device,
+                                                  casts=(lin.weight, lin.bias), cast_out=casts)
+    torch.cuda.synchronize()
+    assert torch.equal(pp.wih_p, wih_p)
+    assert torch.equal(pp.whh_p, whh_p)
+    assert torch.equal(pp.whhT_p, whhT_p)
+    n = bias_p.numel()
+    assert torch.equal(pp.bias_p[:n] + pp.bias_p[n:], bias_p)
+    for a, b in zip(pp.casts, casts):
+        assert torch.equal(a, b)
+
