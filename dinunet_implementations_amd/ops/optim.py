@@ -140,6 +140,10 @@ class FusedAdam:
     # HIP-graph form --------------------------------------------------------------------------
     def sync_device_step(self):
         """Copy the host step count to the device counter :meth:`step_graphable` reads."""
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # inside a capture the fill (and a first allocation) would become graph nodes that
+            # reset the counter at every replay
+            raise RuntimeError("FusedAdam.sync_device_step inside a HIP graph capture")
         if self._tdev is None:
             self._tdev = torch.zeros(1, dtype=torch.int32, device=self.flat.data.device)
         self._tdev.fill_(self.step_count)
@@ -205,7 +209,7 @@ class FusedAdam:
         """The device step counter (int32[1]) the graph-captured update reads; a step prologue
         given it advances it once per launch."""
         if self._tdev is None:
-            self.sync_device_step()
+            self.sync_device_step()  # (raises inside a capture: create it before)
         return self._tdev
 
     def state_dict(self) -> Dict:

@@ -19,6 +19,7 @@ RCCL's stream and runs under graph B; only the small stem bucket's all-reduce is
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Callable, Optional
 
@@ -334,11 +335,16 @@ class TrainStep:
         # gradient + NEXT batch); the eager warm-up steps keep the pack launch
         self._apack = None
         from ..ops.gemm import PLAIN_BLAS
-        if (ADAM_PACK and self.use_graph and self._graph_opt_ok() and not PLAIN_BLAS
-                and self._rides() and hasattr(self.model, "persistent_pack")):
+        # (across sites the update runs after the replays, eagerly: the same launch then)
+        if (ADAM_PACK and self.use_graph and (self._graph_opt_ok() or self.split)
+                and not PLAIN_BLAS and self._rides() and hasattr(self.model, "persistent_pack")):
             pp = self.model.persistent_pack(dev)
             if pp is not None:
                 self.opt.attach_pack(pp, src, self._dsx, self._dsy)
+                # the device step counter must exist before any capture: created inside one, its
+                # allocation and initial fill would become nodes of the graph, resetting the
+                # counter at every replay
+                self.opt.sync_device_step()
                 self._apack = pp
 
     def _rides(self) -> bool:
@@ -354,21 +360,28 @@ class TrainStep:
         self.src.gather(self._dsx, self._dsy, self.flat.grad, bump)
         return _NoDefer()
 
-    def _dev_body_apack(self):
-        """One device-fed step whose operands the previous step's Adam (or :meth:`_apack_prime`)
-        already packed and gathered: the encoder GEMM advances Adam's counter and the cursor."""
-        sx, sy = self._dsx, self._dsy
+    @contextlib.contextmanager
+    def _apack_forward(self):
+        """The forward of a step whose operands the previous step's Adam (or
+        :meth:`_apack_prime`) already packed and gathered: its encoder GEMM advances Adam's device
+        step counter and the batch cursor (``dn_gemm_arm_bump``)."""
         _lib.call("dn_gemm_arm_bump", self.opt.device_step().data_ptr(), self.src.cursor.data_ptr())
         self._apack.used = False
         try:
             with use_persistent(self._apack):
-                out, loss, pred = self._fwd_bwd(sx, sy)
+                yield
         finally:
             armed = int(_lib.lib().dn_gemm_bump_armed())
             _lib.call("dn_gemm_arm_bump", None, None)  # never leaks into a later launch
         if armed or not self._apack.used:
             raise RuntimeError("Adam-emitted pack: the forward did not start with the encoder GEMM "
                                "on the persistent operand images")
+
+    def _dev_body_apack(self):
+        """One whole device-fed step in the Adam-emitted-pack form (single site)."""
+        sx, sy = self._dsx, self._dsy
+        with self._apack_forward():
+            out, loss, pred = self._fwd_bwd(sx, sy)
         if self._pre_reduce is not None:
             self._pre_reduce()
         scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
@@ -433,7 +446,8 @@ class TrainStep:
         self.engine.sync_enabled = False
         try:
             with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
-                with self._dev_prologue(None) as rp:
+                with (self._apack_forward() if self._apack is not None
+                      else self._dev_prologue(None)) as rp:
                     with self.engine.step_context():
                         h = self.model.stem(sx)
                         hd = h.detach().requires_grad_(h.requires_grad)
@@ -502,6 +516,9 @@ class TrainStep:
             if "split" not in self._dgraphs:
                 self._dev_capture_split()
             ga, gb, (out, loss, pred), _ = self._dgraphs["split"]
+            if self._apack is not None and not primed:
+                self._apack_prime()
+                primed = True
             with self.timers.phase("fwd_bwd"):
                 ga.replay()
                 for b in self._first_buckets:  # all-reduce under the stem backward
@@ -511,7 +528,11 @@ class TrainStep:
             with self.timers.phase("reduce"):
                 scale = self._reduce_after_replay()
             with self.timers.phase("optim"):
-                self.opt.step(grad_scale=scale)
+                if self._apack is not None:
+                    self.opt.step_pack(grad_scale=scale)  # + next operands and batch
+                    self.opt.step_count += 1
+                else:
+                    self.opt.step(grad_scale=scale)
             self.last_out, self.last_loss, self.last_pred = out, loss, pred
             return loss, done + 1, primed
         k = self._dK if n - done >= self._dK else 1

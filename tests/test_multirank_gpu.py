@@ -28,6 +28,10 @@ CASES = [
     (3, ["--engine", "dSGD", "--precision", "16", "--oracle", "--ragged"]),
     (2, ["--engine", "dSGD", "--precision", "16", "--payload", "bf16", "--oracle"]),
     (2, ["--engine", "dSGD", "--precision", "16", "--collective", "allreduce", "--oracle"]),
+    # the bench path across sites: HBM-resident batches, split capture, the fused Adam emitting
+    # the next step's operands after the all-reduce
+    (2, ["--engine", "dSGD", "--precision", "32", "--feed", "device", "--oracle"]),
+    (3, ["--engine", "dSGD", "--precision", "16", "--feed", "device", "--oracle"]),
 ]
 
 
@@ -51,4 +55,6 @@ def test_replicas_bit_identical(world, args):
             f.write(json.dumps({"test": "multirank", "args": args, **res}) + "\n")
     assert res["ok"], res
     assert res["graph"] and res["world"] == world
+    if "device" in args:  # the bench path: the update emits the next step's operands
+        assert res["adam_pack"] and res["split"], res
     assert r.returncode == 0, r.stderr[-3000:]

@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--oracle-tol", type=float, default=1e-3)
     ap.add_argument("--payload", default=None, help="payload_dtype (fp16 | bf16 | fp32)")
     ap.add_argument("--collective", default="auto", help="dsgd_collective (auto | direct | allreduce)")
+    ap.add_argument("--feed", default="host", choices=["host", "device"],
+                    help="device: each site's batches resident in HBM (bf16), TrainStep.bind/run "
+                         "(the bench path: split capture across sites, Adam-emitted operand pack)")
     a = ap.parse_args()
 
     import torch
@@ -102,7 +105,15 @@ def main():
             yield i, x, y
 
     g_first = None
-    for i, x, y in site_batches(grp.rank):
+    if a.feed == "device":
+        if a.ragged or a.accum != 1:
+            raise SystemExit("--feed device takes neither --ragged nor --accum")
+        from dinunet_implementations_amd.ops import DeviceSource
+        xs, ys = zip(*[(x, y) for _, x, y in site_batches(grp.rank)])
+        src = DeviceSource(torch.cat(xs).to(torch.bfloat16), torch.cat(ys), a.batch)
+        step.bind(src, steps_per_graph=2)
+        step.run(a.steps)
+    for i, x, y in (site_batches(grp.rank) if a.feed == "host" else ()):
         step(x, y, first=i % a.accum == 0, last=i % a.accum == a.accum - 1)
         if i == a.accum - 1:  # the first step's reduced gradient (the payload's own error)
             g_first = (flat.grad.double() * getattr(eng, "last_scale", 1.0)).clone()
@@ -114,8 +125,9 @@ def main():
     maxdiff = max(float((p - allp[0]).abs().max()) for p in allp)
     res = {"ok": bool(same), "world": grp.world, "engine": a.engine, "precision": a.precision,
            "payload": eng.wire, "collective": a.collective,
-           "accum": a.accum, "ragged": a.ragged, "graph": step.graph is not None,
+           "accum": a.accum, "ragged": a.ragged, "graph": step.graph is not None or bool(getattr(step, "_dgraphs", None)),
            "split": bool(step.split), "steps": opt.step_count, "max_abs_diff": maxdiff,
+           "feed": a.feed, "adam_pack": getattr(step, "_apack", None) is not None,
            "param_sum": float(mine.double().sum())}
     if a.oracle:
         ok_o = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -136,7 +148,7 @@ def main():
                         _, loss, _ = mo.forward_loss(x, y)
                         (loss / a.accum).backward()
                     gsum += fo.grad.double()
-                if s_i == 0 and a.engine == "dSGD":
+                if s_i == 0 and a.engine == "dSGD" and g_first is not None:
                     gm = gsum / grp.world
                     res["grad_rel_err"] = float((g_first - gm).norm() / gm.norm().clamp_min(1e-30))
                     res["grad_max_abs_err"] = float((g_first - gm).abs().max())
