@@ -613,6 +613,404 @@ pi_reconstruct_kernel(const PiRecon* __restrict__ R, int n, long total, long str
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// rank-dAD power iteration, ALL iterations of ALL layers in ONE launch.
+// Layer l is owned by J_l member workgroups (blocks 8 j + l: one layer's members share an XCD
+// when the dispatcher deals blocks round-robin over the 8 XCDs -- for speed only, the hand-offs
+// below are valid at any placement).  Member j keeps two slices of G in REGISTERS for the whole
+// launch: rows [16 rb_per j, ..) x all columns (P = G Q) and all rows x columns [16 cb_per j, ..)
+// (H = G^T P).  One iteration = two phases and two per-layer barriers:
+//   A  P[my rows] = G[my rows] Q (Q staged in LDS from Qsend), published with sc1 stores, plus my
+//      rows' partial Gram P^T P (fp64), published likewise;            -> barrier
+//   B  Gram = sum of the J partials (fixed order), scaled Cholesky (wave 0, as lr_gtp), P staged
+//      in LDS, H = G[:, my cols]^T P, Q[my cols] = H R^{-1} -> Qsend + change norms, Psend for my
+//      rows = P R^{-1};                                                  -> barrier
+// The dad_tol decision of iteration it > 0 is taken by every member from all members' norms (same
+// order: one decision).  Hand-off form (MI355X_MICROARCH.md visibility table, first row): every
+// byte a peer reads is stored sc1 and drained by every storing wave, one lane adds to the layer's
+// arrival counter (agent-scope atomic) and polls it with sc1 loads (bounded: a timeout sets the
+// error word instead of hanging), the other waves follow through a workgroup barrier, and every
+// load of peer data is an sc1 buffer load.  The arrival counters count up within a launch and
+// the last member to finish resets them, so every launch starts from zero.
+constexpr int LP_MAXL = 8;    // layers per launch
+constexpr int LP_MAXJ = 32;   // members per layer
+constexpr int LP_GV = 16;     // G slice registers per lane and slice (f32x4): 64 floats / thread
+constexpr int LP_RB = 4;      // row blocks per member (the phase-A reduction buffer)
+constexpr int LP_LDS = 16384; // floats staged (max(in, out) * r)
+constexpr int LP_SPIN = 1 << 20;  // ~0.1 s of polling before a barrier gives up
+
+struct LpLayer {
+  LrLayer X;
+  int J, rb_per, cb_per;  // members, 16-row / 16-column blocks per member (powers of 2, <= 4)
+  double* gram;   // [J][256] partial Grams
+  float* norms;   // [J][2]
+};
+struct LpArgs {
+  LpLayer L[LP_MAXL];
+  int nl, iters;
+  float tol;
+  unsigned* sync;  // [LP_MAXL][64] (arrivals at 0, done at 32) + error word at [LP_MAXL * 64]
+  unsigned long long* stamps;  // diagnostics (null): member 0 of layer l, [l][1 + 8 it + k]
+};
+#define LP_STAMP(k) do { if (a.stamps && j == 0 && threadIdx.x == 0) \
+  a.stamps[l * 64 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lp_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+typedef __attribute__((ext_vector_type(4))) unsigned lp_u32x4;
+typedef __attribute__((address_space(1))) unsigned lp_gu32;
+__device__ __forceinline__ void lp_st4(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lp_u32x4, v), r, off, 0, 16);
+}
+__device__ __forceinline__ void lp_st1(__amdgpu_buffer_rsrc_t r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 16);
+}
+__device__ __forceinline__ f32x4 lp_ld4(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+__device__ __forceinline__ float lp_ld1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
+
+// every storing wave drains, one lane arrives and polls, the workgroup follows
+__device__ __forceinline__ void lp_barrier(unsigned* sync, int l, unsigned target, unsigned code) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    lp_gu32* c = (lp_gu32*)(sync + l * 64);
+    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int it = 0;
+    for (; it < LP_SPIN; ++it) {
+      const unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)(v - target) >= 0) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (it == LP_SPIN)
+      __hip_atomic_store((lp_gu32*)(sync + LP_MAXL * 64), code, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+}
+
+// stage nf floats of a peer-written buffer into LDS (16-B sc1 loads; nf % 4 == 0), 8 loads per
+// thread in flight per round (a load-store loop made every 16 B a serial memory round trip)
+__device__ __forceinline__ void lp_stage(float* dst, __amdgpu_buffer_rsrc_t src, int nf, int tid) {
+  const int n4 = nf >> 2;
+  for (int i0 = 0; i0 < n4; i0 += 8 * 256) {
+    f32x4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = i0 + q * 256 + tid;
+      v[q] = lp_ld4(src, 16 * (i < n4 ? i : 0));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = i0 + q * 256 + tid;
+      if (i < n4) reinterpret_cast<f32x4*>(dst)[i] = v[q];
+    }
+  }
+}
+
+// publish rows [r0, r1) of an [., r] matrix held in LDS rows 0.. (lds row stride r) with sc1
+// stores: 16-B where the flat range allows, 4-B at the ragged end
+__device__ __forceinline__ void lp_publish(__amdgpu_buffer_rsrc_t dst, const float* src, int r0,
+                                           int r1, int r, int tid) {
+  const int e0 = r0 * r, e1 = r1 * r;  // e0 % 4 == 0 (r0 a multiple of 16)
+  const int q1 = e1 & ~3;
+  for (int e = e0 + 4 * tid; e < q1; e += 1024)
+    lp_st4(dst, 4 * e, *reinterpret_cast<const f32x4*>(src + (e - e0)));
+  for (int e = q1 + tid; e < e1; e += 256) lp_st1(dst, 4 * e, src[e - e0]);
+}
+
+
+// Scaled Cholesky of the fp64 Gram gm (the lr_gtp_kernel factorisation), wave 0, unrolled to the
+// rank bound R >= r (R x R steps instead of LR_MAXR x LR_MAXR): Rh / Sv as lr_solve_row reads them.
+template <int R>
+__device__ __forceinline__ void lp_chol(const double* gm, float* Rh, float* Sv, int r, int lane) {
+  const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
+  double dmax = di;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) dmax = fmax(dmax, shfl_d(dmax, lane ^ o));
+  const bool live = lane < r && di > fmax(1e-13 * dmax, 1e-280);
+  const double si = live ? 1.0 / sqrt(di) : 0.0;
+  float sv[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) sv[jj] = rlane((float)si, jj);
+  float av[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj)
+    av[jj] = (lane < r && jj < r) ? (float)(gm[(lane & 15) * 16 + jj] * si) * sv[jj] : 0.f;
+  unsigned dead = ~(unsigned)__ballot(live) & ((1u << r) - 1u);
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const float akk = rlane(av[k], k);
+    const bool dk = ((dead >> k) & 1u) || akk <= 1e-6f;
+    const float inv = dk ? 0.f : __builtin_amdgcn_rsqf(akk);
+    dead |= dk ? 1u << k : 0u;
+    const float rki = av[k] * inv;
+    if (lane < LR_MAXR) Rh[k * LR_MAXR + lane] = lane > k ? rki : (lane == k ? inv : 0.f);
+    const float sk = rki * inv;
+#pragma unroll
+    for (int jj = k + 1; jj < R; ++jj) av[jj] = __builtin_fmaf(-sk, rlane(av[jj], k), av[jj]);
+  }
+  if (lane < LR_MAXR) Sv[lane] = lane < R ? (float)si : 0.f;
+}
+
+// lr_solve_row bounded by R (entries >= R of x stay untouched: zero on entry, never read)
+template <int R>
+__device__ __forceinline__ void lp_solve(float (&x)[LR_MAXR], const float* Rh, const float* Sv) {
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) x[jj] *= Sv[jj];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
+    float rw[LR_MAXR];
+#pragma unroll
+    for (int q4 = 0; q4 < R / 4; ++q4) {
+      const f32x4 v = reinterpret_cast<const f32x4*>(Rh + jj * LR_MAXR)[q4];
+      rw[4 * q4] = v[0]; rw[4 * q4 + 1] = v[1]; rw[4 * q4 + 2] = v[2]; rw[4 * q4 + 3] = v[3];
+    }
+    x[jj] *= rw[jj];
+#pragma unroll
+    for (int mm = jj + 1; mm < R; ++mm) x[mm] = __builtin_fmaf(-x[jj], rw[mm], x[mm]);
+  }
+}
+__device__ __forceinline__ void lp_solve_r(float (&x)[LR_MAXR], const float* Rh, const float* Sv,
+                                           int r) {
+  if (r <= 4) lp_solve<4>(x, Rh, Sv);
+  else if (r <= 8) lp_solve<8>(x, Rh, Sv);
+  else if (r <= 12) lp_solve<12>(x, Rh, Sv);
+  else lp_solve<16>(x, Rh, Sv);
+}
+
+__global__ void __launch_bounds__(256)
+lr_persist_kernel(LpArgs a) {
+  __shared__ __attribute__((aligned(16))) float stg[LP_LDS];        // Q (phase A) / P (phase B)
+  __shared__ __attribute__((aligned(16))) float red[4 * 256];
+  __shared__ __attribute__((aligned(16))) float mine[LP_RB * 16 * LR_MAXR];  // my P / H rows
+  __shared__ float qold[LP_RB * 16 * LR_MAXR];  // my Q rows of the last commit
+  __shared__ double gpart[4 * 256];
+  __shared__ double gm[256];
+  __shared__ __attribute__((aligned(16))) float Rh[LR_MAXR * LR_MAXR];
+  __shared__ float Sv[LR_MAXR];
+  __shared__ float dq[2 * 4];
+  const int l = blockIdx.x & (LP_MAXL - 1), j = blockIdx.x / LP_MAXL;
+  if (l >= a.nl || j >= a.L[l].J) return;
+  const LpLayer& Y = a.L[l];
+  const LrLayer& X = Y.X;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, kr = lane >> 4;
+  const int n = X.out, m = X.in, r = X.r, J = Y.J;
+  const int cc = c < r ? c : 0;
+  const float cmask = c < r ? 1.f : 0.f;
+  // my row slice (phase A): row blocks [rb0, rb1), chunks (rb, ch) dealt to waves w, w+4, ...
+  const int nrb = (n + 15) >> 4, nch = (m + 15) >> 4, ncb = nch;
+  const int rb0 = min(nrb, j * Y.rb_per), rb1 = min(nrb, rb0 + Y.rb_per);
+  const int cb0 = min(ncb, j * Y.cb_per), cb1 = min(ncb, cb0 + Y.cb_per);
+  // wave -> block maps, no divisions in the loops: phase A gives each row block WA = 4 / rb_per
+  // waves, which split its column chunks (wave slot i = chunk chw + WA i); phase B likewise gives
+  // each column block WB waves splitting the row chunks.  Every slot runs (zero operands past the
+  // edge): straight-line MFMA code the compiler can schedule
+  const int WA = 4 / Y.rb_per, rbw = w / WA, chw = w % WA;
+  const int WB = 4 / Y.cb_per, cbw = w / WB, rlw = w % WB;
+  gfloat* G = (gfloat*)X.G;
+  f32x4 ga[LP_GV], gb[LP_GV];
+#pragma unroll
+  for (int i = 0; i < LP_GV; ++i) {
+    const int row = 16 * (rb0 + rbw) + c, k0 = 16 * (chw + WA * i) + 4 * kr;
+    const bool ok = rb0 + rbw < rb1 && row < n && k0 < m;  // m % 4 == 0: runs never straddle m
+    ga[i] = ((gfloat4*)(G + (long)(ok ? row : 0) * m))[(ok ? k0 : 0) >> 2] * (ok ? 1.f : 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < LP_GV; ++i) {
+    const int col = 16 * (cb0 + cbw) + c;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int row = 16 * (rlw + WB * i) + 4 * s2 + kr;
+      const bool ok = cb0 + cbw < cb1 && row < n && col < m;
+      gb[i][s2] = G[(ok ? (long)row * m + col : 0)] * (ok ? 1.f : 0.f);
+    }
+  }
+  LP_STAMP(0);
+  const __amdgpu_buffer_rsrc_t rP = lp_rsrc(X.P), rQ = lp_rsrc(X.Qsend);
+  const __amdgpu_buffer_rsrc_t rG = lp_rsrc(Y.gram), rN = lp_rsrc(Y.norms);
+  unsigned bar = 0;
+  int it = 0;
+  for (; it < a.iters; ++it) {
+    if (it > 0 && a.tol > 0.f) {
+      // dad_tol: lane b of every wave loads member b's norms (one round trip) and the butterfly
+      // sums them the same way in every wave of every member: one decision everywhere
+      float D = lane < J ? lp_ld1(rN, 8 * lane) : 0.f;
+      float Qn = lane < J ? lp_ld1(rN, 8 * lane + 4) : 0.f;
+      D = wave_sum(D);
+      Qn = wave_sum(Qn);
+      if (sqrtf(D) / (sqrtf(Qn) + 1e-8f) < a.tol) break;
+    }
+    if (j == 0 && tid == 0) *X.iters += 1;
+    // ---- phase A: P[my rows] = G[my rows] Q ----
+    const int sb = 1 + 8 * (it < 7 ? it : 7);
+    LP_STAMP(sb);
+    lp_stage(stg, rQ, (m * r + 3) & ~3, tid);
+    __syncthreads();
+    const int ncol = min(m, 16 * cb1) - 16 * cb0;
+    for (int e = tid; e < ncol * r; e += 256) qold[e] = stg[16 * cb0 * r + e];  // my Q rows now
+    {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < LP_GV; ++i) {
+        float bq[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int k = 16 * (chw + WA * i) + 4 * kr + s2;
+          bq[s2] = stg[(k < m ? k : 0) * r + cc] * cmask;  // k >= m meets a zero A entry
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[i][s2], bq[s2], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[w * 256 + (4 * kr + e) * 16 + c] = acc[e];
+    }
+    __syncthreads();
+    LP_STAMP(sb + 1);
+    const int nr = min(n, 16 * rb1) - 16 * rb0;  // my rows
+    for (int e = tid; e < (rb1 - rb0) * 256; e += 256) {
+      const int rb = e >> 8, i = (e >> 4) & 15, c2 = e & 15;
+      const int rr = 16 * rb + i;
+      if (rr < nr && c2 < r) {  // the WA waves of row block rb, in wave order
+        float v = 0.f;
+        for (int q = 0; q < WA; ++q) v += red[(rb * WA + q) * 256 + i * 16 + c2];
+        mine[rr * r + c2] = v;
+      }
+    }
+    __syncthreads();
+    lp_publish(rP, mine, 16 * rb0, 16 * rb0 + nr, r, tid);
+    {  // my rows' partial Gram on the fp64 matrix cores (fp32 values, exact products): wave w
+       // takes my rows 16 w .. 16 w + 15 (<= 64 rows), lane l feeds A[l & 15][k] = B[k][l & 15] =
+       // P[row k][col l & 15]; the four wave partials are added in a fixed order
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int rr = 16 * w + 4 * s2 + kr;
+        const double v = (rr < nr && c < r) ? (double)mine[(rr < nr ? rr : 0) * r + cc] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gpart[w * 256 + (kr + 4 * e) * 16 + c] = acc[e];  // f64 C map
+    }
+    __syncthreads();
+    gm[tid] = (gpart[tid] + gpart[256 + tid]) + (gpart[512 + tid] + gpart[768 + tid]);
+    __syncthreads();
+    if (tid < 128) {
+      const double2 v = {gm[2 * tid], gm[2 * tid + 1]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lp_u32x4, v), rG,
+                                             (j * 256 + 2 * tid) * 8, 0, 16);
+    }
+    LP_STAMP(sb + 2);
+    lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x100u + (unsigned)l);
+    LP_STAMP(sb + 3);
+    // ---- phase B: Gram, Cholesky, H = G[:, my cols]^T P, Q[my cols], Psend[my rows] ----
+    if (tid < 128) {  // member partials in a fixed order, 8 loads in flight per round
+      double s0 = 0.0, s1 = 0.0;
+      for (int b0 = 0; b0 < J; b0 += 8) {
+        double2 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          v[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+              rG, ((b0 + q < J ? b0 + q : 0) * 256 + 2 * tid) * 8, 0, 16));
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (b0 + q < J) { s0 += v[q].x; s1 += v[q].y; }
+      }
+      gm[2 * tid] = s0;
+      gm[2 * tid + 1] = s1;
+    }
+    lp_stage(stg, rP, (n * r + 3) & ~3, tid);
+    __syncthreads();
+    LP_STAMP(sb + 4);
+    if (w == 0) {  // scaled Cholesky of the Gram, wave 0, unrolled to the rank bound
+      if (r <= 4) lp_chol<4>(gm, Rh, Sv, r, lane);
+      else if (r <= 8) lp_chol<8>(gm, Rh, Sv, r, lane);
+      else if (r <= 12) lp_chol<12>(gm, Rh, Sv, r, lane);
+      else lp_chol<16>(gm, Rh, Sv, r, lane);
+    }
+    {  // H = G[:, my cols]^T P on the matrix cores (the WB waves of a column block meet in red)
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < LP_GV; ++i) {
+        float pv[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int row = 16 * (rlw + WB * i) + 4 * s2 + kr;
+          pv[s2] = stg[(row < n ? row : 0) * r + cc] * cmask;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(gb[i][s2], pv[s2], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[w * 256 + (4 * kr + e) * 16 + c] = acc[e];
+    }
+    __syncthreads();  // red complete, Rh / Sv visible
+    LP_STAMP(sb + 5);
+    float dd = 0.f, qq = 0.f;
+    if (tid < ncol) {  // wave 0: one Q row per lane, H[col][:] D^{-1/2} R_s^{-1}
+      const int cb = tid >> 4, i = tid & 15;
+      float old[LR_MAXR], x[LR_MAXR];
+#pragma unroll
+      for (int e = 0; e < LR_MAXR; ++e) old[e] = e < r ? qold[tid * r + e] : 0.f;
+#pragma unroll
+      for (int e = 0; e < LR_MAXR; ++e) {
+        float v = 0.f;
+        for (int q = 0; q < WB; ++q) v += red[(cb * WB + q) * 256 + i * 16 + e];
+        x[e] = e < r ? v : 0.f;
+      }
+      lp_solve_r(x, Rh, Sv, r);
+#pragma unroll
+      for (int e = 0; e < LR_MAXR; ++e) {
+        if (e < r) {
+          dd += (x[e] - old[e]) * (x[e] - old[e]);
+          qq += x[e] * x[e];
+          mine[tid * r + e] = x[e];
+        }
+      }
+    } else if (tid >= 128 && tid - 128 < nr) {  // waves 2-3: Psend rows, P D^{-1/2} R_s^{-1}
+      float x[LR_MAXR];
+      const int row = 16 * rb0 + tid - 128;
+#pragma unroll
+      for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? stg[row * r + e] : 0.f;
+      lp_solve_r(x, Rh, Sv, r);
+#pragma unroll
+      for (int e = 0; e < LR_MAXR; ++e)
+        if (e < r) X.Psend[(long)row * r + e] = x[e];
+    }
+    dd = wave_sum(dd);
+    qq = wave_sum(qq);
+    if (lane == 0) { dq[2 * w] = dd; dq[2 * w + 1] = qq; }
+    __syncthreads();
+    lp_publish(rQ, mine, 16 * cb0, 16 * cb0 + ncol, r, tid);
+    if (tid == 0) {
+      lp_st1(rN, 8 * j, (dq[0] + dq[2]) + (dq[4] + dq[6]));
+      lp_st1(rN, 8 * j + 4, (dq[1] + dq[3]) + (dq[5] + dq[7]));
+    }
+    LP_STAMP(sb + 6);
+    lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x200u + (unsigned)l);
+    LP_STAMP(sb + 7);
+  }
+  // the last member out resets the layer's counters for the next launch (every member has
+  // passed every poll of this launch when it arrives here)
+  if (tid == 0) {
+    lp_gu32* d = (lp_gu32*)(a.sync + l * 64 + 32);
+    const unsigned prev = __hip_atomic_fetch_add(d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)J - 1u) {
+      __hip_atomic_store((lp_gu32*)(a.sync + l * 64), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace
 
 #ifdef LR_STAMPS
@@ -665,3 +1063,57 @@ DN_API int dn_pi_reconstruct(const void* recon, int n, long total, long stride, 
                      (const PiRecon*)recon, n, total, stride, W, 1.f / (float)W);
   return dn_launch_status();
 }
+
+// Members per layer for the persistent launch: the fewest J <= LP_MAXJ whose two register slices
+// fit (row-block and column-block chunks per wave <= LP_GV); 0 when a layer cannot take it.
+static int lp_plan(int out, int in, int r, int& J, int& rbp, int& cbp) {
+  if (in % 4 || r < 1 || r > LR_MAXR || (long)in * r > LP_LDS || (long)out * r > LP_LDS) return 0;
+  const int nrb = (out + 15) / 16, ncb = (in + 15) / 16;
+  auto p2 = [](int v) { return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : 8; };
+  for (J = 1; J <= LP_MAXJ; ++J) {
+    rbp = p2((nrb + J - 1) / J);
+    cbp = p2((ncb + J - 1) / J);
+    // per wave: one row (column) block and at most LP_GV of its chunks
+    if (rbp <= LP_RB && cbp <= LP_RB && ncb <= LP_GV * (4 / rbp) && nrb <= LP_GV * (4 / cbp))
+      return 1;
+  }
+  return 0;
+}
+
+// ALL `iters` power iterations of every layer of a host-side LrLayer table in one launch
+// (lr_persist_kernel); DN_UNSUPPORTED when the table does not fit it (the caller then runs
+// dn_lr_stage).  gram: >= nl * LP_MAXJ * 256 doubles; norms: >= nl * LP_MAXJ * 2 floats; sync:
+// (LP_MAXL * 64 + 1) zeroed unsigned words, owned by this table (counters reset by each launch).
+static unsigned long long* g_lp_stamps = nullptr;
+DN_API int dn_lr_persist_set_stamps(void* p) {
+  g_lp_stamps = (unsigned long long*)p;
+  return DN_OK;
+}
+
+DN_API int dn_lr_persist(const void* host_layers, int nl, int iters, float tol, double* gram,
+                         float* norms, unsigned* sync, hipStream_t st) {
+  if (nl <= 0) return DN_OK;
+  if (nl > LP_MAXL || iters < 1 || !gram || !norms || !sync) return DN_UNSUPPORTED;
+  LpArgs a{};
+  a.nl = nl;
+  a.iters = iters;
+  a.tol = tol;
+  a.sync = sync;
+  a.stamps = g_lp_stamps;
+  int jmax = 1;
+  const LrLayer* hl = reinterpret_cast<const LrLayer*>(host_layers);
+  for (int l = 0; l < nl; ++l) {
+    LpLayer& Y = a.L[l];
+    Y.X = hl[l];
+    if (Y.X.err) return DN_UNSUPPORTED;  // PowerSGD keeps the staged kernels
+    if (!lp_plan(Y.X.out, Y.X.in, Y.X.r, Y.J, Y.rb_per, Y.cb_per)) return DN_UNSUPPORTED;
+    Y.gram = gram + (long)l * LP_MAXJ * 256;
+    Y.norms = norms + (long)l * LP_MAXJ * 2;
+    jmax = Y.J > jmax ? Y.J : jmax;
+  }
+  hipLaunchKernelGGL(lr_persist_kernel, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
+  return dn_launch_status();
+}
+
+DN_API long dn_lr_persist_words() { return LP_MAXL * 64 + 1; }
+DN_API long dn_lr_persist_maxj() { return LP_MAXJ; }

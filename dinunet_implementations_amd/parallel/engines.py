@@ -425,6 +425,8 @@ class RankDADEngine(Engine):
         ``dad_tol`` stop decided on the device: no host sync, HIP-graph capturable."""
         if not self.fast or not self.fast_layers:
             return
+        if self._table.persist(max(1, self.iters), self.tol):
+            return  # every iteration in one launch (lr_persist_kernel)
         for it in range(max(1, self.iters)):
             self._table.gq(it, self.tol)
             self._table.orth_gtp(it)

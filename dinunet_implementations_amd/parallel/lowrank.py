@@ -141,8 +141,42 @@ class LowRankTable:
             starts.append(total)
             total += out_f * in_f
         self.blocks1, self.blocks3, self.total = b1, b3, total
+        self._host_tab = tab  # the persistent launch takes the table by value
         self.table = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
+        # (gram partials, norms, barrier words) of dn_lr_persist: allocated (zeroed) here, never
+        # inside a capture
+        L.dn_lr_persist_words.restype = ctypes.c_long
+        L.dn_lr_persist_maxj.restype = ctypes.c_long
+        mj = int(L.dn_lr_persist_maxj())
+        self._persist = (torch.zeros(max(n, 1) * mj * 256, dtype=torch.float64, device=device),
+                         torch.zeros(max(n, 1) * mj * 2, dtype=torch.float32, device=device),
+                         torch.zeros(int(L.dn_lr_persist_words()), dtype=torch.int32, device=device))
         self.starts = torch.tensor(starts or [0], dtype=torch.int64).to(device)
+
+    def persist(self, iters: int, tol: float = 0.0) -> bool:
+        """ALL ``iters`` power iterations of every layer in ONE launch (``lr_persist_kernel``:
+        each layer's G slices stay in registers, members meet at per-layer barriers).  False when
+        the table does not fit it (or ``DINUNET_LR_PERSIST=0``): run :meth:`gq` / :meth:`orth_gtp`."""
+        import ctypes
+        import os
+        if not self.n or os.environ.get("DINUNET_LR_PERSIST", "1") == "0":
+            return False
+        L = _lib.lib()
+        gram, norms, sync = self._persist
+        rc = L.dn_lr_persist(ctypes.c_void_p(ctypes.addressof(self._host_tab)), ctypes.c_int(self.n),
+                             ctypes.c_int(int(iters)), ctypes.c_float(tol),
+                             ctypes.c_void_p(gram.data_ptr()), ctypes.c_void_p(norms.data_ptr()),
+                             ctypes.c_void_p(sync.data_ptr()), ctypes.c_void_p(_lib.stream()))
+        if rc == 3:  # DN_UNSUPPORTED: the staged kernels
+            return False
+        if rc != 0:
+            raise RuntimeError(f"dn_lr_persist failed with status {rc}")
+        return True
+
+    def persist_error(self) -> int:
+        """Error word of the persistent launch (0: every barrier met; else 0x100 / 0x200 + layer
+        of a barrier wait that timed out)."""
+        return int(self._persist[2][-1].item())
 
     def iterations(self) -> list:
         """Cumulative power iterations run per layer (host sync)."""

@@ -415,3 +415,53 @@ def test_adam_pack_images_match_pack_kernel(hidden):
     for a, b in zip(pp.casts, casts):
         assert torch.equal(a, b)
 
+
+@pytest.mark.parametrize("hidden,tol", [(128, 0.0), (384, 0.0), (384, 1e-3)])
+def test_rankdad_persistent_launch_matches_staged(hidden, tol, monkeypatch):
+    """All power iterations of every layer in ONE launch (lr_persist_kernel, per-layer barriers)
+    give the staged two-launches-per-iteration factorisation: same warm start, same Gram /
+    Cholesky math, sums in another order.  Repeated launches (the barrier counters reset by each
+    launch) stay consistent, no barrier times out, and the iterations run are counted."""
+    from dinunet_implementations_amd.models import ICALstm
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    torch.manual_seed(0)
+    m = ICALstm(input_size=256, hidden_size=hidden, num_comps=100, window_size=10).cuda()
+    flat = FlatParams(m.parameters())
+    cfg = {"dad_reduction_rank": 10, "dad_num_pow_iters": 5, "dad_tol": tol, "seed": 3}
+    grp = SiteGroup(device=torch.device("cuda"))
+    ep = make_engine("rankDAD", m, flat, grp, cfg)
+    es = make_engine("rankDAD", m, flat, grp, cfg)
+    assert ep.fast and ep.fast_layers
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for call in range(3):
+        G0 = torch.randn(flat.grad.shape, device="cuda", generator=g)
+        # a low-rank-ish gradient: the power iteration then converges like on real gradients
+        for p_, o, n in flat.segments():
+            if p_.dim() == 2:
+                u = torch.randn(p_.shape[0], 12, device="cuda", generator=g)
+                v = torch.randn(12, p_.shape[1], device="cuda", generator=g)
+                G0[o:o + n] += (u @ v).reshape(-1) * 0.5
+        flat.grad.copy_(G0)
+        monkeypatch.setenv("DINUNET_LR_PERSIST", "1")
+        it0 = ep.power_iterations()
+        ep.reduce()
+        torch.cuda.synchronize()
+        gp = flat.grad.clone()
+        assert ep._table.persist_error() == 0
+        it1 = ep.power_iterations()
+        flat.grad.copy_(G0)
+        monkeypatch.setenv("DINUNET_LR_PERSIST", "0")
+        es.reduce()
+        torch.cuda.synchronize()
+        gs = flat.grad.clone()
+        for (mod, o, out_f, in_f, *_r) in ep.fast_layers:
+            a_, b_ = gp[o:o + out_f * in_f], gs[o:o + out_f * in_f]
+            rel = float((a_ - b_).norm() / b_.norm().clamp_min(1e-30))
+            assert rel < 2e-3, (call, out_f, in_f, rel)
+        runs = [b - a for a, b in zip(it0, it1)]
+        assert all(1 <= x <= 5 for x in runs), runs
+        if tol == 0.0:
+            assert all(x == 5 for x in runs), runs
+

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Phase stamps (s_memrealtime, 100 MHz) of the one-launch rank-dAD power iteration
+(lowrank.hip lr_persist_kernel), member 0 of every layer, ICA-LSTM headline geometry; plus the
+launch time by events.  Per iteration: A = Q staged + P = G Q, pub = P / Gram partials published,
+bar1 = first barrier, gram = partial sums + P staged, chol+H = Cholesky + G^T P, solve = Q rows /
+Psend published, bar2 = second barrier (us)."""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from dinunet_implementations_amd.models import ICALstm
+    from dinunet_implementations_amd.ops import FlatParams, _lib
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    torch.manual_seed(0)
+    m = ICALstm(input_size=256, hidden_size=384, num_comps=100, window_size=10).cuda()
+    flat = FlatParams(m.parameters())
+    eng = make_engine("rankDAD", m, flat, SiteGroup(device=torch.device("cuda")),
+                      {"dad_reduction_rank": 10, "dad_num_pow_iters": 5, "dad_tol": 0.0})
+    flat.grad.normal_()
+    t = eng._table
+    for _ in range(5):
+        t.persist(5, 0.0)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(20):
+        ev[0].record()
+        t.persist(5, 0.0)
+        ev[1].record()
+        ev[1].synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
+    ts.sort()
+    st = torch.zeros(8 * 64, dtype=torch.int64, device="cuda")
+    L = _lib.lib()
+    L.dn_lr_persist_set_stamps(ctypes.c_void_p(st.data_ptr()))
+    t.persist(5, 0.0)
+    torch.cuda.synchronize()
+    L.dn_lr_persist_set_stamps(ctypes.c_void_p(None))
+    v = st.view(8, 64).tolist()
+    print(f"persistent launch (5 iterations, {t.n} layers): median {ts[len(ts)//2]:.1f} us by events")
+    names = ["A", "pub", "bar1", "gram", "chol+H", "solve", "bar2", "next"]
+    for l in range(t.n):
+        row = v[l]
+        base = row[0]
+        out = [f"layer {l}: G load {(row[1] - base) / 100:.2f}"]
+        for it in range(5):
+            sb = 1 + 8 * it
+            seg = [(row[sb + k + 1] - row[sb + k]) / 100 for k in range(7)]
+            out.append(f"it{it} " + " ".join(f"{n_}={x:.2f}" for n_, x in zip(names, seg)))
+        print(" | ".join(out))
+
+
+if __name__ == "__main__":
+    main()
