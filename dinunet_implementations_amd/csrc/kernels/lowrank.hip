@@ -674,10 +674,20 @@ __device__ __forceinline__ float lp_ld1(__amdgpu_buffer_rsrc_t r, int off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
 }
 
+// LDS-only workgroup barrier: orders the waves and their LDS traffic without waiting for
+// outstanding global stores (a __syncthreads is also a device-scope fence: each phase ending in
+// global stores -- Psend, published payloads -- then waited a memory round trip); lp_barrier
+// drains explicitly where peers need the stores
+__device__ __forceinline__ void lp_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // every storing wave drains, one lane arrives and polls, the workgroup follows
 __device__ __forceinline__ void lp_barrier(unsigned* sync, int l, unsigned target, unsigned code) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  lp_sync();
   if (threadIdx.x == 0) {
     lp_gu32* c = (lp_gu32*)(sync + l * 64);
     __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -691,7 +701,7 @@ __device__ __forceinline__ void lp_barrier(unsigned* sync, int l, unsigned targe
       __hip_atomic_store((lp_gu32*)(sync + LP_MAXL * 64), code, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
-  __syncthreads();
+  lp_sync();
 }
 
 // stage nf floats of a peer-written buffer into LDS (16-B sc1 loads; nf % 4 == 0), 8 loads per
@@ -838,22 +848,13 @@ lr_persist_kernel(LpArgs a) {
   const __amdgpu_buffer_rsrc_t rG = lp_rsrc(Y.gram), rN = lp_rsrc(Y.norms);
   unsigned bar = 0;
   int it = 0;
-  for (; it < a.iters; ++it) {
-    if (it > 0 && a.tol > 0.f) {
-      // dad_tol: lane b of every wave loads member b's norms (one round trip) and the butterfly
-      // sums them the same way in every wave of every member: one decision everywhere
-      float D = lane < J ? lp_ld1(rN, 8 * lane) : 0.f;
-      float Qn = lane < J ? lp_ld1(rN, 8 * lane + 4) : 0.f;
-      D = wave_sum(D);
-      Qn = wave_sum(Qn);
-      if (sqrtf(D) / (sqrtf(Qn) + 1e-8f) < a.tol) break;
-    }
+  for (;; ++it) {
     if (j == 0 && tid == 0) *X.iters += 1;
     // ---- phase A: P[my rows] = G[my rows] Q ----
     const int sb = 1 + 8 * (it < 7 ? it : 7);
     LP_STAMP(sb);
     lp_stage(stg, rQ, (m * r + 3) & ~3, tid);
-    __syncthreads();
+    lp_sync();
     const int ncol = min(m, 16 * cb1) - 16 * cb0;
     for (int e = tid; e < ncol * r; e += 256) qold[e] = stg[16 * cb0 * r + e];  // my Q rows now
     {
@@ -873,7 +874,7 @@ lr_persist_kernel(LpArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[w * 256 + (4 * kr + e) * 16 + c] = acc[e];
     }
-    __syncthreads();
+    lp_sync();
     LP_STAMP(sb + 1);
     const int nr = min(n, 16 * rb1) - 16 * rb0;  // my rows
     for (int e = tid; e < (rb1 - rb0) * 256; e += 256) {
@@ -885,7 +886,7 @@ lr_persist_kernel(LpArgs a) {
         mine[rr * r + c2] = v;
       }
     }
-    __syncthreads();
+    lp_sync();
     lp_publish(rP, mine, 16 * rb0, 16 * rb0 + nr, r, tid);
     {  // my rows' partial Gram on the fp64 matrix cores (fp32 values, exact products): wave w
        // takes my rows 16 w .. 16 w + 15 (<= 64 rows), lane l feeds A[l & 15][k] = B[k][l & 15] =
@@ -900,9 +901,9 @@ lr_persist_kernel(LpArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) gpart[w * 256 + (kr + 4 * e) * 16 + c] = acc[e];  // f64 C map
     }
-    __syncthreads();
+    lp_sync();
     gm[tid] = (gpart[tid] + gpart[256 + tid]) + (gpart[512 + tid] + gpart[768 + tid]);
-    __syncthreads();
+    lp_sync();
     if (tid < 128) {
       const double2 v = {gm[2 * tid], gm[2 * tid + 1]};
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lp_u32x4, v), rG,
@@ -928,7 +929,7 @@ lr_persist_kernel(LpArgs a) {
       gm[2 * tid + 1] = s1;
     }
     lp_stage(stg, rP, (n * r + 3) & ~3, tid);
-    __syncthreads();
+    lp_sync();
     LP_STAMP(sb + 4);
     if (w == 0) {  // scaled Cholesky of the Gram, wave 0, unrolled to the rank bound
       if (r <= 4) lp_chol<4>(gm, Rh, Sv, r, lane);
@@ -953,8 +954,18 @@ lr_persist_kernel(LpArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[w * 256 + (4 * kr + e) * 16 + c] = acc[e];
     }
-    __syncthreads();  // red complete, Rh / Sv visible
+    lp_sync();  // red complete, Rh / Sv visible
     LP_STAMP(sb + 5);
+    // the WB wave partials of each column block summed by all threads (one element each, wave
+    // order), in place into the block's first slot: the solve lanes then read finished sums
+    // (a per-lane reduction loop made each of its 16 entries a chain of WB dependent LDS reads)
+    for (int e = tid; e < (cb1 - cb0) * 256; e += 256) {
+      const int cb = e >> 8, o = e & 255;
+      float v = 0.f;
+      for (int q = 0; q < WB; ++q) v += red[(cb * WB + q) * 256 + o];
+      red[cb * WB * 256 + o] = v;
+    }
+    lp_sync();
     float dd = 0.f, qq = 0.f;
     if (tid < ncol) {  // wave 0: one Q row per lane, H[col][:] D^{-1/2} R_s^{-1}
       const int cb = tid >> 4, i = tid & 15;
@@ -962,11 +973,7 @@ lr_persist_kernel(LpArgs a) {
 #pragma unroll
       for (int e = 0; e < LR_MAXR; ++e) old[e] = e < r ? qold[tid * r + e] : 0.f;
 #pragma unroll
-      for (int e = 0; e < LR_MAXR; ++e) {
-        float v = 0.f;
-        for (int q = 0; q < WB; ++q) v += red[(cb * WB + q) * 256 + i * 16 + e];
-        x[e] = e < r ? v : 0.f;
-      }
+      for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? red[cb * WB * 256 + i * 16 + e] : 0.f;
       lp_solve_r(x, Rh, Sv, r);
 #pragma unroll
       for (int e = 0; e < LR_MAXR; ++e) {
@@ -976,20 +983,11 @@ lr_persist_kernel(LpArgs a) {
           mine[tid * r + e] = x[e];
         }
       }
-    } else if (tid >= 128 && tid - 128 < nr) {  // waves 2-3: Psend rows, P D^{-1/2} R_s^{-1}
-      float x[LR_MAXR];
-      const int row = 16 * rb0 + tid - 128;
-#pragma unroll
-      for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? stg[row * r + e] : 0.f;
-      lp_solve_r(x, Rh, Sv, r);
-#pragma unroll
-      for (int e = 0; e < LR_MAXR; ++e)
-        if (e < r) X.Psend[(long)row * r + e] = x[e];
     }
     dd = wave_sum(dd);
     qq = wave_sum(qq);
     if (lane == 0) { dq[2 * w] = dd; dq[2 * w + 1] = qq; }
-    __syncthreads();
+    lp_sync();
     lp_publish(rQ, mine, 16 * cb0, 16 * cb0 + ncol, r, tid);
     if (tid == 0) {
       lp_st1(rN, 8 * j, (dq[0] + dq[2]) + (dq[4] + dq[6]));
@@ -998,6 +996,31 @@ lr_persist_kernel(LpArgs a) {
     LP_STAMP(sb + 6);
     lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x200u + (unsigned)l);
     LP_STAMP(sb + 7);
+    // stop after this commit?  dad_tol: lane b of every wave loads member b's norms (one round
+    // trip) and the butterfly sums them the same way in every wave of every member: one decision
+    bool stop = it + 1 >= a.iters;
+    if (!stop && a.tol > 0.f) {
+      float D = lane < J ? lp_ld1(rN, 8 * lane) : 0.f;
+      float Qn = lane < J ? lp_ld1(rN, 8 * lane + 4) : 0.f;
+      D = wave_sum(D);
+      Qn = wave_sum(Qn);
+      stop = sqrtf(D) / (sqrtf(Qn) + 1e-8f) < a.tol;
+    }
+    if (stop) {
+      // Psend for my rows from the last iteration's P (still staged) and factor, once per launch
+      const int nr = min(n, 16 * rb1) - 16 * rb0;
+      if (tid < nr) {
+        float x[LR_MAXR];
+        const int row = 16 * rb0 + tid;
+#pragma unroll
+        for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? stg[row * r + e] : 0.f;
+        lp_solve_r(x, Rh, Sv, r);
+#pragma unroll
+        for (int e = 0; e < LR_MAXR; ++e)
+          if (e < r) X.Psend[(long)row * r + e] = x[e];
+      }
+      break;
+    }
   }
   // the last member out resets the layer's counters for the next launch (every member has
   // passed every poll of this launch when it arrives here)
