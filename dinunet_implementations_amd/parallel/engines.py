@@ -329,6 +329,11 @@ class RankDADEngine(Engine):
         # delta factors gives the same factors without capturing them, with no host sync (the
         # dad_tol early stop is a device-side mask), so it is captured in the step's HIP graph.
         self.fast = bool(flat.data.is_cuda and self.cfg.get("dad_gradient_space", True))
+        # the one-launch power iteration spins on per-layer barriers, so all of a launch's
+        # workgroups must be resident together: never when several site processes share one GPU
+        # (the gloo rehearsal), whose persistent launches could then hold each other's CUs
+        self._persist_ok = bool(self.fast and not (
+            group.distributed and group.world > max(1, torch.cuda.device_count())))
         if self.fast:
             self._init_fast()
 
@@ -425,7 +430,7 @@ class RankDADEngine(Engine):
         ``dad_tol`` stop decided on the device: no host sync, HIP-graph capturable."""
         if not self.fast or not self.fast_layers:
             return
-        if self._table.persist(max(1, self.iters), self.tol):
+        if self._persist_ok and self._table.persist(max(1, self.iters), self.tol):
             return  # every iteration in one launch (lr_persist_kernel)
         for it in range(max(1, self.iters)):
             self._table.gq(it, self.tol)
