@@ -213,6 +213,8 @@ struct Epi {
   int ncol;  // > 0: only output columns < ncol are stored (e.g. a ones-operand column sum)
   const bf16* mask;  // optional [M][ldm] bf16: outputs where mask <= 0 are zeroed (ReLU backward)
   long ldm;
+  void* C2;  // optional second output (same ldc, its own beta accumulate): the LSTM's b_ih and
+             // b_hh gradients are the same column sum of the gate gradient, formed once
 };
 
 constexpr int GMAX = 12;  // problems per grouped launch (kernarg: ~1.6 KB)
@@ -263,14 +265,15 @@ __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int
   if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col] > 0.f)) v = 0.f;
   const long orow = epi.row_map ? epi.row_map[row] : row;
   if (orow < 0) return;  // dropped row (e.g. zero-padded LSTM units)
-  if (epi.out_bf16) {
-    bf16* cp = reinterpret_cast<bf16*>(C) + orow * ldc + col;
-    if (epi.beta != 0.f) v += epi.beta * (float)*cp;
-    *cp = (bf16)v;
-  } else {
-    float* cp = reinterpret_cast<float*>(C) + orow * ldc + col;
-    if (epi.beta != 0.f) v += epi.beta * *cp;
-    *cp = v;
+  for (int o = 0; o < (epi.C2 ? 2 : 1); ++o) {
+    void* Co = o ? epi.C2 : C;
+    if (epi.out_bf16) {
+      bf16* cp = reinterpret_cast<bf16*>(Co) + orow * ldc + col;
+      *cp = (bf16)(epi.beta != 0.f ? v + epi.beta * (float)*cp : v);
+    } else {
+      float* cp = reinterpret_cast<float*>(Co) + orow * ldc + col;
+      *cp = epi.beta != 0.f ? v + epi.beta * *cp : v;
+    }
   }
 }
 
@@ -787,25 +790,29 @@ __device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, in
     if (epi.relu) v[e] = fmaxf(v[e], 0.f);
     if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col + e] > 0.f)) v[e] = 0.f;
   }
-  if (epi.out_bf16) {
-    bf16x4* cp = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(C) + orow * ldc + col);
-    if (epi.beta != 0.f) {
-      const bf16x4 o = *cp;
+  for (int oo = 0; oo < (epi.C2 ? 2 : 1); ++oo) {
+    void* Co = oo ? epi.C2 : C;
+    f32x4 u = v;
+    if (epi.out_bf16) {
+      bf16x4* cp = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(Co) + orow * ldc + col);
+      if (epi.beta != 0.f) {
+        const bf16x4 o = *cp;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += epi.beta * (float)o[e];
+        for (int e = 0; e < 4; ++e) u[e] += epi.beta * (float)o[e];
+      }
+      bf16x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (bf16)u[e];
+      *cp = w;
+    } else {
+      f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Co) + orow * ldc + col);
+      if (epi.beta != 0.f) {
+        const f32x4 o = *cp;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] += epi.beta * o[e];
+      }
+      *cp = u;
     }
-    bf16x4 w;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) w[e] = (bf16)v[e];
-    *cp = w;
-  } else {
-    f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + orow * ldc + col);
-    if (epi.beta != 0.f) {
-      const f32x4 o = *cp;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += epi.beta * o[e];
-    }
-    *cp = v;
   }
 }
 
@@ -1011,7 +1018,7 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   P.kchunk = kchunk_for(K, g.splits);
   if (g.splits > 1) g.splits = (K + P.kchunk - 1) / P.kchunk;
   P.slab = g.splits > 1 ? slab : nullptr;
-  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0, (const bf16*)mask, ldm};
+  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0, (const bf16*)mask, ldm, nullptr};
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }
 
@@ -1023,7 +1030,7 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
                            const long* ldb, void* const* C, const long* ldc, const int* M,
                            const int* N, const int* K, const float* alpha, const float* beta,
                            const void* const* bias, const void* const* row_map,
-                           const int* ncol, int relu,
+                           const int* ncol, void* const* C2, int relu,
                            int a_bf16, int b_bf16, int ta, int tb, int c_bf16, int tile,
                            int splits, float* slab, int* counters, hipStream_t st) {
   if (n < 1 || n > GMAX) return DN_BAD_SHAPE;
@@ -1045,7 +1052,8 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
     soff += (long)g.splits * M[i] * N[i];
     if ((long)g.splits * M[i] * N[i] >= (1L << 29)) g.cnt = nullptr;  // 32-bit slab offsets
     P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16,
-                ncol ? ncol[i] : 0, nullptr, 0};
+                ncol ? ncol[i] : 0, nullptr, 0, C2 ? C2[i] : nullptr};
+    if (P.epi.C2 && !P.epi.ncol) return DN_BAD_SHAPE;  // second outputs: column sums only
   }
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }

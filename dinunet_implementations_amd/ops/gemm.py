@@ -28,7 +28,7 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
 _lib.register("dn_gemm_arm_bump", [_lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_gemm_bump_armed", [])
-_lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 14 + [_lib.c_int] * 8
+_lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 15 + [_lib.c_int] * 8
               + [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p])
 
 # DINUNET_SPLITK_INLAUNCH=1: split-K partials are combined inside the GEMM launch by each
@@ -206,13 +206,15 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
             if q.get("ncol"):
                 nc = int(q["ncol"])
                 q = dict(q, b=(q["b"][:nc] if trans_b else q["b"][:, :nc]))
-            mm(q["a"], q["b"], trans_a=trans_a, trans_b=trans_b, out=q["out"],
-               alpha=q.get("alpha", 1.0), beta=q.get("beta", 0.0), bias=q.get("bias"),
-               row_map=q.get("row_map"))
+            for out in (q["out"], q.get("out2")):
+                if out is not None:
+                    mm(q["a"], q["b"], trans_a=trans_a, trans_b=trans_b, out=out,
+                       alpha=q.get("alpha", 1.0), beta=q.get("beta", 0.0), bias=q.get("bias"),
+                       row_map=q.get("row_map"))
         return
     n = len(probs)
     arrs = {k: [] for k in ("A", "lda", "B", "ldb", "C", "ldc", "M", "N", "K", "alpha", "beta",
-                            "bias", "rmap", "ncol")}
+                            "bias", "rmap", "ncol", "C2")}
     keep = []
     ta = tb = None
     a_bf = b_bf = c_bf = None
@@ -235,6 +237,10 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         out = q["out"]
         if out.stride(1) != 1:
             raise ValueError("mm_grouped output must be row-contiguous")
+        out2 = q.get("out2")  # a second output of a column-sum problem (same shape / strides)
+        if out2 is not None and (out2.shape != out.shape or out2.stride() != out.stride()
+                                 or out2.dtype != out.dtype or not q.get("ncol")):
+            raise ValueError("mm_grouped out2: a column-sum problem's twin output")
         bias = q.get("bias")
         bias = bias.float().contiguous() if bias is not None else None
         rmap = q.get("row_map")
@@ -245,7 +251,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
                      ("C", out.data_ptr()), ("ldc", out.stride(0)), ("M", M), ("N", N), ("K", K),
                      ("alpha", float(q.get("alpha", 1.0))), ("beta", float(q.get("beta", 0.0))),
                      ("bias", _lib.ptr(bias)), ("rmap", _lib.ptr(rmap)),
-                     ("ncol", int(q.get("ncol", 0) or 0))):
+                     ("ncol", int(q.get("ncol", 0) or 0)), ("C2", _lib.ptr(out2))):
             arrs[k].append(v)
         maxk = max(maxk, K)
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
@@ -277,7 +283,8 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               (P * n)(*arrs["B"]), (L * n)(*arrs["ldb"]), (P * n)(*arrs["C"]),
               (L * n)(*arrs["ldc"]), (I * n)(*arrs["M"]), (I * n)(*arrs["N"]),
               (I * n)(*arrs["K"]), (F * n)(*arrs["alpha"]), (F * n)(*arrs["beta"]),
-              (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), (I * n)(*arrs["ncol"]), 0,
+              (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), (I * n)(*arrs["ncol"]),
+              (P * n)(*arrs["C2"]), 0,
               int(a_bf), int(b_bf), ta, tb,
               int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.ptr(cnt),
               _lib.stream())

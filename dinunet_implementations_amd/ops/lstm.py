@@ -448,11 +448,13 @@ def _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
         probs.append(dict(a=dsl, b=x2d, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap))
         probs.append(dict(a=dsl, b=hprev[d].view(Bp * S, HD)[:N, :Hd],
                           out=_grad.grad_buffer(w_hh), beta=1.0, row_map=rmap))
-        # bias grads = column sums of dpre = dpre^T @ ones: extra problems of the same launch
-        for b in (b_ih, b_hh):
-            if b is not None:
-                probs.append(dict(a=dsl, b=ones, out=_grad.grad_buffer(b).view(-1, 1), beta=1.0,
-                                  row_map=rmap, ncol=1))
+        # bias grads = column sums of dpre = dpre^T @ ones: an extra problem of the same launch.
+        # d b_ih == d b_hh (both add to the same pre-activation): ONE column sum, stored twice
+        bs = [b for b in (b_ih, b_hh) if b is not None]
+        if bs:
+            probs.append(dict(a=dsl, b=ones, out=_grad.grad_buffer(bs[0]).view(-1, 1), beta=1.0,
+                              row_map=rmap, ncol=1,
+                              out2=_grad.grad_buffer(bs[1]).view(-1, 1) if len(bs) > 1 else None))
     return probs
 
 
