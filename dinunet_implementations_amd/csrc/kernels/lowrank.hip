@@ -851,7 +851,7 @@ lr_persist_kernel(LpArgs a) {
   for (;; ++it) {
     if (j == 0 && tid == 0) *X.iters += 1;
     // ---- phase A: P[my rows] = G[my rows] Q ----
-    const int sb = 1 + 8 * (it < 7 ? it : 7);
+    const int sb = 1 + 10 * (it < 5 ? it : 5);
     LP_STAMP(sb);
     lp_stage(stg, rQ, (m * r + 3) & ~3, tid);
     lp_sync();
@@ -937,6 +937,7 @@ lr_persist_kernel(LpArgs a) {
       else if (r <= 12) lp_chol<12>(gm, Rh, Sv, r, lane);
       else lp_chol<16>(gm, Rh, Sv, r, lane);
     }
+    LP_STAMP(sb + 8);
     {  // H = G[:, my cols]^T P on the matrix cores (the WB waves of a column block meet in red)
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

@@ -45,15 +45,16 @@ def main():
     L.dn_lr_persist_set_stamps(ctypes.c_void_p(None))
     v = st.view(8, 64).tolist()
     print(f"persistent launch (5 iterations, {t.n} layers): median {ts[len(ts)//2]:.1f} us by events")
-    names = ["A", "pub", "bar1", "gram", "chol+H", "solve", "bar2", "next"]
     for l in range(t.n):
         row = v[l]
         base = row[0]
         out = [f"layer {l}: G load {(row[1] - base) / 100:.2f}"]
         for it in range(5):
-            sb = 1 + 8 * it
-            seg = [(row[sb + k + 1] - row[sb + k]) / 100 for k in range(7)]
-            out.append(f"it{it} " + " ".join(f"{n_}={x:.2f}" for n_, x in zip(names, seg)))
+            sb = 1 + 10 * it
+            d = lambda a_, b_: (row[sb + b_] - row[sb + a_]) / 100  # noqa: E731
+            out.append(f"it{it} A={d(0, 1):.2f} pub={d(1, 2):.2f} bar1={d(2, 3):.2f} "
+                       f"gram={d(3, 4):.2f} chol={d(4, 8):.2f} H={d(8, 5):.2f} "
+                       f"solve={d(5, 6):.2f} bar2={d(6, 7):.2f}")
         print(" | ".join(out))
 
 
