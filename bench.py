@@ -9,6 +9,12 @@ timed step is a complete training step: fused encoder GEMM, persistent bi-LSTM f
 classifier + softmax-CE, full backward, dSGD all-reduce (RCCL over xGMI for N>1), fused Adam.
 Synthetic data (the ICA dataset is not shipped, ``.gitignore:123``) and random-init weights.
 
+The timed steps run through ``runtime.feed.DeviceFeed`` -- the object the production site loop
+(``runtime.site.FederatedSite``) trains its epochs with, per-step train records included.  At one
+site the run then trains a synthetic hard cohort through ``FederatedSite`` itself and adds the
+second half of the BASELINE metric, wall-clock to the target validation AUC
+(``time_to_auc_s``), and the site loop's own logged throughput (``site_loop_samples_per_sec``).
+
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 --master-addr 127.0.0.1 bench.py --gpus N``.  Rank 0 prints ONE JSON line; ``value`` is the
 whole-job aggregate (samples/s summed over all sites), ``per_site`` the per-GPU rate.
@@ -50,7 +56,81 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps per HIP graph in device-feed mode (0: the largest divisor of "
                          "--steps up to 10)")
+    ap.add_argument("--site-loop", default="auto", choices=["auto", "0", "1"],
+                    help="after the timed steps, train a synthetic hard ICA cohort through the "
+                         "production site loop (runtime.site.FederatedSite: device-fed epochs, "
+                         "validation, early stopping, checkpoints) and report its wall-clock to "
+                         "the target validation AUC and its logged samples/s (auto: N == 1)")
+    ap.add_argument("--target-auc", type=float, default=0.75)
+    ap.add_argument("--tta-subjects", type=int, default=2560,
+                    help="site-loop cohort size (split 0.8/0.1/0.1)")
+    ap.add_argument("--tta-epochs", type=int, default=30)
     return ap.parse_args()
+
+
+def site_loop(grp, args):
+    """Wall-clock to the target validation AUC through the production runtime: this rank's site
+    gets a synthetic hard ICA cohort (``data.synthetic.ica_cohort_hard``: connectivity labels,
+    site shift, 10% label noise) written in the reference layout (``[N, C, T]`` npy + labels
+    CSV), and ``FederatedSite.run`` trains it exactly as ``python -m
+    dinunet_implementations_amd.run`` would (device-fed epochs, global validation AUC, best /
+    last checkpoints, logs.json).  Returns the clock of the first epoch whose global validation
+    AUC reached the target (``cumulative_total_duration``, reference ``local.py:52``) and the
+    steady-state train throughput the site logged (``samples_per_sec``, epochs after the first)."""
+    import csv
+    import shutil
+    import statistics
+    import tempfile
+
+    import numpy as np
+    from dinunet_implementations_amd.config import build_config
+    from dinunet_implementations_amd.data.synthetic import ica_cohort_hard
+    from dinunet_implementations_amd.runtime.site import FederatedSite
+    from dinunet_implementations_amd.tasks import get_task
+
+    root = tempfile.mkdtemp(prefix=f"dinunet_bench_{grp.rank}_")
+    try:
+        base = os.path.join(root, "input", f"local{grp.rank}", "simulatorRun")
+        os.makedirs(base)
+        x, y = ica_cohort_hard(args.tta_subjects, args.comps, args.temporal, seed=300 + grp.rank,
+                               site=grp.rank, signal=0.35, label_noise=0.1)
+        np.save(os.path.join(base, "ica_data.npy"), x)
+        del x
+        with open(os.path.join(base, "labels.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["data_index", "label"])
+            w.writerows([[i, int(v)] for i, v in enumerate(y)])
+        cfg = build_config(overrides={
+            "task_id": "ICA-Classification", "agg_engine": args.engine,
+            "precision_bits": args.precision_bits, "batch_size": args.batch,
+            "epochs": args.tta_epochs, "patience": args.tta_epochs, "split_ratio": [0.8, 0.1, 0.1],
+            "data_file": "ica_data.npy", "labels_file": "labels.csv",
+            "input_size": args.input_size, "hidden_size": args.hidden,
+            "window_size": args.window, "window_stride": args.window,
+            "temporal_size": args.temporal, "num_components": args.comps, "num_class": 2,
+            "learning_rate": 1e-3, "seed": 11})
+        T, D, H = get_task(cfg["task_id"])
+        site = FederatedSite(cfg, grp, T, D, H, {"baseDirectory": base, "clientId": f"local{grp.rank}"},
+                             os.path.join(root, "out"), site_name=f"local{grp.rank}", verbose=False)
+        logs = site.run()[0]
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    val = [float(r[-1]) for r in logs.get("validation_log", [])]
+    cum = logs.get("cumulative_total_duration", [])
+    hit = next((i for i, a in enumerate(val) if a >= args.target_auc), None)
+    sps = logs.get("samples_per_sec", [])
+    return {
+        "time_to_auc_s": round(cum[hit], 3) if hit is not None else None,
+        "target_auc": args.target_auc,
+        "epochs_to_auc": hit + 1 if hit is not None else None,
+        "steps_per_epoch": int(logs["split_sizes"]["train"]) // args.batch,
+        "best_val_auc": round(max(val), 4) if val else None,
+        "test_auc": round(float(logs["test_metrics"][-1]), 4) if logs.get("test_metrics") else None,
+        "site_loop_samples_per_sec": round(statistics.median(sps[1:] or sps), 1) if sps else None,
+        "site_loop_feed": logs.get("feed", "host"),
+        "tta_data": (f"synthetic hard ICA cohort, {args.tta_subjects} subjects/site "
+                     "(signal 0.35, label noise 0.1), split 0.8/0.1/0.1"),
+    }
 
 
 def main():
@@ -83,21 +163,21 @@ def main():
     pi, it0 = getattr(engine, "power_iterations", None), None
     if args.feed == "device":
         # the site's (synthetic) dataset resident in HBM as bf16, batches gathered on the device
-        # by the step's first launch; the timed steps run as replays of K-step graphs
-        from dinunet_implementations_amd.ops import DeviceSource
-        src = DeviceSource(xs.view(args.pool * args.batch, S, args.comps, args.window)
-                           .to(torch.bfloat16), ys.view(-1), args.batch)
-        del xs
+        # by the step's first launch, per-step train records kept on the device: the same
+        # runtime object (runtime.feed.DeviceFeed) FederatedSite trains its epochs with
+        from dinunet_implementations_amd.runtime.feed import DeviceFeed
         K = args.graph_steps or max(d for d in range(1, 11) if args.steps % d == 0)
-        step.bind(src, steps_per_graph=K)
-        step.run(args.warmup)
-        step.prepare(args.steps)
+        feed = DeviceFeed(step, xs.view(args.pool * args.batch, S, args.comps, args.window),
+                          ys.view(-1), args.batch, nb=args.pool, col=1, steps_per_graph=K)
+        del xs
+        feed.run(args.warmup)
+        feed.prepare(args.steps)
         it0 = pi() if pi else None
         torch.cuda.synchronize()
         grp.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        step.run(args.steps)
+        feed.run(args.steps)
         torch.cuda.synchronize()
         grp.barrier()
         torch.cuda.synchronize()
@@ -125,6 +205,13 @@ def main():
     loss = float(step.last_loss.detach())
     n = grp.world
     total = n * args.batch * args.steps / dt
+    peak = torch.cuda.max_memory_allocated(dev)
+    tta = None
+    if args.site_loop == "1" or (args.site_loop == "auto" and n == 1):
+        try:
+            tta = site_loop(grp, args)
+        except Exception as e:  # never lose the throughput line to the study
+            tta = {"time_to_auc_s": None, "site_loop_error": f"{type(e).__name__}: {e}"}
     if grp.is_master:
         rec = {
             # the headline metric names dSGD; other engines report the same quantity under
@@ -156,10 +243,12 @@ def main():
             **({"dad_iters_per_step": iters} if iters is not None else {}),
             # HBM high-water mark of the run (allocator view: model, optimizer state, activations,
             # graph pools and the resident synthetic dataset of --pool batches)
-            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
+            "peak_hbm_gib": round(peak / 2**30, 3),
             "dataset_hbm_gib": round(args.pool * args.batch * S * args.comps * args.window
                                      * (2 if args.feed == "device" else 4) / 2**30, 3),
         }
+        if tta is not None:
+            rec.update(tta)
         print(json.dumps(rec), flush=True)
     from dinunet_implementations_amd.parallel import shutdown
     shutdown()

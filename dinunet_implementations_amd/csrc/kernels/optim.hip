@@ -119,16 +119,48 @@ __device__ __forceinline__ void pack_store(const PackPlan& pl, const PackSeg& sg
   }
 }
 
+// Per-step train-metric record of a device-fed epoch (runtime.feed.DeviceFeed): the step's score
+// column out[b][col] (ICA: prob[:, 1], reference comps/icalstm/__init__.py:64-65) and its loss
+// land in rings indexed by the batch cursor, so an epoch of K-step graph replays yields the exact
+// per-sample (score, label) pairs for the train AUC and the per-step losses for the train average
+// with no host work between steps.  Slot c = (*cursor + cofs) mod n.
+struct StepRecord {
+  const float* out;
+  long ld;
+  int col, B;
+  const float* loss;
+  float* rs;  // [n][B] scores
+  float* rl;  // [n] losses
+  long n;
+  const long long* cursor;
+};
+
+__device__ __forceinline__ void record_step(const StepRecord& r, int cofs) {
+  long c = (*r.cursor + cofs) % r.n;
+  if (c < 0) c += r.n;
+  for (int b = threadIdx.x; b < r.B; b += blockDim.x) r.rs[c * r.B + b] = r.out[b * r.ld + r.col];
+  if (threadIdx.x == 0) r.rl[c] = *r.loss;
+}
+
+__global__ void __launch_bounds__(256) record_kernel(StepRecord r, int cofs) { record_step(r, cofs); }
+
 __global__ void __launch_bounds__(256)
 adam_pack_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                  float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
                  float grad_scale, const int* __restrict__ tdev, double b1d, double b2d, int update,
-                 int zero_grad, PackPlan pl, StepPrologue sp, int gofs, int ublocks) {
+                 int zero_grad, PackPlan pl, StepPrologue sp, int gofs, int ublocks, StepRecord rec) {
+  // the step's train record (rec.out set): the LAST workgroup; the cursor was advanced by this
+  // step's encoder GEMM, so it names the batch this step trained on
+  if (rec.out && blockIdx.x == gridDim.x - 1) {
+    record_step(rec, 0);
+    return;
+  }
   // blocks [0, ublocks) update the parameters (one float4 per thread and round), the rest gather
   // the next batch: no divergent work mix inside a wave, every load of a round issued at once
   if ((int)blockIdx.x >= ublocks) {
     const long c = (*sp.cursor + gofs) % sp.nb;
-    const long ng = sp.ux + sp.ny, stride = (long)(gridDim.x - ublocks) * blockDim.x;
+    const long ng = sp.ux + sp.ny;
+    const long stride = (long)(gridDim.x - ublocks - (rec.out ? 1 : 0)) * blockDim.x;
     for (long i = (blockIdx.x - ublocks) * (long)blockDim.x + threadIdx.x; i < ng; i += stride)
       prologue_item(sp, i, c);  // sp.ug == 0: the zeroing rides in the update below
     return;
@@ -241,8 +273,15 @@ DN_API int dn_adam_pack(float* p, float* g, float* m, float* v, long n, float lr
                         int update, int zero_grad, const void* segs, int cnt, int I, int Hd,
                         int HD, const void* gx, int gx_bf16, long row_elems, const long long* gy,
                         const long long* order, long nb, const long long* cursor, int B,
-                        void* xb, long long* yd, int gofs, hipStream_t st) {
+                        void* xb, long long* yd, int gofs, const void* record, hipStream_t st) {
   if (n <= 0 || n % 4 || cnt < 0 || cnt > PACK_SEGS) return DN_BAD_SHAPE;
+  StepRecord rec{};
+  if (record && update) {
+    rec = *reinterpret_cast<const StepRecord*>(record);
+    if (!rec.out || !rec.loss || !rec.rs || !rec.rl || !rec.cursor || rec.n <= 0 || rec.B <= 0 ||
+        rec.col < 0 || rec.ld <= rec.col)
+      return DN_BAD_SHAPE;
+  }
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
   if (update && !tdev) return DN_BAD_SHAPE;
   PackPlan pl{};
@@ -270,9 +309,22 @@ DN_API int dn_adam_pack(float* p, float* g, float* m, float* v, long n, float lr
   // rest start as the first retire)
   auto parts = [](long items) { return (int)((items + 255) / 256 < 4096 ? (items + 255) / 256 : 4096); };
   const int ub = parts(n / 4), gb = sp.gx ? parts(sp.ux + sp.ny) : 0;
-  hipLaunchKernelGGL(adam_pack_kernel, dim3(ub + gb), dim3(256), 0, st, p, g, m, v, n, lr,
-                     (float)b1, (float)b2, eps, wd, grad_scale, tdev, b1, b2, update, zero_grad,
-                     pl, sp, gofs, ub);
+  hipLaunchKernelGGL(adam_pack_kernel, dim3(ub + gb + (rec.out ? 1 : 0)), dim3(256), 0, st, p, g,
+                     m, v, n, lr, (float)b1, (float)b2, eps, wd, grad_scale, tdev, b1, b2, update,
+                     zero_grad, pl, sp, gofs, ub, rec);
+  return dn_launch_status();
+}
+
+// the standalone record (eager steps, and steps whose update is not the packing Adam): slot
+// (*cursor + cofs) mod n, cofs = -1 after an update that advanced the cursor
+DN_API long dn_step_record_size() { return (long)sizeof(StepRecord); }
+DN_API int dn_step_record(const void* record, int cofs, hipStream_t st) {
+  if (!record) return DN_BAD_SHAPE;
+  const StepRecord r = *reinterpret_cast<const StepRecord*>(record);
+  if (!r.out || !r.loss || !r.rs || !r.rl || !r.cursor || r.n <= 0 || r.B <= 0 || r.col < 0 ||
+      r.ld <= r.col)
+    return DN_BAD_SHAPE;
+  hipLaunchKernelGGL(record_kernel, dim3(1), dim3(256), 0, st, r, cofs);
   return dn_launch_status();
 }
 

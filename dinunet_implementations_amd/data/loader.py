@@ -48,7 +48,8 @@ class DeviceLoader:
     def set_epoch(self, epoch: int):
         self.epoch = epoch
 
-    def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+    def _spans(self) -> Iterator[Tuple[int, int, Optional[torch.Tensor]]]:
+        """One pass: ``(start, end, perm)`` per batch (``perm`` None when not shuffling)."""
         n = self.inputs.shape[0]
         dev = self.inputs.device
         if self.shuffle:
@@ -63,6 +64,11 @@ class DeviceLoader:
             self._pos = b + 1
             s = b * self.batch_size
             e = n if b == nb - 1 and not self.drop_last else min(n, s + self.batch_size)
+            yield s, e, perm
+
+    def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+        dev = self.inputs.device
+        for s, e, perm in self._spans():
             if perm is None:
                 ix = torch.arange(s, e, device=dev)
                 yield self.inputs[s:e], self.labels[s:e], ix
@@ -70,16 +76,31 @@ class DeviceLoader:
                 ix = perm[s:e]
                 yield self.inputs.index_select(0, ix), self.labels.index_select(0, ix), ix
 
+    def iter_indices(self) -> Iterator[torch.Tensor]:
+        """The sample indices of the batches :meth:`__iter__` would yield, same passes, same
+        shuffles, same resume position, without gathering the batches (a device-fed epoch
+        gathers them on the device: ``runtime.feed.DeviceFeed``)."""
+        dev = self.inputs.device
+        for s, e, perm in self._spans():
+            yield torch.arange(s, e, device=dev) if perm is None else perm[s:e]
+
+    @property
+    def full_batches(self) -> bool:
+        """Every batch of a pass holds exactly ``batch_size`` samples."""
+        n = self.inputs.shape[0]
+        return n >= self.batch_size and (self.drop_last or n % self.batch_size == 0)
+
     # ---- resume ------------------------------------------------------------------------------
     def state(self) -> dict:
         """Position for an exact resume: passes started and batches consumed in the current one
         (the shuffle of a pass is a pure function of ``seed`` and its pass number)."""
         return {"epoch": int(self.epoch), "pos": int(self._pos)}
 
-    def resume_iter(self, state: dict):
-        """An iterator that continues where :meth:`state` was taken."""
+    def resume_iter(self, state: dict, indices: bool = False):
+        """An iterator that continues where :meth:`state` was taken (of batch indices only,
+        :meth:`iter_indices`, with ``indices``)."""
         self.epoch = max(0, int(state.get("epoch", 0)) - 1)
-        it = iter(self)
+        it = self.iter_indices() if indices else iter(self)
         for _ in range(int(state.get("pos", 0))):
             next(it, None)
         return it

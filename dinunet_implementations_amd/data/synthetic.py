@@ -100,8 +100,13 @@ def ica_cohort_hard(n: int, comps: int = 100, T: int = 980, seed: int = 0, site:
     y_true = rng.integers(0, 2, n)
     ar = np.clip(rng.normal(0.55 + ar_site, 0.1, (n, 1)), 0.05, 0.9).astype(np.float32)
     x = rng.normal(0, 1, (n, comps, T)).astype(np.float32)
+    # the AR(1) recursion on a time-major copy (contiguous slabs; 3x faster, same values)
+    xt = np.ascontiguousarray(x.transpose(2, 0, 1))
+    del x
     for k in range(1, T):
-        x[:, :, k] = ar * x[:, :, k - 1] + x[:, :, k]
+        xt[k] = ar * xt[k - 1] + xt[k]
+    x = np.ascontiguousarray(xt.transpose(1, 2, 0))
+    del xt
     x /= np.sqrt(1.0 / (1.0 - ar[:, :, None] ** 2))  # unit variance noise
     t = np.arange(T, dtype=np.float32)
     f = rng.uniform(0.02, 0.06, (n, 1, 1)).astype(np.float32)

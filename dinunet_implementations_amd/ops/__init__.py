@@ -5,8 +5,8 @@ from ._lib import native_available
 from .gemm import PLAIN_BLAS, mm, mm_grouped, mm_plain
 from .linear import linear_bias_relu
 from .lstm import bilstm as _bilstm_fused, lstm_supported, padded_hidden
-from .optim import (DeviceSource, FlatParams, FusedAdam, cast_bf16_to_f32, cast_f32_to_bf16,
-                    step_prologue)
+from .optim import (DeviceSource, FlatParams, FusedAdam, StepRecorder, cast_bf16_to_f32,
+                    cast_f32_to_bf16, step_prologue)
 from .heads import softmax_ce, log_softmax_nll
 from .head import HeadSpec, head_loss
 
@@ -19,6 +19,6 @@ def bilstm(x, params, reduce: str = "none", modules=None, packed=None, xp=None,
 
 __all__ = [
     "mm", "linear_bias_relu", "bilstm", "lstm_supported", "padded_hidden", "FlatParams",
-    "DeviceSource", "FusedAdam", "cast_bf16_to_f32", "cast_f32_to_bf16", "step_prologue", "HeadSpec", "head_loss",
+    "DeviceSource", "StepRecorder", "FusedAdam", "cast_bf16_to_f32", "cast_f32_to_bf16", "step_prologue", "HeadSpec", "head_loss",
     "softmax_ce", "log_softmax_nll", "native_available", "capture", "reference",
 ]

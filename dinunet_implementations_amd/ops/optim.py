@@ -46,7 +46,8 @@ _lib.register("dn_adam_pack", [_lib.c_void_p] * 4 + [_lib.c_long, _lib.c_float, 
                                _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int,
                                _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                                _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                               _lib.c_int, _lib.c_void_p])
+                               _lib.c_int, _lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_step_record", [_lib.c_void_p, _lib.c_int, _lib.c_void_p])
 
 
 def ctypes_addr(obj) -> int:
@@ -184,11 +185,14 @@ class FusedAdam:
             tab[i] = _Seg(off, n, kind, d, dst, dst2 or None)
         self._pack = (pack, tab, len(rows), src, xb, yd)
 
-    def step_pack(self, grad_scale: float = 1.0, update: bool = True, gofs: int = 1):
+    def step_pack(self, grad_scale: float = 1.0, update: bool = True, gofs: int = 1,
+                  record=None):
         """ONE launch: the graph-capturable Adam step (bias corrections from the device counter,
         which the step's first GEMM advanced: ``dn_gemm_arm_bump``), the attached packed images
         rewritten from the updated parameters, the gradient zeroed, and the batch at
-        ``cursor + gofs`` gathered.  ``update=False``: images + gather + zeroing only (priming)."""
+        ``cursor + gofs`` gathered.  ``update=False``: images + gather + zeroing only (priming).
+        ``record``: a :meth:`StepRecorder.args` struct -- the step's score column and loss go to
+        the recorder's rings at the cursor (one more workgroup of the same launch)."""
         pack, tab, cnt, src, xb, yd = self._pack
         d = self.flat.data
         if self._tdev is None:
@@ -203,7 +207,8 @@ class FusedAdam:
         _lib.call("dn_adam_pack", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
                   self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
                   self.weight_decay, grad_scale, self._tdev.data_ptr(), int(update), 1,
-                  ctypes_addr(tab), cnt, pack.I, pack.Hd, pack.HD, *gx, int(gofs), _lib.stream())
+                  ctypes_addr(tab), cnt, pack.I, pack.Hd, pack.HD, *gx, int(gofs),
+                  ctypes_addr(record) if (record is not None and update) else None, _lib.stream())
 
     def device_step(self) -> torch.Tensor:
         """The device step counter (int32[1]) the graph-captured update reads; a step prologue
@@ -315,9 +320,65 @@ class DeviceSource:
                   self.cursor.data_ptr(), self.B, xb.data_ptr(), yd.data_ptr(), grad.data_ptr(),
                   grad.numel(), _lib.ptr(bump), _lib.stream())
 
+    def labels_of(self, steps: int) -> torch.Tensor:
+        """Labels of batches ``0 .. steps-1`` of the current order, flattened (what a
+        :class:`StepRecorder`'s score ring pairs with)."""
+        rows = (self.order[:steps * self.B] if self.order is not None
+                else torch.arange(steps * self.B, device=self.X.device) % self.X.shape[0])
+        return self.Y[rows]
+
     def prologue_args(self, xb, yd, grad, bump=None):
         """Argument tail of ``dn_lstm_pack_gather`` (the prologue riding in the weight pack)."""
         return [self.X.data_ptr(), int(self.X.dtype == torch.bfloat16), self.row,
                 self.Y.data_ptr(), _lib.ptr(self.order), self.nb, self.cursor.data_ptr(),
                 self.B, xb.data_ptr(), yd.data_ptr(), grad.data_ptr(), grad.numel(),
                 _lib.ptr(bump)]
+
+
+class StepRecorder:
+    """Per-step train records of device-fed steps (``runtime.feed.DeviceFeed``): ring slot
+    ``c mod n`` of batch cursor ``c`` holds the step's score column ``out[:, col]`` (``[B]``; ICA:
+    ``prob[:, 1]``, the reference's train-AUC input, ``comps/icalstm/__init__.py:64-65``) and its
+    loss (``:67-68``).  The write rides in the packing Adam launch (one more workgroup,
+    ``optim.hip adam_pack_kernel``) or is a one-workgroup launch of its own (``dn_step_record``)
+    after an update that already advanced the cursor; either way K-step graph replays keep exact
+    per-sample train metrics with no host work between steps."""
+
+    def __init__(self, n: int, B: int, cursor: torch.Tensor, col: int = 1):
+        self.n, self.B, self.col = int(n), int(B), int(col)
+        dev = cursor.device
+        self.scores = torch.zeros(self.n, self.B, dtype=torch.float32, device=dev)
+        self.losses = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.cursor = cursor
+
+    def args(self, out: torch.Tensor, loss: torch.Tensor):
+        """The ``StepRecord`` struct for a step whose outputs are ``out`` [B, C] / ``loss`` []."""
+        import ctypes
+
+        class _Rec(ctypes.Structure):
+            _fields_ = [("out", ctypes.c_void_p), ("ld", ctypes.c_long), ("col", ctypes.c_int),
+                        ("B", ctypes.c_int), ("loss", ctypes.c_void_p), ("rs", ctypes.c_void_p),
+                        ("rl", ctypes.c_void_p), ("n", ctypes.c_long), ("cursor", ctypes.c_void_p)]
+        L = _lib.lib()
+        L.dn_step_record_size.restype = ctypes.c_long
+        if ctypes.sizeof(_Rec) != L.dn_step_record_size():
+            raise RuntimeError("step record layout mismatch with the kernel library")
+        if (out.dim() != 2 or out.shape[0] != self.B or out.dtype != torch.float32
+                or not out.is_contiguous() or loss.dtype != torch.float32 or loss.numel() != 1):
+            raise ValueError("StepRecorder: out must be contiguous fp32 [B, C], loss fp32 scalar")
+        return _Rec(out.data_ptr(), out.shape[1], self.col, self.B, loss.data_ptr(),
+                    self.scores.data_ptr(), self.losses.data_ptr(), self.n, self.cursor.data_ptr())
+
+    def record(self, out: torch.Tensor, loss: torch.Tensor, cofs: int = -1):
+        """Standalone record into slot ``(cursor + cofs) mod n``."""
+        if out.is_cuda:
+            rec = self.args(out, loss)  # (held: the launcher reads it through its address)
+            _lib.call("dn_step_record", ctypes_addr(rec), int(cofs), _lib.stream())
+            return
+        c = (int(self.cursor.item()) + cofs) % self.n
+        self.scores[c].copy_(out[:, self.col].float())
+        self.losses[c] = loss.detach().float()
+
+    def reset(self):
+        self.scores.zero_()
+        self.losses.zero_()

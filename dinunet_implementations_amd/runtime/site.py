@@ -37,6 +37,8 @@ from ..data.splits import make_splits
 from ..parallel import SiteGroup, make_engine
 from ..utils import logs as L
 from ..utils.metrics import Averages, Metrics, improved, metric_value
+from ..ops import FusedAdam
+from .feed import DeviceFeed
 from .step import TrainStep
 from .trainer import NNTrainer, set_seed
 
@@ -163,8 +165,14 @@ class FederatedSite:
                 step = TrainStep(trainer.modules(), trainer.flat, trainer.optimizer, engine,
                                  use_graph=use_graph, accum=li,
                                  forward_loss=lambda m, x, y: trainer.forward_loss(x, y))
-        it = tr.resume_iter(resume["loader"]) if resume and resume.get("loader") else iter(tr)
         fault_at = _fault_step(group.rank)
+        feed = self._device_feed(trainer, step, engine, tr, bs, li, steps, cfg, fault_at)
+        if resume and resume.get("loader"):
+            it = tr.resume_iter(resume["loader"], indices=feed is not None)
+        else:
+            it = tr.iter_indices() if feed is not None else iter(tr)
+        if feed is not None:
+            logs[f"{tag}feed"] = "device"
         tl = logs.setdefault(f"{tag}train_log", [])
         vl = logs.setdefault(f"{tag}validation_log", [])
         lvl = logs.setdefault(f"{tag}local_validation_log", [])
@@ -180,7 +188,21 @@ class FederatedSite:
             t0 = time.time()
             avg, met = trainer.new_averages(), trainer.new_metrics()
             nsamp = 0
-            for _ in range(steps):
+            if feed is not None:
+                # ONE host call per epoch: the epoch's batch order (the loader's own passes),
+                # then K-step graph replays with the train records kept on the device
+                order = []
+                for _ in range(steps):
+                    try:
+                        order.append(next(it))
+                    except StopIteration:
+                        it = tr.iter_indices()
+                        order.append(next(it))
+                losses, scores, labels = feed.run_epoch(torch.cat(order))
+                avg.add(losses.mean(), steps * bs)
+                met.add(scores.clone(), labels)
+                nsamp += steps * bs
+            for _ in range(steps if feed is None else 0):
                 if fault_at is not None:  # failure-path tests (DINUNET_FAULT=<rank>:<step>)
                     fault_at -= 1
                     if fault_at < 0:
@@ -271,6 +293,22 @@ class FederatedSite:
         if step is not None and step.timers.summary():
             logs[f"{tag}phase_ms"] = step.timers.summary()  # DINUNET_PHASE_TIMERS=1
         return best
+
+    def _device_feed(self, trainer: NNTrainer, step, engine, tr: DeviceLoader, bs: int, li: int,
+                     steps: int, cfg: Dict[str, Any], fault_at) -> Optional[DeviceFeed]:
+        """The device-fed epoch (``runtime.feed``) when this site's step can take it: a captured
+        step on the GPU, a model that takes a bf16 batch, a plugin with a score column, full
+        batches, no accumulation, an engine that runs inside the captured step.  ``device_feed``
+        (default on) turns it off; the fault-injection hook keeps the per-step host loop."""
+        col = getattr(trainer, "score_column", None)
+        if (step is None or not step.use_graph or self.device.type != "cuda" or li != 1
+                or not cfg.get("device_feed", True) or fault_at is not None or col is None
+                or not tr.full_batches or steps < 1
+                or not getattr(step.model, "accepts_bf16_input", False)
+                or not isinstance(trainer.optimizer, FusedAdam)
+                or not (engine.name.startswith("dSGD") or getattr(engine, "fast", False))):
+            return None
+        return DeviceFeed(step, tr.inputs, tr.labels, bs, steps, col=col)
 
     def _pretrain(self, trainer: NNTrainer, data, fold_dir: str, seed: int, logs: Dict[str, Any]):
         sizes = self.group.all_gather_object(int(data["train"][0].shape[0]))

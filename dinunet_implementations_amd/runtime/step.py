@@ -116,6 +116,7 @@ class TrainStep:
         self._bf16_in = False
         self._packs: list = []  # LSTM repacks deferred out of the captured graph
         self.src = None  # device-fed batches (bind)
+        self.rec = None  # device-side train records of device-fed steps (bind)
 
     def _grad_one(self, device, dtype=torch.float32):
         # a persistent d(loss)/d(loss) = 1: loss.backward() would launch a fill kernel for it
@@ -307,7 +308,7 @@ class TrainStep:
         return loss
 
     # ---- device-fed steps ---------------------------------------------------------------------
-    def bind(self, src, steps_per_graph: int = 8):
+    def bind(self, src, steps_per_graph: int = 8, recorder=None):
         """Train from an ``ops.DeviceSource`` (batches resident in HBM, gathered on the device).
 
         Every step is then device-only: its first launch gathers the batch at the source's cursor
@@ -315,7 +316,10 @@ class TrainStep:
         ``ops.lstm.ride_pack``), zeroes the gradient and advances Adam's counter; its Adam
         launch advances the cursor.  With one site (the update inside the graph) ``run``
         replays graphs holding ``steps_per_graph`` whole steps, so there is no host work and no
-        graph boundary between them."""
+        graph boundary between them.  ``recorder`` (``ops.StepRecorder`` on the source's cursor):
+        every step also writes its score column and loss into the recorder's rings (inside the
+        packing Adam launch when there is one), so the train metrics of an epoch are exact without
+        a host round trip per step (``runtime.feed.DeviceFeed``)."""
         if self.accum != 1:
             raise ValueError("TrainStep.bind: device-fed steps need local_iterations == 1")
         if not getattr(self.model, "accepts_bf16_input", False):
@@ -323,6 +327,9 @@ class TrainStep:
         if not isinstance(self.opt, ops.FusedAdam):
             raise ValueError("TrainStep.bind: device-fed steps need the fused Adam")
         self.src = src
+        self.rec = recorder
+        if recorder is not None and recorder.cursor.data_ptr() != src.cursor.data_ptr():
+            raise ValueError("TrainStep.bind: the recorder must index by the source's cursor")
         self.opt.cursor = src.cursor
         dev = src.X.device
         self._dsx = torch.empty((src.B,) + src.sample_shape, dtype=torch.bfloat16, device=dev)
@@ -386,8 +393,16 @@ class TrainStep:
             self._pre_reduce()
         scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
                  else self.engine.reduce())
-        self.opt.step_pack(grad_scale=scale)
+        self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss))
         return out, loss, pred
+
+    def _rec_args(self, out, loss):
+        return self.rec.args(out, loss) if self.rec is not None else None
+
+    def _record(self, out, loss):
+        """The standalone record of a step whose update already advanced the cursor."""
+        if self.rec is not None:
+            self.rec.record(out, loss, cofs=-1)
 
     def _apack_prime(self):
         """Before the first replay of a run: the persistent images from the current parameters,
@@ -417,6 +432,7 @@ class TrainStep:
             scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
                      else self.engine.reduce())
             self.opt.step_graphable(grad_scale=scale, prebumped=True)
+            self._record(out, loss)
         return out, loss, pred
 
     def _dev_capture(self, k: int):
@@ -474,6 +490,7 @@ class TrainStep:
             scale = self.engine.reduce()
         with T.phase("optim"):
             self.opt.step(grad_scale=scale)  # advances the source cursor too
+            self._record(out, loss)
         self.last_out, self.last_loss, self.last_pred = out.detach(), loss.detach(), pred
         return loss
 
@@ -529,13 +546,15 @@ class TrainStep:
                 scale = self._reduce_after_replay()
             with self.timers.phase("optim"):
                 if self._apack is not None:
-                    self.opt.step_pack(grad_scale=scale)  # + next operands and batch
+                    # + next operands and batch (+ this step's train record)
+                    self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss))
                     self.opt.step_count += 1
                 else:
                     self.opt.step(grad_scale=scale)
+                    self._record(out, loss)
             self.last_out, self.last_loss, self.last_pred = out, loss, pred
             return loss, done + 1, primed
-        k = self._dK if n - done >= self._dK else 1
+        k = min(self._dK, n - done)
         if k not in self._dgraphs:
             self._dev_capture(k)
         g, (out, loss, pred), graph_opt = self._dgraphs[k]
@@ -551,6 +570,7 @@ class TrainStep:
                 scale = self._reduce_after_replay()
             with self.timers.phase("optim"):
                 self.opt.step(grad_scale=scale)
+                self._record(out, loss)
         self.last_out, self.last_loss, self.last_pred = out, loss, pred
         return loss, done + k, primed
 
@@ -563,8 +583,8 @@ class TrainStep:
             if "split" not in self._dgraphs:
                 self._dev_capture_split()
             return
-        for k in ({self._dK, 1} if n <= 0 else ({self._dK} if n % self._dK == 0 else {self._dK, 1})):
-            if k not in self._dgraphs and (k == 1 or n <= 0 or n >= k):
+        for k in ({self._dK} if n <= 0 else {min(self._dK, n), n % self._dK} - {0}):
+            if k not in self._dgraphs:
                 self._dev_capture(k)
 
     @property

@@ -70,6 +70,10 @@ class NNTrainer:
     def score(self, out, pred):
         return pred
 
+    # the column of ``out`` that :meth:`score` returns, when it is one (a device-fed epoch then
+    # records it on the device every step: ``runtime.feed``); None keeps the host-fed loop
+    score_column: Optional[int] = None
+
     @property
     def reference_math(self) -> bool:
         """``compute_path = "reference"``: every model runs the fp32 oracle math

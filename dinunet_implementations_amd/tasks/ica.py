@@ -88,6 +88,10 @@ class ICADataset(SiteDataset):
 
 
 class ICATrainer(NNTrainer):
+    # the train metric ranks prob[:, 1] (comps/icalstm/__init__.py:64-65): a device-fed epoch
+    # records that column of every step's output on the device (runtime.feed)
+    score_column = 1
+
     def _init_nn_model(self):
         c = self.cache
         self.nn["net"] = ICALstm(window_size=c["window_size"], input_size=c["input_size"],

@@ -76,3 +76,19 @@ def test_ica_site_collective_paths_over_rccl(tmp_path):
             assert "best_val_epoch" in json.load(f)
     finally:
         dist.destroy_process_group()
+
+
+def test_ica_site_device_feed_matches_host_feed(tmp_path):
+    """The production site loop trains its epochs device-fed (runtime.feed: HBM-resident bf16
+    split, K-step graphs, train records on the device) and logs what the per-step host loop
+    logs: same train loss / AUC per epoch, same validation curve, same test metrics."""
+    root = _ica_root(tmp_path)
+    ov = {"epochs": 3, "batch_size": 8, "seed": 3}
+    dev = _run_site(root, str(tmp_path / "dev"), dict(ov, device_feed=True))[0]
+    host = _run_site(root, str(tmp_path / "host"), dict(ov, device_feed=False))[0]
+    assert dev.get("feed") == "device" and "feed" not in host
+    for a, b in zip(dev["train_log"], host["train_log"]):
+        assert abs(a[0] - b[0]) < 2e-4 and abs(a[1] - b[1]) < 2e-3, (dev["train_log"], host["train_log"])
+    for a, b in zip(dev["validation_log"], host["validation_log"]):
+        assert abs(a[0] - b[0]) < 2e-4 and abs(a[1] - b[1]) < 2e-3
+    assert len(dev["samples_per_sec"]) == 3

@@ -465,3 +465,41 @@ def test_rankdad_persistent_launch_matches_staged(hidden, tol, monkeypatch):
         if tol == 0.0:
             assert all(x == 5 for x in runs), runs
 
+
+
+@pytest.mark.parametrize("apack", [False, True])
+def test_device_feed_epoch_matches_host_loop(apack, monkeypatch):
+    """runtime.feed.DeviceFeed (what FederatedSite trains its epochs with): one epoch of K-step
+    graph replays over an explicit batch order gives the host-fed loop's trajectory, and the
+    device-side train records hold every step's loss and prob[:, 1] column (the train average and
+    the train AUC of the reference, comps/icalstm/__init__.py:64-68) in step order."""
+    from dinunet_implementations_amd.runtime import step as step_mod
+    from dinunet_implementations_amd.runtime.feed import DeviceFeed
+    monkeypatch.setattr(step_mod, "ADAM_PACK", apack)
+    xs, ys = _batches(n=6)
+    B = xs.shape[1]
+    X = xs.reshape(-1, *xs.shape[2:]).to(torch.bfloat16)
+    Y = ys.reshape(-1)
+    nb = 11  # > the rows: the order cycles, and 11 = 4 + 4 + 3 needs a remainder graph
+    g = torch.Generator(device="cuda").manual_seed(5)
+    _, fh, sh = _trainer(0, use_graph=True)
+    _, fd, sd = _trainer(0, use_graph=True)
+    feed = DeviceFeed(sd, X, Y, B, nb, col=1, steps_per_graph=4)
+    assert (sd._apack is not None) == apack
+    host_loss, host_score = [], []
+    for epoch in range(2):
+        order = torch.randint(0, X.shape[0], (nb * B,), device="cuda", generator=g)
+        for c in range(nb):
+            rows = order[c * B:(c + 1) * B]
+            loss = sh(X[rows].float(), Y[rows])
+            host_loss.append(float(loss))
+            host_score.append(sh.last_out[:, 1].clone())
+        losses, scores, labels = feed.run_epoch(order)
+        torch.cuda.synchronize()
+        assert torch.equal(labels, Y[order])
+        hl = torch.tensor(host_loss[-nb:], device="cuda")
+        assert torch.allclose(losses, hl, rtol=1e-5, atol=1e-6), (losses, hl)
+        hs = torch.cat(host_score[-nb:])
+        assert torch.allclose(scores, hs, rtol=1e-4, atol=1e-6), (scores - hs).abs().max()
+    assert sd.opt.step_count == sh.opt.step_count == 2 * nb
+    assert torch.allclose(fh.data, fd.data, rtol=1e-6, atol=1e-7), (fh.data - fd.data).abs().max()
