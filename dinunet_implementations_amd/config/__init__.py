@@ -80,6 +80,12 @@ FRAMEWORK_DEFAULTS: Dict[str, Any] = {
     # the non-pretraining sites' wait for the pretraining site (not a collective: see
     # runtime.site.FederatedSite._await_pretrain)
     "pretrain_timeout_s": 7 * 86400,
+    # the pretraining site's heartbeat period (None: collective_timeout_s / 4, 0.5-30 s); a site
+    # silent for collective_timeout_s ends the wait with an error
+    "pretrain_heartbeat_s": None,
+    # site loop: train epochs device-fed (runtime.feed: HBM-resident bf16 split, K-step graphs,
+    # on-device train records) when the step supports it
+    "device_feed": True,
     # "fused": gfx950 kernels (bf16 MFMA operands, fp32 accumulation / state);
     # "reference": the fp32 oracle math of ops/reference.py on the same device (fidelity baseline)
     "compute_path": "fused",

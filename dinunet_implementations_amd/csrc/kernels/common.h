@@ -54,3 +54,35 @@ __device__ __forceinline__ void dn_store_f32x4(__amdgpu_buffer_rsrc_t r, uint32_
 static inline int dn_launch_status() {
   return hipGetLastError() == hipSuccess ? DN_OK : DN_LAUNCH_FAILED;
 }
+
+// Poll limit of the in-kernel hand-off / barrier waits (head_step.hip, lowrank.hip): < 0 = each
+// kernel's default (~0.1-0.2 s), else that many polls; 0 makes every wait give up at once -- the
+// negative control of the runtime's hand-off check (runtime.health).  Set by dn_set_spin_limit.
+extern int g_dn_spin_limit;
+static inline int dn_spin_limit(int dflt) { return g_dn_spin_limit >= 0 ? g_dn_spin_limit : dflt; }
+
+// Whole CUs left to concurrent kernels when a launch whose workgroups wait on each other is
+// sized: at N > 1 sites RCCL's collective kernels (one workgroup per channel, <= 64 channels) can
+// run beside a step's persistent launch on other streams.
+constexpr int DN_RESERVE_CUS = 64;
+
+// Can `blocks` workgroups of `fn` (threads, dynamic LDS) ALL be resident at once on the CUs left
+// after `reserve_cus`?  The precondition of a persistent launch: a workgroup that never becomes
+// resident would make its peers' spin waits time out.  (Cached per (fn, threads, lds).)
+static inline bool dn_fits_resident(const void* fn, int blocks, int threads, size_t lds,
+                                    int reserve_cus = DN_RESERVE_CUS) {
+  static const void* c_fn = nullptr;
+  static int c_threads = -1, c_per = 0, c_cus = 0;
+  static size_t c_lds = 0;
+  if (fn != c_fn || threads != c_threads || lds != c_lds) {
+    int per = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    c_fn = fn, c_threads = threads, c_lds = lds, c_per = per, c_cus = cus;
+  }
+  return (long)c_per * (c_cus - reserve_cus) >= blocks;
+}

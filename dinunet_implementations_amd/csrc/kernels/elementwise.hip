@@ -157,3 +157,10 @@ DN_API int dn_relu_bwd_colsum(const void* dy, const void* y, void* dym, float* d
                      accumulate);
   return dn_launch_status();
 }
+
+// in-kernel wait limit (common.h): < 0 restores every kernel's default
+int g_dn_spin_limit = -1;
+DN_API int dn_set_spin_limit(int polls) {
+  g_dn_spin_limit = polls < 0 ? -1 : polls;
+  return DN_OK;
+}

@@ -82,6 +82,7 @@ struct StepArgs {
   // tail LDS: logits + dlogits fp32 [SMP][16] each, labels [SMP]
   int t_logit, t_dlogit, t_y;
   int log_out;
+  int spin;                // poll limit of the hand-off waits (dn_spin_limit)
 };
 
 #define YSTAMP(i) do { if (stamps && threadIdx.x == 0) stamps[(i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -102,9 +103,10 @@ __device__ __forceinline__ void arrive(unsigned* sync, int w) {
   __hip_atomic_fetch_add((gu32*)(sync + w), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // ONE lane polls; wrap-safe `>=`; bounded (the error word records which wait gave up)
-__device__ __forceinline__ void poll_ge(unsigned* sync, int w, unsigned target, unsigned code) {
+__device__ __forceinline__ void poll_ge(unsigned* sync, int w, unsigned target, unsigned code,
+                                        int spin) {
   gu32* p = (gu32*)(sync + w);
-  for (int it = 0; it < SPIN_MAX; ++it) {
+  for (int it = 0; it < spin; ++it) {
     const unsigned v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((int)(v - target) >= 0) return;
     __builtin_amdgcn_s_sleep(1);
@@ -400,7 +402,7 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
     prefetch_late();
 
     // ---- wait for dZ1, then dA1 = dZ1 W1[:, cols] and the layer-0 backward -----------------
-    if (lane == 0) poll_ge(sync, Y_DZ1, E1, 1u);
+    if (lane == 0) poll_ge(sync, Y_DZ1, E1, 1u, a.spin);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (st) YSTAMP(3);
@@ -521,7 +523,7 @@ __device__ __forceinline__ void column_wg(const StepArgs& a, int c, const float*
 
   // ---- dX tiles: dX[:, t] = dZ0 W0[:, t] (+ the layer-0 dropout) ---------------------------
   if (dx) {
-    if (tid == 0) poll_ge(sync, Y_DZ0, E1 * (unsigned)a.G0, 2u);
+    if (tid == 0) poll_ge(sync, Y_DZ0, E1 * (unsigned)a.G0, 2u, a.spin);
     lds_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (st) YSTAMP(5);
@@ -690,7 +692,7 @@ __device__ __forceinline__ void tail_wg(const StepArgs& a, const long long* __re
     }
   }
   // ---- A1 from the column workgroups --------------------------------------------------------
-  if (tid == 0) poll_ge(sync, Y_A1, E1 * (unsigned)a.G0, 3u);
+  if (tid == 0) poll_ge(sync, Y_A1, E1 * (unsigned)a.G0, 3u, a.spin);
   lds_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (st) YSTAMP(9);
@@ -1197,6 +1199,10 @@ DN_API int dn_head_step(int nl, const int* dims, const int* flags, const float* 
     g_step_init = true;
   }
   p.a.log_out = log_out;
+  p.a.spin = dn_spin_limit(SPIN_MAX);
+  // the column workgroups and the tail hand data to each other: all must be resident at once
+  if (!dn_fits_resident(reinterpret_cast<const void*>(head_step_kernel), p.a.G0 + 1, SNT, p.lds))
+    return DN_UNSUPPORTED;
   hipLaunchKernelGGL(head_step_kernel, dim3(p.a.G0 + 1), dim3(SNT), p.lds, st, p.a, x, ldx, y,
                      out, loss, pred, rng, dloss, dx, lddx, (char*)ws, (unsigned*)sync,
                      g_step_stamps);

@@ -652,6 +652,7 @@ struct LpArgs {
   float tol;
   unsigned* sync;  // [LP_MAXL][64] (arrivals at 0, done at 32) + error word at [LP_MAXL * 64]
   unsigned long long* stamps;  // diagnostics (null): member 0 of layer l, [l][1 + 8 it + k]
+  int spin;                    // poll limit of a barrier wait (dn_spin_limit)
 };
 #define LP_STAMP(k) do { if (a.stamps && j == 0 && threadIdx.x == 0) \
   a.stamps[l * 64 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -685,19 +686,20 @@ __device__ __forceinline__ void lp_sync() {
 }
 
 // every storing wave drains, one lane arrives and polls, the workgroup follows
-__device__ __forceinline__ void lp_barrier(unsigned* sync, int l, unsigned target, unsigned code) {
+__device__ __forceinline__ void lp_barrier(unsigned* sync, int l, unsigned target, unsigned code,
+                                           int spin) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lp_sync();
   if (threadIdx.x == 0) {
     lp_gu32* c = (lp_gu32*)(sync + l * 64);
     __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int it = 0;
-    for (; it < LP_SPIN; ++it) {
+    for (; it < spin; ++it) {
       const unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((int)(v - target) >= 0) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    if (it == LP_SPIN)
+    if (it >= spin)
       __hip_atomic_store((lp_gu32*)(sync + LP_MAXL * 64), code, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -910,7 +912,7 @@ lr_persist_kernel(LpArgs a) {
                                              (j * 256 + 2 * tid) * 8, 0, 16);
     }
     LP_STAMP(sb + 2);
-    lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x100u + (unsigned)l);
+    lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x100u + (unsigned)l, a.spin);
     LP_STAMP(sb + 3);
     // ---- phase B: Gram, Cholesky, H = G[:, my cols]^T P, Q[my cols], Psend[my rows] ----
     if (tid < 128) {  // member partials in a fixed order, 8 loads in flight per round
@@ -995,7 +997,7 @@ lr_persist_kernel(LpArgs a) {
       lp_st1(rN, 8 * j + 4, (dq[1] + dq[3]) + (dq[5] + dq[7]));
     }
     LP_STAMP(sb + 6);
-    lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x200u + (unsigned)l);
+    lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x200u + (unsigned)l, a.spin);
     LP_STAMP(sb + 7);
     // stop after this commit?  dad_tol: lane b of every wave loads member b's norms (one round
     // trip) and the butterfly sums them the same way in every wave of every member: one decision
@@ -1135,6 +1137,11 @@ DN_API int dn_lr_persist(const void* host_layers, int nl, int iters, float tol, 
     Y.norms = norms + (long)l * LP_MAXJ * 2;
     jmax = Y.J > jmax ? Y.J : jmax;
   }
+  a.spin = dn_spin_limit(LP_SPIN);
+  // members of a layer meet at barriers: every workgroup must be resident at once (else the
+  // staged kernels, DN_UNSUPPORTED)
+  if (!dn_fits_resident(reinterpret_cast<const void*>(lr_persist_kernel), LP_MAXL * jmax, 256, 0))
+    return DN_UNSUPPORTED;
   hipLaunchKernelGGL(lr_persist_kernel, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
   return dn_launch_status();
 }

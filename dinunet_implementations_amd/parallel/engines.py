@@ -332,8 +332,10 @@ class RankDADEngine(Engine):
         # the one-launch power iteration spins on per-layer barriers, so all of a launch's
         # workgroups must be resident together: never when several site processes share one GPU
         # (the gloo rehearsal), whose persistent launches could then hold each other's CUs
-        self._persist_ok = bool(self.fast and not (
-            group.distributed and group.world > max(1, torch.cuda.device_count())))
+        shared = getattr(group, "gpu_shared", None)
+        if shared is None:  # a group built by hand: assume sharing when ranks outnumber GPUs
+            shared = group.distributed and group.world > max(1, torch.cuda.device_count())
+        self._persist_ok = bool(self.fast and not shared)
         if self.fast:
             self._init_fast()
 

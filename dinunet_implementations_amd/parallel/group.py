@@ -26,6 +26,9 @@ class SiteGroup:
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
     pg: Any = None
+    # does another site process use this rank's GPU? (init_sites: all-gathered (host, device);
+    # None = unknown).  Launches whose workgroups wait on each other are only safe when not.
+    gpu_shared: Optional[bool] = None
 
     @property
     def distributed(self) -> bool:
@@ -184,7 +187,22 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
         pg = dist.group.WORLD
     _GROUP = SiteGroup(rank=rank, world=world, local_rank=local, device=dev,
                        backend=be if world > 1 else None, pg=pg)
+    _GROUP.gpu_shared = _gpu_shared(_GROUP)
     return _GROUP
+
+
+def _gpu_shared(g: SiteGroup) -> Optional[bool]:
+    """Whether several ranks of ``g`` drive the same GPU: decided from the actual (host, device)
+    pairs, not from world vs device count -- explicit ``gpus`` lists, a gloo rehearsal with every
+    site on GPU 0, or more ranks than inputspec entries can all stack sites on one card, while a
+    multi-node run has more ranks than local devices without sharing any."""
+    if g.device.type != "cuda":
+        return False
+    if not g.distributed:
+        return False
+    import socket
+    me = (socket.gethostname(), int(g.device.index or 0))
+    return g.all_gather_object(me).count(me) > 1
 
 
 def current() -> SiteGroup:

@@ -40,6 +40,22 @@ def apply_collective_plan(cfg: Dict[str, Any]):
             os.environ.setdefault(env, str(v))
 
 
+def site_gpus(cfg: Dict[str, Any], rank: int, n_specs: int, device=None):
+    """The ``gpus`` pin of this rank's site input, when that input is this rank's own: with more
+    ranks than inputspec entries, rank r reuses ``specs[r % n]`` and its GPU ids name ANOTHER
+    site's GPU, so those ranks take their own GPU (``LOCAL_RANK``) instead.  ``gpus = []`` (the
+    reference's CPU-only FreeSurfer sites, ``datasets/test_fsl/inputspec.json:15-17``) keeps the
+    CPU unless ``--device`` says otherwise, and says so."""
+    gpus = cfg.get("gpus")
+    if rank >= n_specs:
+        return None
+    if gpus is not None and len(list(gpus if not isinstance(gpus, int) else [gpus])) == 0 \
+            and device in (None, "", "auto"):
+        print(f"[local{rank}] site input gpus=[]: this site runs on the CPU "
+              f"(--device cuda overrides)", file=sys.stderr, flush=True)
+    return gpus
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--data-path", required=True)
@@ -58,7 +74,7 @@ def main(argv=None):
     cfg = build_config(site_input=site_in, overrides=parse_sets(a.set))
     apply_collective_plan(cfg)  # before the communicator exists
     grp = init_sites(device=a.device, timeout_s=cfg.get("collective_timeout_s"),
-                     gpus=cfg.get("gpus"))
+                     gpus=site_gpus(cfg, rank, len(specs), a.device))
     base = os.path.join(a.data_path, "input", f"local{grp.rank}", "simulatorRun")
     if not os.path.isdir(base):
         base = os.path.join(a.data_path, "input", f"local{grp.rank % len(specs)}", "simulatorRun")

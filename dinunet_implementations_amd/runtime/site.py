@@ -38,19 +38,78 @@ from ..parallel import SiteGroup, make_engine
 from ..utils import logs as L
 from ..utils.metrics import Averages, Metrics, improved, metric_value
 from ..ops import FusedAdam
+from . import health
 from .feed import DeviceFeed
 from .step import TrainStep
 from .trainer import NNTrainer, set_seed
 
 
 def _fault_step(rank: int) -> Optional[int]:
-    """``DINUNET_FAULT=<rank>:<step>``: that rank kills itself (SIGKILL, no cleanup) before its
-    <step>-th training step -- the dead-site case the failure-path test exercises."""
+    """``DINUNET_FAULT=<rank>:<step>[:raise]``: that rank kills itself (SIGKILL, no cleanup) --
+    or, with ``:raise``, raises -- before its <step>-th training step: the dead-site and the
+    failing-site cases the failure-path tests exercise."""
     spec = os.environ.get("DINUNET_FAULT", "")
     if not spec:
         return None
     r, _, s = spec.partition(":")
-    return int(s or 0) if int(r) == rank else None
+    return int(s.partition(":")[0] or 0) if int(r) == rank else None
+
+
+def _fault():
+    if os.environ.get("DINUNET_FAULT", "").endswith(":raise"):
+        raise RuntimeError("DINUNET_FAULT: injected site failure")
+    os.kill(os.getpid(), signal.SIGKILL)
+
+
+class _PretrainSignal:
+    """The pretraining site's side of :meth:`FederatedSite._await_pretrain`: a heartbeat counter
+    in the process group's store advanced every ``pretrain_heartbeat_s`` by a daemon thread while
+    it pretrains, then the done key set to "1", or to "fail: <error>" when pretraining raises
+    (the error still propagates)."""
+
+    def __init__(self, group: SiteGroup, tag: str, cfg: Dict[str, Any]):
+        self.store = None
+        if group.distributed and group.pg is not None:
+            import torch.distributed as dist
+            self.store = dist.distributed_c10d._get_default_store()
+        self.key, self.hb = self.keys(tag)
+        self.every = self.period(cfg)
+        self._stop = None
+
+    @staticmethod
+    def keys(tag: str):
+        base = "dinunet/pretrain_done/" + os.path.basename(os.path.normpath(tag))
+        return base, base + "/heartbeat"
+
+    @staticmethod
+    def period(cfg: Dict[str, Any]) -> float:
+        return float(cfg.get("pretrain_heartbeat_s") or
+                     min(30.0, max(0.5, float(cfg.get("collective_timeout_s") or 1800) / 4)))
+
+    def done(self, value: str):
+        if self.store is not None:
+            self.store.set(self.key, value)
+
+    def __enter__(self):
+        if self.store is not None:
+            import threading
+            self._stop = threading.Event()
+
+            def beat():
+                while not self._stop.wait(self.every):
+                    try:
+                        self.store.add(self.hb, 1)
+                    except Exception:
+                        return
+            self.store.add(self.hb, 1)
+            threading.Thread(target=beat, daemon=True, name="pretrain-heartbeat").start()
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if self._stop is not None:
+            self._stop.set()
+        self.done("1" if et is None else f"fail: {et.__name__}: {ev}"[:500])
+        return False
 
 
 class FederatedSite:
@@ -165,7 +224,7 @@ class FederatedSite:
                 step = TrainStep(trainer.modules(), trainer.flat, trainer.optimizer, engine,
                                  use_graph=use_graph, accum=li,
                                  forward_loss=lambda m, x, y: trainer.forward_loss(x, y))
-        fault_at = _fault_step(group.rank)
+        fault_at = _fault_step(self.group.rank)
         feed = self._device_feed(trainer, step, engine, tr, bs, li, steps, cfg, fault_at)
         if resume and resume.get("loader"):
             it = tr.resume_iter(resume["loader"], indices=feed is not None)
@@ -206,7 +265,7 @@ class FederatedSite:
                 if fault_at is not None:  # failure-path tests (DINUNET_FAULT=<rank>:<step>)
                     fault_at -= 1
                     if fault_at < 0:
-                        os.kill(os.getpid(), signal.SIGKILL)
+                        _fault()
                 if step is not None:
                     for k in range(li):
                         try:
@@ -268,6 +327,9 @@ class FederatedSite:
                         stop = True
                 self.log(f"{tag}epoch {epoch} train_loss {avg.average:.4f} val_loss {r['loss']:.4f} "
                          f"val_{monitor} {score:.4f} best@{best['epoch']}")
+                # a persistent kernel whose in-kernel wait timed out used incomplete data:
+                # fail the run instead of training on it (runtime.health)
+                health.check(trainer.nn.values(), engine, f"in epoch {epoch}")
                 if cfg.get("check_replicas") and group.distributed and engine.name != "dSGD-local":
                     ok = self._replica_checksum(trainer)
                     logs.setdefault("replica_check", []).append(bool(ok))
@@ -288,6 +350,7 @@ class FederatedSite:
             trainer.save_checkpoint(os.path.join(fold_dir, f"{tag}checkpoint_best.pt"),
                                     epoch=epochs, best_val_epoch=epochs, best_val_score=None)
             best["epoch"] = epochs
+        health.check(trainer.nn.values(), engine, "in training")
         logs[f"{tag}best_val_epoch"] = best["epoch"]
         logs[f"{tag}best_val_score"] = best["score"]
         if step is not None and step.timers.summary():
@@ -316,21 +379,25 @@ class FederatedSite:
         logs["pretrain_site"] = f"local{src}"
         pa = dict(self.cfg.get("pretrain_args") or {})
         if self.group.rank == src and int(pa.get("epochs", 0)) > 0:
-            delay = float(os.environ.get("DINUNET_PRETRAIN_DELAY_S", "0") or 0)
-            if delay > 0:  # tests: a pretraining phase longer than the collective timeout
-                time.sleep(delay)
-            pcfg = copy.deepcopy(self.cfg)
-            pcfg.update(pa)
-            from ..parallel import DSGDEngine
-            from ..parallel.group import SiteGroup as _SG
-            solo = _SG(device=self.device)
-            trainer.optimizer.lr = float(pa.get("learning_rate", trainer.optimizer.lr))
-            eng = DSGDEngine(trainer.modules(), trainer.flat, solo, pcfg, overlap=False)
-            eng.name = "dSGD-local"
-            self.log(f"pretraining alone on {sizes[src]} samples for {pa.get('epochs')} epochs")
-            b = self._train_epochs(trainer, eng, data, pcfg, solo, fold_dir, seed, logs, tag="pretrain_")
-            trainer.load_checkpoint(os.path.join(fold_dir, "pretrain_checkpoint_best.pt"))
-            logs["pretrain_best_val_epoch"] = b["epoch"]
+            with _PretrainSignal(self.group, fold_dir, self.cfg):
+                delay = float(os.environ.get("DINUNET_PRETRAIN_DELAY_S", "0") or 0)
+                if delay > 0:  # tests: a pretraining phase longer than the collective timeout
+                    time.sleep(delay)
+                pcfg = copy.deepcopy(self.cfg)
+                pcfg.update(pa)
+                from ..parallel import DSGDEngine
+                from ..parallel.group import SiteGroup as _SG
+                solo = _SG(device=self.device)
+                trainer.optimizer.lr = float(pa.get("learning_rate", trainer.optimizer.lr))
+                eng = DSGDEngine(trainer.modules(), trainer.flat, solo, pcfg, overlap=False)
+                eng.name = "dSGD-local"
+                self.log(f"pretraining alone on {sizes[src]} samples for {pa.get('epochs')} epochs")
+                b = self._train_epochs(trainer, eng, data, pcfg, solo, fold_dir, seed, logs,
+                                       tag="pretrain_")
+                trainer.load_checkpoint(os.path.join(fold_dir, "pretrain_checkpoint_best.pt"))
+                logs["pretrain_best_val_epoch"] = b["epoch"]
+        elif self.group.rank == src:
+            _PretrainSignal(self.group, fold_dir, self.cfg).done("1")
         self._await_pretrain(src, fold_dir)
         self._broadcast_model(trainer, src)
         # fresh optimizer state for the federated phase
@@ -340,23 +407,41 @@ class FederatedSite:
         """The other sites wait for the pretraining site OUTSIDE the collectives: a wait inside
         the weight broadcast would be bounded by ``collective_timeout_s`` (the failure detector's
         clock), so a long pretraining phase would make every idle site time out.  They block on a
-        key the pretraining site sets in the process group's store, bounded by its own deadline
-        (``pretrain_timeout_s``); a dead pretraining site ends the wait with an error too (its
-        store connection drops, or the deadline passes)."""
+        key the pretraining site sets in the process group's store when it is done ("1") or has
+        failed ("fail: ..."), bounded by their own deadline (``pretrain_timeout_s``), and they
+        watch its heartbeat counter: no beat for ``collective_timeout_s`` means the pretraining
+        site is gone (killed, hung), and the wait raises instead of lasting the whole deadline."""
         g = self.group
-        if not g.distributed or g.pg is None:
+        if not g.distributed or g.pg is None or g.rank == src:
             return
         if os.environ.get("DINUNET_PRETRAIN_STORE_WAIT", "1") == "0":
             return  # negative control of tests/test_failure.py: wait inside the broadcast
         import datetime
         import torch.distributed as dist
         store = dist.distributed_c10d._get_default_store()
-        key = "dinunet/pretrain_done/" + os.path.basename(os.path.normpath(tag))
-        if g.rank == src:
-            store.set(key, "1")
-        else:
-            timeout = float(self.cfg.get("pretrain_timeout_s") or 7 * 86400)
-            store.wait([key], datetime.timedelta(seconds=timeout))
+        key, hb = _PretrainSignal.keys(tag)
+        deadline = time.time() + float(self.cfg.get("pretrain_timeout_s") or 7 * 86400)
+        silence = float(self.cfg.get("collective_timeout_s") or 1800)
+        beat, t_beat = store.add(hb, 0), time.time()
+        while True:
+            slice_s = max(0.05, min(_PretrainSignal.period(self.cfg), deadline - time.time()))
+            try:
+                store.wait([key], datetime.timedelta(seconds=slice_s))
+                break
+            except Exception:  # (the store's wait timeout) -- check the heartbeat
+                now = time.time()
+                b = store.add(hb, 0)
+                if b != beat:
+                    beat, t_beat = b, now
+                elif now - t_beat > silence:
+                    raise RuntimeError(f"pretraining site local{src} stopped signalling for "
+                                       f"{now - t_beat:.0f} s (collective_timeout_s {silence:g})")
+                if now >= deadline:
+                    raise RuntimeError(f"pretraining site local{src} did not finish within "
+                                       f"pretrain_timeout_s")
+        v = store.get(key).decode(errors="replace")
+        if v != "1":
+            raise RuntimeError(f"pretraining site local{src} failed: {v}")
 
     # ---- folds ------------------------------------------------------------------------------
     def run_fold(self, fold: int, split: Dict[str, List[Any]]) -> Dict[str, Any]:

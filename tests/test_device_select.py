@@ -48,3 +48,20 @@ def test_site_runner_and_local_node_resolve_from_config():
     from dinunet_implementations_amd.compat.nodes import LocalNode
     node = LocalNode()
     assert node.device == torch.device("cpu")  # resolved from the input at setup
+
+
+def test_ranks_beyond_the_inputspec_take_their_own_gpu():
+    """run.py gives rank r the input specs[r % n]: the reference icalstm spec pins site 0 to GPU 0
+    and site 1 to GPU 1, so under RCCL with 4 ranks ranks 2 and 3 must NOT inherit those pins
+    (they would conflict with LOCAL_RANK and raise): they take GPU LOCAL_RANK."""
+    from dinunet_implementations_amd.run import site_gpus
+    specs = [{"gpus": [0]}, {"gpus": [1]}]
+    devs = []
+    for rank in range(4):
+        g = site_gpus(specs[rank % 2], rank, len(specs))
+        devs.append(resolve_device(g, local_rank=rank, world=4, backend="nccl", n_devices=8))
+    assert devs == [torch.device("cuda", r) for r in range(4)]
+    # the spec's own ranks keep their pin, CPU-only sites keep the CPU
+    assert site_gpus({"gpus": [1]}, 1, 2) == [1]
+    assert site_gpus({"gpus": []}, 0, 2) == []
+    assert resolve_device(site_gpus({"gpus": []}, 0, 2), n_devices=8) == torch.device("cpu")

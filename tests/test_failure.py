@@ -74,3 +74,42 @@ def test_pretrain_longer_than_collective_timeout(fs_data_root, tmp_path, store_w
         return
     for r, p in enumerate(procs):
         assert p.returncode == 0, (r, p.returncode, outs[r][1][-3000:])
+
+
+@pytest.mark.parametrize("how", ["kill", "raise"])
+def test_pretraining_site_failure_ends_the_wait(tmp_path, how):
+    """The pretraining site is rank 1 (the larger site), NOT the store host: when it is killed
+    mid-pretraining its heartbeat stops and the waiting site raises after collective_timeout_s of
+    silence; when pretraining raises, it publishes the failure and the waiter raises at once.
+    Either way the waiter exits non-zero long before pretrain_timeout_s (7 days)."""
+    from dinunet_implementations_amd.data.synthetic import make_fs_sites
+    root = make_fs_sites(str(tmp_path / "fs"), sites=2, subjects=(24, 48), seed=1)
+    port = free_port()
+    procs = []
+    fault = "1:3" + (":raise" if how == "raise" else "")
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT,
+                   OMP_NUM_THREADS="1", DINUNET_FAULT=fault)
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "dinunet_implementations_amd.run", "--data-path", root,
+             "--out", str(tmp_path / "out"), "--device", "cpu", "--set", "epochs=2",
+             "--set", "pretrain=true", "--set", 'pretrain_args={"epochs": 50}',
+             "--set", "collective_timeout_s=4", "--set", "pretrain_heartbeat_s=0.5"],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    t0 = time.time()
+    try:
+        outs = [p.communicate(timeout=120) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.time() - t0
+    if how == "kill":
+        assert procs[1].returncode == -signal.SIGKILL, (procs[1].returncode, outs[1][1][-2000:])
+        assert "stopped signalling" in outs[0][1], outs[0][1][-3000:]
+    else:
+        assert procs[1].returncode == 3, (procs[1].returncode, outs[1][1][-2000:])
+        assert "injected site failure" in outs[0][1], outs[0][1][-3000:]
+    assert procs[0].returncode == 3, (procs[0].returncode, outs[0][1][-3000:])
+    assert elapsed < 90

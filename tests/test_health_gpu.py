@@ -1,0 +1,61 @@
+"""Negative controls of the persistent-kernel hand-off check (runtime.health) on the GPU: with the
+in-kernel poll limit forced to 0 every hand-off wait of the one-launch head and every barrier of
+the one-launch rank-dAD iteration gives up at once; the check must then raise -- on the kernels
+directly and through the production site loop -- and stay quiet with the default limit."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def spin_zero():
+    from dinunet_implementations_amd.runtime import health
+    health.set_spin_limit(0)
+    yield health
+    health.set_spin_limit(-1)
+
+
+def _step(engine="dSGD"):
+    from test_step_gpu import _trainer
+    m, flat, st = _trainer(0, engine=engine, use_graph=False, hidden=128)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(32, 12, 20, 10, device="cuda", generator=g)
+    y = torch.randint(0, 2, (32,), device="cuda", generator=g)
+    return m, st, x, y
+
+
+def test_head_step_timeout_raises(spin_zero):
+    health = spin_zero
+    m, st, x, y = _step()
+    st(x, y)
+    torch.cuda.synchronize()
+    assert m._head is not None and m._head._sync is not None, "one-launch head did not run"
+    with pytest.raises(health.HandoffError, match="head_step"):
+        health.check([m], st.engine)
+    health.set_spin_limit(-1)
+    st(x, y)
+    torch.cuda.synchronize()
+    health.check([m], st.engine)  # default limit: no timeout
+
+
+def test_rankdad_barrier_timeout_raises(spin_zero):
+    health = spin_zero
+    m, st, x, y = _step("rankDAD")
+    eng = st.engine
+    assert eng.fast and eng._persist_ok
+    st(x, y)
+    torch.cuda.synchronize()
+    with pytest.raises(health.HandoffError, match="lr_persist"):
+        health.check([m], eng)
+    health.set_spin_limit(-1)
+    st(x, y)
+    torch.cuda.synchronize()
+    health.check([m], eng)
+
+
+def test_site_loop_fails_on_timed_out_handoff(tmp_path, spin_zero):
+    from test_runtime_gpu import _ica_root, _run_site
+    root = _ica_root(tmp_path)
+    with pytest.raises(spin_zero.HandoffError):
+        _run_site(root, str(tmp_path / "out"), {"epochs": 2, "batch_size": 8})
