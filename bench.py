@@ -212,6 +212,9 @@ def main():
             tta = site_loop(grp, args)
         except Exception as e:  # never lose the throughput line to the study
             tta = {"time_to_auc_s": None, "site_loop_error": f"{type(e).__name__}: {e}"}
+    else:
+        tta = {"time_to_auc_s": None,
+               "site_loop": "not run (default at N > 1; --site-loop 1 runs it on every site)"}
     if grp.is_master:
         rec = {
             # the headline metric names dSGD; other engines report the same quantity under

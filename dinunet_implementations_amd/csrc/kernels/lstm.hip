@@ -491,15 +491,28 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
 // (pre = x W_ih^T + h_{t-1} W_hh^T + b) instead of being stored per step by the forward kernel.
 // MFMA output: lane (q, n) holds dh for units u0 + j (u0 = 16w + 4q, j = 0..3) of column n; as in
 // the forward, the BR valid columns are redistributed: lane (q, r, b) owns units u0 + r + s*(16/BR).
-template <int HD, int BR, bool DSEQ, int UG>
-__global__ void __launch_bounds__(HD / (16 * UG) * 64)
-lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time order
-                const float* __restrict__ c_save,  // [ndir][Bp][S][HD]
-                const bf16* __restrict__ whhT,     // [ndir][HD][4*HD]
-                const float* __restrict__ dh_ext, long dh_sb, long dh_st, float dh_scale,
-                const float* __restrict__ dhT, const float* __restrict__ dcT,  // optional [B][ndir*Hd]
-                int B, int S, int Hd, int ndir,
-                bf16* __restrict__ dpre) {          // [Bp*S][ndir][4*HD] permuted, original time
+// Chunk publication of the overlapped backward (lstm_bwd_ov_kernel): after every `tc` steps a
+// recurrence workgroup makes its dpre stores of those steps visible (write-through stores, every
+// wave drained, a workgroup barrier) and ONE lane adds 1 to the block's ready counter
+// (one 128-B line per counter: ready + 32 * (dir * OV_MAXBLK + k)).
+constexpr int OV_MAXBLK = 64;
+struct BwdPub {
+  unsigned* ready;
+  int tc;
+};
+typedef __attribute__((address_space(1))) unsigned ov_gu32;
+typedef __attribute__((ext_vector_type(2))) unsigned ov_u32x2;
+
+template <int HD, int BR, bool DSEQ, int UG, bool PUB>
+__device__ __forceinline__ void
+bwd_recur(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time order
+          const float* __restrict__ c_save,  // [ndir][Bp][S][HD]
+          const bf16* __restrict__ whhT,     // [ndir][HD][4*HD]
+          const float* __restrict__ dh_ext, long dh_sb, long dh_st, float dh_scale,
+          const float* __restrict__ dhT, const float* __restrict__ dcT,  // optional [B][ndir*Hd]
+          int B, int S, int Hd, int ndir,
+          bf16* __restrict__ dpre,            // [Bp*S][ndir][4*HD] permuted, original time
+          const int bx, const int dir, const int gx, const BwdPub pub) {
   constexpr int KS = 4 * HD / 32;
   constexpr int LDD = 4 * HD + 32;  // 16 dwords mod 64 banks: see LDH in the forward
   constexpr bool STREAM = HD > 192;  // W_hh^T streamed from L2 every step (see the forward)
@@ -512,9 +525,8 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane >> 4, n = lane & 15, r = n / BR, bl = n % BR;
-  const int dir = blockIdx.y;
-  const int Bp = gridDim.x * BR;
-  const int b = blockIdx.x * BR + bl;
+  const int Bp = gx * BR;
+  const int b = bx * BR + bl;
   const bool vb = b < B;
   const int bc = vb ? b : B - 1;
   const long rowX = (long)ndir * 4 * HD;
@@ -559,6 +571,11 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   const float* prow = pre + (long)bc * S * rowX + (long)dir * 4 * HD;
   const float* crow = c_save + (long)dir * Bp * S * HD + (long)b * S * HD;
   bf16* drow = dpre + (long)b * S * rowX + (long)dir * 4 * HD;
+  // PUB: write-through (sc1) dpre stores through a descriptor based at this workgroup's first
+  // row (the overlapped weight-gradient workgroups read them during this launch)
+  const __amdgpu_buffer_rsrc_t d_rs =
+      dn_rsrc(dpre + (long)bx * BR * S * rowX, PUB ? (uint32_t)(BR * S * rowX * 2) : 0u);
+  const uint32_t d_off = (uint32_t)((bl * S * rowX + dir * 4 * HD) * 2);
   const float* dhrow = dh_ext + (long)bc * dh_sb + dir * Hd;
   const int tauL = dir == 0 ? S - 1 : 0;
   const int tp0 = S >= 2 ? S - 2 : 0;
@@ -738,12 +755,28 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
       e[2] = (bf16)(m * d_o * go[s] * (1.f - go[s]) * so[s] * (1.f - so[s]));
       e[3] = (bf16)(m * d_g * (1.f - gg[s] * gg[s]));
       *reinterpret_cast<bf16x4*>(&dbuf[nxt][bl][4 * uu[s]]) = e;
-      *reinterpret_cast<bf16x4*>(drow + (long)tau * rowX + 4 * uu[s]) = e;
+      if constexpr (PUB)
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(ov_u32x2, e), d_rs,
+            (int)(d_off + (uint32_t)((tau * rowX + 4 * uu[s]) * 2)), 0, 16);
+      else
+        *reinterpret_cast<bf16x4*>(drow + (long)tau * rowX + 4 * uu[s]) = e;
     }
 #ifdef DN_STAMPS
     STAMP(ts2);
 #endif
-    __syncthreads();
+    if constexpr (PUB) {
+      // every `tc` steps (and after the last): this block of time steps is published
+      const int done = S - t;
+      const bool pub_now = done % pub.tc == 0 || t == 0;
+      if (pub_now) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (pub_now && tid == 0)
+        __hip_atomic_fetch_add((ov_gu32*)(pub.ready + 32 * (dir * OV_MAXBLK + (done - 1) / pub.tc)),
+                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __syncthreads();
+    }
 #ifdef DN_STAMPS
     STAMP(ts3);
     st_a += ts1 - ts0; st_b += ts2 - ts1; st_c += ts3 - ts2;
@@ -757,11 +790,242 @@ lstm_bwd_kernel(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original
   }
   if (t >= 0) step(t, ca, cb);
 #ifdef DN_STAMPS
-  if (lane == 0 && blockIdx.x == 0) {
-    unsigned long long* o = dn_stamp_buf + (256 + blockIdx.y * 64 + w) * 4;
+  if (lane == 0 && bx == 0) {
+    unsigned long long* o = dn_stamp_buf + (256 + dir * 64 + w) * 4;
     o[0] = st_a; o[1] = st_b; o[2] = st_c; o[3] = S;
   }
 #endif
+}
+
+template <int HD, int BR, bool DSEQ, int UG>
+__global__ void __launch_bounds__(HD / (16 * UG) * 64)
+lstm_bwd_kernel(const float* __restrict__ pre, const float* __restrict__ c_save,
+                const bf16* __restrict__ whhT, const float* __restrict__ dh_ext, long dh_sb,
+                long dh_st, float dh_scale, const float* __restrict__ dhT,
+                const float* __restrict__ dcT, int B, int S, int Hd, int ndir,
+                bf16* __restrict__ dpre) {
+  bwd_recur<HD, BR, DSEQ, UG, false>(pre, c_save, whhT, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT,
+                                     B, S, Hd, ndir, dpre, (int)blockIdx.x, (int)blockIdx.y,
+                                     (int)gridDim.x, BwdPub{nullptr, 1});
+}
+
+// ---------------------------------------------------------------------------------------------
+// Overlapped backward: the LSTM weight / bias gradients accumulate WHILE the
+// reverse-time recurrence runs, on the CUs the recurrence leaves idle (it holds 2 * ceil(B/BR)
+// of 256).  One launch, two roles:
+//   * recurrence workgroups (the first 2 * ceil(B/BR)): bwd_recur<..., PUB = true>; every `tc`
+//     steps they publish that block of dpre rows (write-through stores, drained, one agent-scope
+//     add per workgroup on the block's ready counter);
+//   * weight-gradient workgroups: three 64 x 64 output tiles each (one per 4-wave quarter... a
+//     third: waves 4j .. 4j+3), all of one direction, of dW_ih = dpre^T x and dW_hh = dpre^T
+//     h_{t-1} (gate rows m = 4u + g; the tiles with the first input columns also form the bias
+//     column sums).  They take the direction's blocks in the order the recurrence publishes them
+//     (fwd: last times first; rev: first times first), each block as 64-row stages through
+//     k-major LDS images (rows = batch rows, read back by the hardware transpose), and keep the
+//     sums in registers: one fixed summation order, no atomics, no split-K slabs, no reduce launch.
+//     At the end they ADD their tiles into the reference-layout .grad buffers.
+// The weight-gradient workgroups wait only on the recurrence, which never waits on them, and the
+// launcher checks that the whole grid is resident at once: no dependency cycle, no unscheduled
+// producer.  A wait that gives up (bounded polls) sets the error word (runtime.health).  The last
+// workgroup to finish zeroes the counters for the next launch.
+constexpr int OV_C = 64 + 16;            // k-major image row length (elements)
+constexpr int OV_IMG = 64 * OV_C;        // one 64-row stage of one operand
+constexpr int OV_W_READY = 32 * 4;       // word offsets in the sync block
+constexpr int OV_W_DONE = 0, OV_W_ERR = 32;
+constexpr int OV_SYNC_WORDS = OV_W_READY + 32 * 2 * OV_MAXBLK;
+constexpr int OV_SPIN = 1 << 22;
+
+typedef short ov_s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) ov_s16x4 ov_lds_s16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned ov_u32x4;
+
+struct OvJob {
+  const bf16* x;      // [B*S][I] LSTM input (bf16)
+  const bf16* hprev;  // [ndir][Bp][S][HD] h_{t-1}
+  float* gwih[2];     // .grad of W_ih / W_hh / b_ih / b_hh per direction (reference layout)
+  float* gwhh[2];
+  float* gbih[2];
+  float* gbhh[2];
+  unsigned* sync;
+  int I, tc, nblk, nbc, ntile, wpd, spin;
+};
+
+// 16x32 MFMA operand fragment from a k-major image [64 k][OV_C] (operand rows = image columns
+// r0 .. r0+15, k = 32 ks ..): two hardware-transposed reads (ds_read_b64_tr_b16).  k-row k is
+// stored at image row k ^ 4 * ((k >> 3) & 1) so each 32-lane half reads rows 8 apart mod 8
+// (distinct banks; the layout of gemm.hip's register-staged images).
+__device__ __forceinline__ bf16x8 ov_frag(const bf16* img, int r0, int ks, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int kb = 32 * ks + 8 * g + q;
+  const int h0 = (g & 1) ? 4 : 0;
+  const bf16* a0 = img + (kb + h0) * OV_C + r0 + 4 * p;
+  const bf16* a1 = img + (kb + (4 - h0)) * OV_C + r0 + 4 * p;
+  const ov_s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ov_lds_s16x4*)(a0));
+  const ov_s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ov_lds_s16x4*)(a1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// original times of block k of direction d: the forward direction's backward runs t = S-1 .. 0,
+// the reverse direction's runs its input times 0 .. S-1
+__device__ __forceinline__ void ov_block(int d, int k, int S, int tc, int& t0, int& nt) {
+  const int lo = k * tc, hi = min(S, lo + tc);
+  nt = hi - lo;
+  t0 = d == 0 ? S - hi : lo;
+}
+
+template <int HD>
+__device__ void bwd_wgrad_role(const OvJob& J, const bf16* __restrict__ dpre, int B, int S,
+                               int Hd, int ndir, int Bp, int wgi) {
+  __shared__ __attribute__((aligned(16))) bf16 img[3][2][OV_IMG];
+  constexpr int GP = 4 * HD;
+  const int tid = threadIdx.x, sub = tid >> 8, st = tid & 255, lane = st & 63, wv = st >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int d = wgi / J.wpd;
+  const int tile0 = (wgi % J.wpd) * 3 + sub;
+  const bool live = tile0 < J.ntile;
+  const int tile = live ? tile0 : 0;  // an idle third runs tile 0's loop (same barriers), stores nothing
+  const int NI = (J.I + 63) / 64, NH = HD / 64;
+  const int MT = GP / 64;
+  const bool ih = tile < MT * NI;
+  const int mt = ih ? tile / NI : (tile - MT * NI) / NH;
+  const int nt = ih ? tile % NI : (tile - MT * NI) % NH;
+  const int m0 = 64 * mt, n0 = 64 * nt;
+  const int N = ih ? J.I : HD;
+  const bool bias = ih && nt == 0;
+  bf16* As = img[sub][0];
+  bf16* Bs = img[sub][1];
+  const long rowX = (long)ndir * GP;
+  const __amdgpu_buffer_rsrc_t a_rs = dn_rsrc(dpre, (uint32_t)min((long)Bp * S * rowX * 2, 0x7fffffffL));
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  // this thread's two 16-B chunks of each 64-row stage: rows ir, ir + 32, columns ic .. ic+7
+  const int ir = st >> 3, ic = (st & 7) * 8;
+  bf16x8 ra[2], rb[2];
+  bool ok[2];
+  auto load = [&](int t0, int ntt, int s) {  // stage s of the block starting at time t0
+    const int rows = B * ntt;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int i = 64 * s + ir + 32 * c;
+      ok[c] = i < rows;
+      const int ic_ = ok[c] ? i : 0;
+      const int tt = ic_ / B, b = ic_ - tt * B, t = t0 + tt;
+      const uint32_t ao = (uint32_t)((((long)b * S + t) * rowX + (long)d * GP + m0 + ic) * 2);
+      ra[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(a_rs, (int)ao, 0, 16));
+      const bool okb = n0 + ic < N;
+      const bf16* bp = ih ? J.x + ((long)b * S + t) * J.I + (okb ? n0 + ic : 0)
+                          : J.hprev + (((long)d * Bp + b) * S + t) * HD + n0 + ic;
+      rb[c] = *reinterpret_cast<const bf16x8*>(bp);
+      if (!okb) ok[c] = false;  // (B only: a zero A row already zeroes the product)
+      if (!(i < rows)) { ra[c] = bf16x8{}; }
+      if (!ok[c]) rb[c] = bf16x8{};
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int k = ir + 32 * c;
+      const int r = k ^ ((k >> 1) & 4);
+      *reinterpret_cast<bf16x8*>(As + r * OV_C + ic) = ra[c];
+      *reinterpret_cast<bf16x8*>(Bs + r * OV_C + ic) = rb[c];
+    }
+  };
+  for (int k = 0; k < J.nblk; ++k) {
+    int t0, ntt;
+    ov_block(d, k, S, J.tc, t0, ntt);
+    if (tid == 0) {  // ONE lane polls the block's ready counter (sc1), the workgroup follows
+      ov_gu32* c = (ov_gu32*)(J.sync + OV_W_READY + 32 * (d * OV_MAXBLK + k));
+      int it = 0;
+      for (; it < J.spin; ++it) {
+        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)J.nbc) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (it >= J.spin)
+        __hip_atomic_store((ov_gu32*)(J.sync + OV_W_ERR), 0x300u + (unsigned)k, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int nst = (B * ntt + 63) / 64;
+    load(t0, ntt, 0);
+    for (int s = 0; s < nst; ++s) {
+      store();
+      __syncthreads();
+      if (s + 1 < nst) load(t0, ntt, s + 1);  // lands under this stage's MFMAs
+      if (bias && st < 64) {
+#pragma unroll 8
+        for (int r = 0; r < 64; ++r) bsum += (float)As[r * OV_C + st];
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = ov_frag(As, wm * 32 + 16 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr[j] = ov_frag(Bs, wn * 32 + 16 * j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      }
+      __syncthreads();
+    }
+  }
+  if (!live) return;
+  // epilogue: gate row m = 4u + g -> reference row g * Hd + u; added to .grad
+  float* out = ih ? J.gwih[d] : J.gwhh[d];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 32 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + 16 * i + 4 * (lane >> 4) + r;
+        const int u = m >> 2, g = m & 3;
+        if (u < Hd && col < (ih ? N : Hd)) out[(long)(g * Hd + u) * (ih ? N : Hd) + col] += acc[i][j][r];
+      }
+    }
+  if (bias && st < 64) {
+    const int m = m0 + st, u = m >> 2, g = m & 3;
+    if (u < Hd) {
+      if (J.gbih[d]) J.gbih[d][g * Hd + u] += bsum;
+      if (J.gbhh[d]) J.gbhh[d][g * Hd + u] += bsum;
+    }
+  }
+}
+
+template <int HD, int BR>
+__global__ void __launch_bounds__(HD / 16 * 64)
+lstm_bwd_ov_kernel(const float* __restrict__ pre, const float* __restrict__ c_save,
+                   const bf16* __restrict__ whhT, const float* __restrict__ dh_ext, long dh_sb,
+                   float dh_scale, const float* __restrict__ dhT, const float* __restrict__ dcT,
+                   int B, int S, int Hd, int ndir, bf16* __restrict__ dpre, OvJob J) {
+  static_assert(HD / 16 * 64 == 768, "three 256-thread weight-gradient tiles per workgroup");
+  const int nrec = ndir * J.nbc;
+  const int wg = blockIdx.x;
+  if (wg < nrec) {
+    bwd_recur<HD, BR, false, 1, true>(pre, c_save, whhT, dh_ext, dh_sb, 0, dh_scale, dhT, dcT, B,
+                                      S, Hd, ndir, dpre, wg % J.nbc, wg / J.nbc, J.nbc,
+                                      BwdPub{J.sync + OV_W_READY, J.tc});
+  } else {
+    bwd_wgrad_role<HD>(J, dpre, B, S, Hd, ndir, J.nbc * BR, wg - nrec);
+  }
+  // the last workgroup to finish resets the counters for the next launch (nobody polls anymore)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ov_gu32* done = (ov_gu32*)(J.sync + OV_W_DONE);
+    const unsigned old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == gridDim.x) {
+      for (int i = 0; i < ndir * J.nblk; ++i)
+        __hip_atomic_store((ov_gu32*)(J.sync + OV_W_READY + 32 * ((i / J.nblk) * OV_MAXBLK + i % J.nblk)),
+                           0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1086,6 +1350,52 @@ DN_API int dn_lstm_pack_gather(const float* wih0, const float* bih0, const float
                           bias_p, whh_p, whhT_p, ncast, cast_src, cast_dst, cast_n, sp, st);
 }
 
+
+// The overlapped backward (lstm_bwd_ov_kernel): recurrence + the LSTM weight / bias gradients in
+// ONE launch.  Taken for the resident-weight geometry it is built for (HD = 192, 4 rows per
+// workgroup, temporal-mean output) and batches whose operand offsets fit 32 bits; DN_UNSUPPORTED
+// otherwise (the caller then runs dn_lstm_bwd + the grouped weight-gradient GEMM).
+// grads: [8] = W_ih, W_hh, b_ih, b_hh .grad (fp32, reference layout) of direction 0 then 1.
+// sync: dn_lstm_ov_sync_bytes() bytes, zeroed once before the first launch.
+DN_API long dn_lstm_ov_sync_bytes() { return 4L * OV_SYNC_WORDS; }
+DN_API long dn_lstm_ov_err_word() { return OV_W_ERR; }
+DN_API int dn_lstm_bwd_ov(const float* pre, const float* c_save, const void* whhT_p,
+                          const float* dh_ext, long dh_sb, float dh_scale, const float* dhT,
+                          const float* dcT, int B, int S, int Hd, int ndir, void* dpre,
+                          const void* x, int I, const void* hprev, float* const* grads,
+                          void* sync, hipStream_t st) {
+  const int HD = dn_lstm_padded_hidden(Hd);
+  if (HD != 192 || B <= 0 || S <= 0 || ndir < 1 || ndir > 2 || I <= 0 || I % 8 || !sync ||
+      !grads)
+    return DN_UNSUPPORTED;
+  const int BR = pick_br(B, HD);
+  if (BR != 4 || (long)B * S * ndir * 4 * HD * 2 >= (1L << 31)) return DN_UNSUPPORTED;
+  OvJob J{};
+  J.x = (const bf16*)x;
+  J.hprev = (const bf16*)hprev;
+  for (int d = 0; d < 2; ++d) {
+    J.gwih[d] = d < ndir ? grads[4 * d + 0] : nullptr;
+    J.gwhh[d] = d < ndir ? grads[4 * d + 1] : nullptr;
+    J.gbih[d] = d < ndir ? grads[4 * d + 2] : nullptr;
+    J.gbhh[d] = d < ndir ? grads[4 * d + 3] : nullptr;
+    if (d < ndir && (!J.gwih[d] || !J.gwhh[d])) return DN_BAD_SHAPE;
+  }
+  J.sync = (unsigned*)sync;
+  J.I = I;
+  J.tc = S <= 7 * OV_MAXBLK ? 7 : (S + OV_MAXBLK - 1) / OV_MAXBLK;
+  J.nblk = (S + J.tc - 1) / J.tc;
+  J.nbc = (B + BR - 1) / BR;
+  J.ntile = (4 * HD / 64) * ((I + 63) / 64 + HD / 64);
+  J.wpd = (J.ntile + 2) / 3;
+  J.spin = dn_spin_limit(OV_SPIN);
+  const int grid = ndir * (J.nbc + J.wpd);
+  const auto kern = lstm_bwd_ov_kernel<192, 4>;
+  // the weight-gradient workgroups wait on the recurrence ones: all must be resident at once
+  if (!dn_fits_resident(reinterpret_cast<const void*>(kern), grid, 768, 0)) return DN_UNSUPPORTED;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(768), 0, st, pre, c_save, (const bf16*)whhT_p, dh_ext,
+                     dh_sb, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, J);
+  return dn_launch_status();
+}
 
 // rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
 DN_API int dn_lstm_rows_per_wg(int B, int Hd) { return pick_br(B, dn_lstm_padded_hidden(Hd)); }

@@ -25,7 +25,7 @@ Reference math: ``comps/icalstm/models.py:5-66`` (oracle: ``ops.reference.bilstm
 from __future__ import annotations
 
 import ctypes
-
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -58,6 +58,33 @@ _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
                               _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_lstm_rows_per_wg", [_lib.c_int, _lib.c_int])
+_lib.register("dn_lstm_bwd_ov", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_long, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_void_p,
+                                 _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_void_p, _lib.c_void_p])
+_lib.register("dn_lstm_ov_sync_bytes", [])
+_lib.register("dn_lstm_ov_err_word", [])
+
+# The overlapped backward (dn_lstm_bwd_ov: the LSTM weight / bias gradients accumulate on the
+# CUs the recurrence leaves idle, in the same launch); DINUNET_LSTM_OV=0 keeps the recurrence +
+# grouped weight-gradient GEMM
+OVERLAP_BWD = os.environ.get("DINUNET_LSTM_OV", "1") != "0"
+# per-device control block of the overlapped launch (counters + error word, runtime.health)
+OV_SYNC: Dict[str, Tensor] = {}
+
+
+def _ov_sync(device) -> Optional[Tensor]:
+    key = str(device)
+    t = OV_SYNC.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None  # created by an eager step first (never as a node of a graph)
+        L = _lib.lib()
+        L.dn_lstm_ov_sync_bytes.restype = ctypes.c_long
+        t = torch.zeros(int(L.dn_lstm_ov_sync_bytes()) // 4, dtype=torch.int32, device=device)
+        OV_SYNC[key] = t
+    return t
 
 _ROWMAP_CACHE: Dict[Tuple[int, int, str], Tensor] = {}
 
@@ -191,15 +218,37 @@ class _BiLSTMFn(torch.autograd.Function):
         dhT = None if dhT is None else dhT.float().contiguous()
         dcT = None if dcT is None else dcT.float().contiguous()
         dpre = torch.empty(Bp * S, ndir * GP, dtype=torch.bfloat16, device=dev)
-        _lib.call("dn_lstm_bwd", pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
-                  dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir,
-                  dpre.data_ptr(), st)
         dpre_v = dpre[:N]
         capturing = _cap.active() is not None and ctx.modules is not None
-        # (6) parameter grads accumulated into .grad (reference layout via row map): queued for
-        # the end-of-backward grouped launch together with the encoder's (ops._grad.defer)
-        probs = _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
-        _grad.defer(probs, [p for p in params if p is not None])
+        done = False
+        sync = _ov_sync(dev) if (OVERLAP_BWD and mode == "mean" and HD == 192
+                                 and all(p is not None for p in params)) else None
+        if sync is not None:
+            # (5)+(6) in ONE launch: the LSTM weight / bias gradients accumulate into .grad on
+            # the CUs the recurrence leaves idle, block by block as it publishes dpre
+            gl = []
+            for d in range(ndir):
+                w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
+                gl += [_grad.grad_buffer(w_ih), _grad.grad_buffer(w_hh), _grad.grad_buffer(b_ih),
+                       _grad.grad_buffer(b_hh)]
+            gp = (ctypes.c_void_p * 8)(*([g.data_ptr() for g in gl] + [None] * (8 - len(gl))))
+            rc = _lib.lib().dn_lstm_bwd_ov(
+                pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(), dout.data_ptr(), sb, scale,
+                _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir, dpre.data_ptr(), x2d.data_ptr(), I,
+                hprev.data_ptr(), gp, sync.data_ptr(), st)
+            if rc == 0:
+                done = True
+                _grad.notify([p for p in params if p is not None])
+            elif rc != 3:  # 3 = outside the overlapped kernel's envelope
+                raise RuntimeError(f"dn_lstm_bwd_ov failed with status {rc}")
+        if not done:
+            _lib.call("dn_lstm_bwd", pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
+                      dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd,
+                      ndir, dpre.data_ptr(), st)
+            # (6) parameter grads accumulated into .grad (reference layout via row map): queued
+            # for the end-of-backward grouped launch together with the encoder's (ops._grad.defer)
+            probs = _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
+            _grad.defer(probs, [p for p in params if p is not None])
         # (7) input grad
         dx = None
         if ctx.needs_input_grad[0]:

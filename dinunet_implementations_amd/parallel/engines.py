@@ -154,6 +154,16 @@ class DSGDEngine(Engine):
         if coll not in ("auto", "direct", "allreduce"):
             raise ValueError(f"dsgd_collective {coll!r}: expected auto, direct or allreduce")
         self.direct = coll == "direct" or (coll == "auto" and self.half)
+        if self.half and not self.direct and self.wire == "fp16":
+            # RCCL sums an all-reduce buffer in its own type: unscaled fp16 would flush
+            # gradients below ~6e-8 and overflow past 65504 in the sum over sites, and a
+            # per-site block scale cannot be summed.  The 16-bit all-reduce therefore ships
+            # bf16 (fp32's range); the fp16 wire needs the direct exchange (fp32 sum).
+            import warnings
+            warnings.warn("dsgd_collective='allreduce' with an fp16 payload: sending bf16 "
+                          "(RCCL would sum unscaled fp16); use dsgd_collective='direct' for an "
+                          "fp16 wire", RuntimeWarning, stacklevel=2)
+            self.wire = "bf16"
         self._comm_stream = (torch.cuda.Stream(device=flat.grad.device)
                              if self.direct and group.distributed and flat.grad.is_cuda else None)
         self._hooks = []

@@ -118,3 +118,26 @@ def test_payload_config_validation():
     assert payload_name({"precision_bits": 16, "payload_dtype": "BF16"}) == "bf16"
     with pytest.raises(ValueError):
         payload_name({"payload_dtype": "fp8"})
+
+
+def w_engine_wire(grp, cfg):
+    import warnings
+    import torch.nn as nn
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import make_engine
+    m = nn.Linear(4, 4)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        e = make_engine("dSGD", m, FlatParams(m.parameters()), grp, cfg)
+    return e.wire, e.direct, [str(x.message) for x in w]
+
+
+def test_fp16_wire_never_summed_by_a_16bit_allreduce():
+    """RCCL sums an all-reduce buffer in its own type, so the fp16 wire (whose block
+    scale is per site) cannot ride a 16-bit all-reduce: that combination ships bf16 and warns;
+    the direct exchange keeps fp16 (fp32 sum)."""
+    wire, direct, warns = run_world(w_engine_wire, 2, {"precision_bits": "16",
+                                                       "dsgd_collective": "allreduce"})[0]
+    assert wire == "bf16" and not direct and any("bf16" in m for m in warns)
+    wire, direct, warns = run_world(w_engine_wire, 2, {"precision_bits": "16"})[0]
+    assert wire == "fp16" and direct and not warns

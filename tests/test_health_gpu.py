@@ -59,3 +59,24 @@ def test_site_loop_fails_on_timed_out_handoff(tmp_path, spin_zero):
     root = _ica_root(tmp_path)
     with pytest.raises(spin_zero.HandoffError):
         _run_site(root, str(tmp_path / "out"), {"epochs": 2, "batch_size": 8})
+
+
+def test_overlapped_backward_wait_timeout_raises(spin_zero):
+    """The overlapped LSTM backward's weight-gradient workgroups give up waiting for the dpre
+    blocks at once with a zero poll limit: its error word must make the check raise."""
+    health = spin_zero
+    from dinunet_implementations_amd.models import ICALstm
+    torch.manual_seed(0)
+    m = ICALstm(input_size=64, hidden_size=384, num_comps=20, window_size=10).cuda().train()
+    x = torch.randn(32, 14, 20, 10, device="cuda")
+    y = torch.randint(0, 2, (32,), device="cuda")
+    _, loss, _ = m.forward_loss(x, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    with pytest.raises(health.HandoffError, match="lstm_bwd_ov"):
+        health.check([m])
+    health.set_spin_limit(-1)
+    _, loss, _ = m.forward_loss(x, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    health.check([m])

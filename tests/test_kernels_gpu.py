@@ -486,3 +486,35 @@ def test_payload_kernels_match_torch_layout(payload, n, W):
     else:
         r = ((out - x).abs() / x.abs()).max().item()
         assert r <= (2.0 ** -11 if payload == "fp16" else 2.0 ** -8) * 1.01, r
+
+
+@pytest.mark.parametrize("B,S,hidden", [(32, 98, 384), (13, 12, 384), (8, 30, 300)])
+def test_overlapped_lstm_backward_matches_grouped(B, S, hidden, monkeypatch):
+    """dn_lstm_bwd_ov (recurrence + the LSTM weight / bias gradients accumulated block by block
+    on the idle CUs, one launch) gives the gradients of dn_lstm_bwd + the grouped weight-gradient
+    GEMM: same dpre, the sums in another order.  Ragged batches (padded rows), sequences that are
+    not a multiple of the 7-step publication block, and a padded hidden (300 -> 2 x 150 in the
+    192-unit kernel) included."""
+    from dinunet_implementations_amd.models import ICALstm
+    from dinunet_implementations_amd.ops import lstm as L
+    torch.manual_seed(0)
+    m = ICALstm(input_size=256, hidden_size=hidden, num_comps=20, window_size=10).cuda().train()
+    m.classifier[0].p = 0.0
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.randn(B, S, 20, 10, device="cuda", generator=g)
+    y = torch.randint(0, 2, (B,), device="cuda", generator=g)
+    grads = {}
+    for ov in (False, True):
+        monkeypatch.setattr(L, "OVERLAP_BWD", ov)
+        m.zero_grad(set_to_none=True)
+        _, loss, _ = m.forward_loss(x, y)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads[ov] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    assert L.OV_SYNC, "the overlapped launch did not run"
+    sync = next(iter(L.OV_SYNC.values()))
+    assert int(sync[32].item()) == 0, "a weight-gradient wait timed out"
+    for n in grads[False]:
+        a, b = grads[True][n], grads[False][n]
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
+        assert rel < 2e-3, (n, rel)

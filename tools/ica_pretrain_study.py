@@ -60,7 +60,13 @@ def main():
     ap.add_argument("--tag", default="ica_pretrain")
     ap.add_argument("--logdir", default=None, help="per-mode launcher logs (default: --work)")
     ap.add_argument("--set", action="append", default=[], help="extra run.py --set items")
+    ap.add_argument("--lr", type=float, default=1e-3, help="federated learning_rate")
+    ap.add_argument("--pretrain-lr", type=float, default=1e-3)
+    ap.add_argument("--split", default="0.8,0.1,0.1", help="train,validation,test ratios")
+    ap.add_argument("--seeds", default="11", help="comma-separated run seeds (init + splits)")
     a = ap.parse_args()
+    seeds = [int(x) for x in str(a.seeds).split(",") if x.strip()]
+    split = [float(x) for x in a.split.split(",")]
 
     shutil.rmtree(a.work, ignore_errors=True)
     data = os.path.join(a.work, "data")
@@ -72,13 +78,14 @@ def main():
     print(f"# data generated in {time.time() - t0:.1f} s", flush=True)
     rows = []
     port = 29810
-    for mode in a.modes:
-        out = os.path.join(a.work, mode)
+    for seed, mode in [(sd, md) for sd in seeds for md in a.modes]:
+        out = os.path.join(a.work, f"{mode}_s{seed}")
         sets = [f"agg_engine={a.engine}", f"epochs={a.epochs}", f"patience={a.patience}",
-                f"batch_size={a.batch}", "seed=11"] + list(a.set)
+                f"batch_size={a.batch}", f"seed={seed}", f"learning_rate={a.lr}",
+                "split_ratio=" + json.dumps(split)] + list(a.set)
         if mode == "pretrain":
             sets += ["pretrain=true", "pretrain_args=" + json.dumps({
-                "epochs": a.pretrain_epochs, "learning_rate": 1e-3,
+                "epochs": a.pretrain_epochs, "learning_rate": a.pretrain_lr,
                 "batch_size": a.pretrain_batch, "local_iterations": 1, "validation_epochs": 1,
                 "patience": a.pretrain_patience})]
         port += 1
@@ -91,26 +98,28 @@ def main():
         env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
         env.setdefault("DINUNET_BACKEND", "gloo")
         t1 = time.time()
-        logp = os.path.join(a.logdir or a.work, f"{mode}.log")
+        logp = os.path.join(a.logdir or a.work, f"{mode}_s{seed}.log")
         os.makedirs(os.path.dirname(logp), exist_ok=True)
         with open(logp, "w") as f:
             rc = subprocess.call(cmd, stdout=f, stderr=subprocess.STDOUT, env=env)
         wall = time.time() - t1
         if rc != 0:
             print(f"FAILED {mode} rc={rc}; see {logp}", flush=True)
-            rows.append({"mode": mode, "rc": rc})
+            rows.append({"mode": mode, "seed": seed, "rc": rc})
             continue
         fr = analysis.fold_report(out)
         loc0 = analysis.fold_report(out, "local0")["folds"]
         f0 = fr["folds"][0] if fr["folds"] else {}
         with open(analysis.find_logs(out, "remote")[0]) as f:
             rlogs = json.load(f)
-        rec = {"mode": mode, "rc": rc, "wall_s": round(wall, 1), "sites": a.sites,
+        rec = {"mode": mode, "seed": seed, "rc": rc, "wall_s": round(wall, 1), "sites": a.sites,
                "engine": a.engine, "device": a.device,
                "data": (f"synthetic hard ICA cohort (signal {a.signal}, label noise "
                         f"{a.label_noise}); site 0: {a.big} subjects, sites 1..{a.sites - 1}: "
-                        f"{a.small} each; split 0.8/0.1/0.1"),
+                        f"{a.small} each; split {a.split}"),
                "config": {"epochs": a.epochs, "patience": a.patience, "batch_size": a.batch,
+                          "learning_rate": a.lr,
+                          "pretrain_learning_rate": a.pretrain_lr if mode == "pretrain" else None,
                           "pretrain_batch_size": a.pretrain_batch if mode == "pretrain" else None,
                           "pretrain_epochs": a.pretrain_epochs if mode == "pretrain" else None,
                           "hidden_size": a.hidden, "input_size": a.input_size,
@@ -123,26 +132,39 @@ def main():
                "validation_auc_curve": [round(float(r[-1]), 4) if isinstance(r, list) else r
                                         for r in rlogs.get("validation_log", [])]}
         rows.append(rec)
-        with open(os.path.join(a.profiles, f"{a.tag}_{mode}.json"), "w") as f:
+        with open(os.path.join(a.profiles, f"{a.tag}_{mode}_s{seed}.json"), "w") as f:
             json.dump(rec, f, indent=1)
-        print(f"{mode:8s} test AUC {rec['test']['AUC']} best val epoch {rec['best_val_epoch']} "
-              f"pretrain best epoch {rec['pretrain_best_val_epoch']} ({wall:.0f} s)", flush=True)
+        print(f"seed {seed} {mode:8s} test AUC {rec['test']['AUC']} best val epoch "
+              f"{rec['best_val_epoch']} pretrain best epoch {rec['pretrain_best_val_epoch']} "
+              f"({wall:.0f} s)", flush=True)
     md = [f"# ICA-LSTM pretrain -> finetune vs scratch ({a.sites} sites, {a.engine}, "
           f"{a.device}; BASELINE config 5)", "",
           f"Data: {rows[0].get('data', '') if rows else ''}.  Federated phase: batch {a.batch}, "
           f"up to {a.epochs} epochs, patience {a.patience}.  Pretraining (largest site alone): "
           f"batch {a.pretrain_batch}, up to {a.pretrain_epochs} epochs, patience "
-          f"{a.pretrain_patience}.  Reference (FS, `NB.ipynb:200,209`): mean stopping epoch "
-          f"68.5 scratch vs 42.7 pretrain.", "",
-          "| mode | test AUC | test acc | test F1 | federated best-val epoch | pretrain best epoch | wall s |",
-          "|---|---:|---:|---:|---:|---:|---:|"]
+          f"{a.pretrain_patience}.  Learning rate {a.lr} (pretraining {a.pretrain_lr}).  "
+          f"Reference (FS, `NB.ipynb:200,209`): mean stopping epoch 68.5 scratch vs 42.7 "
+          f"pretrain.", "",
+          "| seed | mode | test AUC | test acc | test F1 | federated best-val epoch | stopped at | pretrain best epoch | wall s |",
+          "|---:|---|---:|---:|---:|---:|---:|---:|---:|"]
     for r in rows:
         if r.get("rc"):
-            md.append(f"| {r['mode']} | FAILED rc={r['rc']} | | | | | |")
+            md.append(f"| {r.get('seed')} | {r['mode']} | FAILED rc={r['rc']} | | | | | | |")
             continue
         t = r["test"]
-        md.append(f"| {r['mode']} | {t['AUC']:.3f} | {t['Accuracy']:.3f} | {t['F1']:.3f} | "
-                  f"{r['best_val_epoch']} | {r['pretrain_best_val_epoch'] or '-'} | {r['wall_s']} |")
+        md.append(f"| {r['seed']} | {r['mode']} | {t['AUC']:.3f} | {t['Accuracy']:.3f} | "
+                  f"{t['F1']:.3f} | {r['best_val_epoch']} | {r.get('stopped_epoch') or '-'} | "
+                  f"{r['pretrain_best_val_epoch'] or '-'} | {r['wall_s']} |")
+    import statistics
+    md += ["", "| mode | runs | mean best-val (stopping) epoch | median | mean test AUC |",
+           "|---|---:|---:|---:|---:|"]
+    for mode in a.modes:
+        ok = [r for r in rows if r["mode"] == mode and not r.get("rc")]
+        if not ok:
+            continue
+        ep = [r["best_val_epoch"] for r in ok]
+        md.append(f"| {mode} | {len(ok)} | {statistics.mean(ep):.1f} | {statistics.median(ep)} | "
+                  f"{statistics.mean(r['test']['AUC'] for r in ok):.3f} |")
     with open(os.path.join(a.profiles, f"{a.tag}.md"), "w") as f:
         f.write("\n".join(md) + "\n")
     print("\n".join(md), flush=True)

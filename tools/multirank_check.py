@@ -32,6 +32,78 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _orth(P):
+    """Orthonormal basis of span(P) (fp64 Householder QR; the kernels use Cholesky QR -- the
+    reconstruction P P^T G does not depend on which basis of the span)."""
+    import torch
+    return torch.linalg.qr(P, mode="reduced")[0]
+
+
+def oracle_reducer(engine, model, flat, cfg, world, dev):
+    """``reduce(site_grads) -> mean gradient`` in fp64: the reference semantics of each engine
+    (SURVEY.md E10-E12), replayed from every site's own local gradient with the engine's own
+    initial state (warm-start Q, error feedback) kept per site.
+
+    * dSGD: the mean of the site gradients.
+    * rank-dAD (gradient space, fixed ``dad_num_pow_iters``: run with ``--dad-tol 0``): per large
+      Linear, site s runs its power iteration on its own G_s from its own warm start
+      (P = orth(G_s Q); Q = G_s^T P; the last Q warm-starts its next step) and the layer
+      gradient is mean_s P_s Q_s^T; every other parameter is the dSGD mean.
+    * PowerSGD (Vogels et al. 2019, warm start): M_s = G_s + e_s; P = orth(mean_s M_s Q);
+      Q = mean_s M_s^T P (the next warm start); G = P Q^T; e_s = M_s - G; vectors: mean."""
+    import torch
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    if engine == "dSGD":
+        return lambda gs: sum(gs) / len(gs)
+    tmpl = make_engine(engine, model, flat, SiteGroup(device=dev), dict(cfg))  # initial state
+    seg = {id(p): (o, n) for p, o, n in flat.segments()}
+    if engine == "rankDAD":
+        iters = max(1, tmpl.iters)
+        layers = []  # (offset, out, in, [per-site warm Q])
+        for m, o, out_f, in_f, r, po, qo in tmpl.fast_layers:
+            q0 = tmpl._send[qo:qo + in_f * r].view(in_f, r).double().clone()
+            layers.append((o, out_f, in_f, [q0.clone() for _ in range(world)]))
+
+        def red(gs):
+            g = sum(gs) / len(gs)
+            for o, out_f, in_f, qs in layers:
+                acc = torch.zeros(out_f, in_f, dtype=torch.float64, device=dev)
+                for s, gsite in enumerate(gs):
+                    G = gsite[o:o + out_f * in_f].view(out_f, in_f)
+                    Q = qs[s]
+                    for _ in range(iters):
+                        P = _orth(G @ Q)
+                        Q = G.t() @ P
+                    qs[s] = Q
+                    acc += P @ Q.t()
+                g[o:o + out_f * in_f] = (acc / len(gs)).reshape(-1)
+            return g
+        return red
+    if engine == "powerSGD":
+        mats = []  # (offset, rows, cols, Q, [per-site error])
+        for (p, rows, cols, r), q in zip(tmpl.mats, tmpl.Q):
+            o = seg[id(p)][0]
+            mats.append([o, rows, cols, q.double().clone(),
+                         [torch.zeros(rows, cols, dtype=torch.float64, device=dev)
+                          for _ in range(world)]])
+
+        def red(gs):
+            g = sum(gs) / len(gs)
+            for mt in mats:
+                o, rows, cols, Q, errs = mt
+                Ms = [gsite[o:o + rows * cols].view(rows, cols) + e for gsite, e in zip(gs, errs)]
+                P = _orth(sum(M @ Q for M in Ms) / len(Ms))
+                Qn = sum(M.t() @ P for M in Ms) / len(Ms)
+                Gh = P @ Qn.t()
+                mt[3] = Qn
+                mt[4] = [M - Gh for M in Ms]
+                g[o:o + rows * cols] = Gh.reshape(-1)
+            return g
+        return red
+    raise SystemExit(f"--oracle: no oracle for engine {engine}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--engine", default="dSGD")
@@ -50,6 +122,11 @@ def main():
     ap.add_argument("--oracle-tol", type=float, default=1e-3)
     ap.add_argument("--payload", default=None, help="payload_dtype (fp16 | bf16 | fp32)")
     ap.add_argument("--collective", default="auto", help="dsgd_collective (auto | direct | allreduce)")
+    ap.add_argument("--dad-tol", type=float, default=None,
+                    help="dad_tol (the rank-dAD oracle replays a fixed iteration count: pass 0)")
+    ap.add_argument("--grad-tol", type=float, default=None,
+                    help="bound on the first step's reduced-gradient error vs the fp64 oracle "
+                         "(dSGD; default: 1e-6 at 32 bits, 2e-3 at 16)")
     ap.add_argument("--feed", default="host", choices=["host", "device"],
                     help="device: each site's batches resident in HBM (bf16), TrainStep.bind/run "
                          "(the bench path: split capture across sites, Adam-emitted operand pack)")
@@ -73,6 +150,8 @@ def main():
            "dsgd_overlap": bool(a.overlap), "dsgd_collective": a.collective}
     if a.payload:
         cfg["payload_dtype"] = a.payload
+    if a.dad_tol is not None:
+        cfg["dad_tol"] = a.dad_tol
     eng = make_engine(a.engine, m, flat, grp, cfg)
     counts = {}
     if a.diag and hasattr(eng, "_on_grad"):
@@ -115,7 +194,7 @@ def main():
         step.run(a.steps)
     for i, x, y in (site_batches(grp.rank) if a.feed == "host" else ()):
         step(x, y, first=i % a.accum == 0, last=i % a.accum == a.accum - 1)
-        if i == a.accum - 1:  # the first step's reduced gradient (the payload's own error)
+        if i == a.accum - 1 and a.engine == "dSGD":  # the first reduced gradient (payload error)
             g_first = (flat.grad.double() * getattr(eng, "last_scale", 1.0)).clone()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -138,21 +217,22 @@ def main():
             fo = FlatParams(mo.parameters())
             oo = FusedAdam(fo, lr=1e-3)
             assert torch.equal(fo.data, init)
+            reducer = oracle_reducer(a.engine, mo, fo, cfg, grp.world, dev)
             sites = [site_batches(r) for r in range(grp.world)]
             for s_i in range(a.steps):
-                gsum = torch.zeros(fo.numel, dtype=torch.float64, device=dev)
+                gs = []
                 for r in range(grp.world):
                     fo.zero_grad()
                     for _k in range(a.accum):
                         _, x, y = next(sites[r])
                         _, loss, _ = mo.forward_loss(x, y)
                         (loss / a.accum).backward()
-                    gsum += fo.grad.double()
-                if s_i == 0 and a.engine == "dSGD" and g_first is not None:
-                    gm = gsum / grp.world
+                    gs.append(fo.grad.double().clone())
+                gm = reducer(gs)  # what the engine's reduction means, in fp64
+                if s_i == 0 and g_first is not None:
                     res["grad_rel_err"] = float((g_first - gm).norm() / gm.norm().clamp_min(1e-30))
                     res["grad_max_abs_err"] = float((g_first - gm).abs().max())
-                fo.grad.copy_((gsum / grp.world).float())
+                fo.grad.copy_(gm.float())
                 oo.step()
             d_n = (flat.data - init).double()
             d_o = (fo.data - init).double()
@@ -160,7 +240,12 @@ def main():
             res["update_rel_err"] = err
             res["update_max_abs_err"] = float((d_n - d_o).abs().max())
             res["update_norm"] = float(d_o.norm())
-            good = err <= a.oracle_tol if (a.precision == "32" and a.engine == "dSGD") else True
+            good = err <= a.oracle_tol
+            if "grad_rel_err" in res:
+                gt = a.grad_tol if a.grad_tol is not None else (1e-6 if a.precision == "32" else 2e-3)
+                res["grad_tol"] = gt
+                good = good and res["grad_rel_err"] <= gt
+            res["oracle_tol"] = a.oracle_tol
             res["oracle_ok"] = bool(good)
             ok_o.fill_(1.0 if good else 0.0)
         grp.broadcast(ok_o, 0)
