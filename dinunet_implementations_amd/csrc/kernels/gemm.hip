@@ -979,6 +979,16 @@ DN_API int dn_gemm_arm_bump(int* t, long long* c) {
 
 DN_API int dn_gemm_bump_armed() { return g_bump_t != nullptr; }
 
+// Hand the armed bump to a launch that is not a GEMM but starts with the encoder GEMM's work (the
+// overlapped LSTM forward, lstm.hip dn_lstm_fwd_ov), disarming it; null pointers when none is armed.
+DN_API int dn_gemm_take_bump(int** t, long long** c) {
+  *t = g_bump_t;
+  *c = g_bump_c;
+  g_bump_t = nullptr;
+  g_bump_c = nullptr;
+  return DN_OK;
+}
+
 // 1: bf16 x bf16 GEMMs use the LDS-DMA kernel (default); 0: the register-staged kernel.
 DN_API int dn_gemm_set_dma(int on) {
   g_gemm_dma = on != 0;

@@ -185,19 +185,47 @@ template <> struct LdsSplit<192, 16> { static constexpr int FWD_MT = 1, BWD_KS =
 // UG = 3 is ONE wave per SIMD owning 12 m-tiles -- the 72 MFMAs of a SIMD come from 12
 // independent accumulator chains of one wave (no issue arbitration between waves) and the h
 // tile is read once per k-step for 12 MFMAs instead of 4.
-template <int HD, int BR, bool SEQ, int UG>
-__global__ void __launch_bounds__(HD / (16 * UG) * 64)
-lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, no bias (bf16)
-                const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
-                const bf16* __restrict__ whh,    // [ndir][4*HD][HD] permuted rows, zero padded
-                int B, int S, int Hd, int ndir,
-                float* __restrict__ c_save,      // [ndir][Bp][S][HD]   c_t at original time idx
-                bf16* __restrict__ hprev,        // [ndir][Bp][S][HD]   h_{t-1} at original time idx
-                float* __restrict__ hseq,        // SEQ: [Bp][S][ndir*HD] (processing order)
-                float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
-                float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
-                float* __restrict__ pre,  // [B*S][ndir][4*HD] fp32 gate pre-activations (+ bias), or null
-                int bsplit) {  // > 0: bias holds b_ih at [0] and b_hh at [bsplit], summed here
+// Chunk hand-off of the overlapped forward (lstm_fwd_ov_kernel): the input projection of time
+// chunk c (original times [c tc, (c+1) tc)) is ready for direction d when the counter at
+// ready + 32 (d FOV_MAXCH + c) reaches `need`; the recurrence waits on it before its first load of
+// that chunk and reads the projection with device-scope (sc1) loads.
+constexpr int FOV_MAXCH = 64;
+struct FwdWait {
+  const unsigned* ready;
+  unsigned* err;
+  int tc, need, spin;
+};
+typedef __attribute__((address_space(1))) unsigned fov_gu32;
+
+__device__ __forceinline__ void fov_wait(const FwdWait& fw, int dir, int chunk) {
+  const fov_gu32* c = (const fov_gu32*)(fw.ready + 32 * (dir * FOV_MAXCH + chunk));
+  int it = 0;
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
+         (unsigned)fw.need) {
+    if (++it >= fw.spin) {  // gives up: error word (runtime.health), the data read is wrong
+      __hip_atomic_store((fov_gu32*)fw.err, 0x400u + (unsigned)chunk, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load hoisted above the poll
+}
+
+template <int HD, int BR, bool SEQ, int UG, bool OV>
+__device__ __forceinline__ void
+fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, no bias (bf16)
+          const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
+          const bf16* __restrict__ whh,    // [ndir][4*HD][HD] permuted rows, zero padded
+          int B, int S, int Hd, int ndir,
+          float* __restrict__ c_save,      // [ndir][Bp][S][HD]   c_t at original time idx
+          bf16* __restrict__ hprev,        // [ndir][Bp][S][HD]   h_{t-1} at original time idx
+          float* __restrict__ hseq,        // SEQ: [Bp][S][ndir*HD] (processing order)
+          float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
+          float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
+          float* __restrict__ pre,  // [B*S][ndir][4*HD] fp32 gate pre-activations (+ bias), or null
+          int bsplit,  // > 0: bias holds b_ih at [0] and b_hh at [bsplit], summed here
+          const int bx, const int dir, const int gx, const FwdWait fw) {
   constexpr int NW = HD / (16 * UG);
   constexpr int NT = NW * 64;
   constexpr int MT = 4 * UG;   // m-tiles per wave
@@ -220,9 +248,8 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane >> 4, n = lane & 15, r = n / BR, bl = n % BR;
-  const int dir = blockIdx.y;
-  const int Bp = gridDim.x * BR;
-  const int b = blockIdx.x * BR + bl;           // padded row (always < Bp)
+  const int Bp = gx * BR;
+  const int b = bx * BR + bl;                   // padded row (always < Bp)
   const int bc = b < B ? b : B - 1;             // clamped row for loads
   const long rowX = (long)ndir * 4 * HD;
 
@@ -276,7 +303,7 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
   // branch, see common.h); without a backward the descriptor has no records and every such store
   // is dropped.
   const int rowXi = ndir * 4 * HD;
-  const int b0 = blockIdx.x * BR;                 // first batch row of this workgroup (< B)
+  const int b0 = bx * BR;                         // first batch row of this workgroup (< B)
   const int nrow = B - b0 < BR ? B - b0 : BR;     // its valid rows
   const __amdgpu_buffer_rsrc_t x_rs = dn_rsrc(xp + (long)b0 * S * rowXi, (uint32_t)(nrow * S * rowXi * 2));
   const __amdgpu_buffer_rsrc_t pre_rs =
@@ -295,6 +322,10 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
   const uint32_t xstep = (uint32_t)(rowXi * 2);  // bytes per time index (bf16 projection)
   const uint32_t pstep = (uint32_t)(rowXi * 4);  // (fp32 pre-activations)
   // the 4 gate inputs of a slot stay packed (2 VGPRs, unconverted) while the load is in flight
+  // (OV: the projection of a chunk is read only after its ready counter, and every 128-B line
+  // of it was written whole by ONE producer wave through the write-through path before that
+  // counter moved, so no cache on the way holds an older copy: plain loads, no device-scope
+  // (sc1) round trip on the recurrence's critical path)
   auto load_x = [&](int s, int tau) {  // time index -1 / S wraps out of range: reads 0
     return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
         x_rs, (int)(xo[s] + (uint32_t)tau * xstep), 0, 0));
@@ -309,6 +340,20 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
                                             (int)(ho[s] + (uint32_t)(tau0 * HD * 2)), 0, 0);
   }
 
+  // OV: the ready count of the NEXT chunk is read one chunk ahead (a device-scope load lands long
+  // before the boundary), so a boundary whose chunk is already projected costs no round trip
+  unsigned fv_pend = 0u;
+  auto fov_peek = [&](int chunk) -> unsigned {
+    const bool ok = chunk >= 0 && chunk * fw.tc < S;
+    return ok ? __hip_atomic_load((const fov_gu32*)(fw.ready + 32 * (dir * FOV_MAXCH + chunk)),
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+              : 0u;
+  };
+  if constexpr (OV) {
+    const int c0 = (dir == 0 ? 0 : S - 1) / fw.tc;
+    fov_wait(fw, dir, c0);
+    fv_pend = fov_peek(dir == 0 ? c0 + 1 : c0 - 1);
+  }
   float c[NSL], hs[NSL], hl[NSL];
   // xa / xb: the input projection of the current / next step, ping-ponged over a 2-step
   // unrolled loop so that no register copy (and no vmcnt wait) sits between a prefetch and its
@@ -340,6 +385,15 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
 #endif
     const int tau = dir == 0 ? t : S - 1 - t;
     const int tau1 = dir == 0 ? t + 1 : S - 2 - t;  // past the end at the last step: reads 0
+    if constexpr (OV) {
+      static_assert(EARLY, "the overlapped forward prefetches one step ahead");
+      if (t + 1 < S && tau1 / fw.tc != tau / fw.tc) {
+        const int c1 = tau1 / fw.tc;
+        if (__builtin_amdgcn_readfirstlane(fv_pend) < (unsigned)fw.need) fov_wait(fw, dir, c1);
+        fv_pend = fov_peek(dir == 0 ? c1 + 1 : c1 - 1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load hoisted above the check
+    }
     if constexpr (EARLY) {
 #pragma unroll
       for (int s = 0; s < NSL; ++s) xnn[s] = load_x(s, tau1);
@@ -467,8 +521,8 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
   }
   if (t < S) step(t, xa, xb);
 #ifdef DN_STAMPS
-  if (lane == 0 && blockIdx.x == 0) {
-    unsigned long long* o = dn_stamp_buf + (blockIdx.y * 64 + w) * 4;
+  if (lane == 0 && bx == 0) {
+    unsigned long long* o = dn_stamp_buf + (dir * 64 + w) * 4;
     o[0] = st_a; o[1] = st_b; o[2] = st_c; o[3] = S;
   }
 #endif
@@ -482,6 +536,18 @@ lstm_fwd_kernel(const bf16* xp,                  // [B*S][ndir][4*HD] permuted c
       if (cT) cT[o] = c[s];
     }
   }
+}
+
+template <int HD, int BR, bool SEQ, int UG>
+__global__ void __launch_bounds__(HD / (16 * UG) * 64)
+lstm_fwd_kernel(const bf16* xp, const float* __restrict__ bias, const bf16* __restrict__ whh,
+                int B, int S, int Hd, int ndir, float* __restrict__ c_save,
+                bf16* __restrict__ hprev, float* __restrict__ hseq, float* __restrict__ hmean,
+                float mean_scale, float* __restrict__ hT, float* __restrict__ cT,
+                float* __restrict__ pre, int bsplit) {
+  fwd_recur<HD, BR, SEQ, UG, false>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
+                                    mean_scale, hT, cT, pre, bsplit, (int)blockIdx.x,
+                                    (int)blockIdx.y, (int)gridDim.x, FwdWait{});
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -766,14 +832,30 @@ bwd_recur(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time 
     STAMP(ts2);
 #endif
     if constexpr (PUB) {
-      // every `tc` steps (and after the last): this block of time steps is published
+      // A block of `tc` steps is published one block LATE: at the end of block k, block k-1's
+      // stores were issued >= tc steps ago, so waiting until at most 6 vector-memory ops are
+      // outstanding (every step issues >= 1 store and tc >= 7: all of block k-1 is older than
+      // the newest 6) costs nothing, where a drain (vmcnt 0) right after the stores waited a
+      // write-through round trip every block on the critical path.  The last step drains and
+      // publishes what is left.
       const int done = S - t;
-      const bool pub_now = done % pub.tc == 0 || t == 0;
-      if (pub_now) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (pub_now && tid == 0)
-        __hip_atomic_fetch_add((ov_gu32*)(pub.ready + 32 * (dir * OV_MAXBLK + (done - 1) / pub.tc)),
-                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int k = (done - 1) / pub.tc;
+      ov_gu32* rb = (ov_gu32*)(pub.ready + 32 * dir * OV_MAXBLK);
+      if (t == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          if (k >= 1) __hip_atomic_fetch_add(rb + 32 * (k - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(rb + 32 * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else if (done % pub.tc == 0 && k >= 1) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+          __hip_atomic_fetch_add(rb + 32 * (k - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __syncthreads();
+      }
     } else {
       __syncthreads();
     }
@@ -847,7 +929,7 @@ struct OvJob {
   float* gbih[2];
   float* gbhh[2];
   unsigned* sync;
-  int I, tc, nblk, nbc, ntile, wpd, spin;
+  int I, tc, nblk, nbc, ntile, wpd, spin, probe;
 };
 
 // 16x32 MFMA operand fragment from a k-major image [64 k][OV_C] (operand rows = image columns
@@ -941,7 +1023,8 @@ __device__ void bwd_wgrad_role(const OvJob& J, const bf16* __restrict__ dpre, in
       ov_gu32* c = (ov_gu32*)(J.sync + OV_W_READY + 32 * (d * OV_MAXBLK + k));
       int it = 0;
       for (; it < J.spin; ++it) {
-        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)J.nbc) break;
+        if (J.probe == 1 ||
+            __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)J.nbc) break;
         __builtin_amdgcn_s_sleep(1);
       }
       if (it >= J.spin)
@@ -1011,7 +1094,7 @@ lstm_bwd_ov_kernel(const float* __restrict__ pre, const float* __restrict__ c_sa
     bwd_recur<HD, BR, false, 1, true>(pre, c_save, whhT, dh_ext, dh_sb, 0, dh_scale, dhT, dcT, B,
                                       S, Hd, ndir, dpre, wg % J.nbc, wg / J.nbc, J.nbc,
                                       BwdPub{J.sync + OV_W_READY, J.tc});
-  } else {
+  } else if (J.probe != 2) {
     bwd_wgrad_role<HD>(J, dpre, B, S, Hd, ndir, J.nbc * BR, wg - nrec);
   }
   // the last workgroup to finish resets the counters for the next launch (nobody polls anymore)
@@ -1025,6 +1108,220 @@ lstm_bwd_ov_kernel(const float* __restrict__ pre, const float* __restrict__ c_sa
                            0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Overlapped forward: the encoder GEMM and the input projection run INSIDE the
+// recurrence's launch, on the CUs the recurrence leaves idle, so the recurrence starts after the
+// first time chunk is projected instead of after both whole GEMMs.  One launch, two roles:
+//   * recurrence workgroups (the first ndir * ceil(B/4)): fwd_recur<..., OV = true>, which waits on
+//     a chunk's ready counter before its first (device-scope) load of that chunk's projection;
+//   * producer workgroups: every wave runs independent 32 x 64 output tiles (jobs), operands
+//     loaded straight from global memory in MFMA fragment layout (k-contiguous rows: one 16-B load
+//     per lane and fragment, 2 k-steps in flight), no LDS images and no workgroup barrier.  Jobs
+//     are enumerated chunk by chunk in the order the recurrence needs them (ndir = 2: first chunk,
+//     last chunk, second, second-to-last, ...); within a chunk the encoder tiles
+//     enc = ReLU(x W_e^T + b_e) come first, then the projection tiles xp = enc W_ih^T (the columns
+//     of the direction that needs the chunk first, then the other's).  A projection job waits on
+//     its row tile's encoder counter; a finished job stores through the write-through (sc1) path,
+//     drains, and adds 1 to its counter.
+// Waves take jobs j = wave, wave + nwaves, ... in increasing order, and a job waits only on jobs
+// earlier in that order, so the earliest unfinished job is always runnable; the launcher checks
+// that the whole grid is resident.  Waits are bounded (error word, runtime.health).  The sums
+// are the same k-order MFMA chains as the standalone GEMMs (ops.gemm): same enc / xp values.
+constexpr int FOV_W_DONE = 0, FOV_W_ERR = 32, FOV_W_READY = 64;
+constexpr int FOV_MAXRT = 64;  // 32-row tiles per chunk
+constexpr int FOV_W_ENC = FOV_W_READY + 32 * 2 * FOV_MAXCH;
+constexpr int FOV_SYNC_WORDS = FOV_W_ENC + FOV_MAXCH * FOV_MAXRT;
+constexpr int FOV_SPIN = 1 << 22;
+constexpr int FOV_LDE = 72;  // per-wave epilogue tile row (bf16): 64 + 8, 144-B rows
+
+struct FovJob {
+  const bf16* x;    // [B*S][CW] encoder input
+  const bf16* we;   // [I][CW] encoder weight (bf16 image)
+  const float* be;  // [I] encoder bias
+  bf16* enc;        // [B*S][I] ReLU(x W_e^T + b_e), kept for the backward
+  const bf16* wih;  // [ndir*GP][I] packed input weights
+  bf16* xp;         // [B*S][ndir*GP] input projection (no bias: the recurrence adds it)
+  unsigned* sync;
+  int* bump_t;
+  long long* bump_c;
+  int CW, I, GP, GPN, B, S, tc, nch, nrt, ndir, nbc, jpc, njobs, nwaves, need, spin, probe;
+  int enc_in;  // 1: enc was produced before the launch (projection jobs only, no encoder wait)
+};
+
+// one 32 x 64 tile of enc (ENC) or xp for rows [32 rt, 32 rt + 32) of chunk `chunk` and columns
+// [col0, col0 + 64), by one wave.  64 columns = one whole 128-B line of every output row, so each
+// line has ONE writer (the consumers then read it with plain loads: see fwd_recur's load_x)
+template <bool ENC>
+__device__ __forceinline__ void fov_tile(const FovJob& J, int chunk, int rt, int col0, int lane,
+                                         bf16* __restrict__ lds) {
+  const int t0 = chunk * J.tc, ntc = min(J.tc, J.S - t0), rows = J.B * ntc;
+  const int K = ENC ? J.CW : J.I;
+  const int N = ENC ? J.I : J.GPN;
+  auto grow = [&](int i) { return (i % J.B) * J.S + t0 + i / J.B; };  // chunk row -> batch row
+  const __amdgpu_buffer_rsrc_t a_rs =
+      dn_rsrc(ENC ? (const void*)J.x : (const void*)J.enc, (uint32_t)((long)J.B * J.S * K * 2));
+  const __amdgpu_buffer_rsrc_t b_rs =
+      dn_rsrc(ENC ? (const void*)J.we : (const void*)J.wih, (uint32_t)((long)N * K * 2));
+  const int kq = 8 * (lane >> 4);
+  uint32_t ao[2], bo[4];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int i = 32 * rt + 16 * f + (lane & 15);
+    ao[f] = i < rows ? (uint32_t)(((long)grow(i) * K + kq) * 2) : DN_OOB;
+  }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) bo[f] = (uint32_t)(((long)(col0 + 16 * f + (lane & 15)) * K + kq) * 2);
+  auto ld = [&](int ks, bf16x8 (&a)[2], bf16x8 (&b)[4]) {
+    const bool kin = 32 * ks + kq < K;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+      a[f] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+          a_rs, (int)(kin && ao[f] != DN_OOB ? ao[f] + 64u * ks : DN_OOB), 0, 0));
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+      b[f] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+          b_rs, (int)(kin ? bo[f] + 64u * ks : DN_OOB), 0, 0));
+  };
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const bf16x8 (&a)[2], const bf16x8 (&b)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+  };
+  // two k-steps in flight (a k-step is 8 MFMAs; the operands come from L2; a third register
+  // stage spilled beside the recurrence role's 168 VGPRs)
+  const int nks = (K + 31) / 32;
+  bf16x8 a0[2], b0[4], a1[2], b1[4];
+  ld(0, a0, b0);
+  ld(1, a1, b1);
+  for (int ks = 0; ks < nks; ks += 2) {
+    mm(a0, b0);
+    if (ks + 2 < nks) ld(ks + 2, a0, b0);
+    if (ks + 1 >= nks) break;
+    mm(a1, b1);
+    if (ks + 3 < nks) ld(ks + 3, a1, b1);
+  }
+  // epilogue: (bias + ReLU) -> bf16 -> the wave's LDS tile -> 16-B rows, write-through stores
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int lc = 16 * j + (lane & 15);
+    const float bb = ENC ? J.be[col0 + lc] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r];
+        if constexpr (ENC) v = fmaxf(v + bb, 0.f);
+        lds[(16 * i + 4 * (lane >> 4) + r) * FOV_LDE + lc] = (bf16)v;
+      }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  const __amdgpu_buffer_rsrc_t o_rs =
+      dn_rsrc(ENC ? (void*)J.enc : (void*)J.xp, (uint32_t)((long)J.B * J.S * N * 2));
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int c = lane + 64 * p, row = c >> 3, cc = (c & 7) * 8;
+    const int i = 32 * rt + row;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * FOV_LDE + cc);
+    const uint32_t off = i < rows ? (uint32_t)(((long)grow(i) * N + col0 + cc) * 2) : DN_OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ov_u32x4, v), o_rs, (int)off, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void fov_produce(const FovJob& J, int gw, int lane, bf16* lds) {
+  const int nct_e = J.I / 64, nct_p = J.GP / 64;
+  const int ne = J.enc_in ? 0 : J.nrt * nct_e, npd = J.nrt * nct_p;
+  for (int j = gw; j < J.njobs; j += J.nwaves) {
+    const int ci = j / J.jpc;
+    int r = j - ci * J.jpc;
+    const bool back = J.ndir == 2 && (ci & 1);
+    const int chunk = J.ndir == 2 ? (back ? J.nch - 1 - (ci >> 1) : (ci >> 1)) : ci;
+    if (r < ne) {
+      const int rt = r / nct_e, ct = r - rt * nct_e;
+      fov_tile<true>(J, chunk, rt, 64 * ct, lane, lds);
+      if (lane == 0)
+        __hip_atomic_fetch_add((fov_gu32*)(J.sync + FOV_W_ENC + chunk * FOV_MAXRT + rt), 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      r -= ne;
+      const int dd = r / npd, r2 = r - dd * npd;
+      const int rt = r2 / nct_p, ct = r2 - rt * nct_p;
+      const int d = dd == 0 ? (back ? 1 : 0) : (back ? 0 : 1);
+      // this row tile's encoder output (all its column tiles)
+      const fov_gu32* ec = (const fov_gu32*)(J.sync + FOV_W_ENC + chunk * FOV_MAXRT + rt);
+      int it = 0;
+      while (!J.enc_in && __builtin_amdgcn_readfirstlane(
+                 __hip_atomic_load(ec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < (unsigned)nct_e) {
+        if (++it >= J.spin) {
+          __hip_atomic_store((fov_gu32*)(J.sync + FOV_W_ERR), 0x500u + (unsigned)chunk,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      fov_tile<false>(J, chunk, rt, d * J.GP + 64 * ct, lane, lds);
+      if (lane == 0)
+        __hip_atomic_fetch_add((fov_gu32*)(J.sync + FOV_W_READY + 32 * (d * FOV_MAXCH + chunk)), 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int HD, int BR>
+__global__ void __launch_bounds__(HD / 16 * 64)
+lstm_fwd_ov_kernel(const float* __restrict__ bias, const bf16* __restrict__ whh, int B, int S,
+                   int Hd, int ndir, float* __restrict__ c_save, bf16* __restrict__ hprev,
+                   float* __restrict__ hmean, float mean_scale, float* __restrict__ hT,
+                   float* __restrict__ cT, float* __restrict__ pre, int bsplit, FovJob J) {
+  __shared__ __attribute__((aligned(16))) bf16 fov_lds[HD / 16][32 * FOV_LDE];
+  const int nrec = ndir * J.nbc;
+  const int wg = blockIdx.x;
+  if (wg == 0 && threadIdx.x == 0 && J.bump_t) {  // the encoder GEMM's step-counter bump
+    *J.bump_t += 1;
+    if (J.bump_c) *J.bump_c += 1;
+  }
+  if (wg < nrec) {
+    if (J.probe != 2)
+    fwd_recur<HD, BR, false, 1, true>(J.xp, bias, whh, B, S, Hd, ndir, c_save, hprev, nullptr,
+                                      hmean, mean_scale, hT, cT, pre, bsplit, wg % J.nbc,
+                                      wg / J.nbc, J.nbc,
+                                      FwdWait{J.sync + FOV_W_READY, J.sync + FOV_W_ERR, J.tc,
+                                              J.need, J.spin});
+  } else if (J.probe != 3) {
+    const int wave = threadIdx.x >> 6;
+    fov_produce(J, (wg - nrec) * (HD / 16) + wave, threadIdx.x & 63, fov_lds[wave]);
+  }
+  // the last workgroup to finish resets the counters for the next launch (nobody polls anymore)
+  __syncthreads();
+  __shared__ int fov_last;
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add((fov_gu32*)(J.sync + FOV_W_DONE), 1u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fov_last = old + 1 == gridDim.x;
+  }
+  __syncthreads();
+  if (fov_last) {
+    const int nr = 2 * FOV_MAXCH, nen = J.nch * FOV_MAXRT;
+    for (int i = threadIdx.x; i < nr + nen; i += blockDim.x) {
+      const int w = i < nr ? FOV_W_READY + 32 * i : FOV_W_ENC + (i - nr);
+      __hip_atomic_store((fov_gu32*)(J.sync + w), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store((fov_gu32*)(J.sync + FOV_W_DONE), 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1388,6 +1685,10 @@ DN_API int dn_lstm_bwd_ov(const float* pre, const float* c_save, const void* whh
   J.ntile = (4 * HD / 64) * ((I + 63) / 64 + HD / 64);
   J.wpd = (J.ntile + 2) / 3;
   J.spin = dn_spin_limit(OV_SPIN);
+  // diagnostic knobs (tools/fov_probe.py): DN_BOV_PROBE=1 the weight-gradient workgroups do not
+  // wait (wrong results; interference), =2 they exit at once (the recurrence role alone)
+  J.probe = 0;
+  if (const char* e = getenv("DN_BOV_PROBE")) J.probe = atoi(e);
   const int grid = ndir * (J.nbc + J.wpd);
   const auto kern = lstm_bwd_ov_kernel<192, 4>;
   // the weight-gradient workgroups wait on the recurrence ones: all must be resident at once
@@ -1397,9 +1698,6 @@ DN_API int dn_lstm_bwd_ov(const float* pre, const float* c_save, const void* whh
   return dn_launch_status();
 }
 
-// rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
-DN_API int dn_lstm_rows_per_wg(int B, int Hd) { return pick_br(B, dn_lstm_padded_hidden(Hd)); }
-
 // the forward's per-workgroup buffer descriptors span BR rows (32-bit offsets); the backward
 // addresses with 64-bit pointers.  Only a single sequence longer than the descriptors can hold
 // (BR * S * ndir * 4 * HD * 4 >= 2 GiB, S in the millions) is refused.
@@ -1407,6 +1705,84 @@ static bool lstm_fits_32bit(int B, int S, int HD, int ndir, int BR) {
   (void)B;
   return (long)BR * S * ndir * 4 * HD * 4 < (1L << 31);
 }
+
+// The overlapped forward (lstm_fwd_ov_kernel): encoder GEMM (bias + ReLU) + input projection +
+// recurrence in ONE launch.  Taken for the geometry it is built for (HD = 192, 4 rows per
+// workgroup, temporal-mean output, encoder widths CW % 8 == 0 and I % 64 == 0) when the whole grid
+// can be resident; DN_UNSUPPORTED otherwise (the caller then runs the encoder GEMM, the projection
+// GEMM and dn_lstm_fwd).  x [B*S][CW], enc_w [I][CW] and wih_p [ndir*4HD][I] bf16; enc_b fp32.
+// Outputs enc [B*S][I] and xp [B*S][ndir*4HD] (bf16) besides dn_lstm_fwd's.  tc: time steps per
+// chunk (<= 0: 4); nprod: producer workgroups (<= 0: 64); enc_in: enc is an input computed before
+// the launch (the producers run the projection only).  sync: dn_lstm_fwd_ov_sync_bytes()
+// bytes, zeroed once before the first launch.  An armed GEMM bump (dn_gemm_arm_bump) is consumed.
+DN_API long dn_lstm_fwd_ov_sync_bytes() { return 4L * FOV_SYNC_WORDS; }
+DN_API long dn_lstm_fwd_ov_err_word() { return FOV_W_ERR; }
+extern "C" int dn_gemm_take_bump(int** t, long long** c);
+DN_API int dn_lstm_fwd_ov(const void* x, int CW, const void* enc_w, const float* enc_b, void* enc,
+                          int I, const void* wih_p, void* xp, const float* bias, int bias_split,
+                          const void* whh_p, int B, int S, int Hd, int ndir, float* c_save,
+                          void* hprev, float* hmean, float mean_scale, float* hT, float* cT,
+                          float* pre, void* sync, int tc, int nprod, int enc_in,
+                          hipStream_t st) {
+  const int HD = dn_lstm_padded_hidden(Hd);
+  if (HD != 192 || B <= 0 || S <= 0 || ndir < 1 || ndir > 2 || !sync || !hmean || !enc ||
+      (!enc_in && (!x || !enc_w || !enc_b || CW <= 0 || CW % 8)) || I <= 0 || I % 64)
+    return DN_UNSUPPORTED;
+  if (bias_split != 0 && bias_split != ndir * 4 * HD) return DN_BAD_SHAPE;
+  if (pick_br(B, HD) != 4) return DN_UNSUPPORTED;
+  const long rows = (long)B * S;
+  const long lim = 1L << 31;
+  if ((!enc_in && rows * CW * 2 >= lim) || rows * ndir * 4 * HD * 2 >= lim || rows * I * 2 >= lim ||
+      !lstm_fits_32bit(B, S, HD, ndir, 4))
+    return DN_UNSUPPORTED;
+  if (tc <= 0) tc = 4;
+  if ((S + tc - 1) / tc > FOV_MAXCH) tc = (S + FOV_MAXCH - 1) / FOV_MAXCH;
+  FovJob J{};
+  J.x = (const bf16*)x;
+  J.we = (const bf16*)enc_w;
+  J.be = enc_b;
+  J.enc = (bf16*)enc;
+  J.wih = (const bf16*)wih_p;
+  J.xp = (bf16*)xp;
+  J.sync = (unsigned*)sync;
+  J.CW = CW;
+  J.I = I;
+  J.GP = 4 * HD;
+  J.GPN = ndir * 4 * HD;
+  J.B = B;
+  J.S = S;
+  J.tc = tc;
+  J.nch = (S + tc - 1) / tc;
+  J.nrt = (B * tc + 31) / 32;
+  if (J.nrt > FOV_MAXRT) return DN_UNSUPPORTED;
+  J.ndir = ndir;
+  J.nbc = (B + 3) / 4;
+  J.enc_in = enc_in != 0;
+  J.jpc = (J.enc_in ? 0 : J.nrt * (I / 64)) + ndir * J.nrt * (J.GP / 64);
+  J.njobs = J.nch * J.jpc;
+  J.need = J.nrt * (J.GP / 64);
+  J.spin = dn_spin_limit(FOV_SPIN);
+  if (nprod <= 0) nprod = 64;
+  // diagnostic knobs (tools/fov_probe.py): DN_FOV_PROBE=1 the recurrence does not wait for the
+  // producers (wrong results; measures the interference of the two roles), =2 the recurrence
+  // workgroups exit at once (producer time), =3 the producers exit at once and nothing waits
+  // (the recurrence role alone)
+  J.probe = 0;
+  if (const char* e = getenv("DN_FOV_PROBE")) J.probe = atoi(e);
+  if (J.probe == 1 || J.probe == 3) J.need = 0;
+  const int grid = ndir * J.nbc + nprod;
+  J.nwaves = nprod * (HD / 16);
+  const auto kern = lstm_fwd_ov_kernel<192, 4>;
+  // the recurrence waits on the producers: all workgroups must be resident at once
+  if (!dn_fits_resident(reinterpret_cast<const void*>(kern), grid, 768, 0)) return DN_UNSUPPORTED;
+  dn_gemm_take_bump(&J.bump_t, &J.bump_c);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(768), 0, st, bias, (const bf16*)whh_p, B, S, Hd, ndir,
+                     c_save, (bf16*)hprev, hmean, mean_scale, hT, cT, pre, bias_split, J);
+  return dn_launch_status();
+}
+
+// rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
+DN_API int dn_lstm_rows_per_wg(int B, int Hd) { return pick_br(B, dn_lstm_padded_hidden(Hd)); }
 
 // xp: the bf16 input projection [B*S][ndir][4*HD]; pre (fp32, same layout, or null when no
 // backward follows) receives the gate pre-activations (+ bias) the backward consumes

@@ -86,12 +86,7 @@ def _relu_linear_backward(ctx, dy):
             dym = torch.empty_like(dy)
             _lib.call("dn_relu_bwd", dy.data_ptr(), y.data_ptr(), dym.data_ptr(), N * O,
                       _lib.stream())
-        probs = [dict(a=dym, b=x2d, out=_grad.grad_buffer(weight), beta=1.0)]
-        if bias is not None:
-            from .lstm import _ones
-            probs.append(dict(a=dym, b=_ones(N, dy.device), out=_grad.grad_buffer(bias).view(-1, 1),
-                              beta=1.0, ncol=1))
-        _grad.defer(probs, [weight] + ([bias] if bias is not None else []))
+        defer_linear_grads(x2d, dym, weight, bias)
     else:
         dym = torch.empty_like(dy)
         ws = torch.empty(_RB_SLABS * O, dtype=torch.float32, device=dy.device)
@@ -107,6 +102,22 @@ def _relu_linear_backward(ctx, dy):
     if ctx.module is not None and _cap.active() is not None:
         _cap.record(ctx.module, x2d, dym)
     return dx, None, None, None
+
+
+def defer_linear_grads(x2d: torch.Tensor, dym: torch.Tensor, weight: torch.Tensor,
+                       bias: Optional[torch.Tensor], module: Optional[nn.Module] = None) -> None:
+    """Queue ``dW += dym^T x2d`` and ``db += dym^T 1`` (``dym``: the masked output gradient,
+    bf16 ``[N, O]``) into the end-of-backward grouped launch (``ops._grad.defer``); record the
+    pair for activation capture (rank-dAD) when one is active and ``module`` is given."""
+    N = dym.shape[0]
+    probs = [dict(a=dym, b=x2d, out=_grad.grad_buffer(weight), beta=1.0)]
+    if bias is not None:
+        from .lstm import _ones
+        probs.append(dict(a=dym, b=_ones(N, dym.device), out=_grad.grad_buffer(bias).view(-1, 1),
+                          beta=1.0, ncol=1))
+    _grad.defer(probs, [weight] + ([bias] if bias is not None else []))
+    if module is not None and _cap.active() is not None:
+        _cap.record(module, x2d, dym)
 
 
 def linear_bias_relu(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],

@@ -65,26 +65,59 @@ _lib.register("dn_lstm_bwd_ov", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _l
                                  _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_lstm_ov_sync_bytes", [])
 _lib.register("dn_lstm_ov_err_word", [])
+_lib.register("dn_lstm_fwd_ov", [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_int,
+                                 _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
+                                 _lib.c_int, _lib.c_void_p])
+_lib.register("dn_lstm_fwd_ov_sync_bytes", [])
+_lib.register("dn_lstm_fwd_ov_err_word", [])
 
 # The overlapped backward (dn_lstm_bwd_ov: the LSTM weight / bias gradients accumulate on the
-# CUs the recurrence leaves idle, in the same launch); DINUNET_LSTM_OV=0 keeps the recurrence +
-# grouped weight-gradient GEMM
-OVERLAP_BWD = os.environ.get("DINUNET_LSTM_OV", "1") != "0"
+# CUs the recurrence leaves idle, in the same launch) is opt-in (DINUNET_LSTM_OV=1): measured on
+# MI355X at the headline step (tools/_gpu_probe.sh, profiles/r4_overlap_probe.jsonl) it costs
+# 26 us per step -- the grouped weight-gradient GEMM it replaces took ~5 us, and the dpre
+# publication (write-through drains, block waits, the tail of the last blocks) takes more
+OVERLAP_BWD = os.environ.get("DINUNET_LSTM_OV", "0") == "1"
 # per-device control block of the overlapped launch (counters + error word, runtime.health)
 OV_SYNC: Dict[str, Tensor] = {}
 
 
-def _ov_sync(device) -> Optional[Tensor]:
+# The overlapped forward (dn_lstm_fwd_ov: the input projection -- and with FOV_MODE "full" the
+# encoder GEMM too -- produced time chunk by time chunk on the CUs the recurrence leaves idle, in
+# the recurrence's launch) is opt-in (DINUNET_LSTM_FOV=1).  Measured on MI355X at the headline
+# step (profiles/r4_overlap_probe.jsonl): 0.348 ms/step vs 0.3115 for the three launches.  The
+# producer waves load MFMA fragments straight from global memory (16 half-used cache lines per
+# load instruction: address-bound, 66 us for what the LDS-DMA GEMM does in 10 us) and the
+# recurrence role alone runs ~10 us slower than the standalone kernel, so the 10-19 us of GEMM it
+# hides never pays.  DINUNET_LSTM_FOV_TC: time steps per chunk; DINUNET_LSTM_FOV_WG: producer
+# workgroups
+OVERLAP_FWD = os.environ.get("DINUNET_LSTM_FOV", "0") == "1"
+# "proj": the encoder stays a standalone GEMM before the launch, only the projection overlaps;
+# "full": encoder tiles are produced in the launch too
+FOV_MODE = os.environ.get("DINUNET_LSTM_FOV_MODE", "proj")
+FOV_TC = int(os.environ.get("DINUNET_LSTM_FOV_TC", "4"))
+FOV_WG = int(os.environ.get("DINUNET_LSTM_FOV_WG", "64"))
+FOV_SYNC: Dict[str, Tensor] = {}
+
+
+def _sync_block(table: Dict[str, Tensor], bytes_fn: str, device) -> Optional[Tensor]:
     key = str(device)
-    t = OV_SYNC.get(key)
+    t = table.get(key)
     if t is None:
         if torch.cuda.is_current_stream_capturing():
             return None  # created by an eager step first (never as a node of a graph)
         L = _lib.lib()
-        L.dn_lstm_ov_sync_bytes.restype = ctypes.c_long
-        t = torch.zeros(int(L.dn_lstm_ov_sync_bytes()) // 4, dtype=torch.int32, device=device)
-        OV_SYNC[key] = t
+        getattr(L, bytes_fn).restype = ctypes.c_long
+        t = torch.zeros(int(getattr(L, bytes_fn)()) // 4, dtype=torch.int32, device=device)
+        table[key] = t
     return t
+
+
+def _ov_sync(device) -> Optional[Tensor]:
+    return _sync_block(OV_SYNC, "dn_lstm_ov_sync_bytes", device)
 
 _ROWMAP_CACHE: Dict[Tuple[int, int, str], Tensor] = {}
 
@@ -197,79 +230,227 @@ class _BiLSTMFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout: Optional[Tensor], dhT: Optional[Tensor], dcT: Optional[Tensor]):
-        x2d, wih_p, whh_p, whhT_p, bias_p, pre, c_save, hprev = ctx.saved_tensors
-        params = ctx.params
-        B, S, I, Hd, HD, ndir, mode, enc_dtype = ctx.meta
+        dx, dpre_v = _lstm_backward(ctx, ctx.saved_tensors, dout, dhT, dcT,
+                                    ctx.needs_input_grad[0])
+        # a differentiable precomputed projection (``project``: split capture at the projection
+        # output) receives the gate gradients themselves: d xp = dpre
+        dxp = dpre_v if ctx.needs_input_grad[4] else None
+        return (dx, None, None, None, dxp, None) + (None,) * len(ctx.params)
+
+
+def _lstm_backward(ctx, saved, dout: Optional[Tensor], dhT: Optional[Tensor],
+                   dcT: Optional[Tensor], need_dx: bool):
+    """Backward of the fused bi-LSTM (steps 4-7 of the module docstring); ``saved`` = the
+    forward's ``(x2d, wih_p, whh_p, whhT_p, bias_p, pre, c_save, hprev)``.  Returns ``(dx,
+    dpre)``: the input gradient (``need_dx``, premasked by the input ReLU when ``ctx.relu_in``)
+    and the gate gradients ``[B*S, ndir*4HD]`` (bf16)."""
+    x2d, wih_p, whh_p, whhT_p, bias_p, pre, c_save, hprev = saved
+    params = ctx.params
+    B, S, I, Hd, HD, ndir, mode, enc_dtype = ctx.meta
+    GP = 4 * HD
+    N = B * S
+    Bp = c_save.shape[1]
+    dev = x2d.device
+    st = _lib.stream()
+    # (4) the forward kernel stored the gate pre-activations
+    # (5) reverse-time recurrence
+    if dout is None:
+        dout = torch.zeros((B, ndir * Hd) if mode == "mean" else (B, S, ndir * Hd),
+                           dtype=torch.float32, device=dev)
+    dout = dout.float().contiguous()
+    if mode == "mean":
+        sb, stt, scale = ndir * Hd, 0, 1.0 / S
+    else:
+        sb, stt, scale = S * ndir * Hd, ndir * Hd, 1.0
+    dhT = None if dhT is None else dhT.float().contiguous()
+    dcT = None if dcT is None else dcT.float().contiguous()
+    dpre = torch.empty(Bp * S, ndir * GP, dtype=torch.bfloat16, device=dev)
+    dpre_v = dpre[:N]
+    capturing = _cap.active() is not None and ctx.modules is not None
+    done = False
+    sync = _ov_sync(dev) if (OVERLAP_BWD and mode == "mean" and HD == 192
+                             and all(p is not None for p in params)) else None
+    if sync is not None:
+        # (5)+(6) in ONE launch: the LSTM weight / bias gradients accumulate into .grad on
+        # the CUs the recurrence leaves idle, block by block as it publishes dpre
+        gl = []
+        for d in range(ndir):
+            w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
+            gl += [_grad.grad_buffer(w_ih), _grad.grad_buffer(w_hh), _grad.grad_buffer(b_ih),
+                   _grad.grad_buffer(b_hh)]
+        gp = (ctypes.c_void_p * 8)(*([g.data_ptr() for g in gl] + [None] * (8 - len(gl))))
+        rc = _lib.lib().dn_lstm_bwd_ov(
+            pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(), dout.data_ptr(), sb, scale,
+            _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir, dpre.data_ptr(), x2d.data_ptr(), I,
+            hprev.data_ptr(), gp, sync.data_ptr(), st)
+        if rc == 0:
+            done = True
+            _grad.notify([p for p in params if p is not None])
+        elif rc != 3:  # 3 = outside the overlapped kernel's envelope
+            raise RuntimeError(f"dn_lstm_bwd_ov failed with status {rc}")
+    if not done:
+        _lib.call("dn_lstm_bwd", pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
+                  dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd,
+                  ndir, dpre.data_ptr(), st)
+        # (6) parameter grads accumulated into .grad (reference layout via row map): queued
+        # for the end-of-backward grouped launch together with the encoder's (ops._grad.defer)
+        probs = _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
+        _grad.defer(probs, [p for p in params if p is not None])
+    # (7) input grad
+    dx = None
+    if need_dx:
+        if ctx.relu_in and not PLAIN_BLAS:
+            # the input is a ReLU output consumed only here: the ReLU backward's mask rides
+            # in this GEMM's epilogue (d input where input <= 0 cannot reach anything), and
+            # the encoder backward skips its own mask launch for exactly this tensor
+            dx = mm(dpre_v, wih_p, out_dtype=torch.bfloat16, mask=x2d)
+            from .linear import mark_premasked
+            mark_premasked(dx)
+            dx = dx.view(B, S, I)
+        else:
+            dx = mm_plain(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
+        if enc_dtype != torch.bfloat16:
+            dx = dx.to(enc_dtype)
+    if capturing:
+        dref = dpre_v.view(N, ndir, HD, 4)[:, :, :Hd, :].transpose(2, 3).reshape(N, ndir, 4 * Hd)
+        for d, cell in enumerate(ctx.modules):
+            _cap.record(cell.i2h, x2d, dref[:, d])
+            _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
+    return dx, dpre_v
+
+
+class _EncBiLSTMFn(torch.autograd.Function):
+    """The ICA encoder ``ReLU(x W_e^T + b_e)`` and the bi-LSTM (temporal mean) in ONE forward
+    launch (``dn_lstm_fwd_ov``: encoder and input-projection tiles produced time chunk by time
+    chunk on the CUs the recurrence leaves idle, the recurrence waiting per chunk).  Outside that
+    kernel's envelope the same values come from the three-launch form (encoder GEMM, projection
+    GEMM, ``dn_lstm_fwd``).  Backward: the LSTM backward (``_lstm_backward``, its input gradient
+    masked by the ReLU in the GEMM epilogue), then the encoder's weight / bias gradients deferred
+    into the end-of-backward grouped launch -- the same launches as encoder + ``_BiLSTMFn``."""
+
+    @staticmethod
+    def forward(ctx, x2d: Tensor, enc_w: Tensor, enc_b: Tensor, enc_wb: Tensor, enc_module,
+                modules, packed, B: int, S: int, *params: Tensor):
+        ctx.set_materialize_grads(False)
+        ndir = len(params) // 4
+        Hd = params[2].shape[1]
+        HD = padded_hidden(Hd)
         GP = 4 * HD
-        N = B * S
-        Bp = c_save.shape[1]
+        I, CW = enc_w.shape
+        BR = int(_lib.lib().dn_lstm_rows_per_wg(B, Hd))
+        Bp = (B + BR - 1) // BR * BR
         dev = x2d.device
         st = _lib.stream()
-        # (4) the forward kernel stored the gate pre-activations
-        # (5) reverse-time recurrence
-        if dout is None:
-            dout = torch.zeros((B, ndir * Hd) if mode == "mean" else (B, S, ndir * Hd),
-                               dtype=torch.float32, device=dev)
-        dout = dout.float().contiguous()
-        if mode == "mean":
-            sb, stt, scale = ndir * Hd, 0, 1.0 / S
-        else:
-            sb, stt, scale = S * ndir * Hd, ndir * Hd, 1.0
-        dhT = None if dhT is None else dhT.float().contiguous()
-        dcT = None if dcT is None else dcT.float().contiguous()
-        dpre = torch.empty(Bp * S, ndir * GP, dtype=torch.bfloat16, device=dev)
-        dpre_v = dpre[:N]
-        capturing = _cap.active() is not None and ctx.modules is not None
-        done = False
-        sync = _ov_sync(dev) if (OVERLAP_BWD and mode == "mean" and HD == 192
-                                 and all(p is not None for p in params)) else None
+        wih_p, bias_p, whh_p, whhT_p, ev = packed
+        if ev is not None:
+            torch.cuda.current_stream(dev).wait_event(ev)
+        enc = torch.empty(B * S, I, dtype=torch.bfloat16, device=dev)
+        xp = torch.empty(B * S, ndir * GP, dtype=torch.bfloat16, device=dev)
+        c_save = torch.empty(ndir, Bp, S, HD, dtype=torch.float32, device=dev)
+        hprev = torch.empty(ndir, Bp, S, HD, dtype=torch.bfloat16, device=dev)
+        hT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
+        cT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
+        hmean = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
+        need_bwd = any(ctx.needs_input_grad)
+        pre = torch.empty(B * S, ndir * GP, dtype=torch.float32, device=dev) if need_bwd else None
+        bsplit = ndir * GP if bias_p.numel() == 2 * ndir * GP else 0
+        sync = _sync_block(FOV_SYNC, "dn_lstm_fwd_ov_sync_bytes", dev)
+        rc = 3
+        enc_in = FOV_MODE != "full"
+        if enc_in:
+            enc = mm(x2d, enc_wb, trans_b=True, bias=enc_b, relu=True, out_dtype=torch.bfloat16)
         if sync is not None:
-            # (5)+(6) in ONE launch: the LSTM weight / bias gradients accumulate into .grad on
-            # the CUs the recurrence leaves idle, block by block as it publishes dpre
-            gl = []
-            for d in range(ndir):
-                w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
-                gl += [_grad.grad_buffer(w_ih), _grad.grad_buffer(w_hh), _grad.grad_buffer(b_ih),
-                       _grad.grad_buffer(b_hh)]
-            gp = (ctypes.c_void_p * 8)(*([g.data_ptr() for g in gl] + [None] * (8 - len(gl))))
-            rc = _lib.lib().dn_lstm_bwd_ov(
-                pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(), dout.data_ptr(), sb, scale,
-                _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir, dpre.data_ptr(), x2d.data_ptr(), I,
-                hprev.data_ptr(), gp, sync.data_ptr(), st)
-            if rc == 0:
-                done = True
-                _grad.notify([p for p in params if p is not None])
-            elif rc != 3:  # 3 = outside the overlapped kernel's envelope
-                raise RuntimeError(f"dn_lstm_bwd_ov failed with status {rc}")
-        if not done:
-            _lib.call("dn_lstm_bwd", pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
-                      dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd,
-                      ndir, dpre.data_ptr(), st)
-            # (6) parameter grads accumulated into .grad (reference layout via row map): queued
-            # for the end-of-backward grouped launch together with the encoder's (ops._grad.defer)
-            probs = _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
-            _grad.defer(probs, [p for p in params if p is not None])
-        # (7) input grad
-        dx = None
-        if ctx.needs_input_grad[0]:
-            if ctx.relu_in and not PLAIN_BLAS:
-                # the input is a ReLU output consumed only here: the ReLU backward's mask rides
-                # in this GEMM's epilogue (d input where input <= 0 cannot reach anything), and
-                # the encoder backward skips its own mask launch for exactly this tensor
-                dx = mm(dpre_v, wih_p, out_dtype=torch.bfloat16, mask=x2d)
-                from .linear import mark_premasked
-                mark_premasked(dx)
-                dx = dx.view(B, S, I)
-            else:
-                dx = mm_plain(dpre_v, wih_p, out_dtype=torch.bfloat16).view(B, S, I)
-            if enc_dtype != torch.bfloat16:
-                dx = dx.to(enc_dtype)
-        if capturing:
-            dref = dpre_v.view(N, ndir, HD, 4)[:, :, :Hd, :].transpose(2, 3).reshape(N, ndir, 4 * Hd)
-            for d, cell in enumerate(ctx.modules):
-                _cap.record(cell.i2h, x2d, dref[:, d])
-                _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
-        return (dx, None, None, None, None, None) + (None,) * len(params)
+            rc = _lib.lib().dn_lstm_fwd_ov(
+                x2d.data_ptr(), CW, enc_wb.data_ptr(), enc_b.data_ptr(), enc.data_ptr(), I,
+                wih_p.data_ptr(), xp.data_ptr(), bias_p.data_ptr(), bsplit, whh_p.data_ptr(), B, S,
+                Hd, ndir, c_save.data_ptr(), hprev.data_ptr(), hmean.data_ptr(), 1.0 / S,
+                hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), sync.data_ptr(), FOV_TC, FOV_WG,
+                int(enc_in), st)
+        if rc == 3:  # outside the overlapped kernel's envelope: the three-launch form
+            if not enc_in:
+                enc = mm(x2d, enc_wb, trans_b=True, bias=enc_b, relu=True,
+                         out_dtype=torch.bfloat16)
+            xp = mm_plain(enc, wih_p, trans_b=True, out_dtype=torch.bfloat16)
+            _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
+                      ndir, c_save.data_ptr(), hprev.data_ptr(), None, hmean.data_ptr(), 1.0 / S,
+                      hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), bsplit, st)
+        elif rc != 0:
+            raise RuntimeError(f"dn_lstm_fwd_ov failed with status {rc}")
+        ctx.save_for_backward(enc, wih_p, whh_p, whhT_p, bias_p, pre, c_save, hprev, x2d)
+        ctx.params = params
+        ctx.relu_in = True
+        ctx.meta = (B, S, I, Hd, HD, ndir, "mean", torch.bfloat16)
+        ctx.modules = modules
+        ctx.enc = (enc_w, enc_b, enc_module)
+        ctx.overlapped = rc == 0
+        return hmean, hT, cT
+
+    @staticmethod
+    def backward(ctx, dout: Optional[Tensor], dhT: Optional[Tensor], dcT: Optional[Tensor]):
+        saved = ctx.saved_tensors
+        B, S, I = ctx.meta[:3]
+        dx, _ = _lstm_backward(ctx, saved[:8], dout, dhT, dcT, True)
+        from .linear import _take_premasked, defer_linear_grads
+        dym = dx.view(B * S, I)
+        _take_premasked(dym)  # masked in the input-gradient GEMM's epilogue
+        enc_w, enc_b, enc_module = ctx.enc
+        defer_linear_grads(saved[8], dym, enc_w, enc_b, enc_module)
+        return (None,) * 9 + (None,) * len(ctx.params)
+
+
+class _ProjFn(torch.autograd.Function):
+    """The LSTM input projection of both directions, ``xp = enc W_ih^T`` (bf16, packed gate
+    columns), as an autograd node of its own: the split capture of a multi-site step cuts the
+    backward HERE (``runtime.step.TrainStep``), so everything after the projection -- the
+    recurrences, the head and every LSTM / head weight gradient -- is final before the input
+    gradient ``d enc = dpre W_ih`` (ReLU mask in its epilogue) and the encoder's gradients run,
+    and the all-reduce of the LSTM + head gradients overlaps those."""
+
+    @staticmethod
+    def forward(ctx, enc: Tensor, wih_p: Tensor, relu_in: bool):
+        B, S, I = enc.shape
+        x2d = enc.reshape(B * S, I)
+        if x2d.dtype != torch.bfloat16:
+            x2d = x2d.to(torch.bfloat16)
+        x2d = x2d.contiguous()
+        ctx.save_for_backward(x2d, wih_p)
+        ctx.meta = (B, S, I, enc.dtype, bool(relu_in))
+        return mm_plain(x2d, wih_p, trans_b=True, out_dtype=torch.bfloat16)
+
+    @staticmethod
+    def backward(ctx, dxp: Tensor):
+        x2d, wih_p = ctx.saved_tensors
+        B, S, I, dt, relu_in = ctx.meta
+        dxp = dxp.to(torch.bfloat16).contiguous()
+        if relu_in and not PLAIN_BLAS:
+            dx = mm(dxp, wih_p, out_dtype=torch.bfloat16, mask=x2d)
+            from .linear import mark_premasked
+            mark_premasked(dx)
+        else:
+            dx = mm_plain(dxp, wih_p, out_dtype=torch.bfloat16)
+        dx = dx.view(B, S, I)
+        return (dx if dt == torch.bfloat16 else dx.to(dt)), None, None
+
+
+def project(enc: Tensor, packed, relu_input: bool = False) -> Tensor:
+    """Differentiable LSTM input projection ``[B, S, I] -> [B*S, ndir*4HD]`` with the packed
+    weights of ``pack_params`` (see :class:`_ProjFn`); feed it to :func:`bilstm` as ``xp``."""
+    wih_p, _, _, _, ev = packed
+    if ev is not None:
+        torch.cuda.current_stream(enc.device).wait_event(ev)
+    return _ProjFn.apply(enc, wih_p, bool(relu_input))
+
+
+def enc_bilstm(x2d: Tensor, lin, w_bf16: Tensor, packed, lstm_module, B: int, S: int) -> Tensor:
+    """``mean_t biLSTM(ReLU(x W^T + b))`` for ``x2d = [B*S, C*W]`` (bf16) through
+    :class:`_EncBiLSTMFn`; ``lin`` is the encoder ``nn.Linear``, ``w_bf16`` its bf16 image and
+    ``packed`` the LSTM's packed operands (``pack_params``).  Returns ``hmean [B, ndir*Hd]``."""
+    if not _lib.native_available():
+        raise RuntimeError("fused encoder + LSTM requested but the gfx950 kernel library is not built")
+    params = [t for cell in lstm_module.lstms for t in cell.params()]
+    hmean, _, _ = _EncBiLSTMFn.apply(x2d.contiguous(), lin.weight, lin.bias, w_bf16, lin,
+                                     list(lstm_module.lstms), packed, B, S, *params)
+    return hmean
 
 
 def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = False,

@@ -12,10 +12,13 @@ copies the labels and zeroes the flat gradient.  With a single site the fused Ad
 captured too (its step number lives on the device), so a step is prologue + one replay.
 
 Split capture (dSGD across sites): the model's ``stem`` (ICA: the encoder) produces the LAST
-gradients of the backward, so the step is captured as TWO graphs cut at the stem output —
-A = zero-grad + forward + backward of everything after the stem (its input gradient included),
-B = the stem's backward.  Between the replays the all-reduce of every non-stem gradient starts on
-RCCL's stream and runs under graph B; only the small stem bucket's all-reduce is exposed.
+gradients of the backward, so the step is captured as TWO graphs cut inside the backward —
+A = zero-grad + forward + backward of everything after the cut, B = the rest.  The cut is the
+LSTM input projection when the model provides ``proj_stem`` (A then ends with every LSTM and head
+gradient final; B = the input-gradient GEMM + the encoder's weight gradients), else the stem
+output (B = the encoder's weight gradients).  Between the replays the all-reduce of every
+non-stem gradient starts on RCCL's stream and runs under graph B; only the small stem bucket's
+all-reduce is exposed.
 """
 from __future__ import annotations
 
@@ -50,6 +53,11 @@ CAPTURE_MODE = "thread_local"
 # The LSTM weight repack leaves the graph and rides in the step prologue's launch
 # (DINUNET_DEFER_PACK=0 keeps it captured)
 DEFER_PACK = os.environ.get("DINUNET_DEFER_PACK", "1") != "0"
+
+# Split capture (dSGD across sites) cuts at the LSTM input projection when the model allows
+# (DINUNET_SPLIT_AT=stem keeps the encoder-output cut): graph B is then the input-gradient GEMM +
+# the encoder's weight gradients, ~25 us at the headline step instead of ~10
+SPLIT_AT_PROJECTION = os.environ.get("DINUNET_SPLIT_AT", "projection") != "stem"
 
 # Device-fed single-site steps: the fused Adam rewrites the packed LSTM / encoder operand images
 # from the parameters it updates, zeroes the gradient and gathers the next batch (one launch
@@ -107,6 +115,7 @@ class TrainStep:
             env = os.environ.get("DINUNET_SPLIT_GRAPH", "")
             split = can_split and (engine.group.distributed if env == "" else env == "1")
         self.split = bool(split and can_split)
+        self.split_at = None  # "projection" | "stem", set at capture
         self._first_buckets = engine.split_buckets(list(model.stem_parameters())) if self.split else []
         self.graph_b = None
         self._one = None
@@ -236,6 +245,24 @@ class TrainStep:
     def _defer_pack(self):
         return defer_pack() if DEFER_PACK else _NoDefer()
 
+    def _split_fwd_bwd(self, sx, sy):
+        """Graph A of a split step: forward, loss and the backward of everything after the cut
+        (returns the cut tensor ``h``, its detached twin ``hd`` holding d loss / d h, and the
+        step outputs).  The cut is the LSTM input projection when the model has the fused path
+        (``proj_stem``: every LSTM / head gradient is then final in graph A and only the input
+        gradient + encoder gradients remain for graph B), else the stem (encoder) output."""
+        at_proj = (SPLIT_AT_PROJECTION and hasattr(self.model, "proj_stem")
+                   and self.model.split_at_projection(sx))
+        self.split_at = "projection" if at_proj else "stem"
+        with self.engine.step_context():
+            h = self.model.proj_stem(sx) if at_proj else self.model.stem(sx)
+            hd = h.detach().requires_grad_(h.requires_grad)
+            with ops.head.loss_grad_hint(self._grad_one(sx.device)):
+                body = self.model.proj_body_loss if at_proj else self.model.body_loss
+                out, loss, pred = body(hd, sy)
+            self._backward(loss)
+        return h, hd, out, loss, pred
+
     def _capture_split(self, x, y):
         sx, sy = self._static_inputs(x, y)
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -243,12 +270,7 @@ class TrainStep:
         self.graph_opt = False
         try:
             with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE), self._defer_pack() as dp:
-                with self.engine.step_context():
-                    h = self.model.stem(sx)
-                    hd = h.detach().requires_grad_(h.requires_grad)
-                    with ops.head.loss_grad_hint(self._grad_one(sx.device)):
-                        out, loss, pred = self.model.body_loss(hd, sy)
-                    self._backward(loss)
+                h, hd, out, loss, pred = self._split_fwd_bwd(sx, sy)
             with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):
                 if h.requires_grad:
                     torch.autograd.backward(h, hd.grad)
@@ -455,8 +477,8 @@ class TrainStep:
 
     def _dev_capture_split(self):
         """Device-fed form of :meth:`_capture_split`: graph A = prologue + forward + backward
-        down to the stem output, graph B = the stem's backward (the all-reduce of every other
-        gradient runs between the two replays)."""
+        down to the cut (:meth:`_split_fwd_bwd`), graph B = the rest (the all-reduce of every
+        non-stem gradient runs between the two replays)."""
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         sx, sy = self._dsx, self._dsy
         self.engine.sync_enabled = False
@@ -464,12 +486,7 @@ class TrainStep:
             with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
                 with (self._apack_forward() if self._apack is not None
                       else self._dev_prologue(None)) as rp:
-                    with self.engine.step_context():
-                        h = self.model.stem(sx)
-                        hd = h.detach().requires_grad_(h.requires_grad)
-                        with ops.head.loss_grad_hint(self._grad_one(sx.device)):
-                            out, loss, pred = self.model.body_loss(hd, sy)
-                        self._backward(loss)
+                    h, hd, out, loss, pred = self._split_fwd_bwd(sx, sy)
                 if isinstance(rp, ride_pack) and not rp.consumed:
                     raise RuntimeError("device-fed prologue was not absorbed by the weight pack")
             with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):

@@ -18,8 +18,10 @@ fused Adam.  Agreement is judged on the parameter UPDATE (final - initial): the 
 of the N-rank update against the oracle's is reported (``update_rel_err``) and, at
 ``--precision 32``, must stay below ``--oracle-tol``; at 16 bits it measures what the payload
 precision costs after Adam (which turns the sign of every near-zero mean gradient into a full
-``lr`` step, so it amplifies payload rounding).  For dSGD the first step's reduced gradient is
-also compared with the fp64 mean (``grad_rel_err``): the payload's own error.  (Bit-identical replicas alone would also pass if every rank applied the same
+``lr`` step, so it amplifies payload rounding).  For every engine the first step's reduced
+gradient is also compared with the oracle's (``grad_rel_err``, bounded by ``--grad-tol``): the
+payload's own error for dSGD, and for rank-dAD / PowerSGD the distance between the engine's
+reconstruction and the fp64 replay of the same factorisation.  (Bit-identical replicas alone would also pass if every rank applied the same
 WRONG update.)
 """
 import argparse
@@ -194,7 +196,7 @@ def main():
         step.run(a.steps)
     for i, x, y in (site_batches(grp.rank) if a.feed == "host" else ()):
         step(x, y, first=i % a.accum == 0, last=i % a.accum == a.accum - 1)
-        if i == a.accum - 1 and a.engine == "dSGD":  # the first reduced gradient (payload error)
+        if i == a.accum - 1:  # the first reduced gradient (every engine writes it to flat.grad)
             g_first = (flat.grad.double() * getattr(eng, "last_scale", 1.0)).clone()
     if dev.type == "cuda":
         torch.cuda.synchronize()
