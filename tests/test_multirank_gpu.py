@@ -22,16 +22,40 @@ CASES = [
     (2, ["--engine", "powerSGD", "--precision", "16", "--accum", "2"]),
     (4, ["--engine", "dSGD", "--precision", "16", "--accum", "2", "--ragged"]),
     (4, ["--engine", "rankDAD", "--precision", "16"]),
-    # against the fp64-mean oracle (tools/multirank_check.py --oracle): fp32 wire, the reference's
-    # fp16 wire through the direct exchange, bf16 wire, and the 16-bit all-reduce it replaces
+    # against the fp64 oracle of each engine (tools/multirank_check.py --oracle: every site's own
+    # gradient, the engine's reduction replayed in fp64).  --grad-tol bounds the FIRST step's
+    # reduced gradient (the engine / payload error itself); --oracle-tol bounds the 8-step
+    # parameter update, which Adam amplifies (a near-zero mean gradient's sign becomes a full lr
+    # step).  Tolerances are ~2-4x the values observed on MI355X (profiles/r4_oracle_obs.jsonl):
+    # dSGD fp32 grad 2.2e-8 / update 5.5e-8; fp16 3.0e-4 / 0.12; bf16 2.3e-3 / 0.11;
+    # rank-dAD fp32 2.7e-7 (w2) 3.2e-7 (w3) / 0.11-0.18, fp16 2.7e-4 / 0.25;
+    # PowerSGD fp32 2.1e-7 / 0.10, fp16 3.7e-4 / 0.17
     (2, ["--engine", "dSGD", "--precision", "32", "--oracle"]),
-    (3, ["--engine", "dSGD", "--precision", "16", "--oracle", "--ragged"]),
-    (2, ["--engine", "dSGD", "--precision", "16", "--payload", "bf16", "--oracle"]),
-    (2, ["--engine", "dSGD", "--precision", "16", "--collective", "allreduce", "--oracle"]),
+    (3, ["--engine", "dSGD", "--precision", "16", "--oracle", "--ragged", "--oracle-tol", "0.3",
+         "--grad-tol", "1e-3"]),
+    (2, ["--engine", "dSGD", "--precision", "16", "--payload", "bf16", "--oracle",
+         "--oracle-tol", "0.3", "--grad-tol", "6e-3"]),
+    (2, ["--engine", "dSGD", "--precision", "16", "--collective", "allreduce", "--oracle",
+         "--oracle-tol", "0.3", "--grad-tol", "6e-3"]),
+    (2, ["--engine", "rankDAD", "--precision", "32", "--dad-tol", "0", "--oracle",
+         "--grad-tol", "1e-6", "--oracle-tol", "0.4"]),
+    (3, ["--engine", "rankDAD", "--precision", "32", "--dad-tol", "0", "--oracle",
+         "--grad-tol", "1e-6", "--oracle-tol", "0.45"]),
+    (2, ["--engine", "rankDAD", "--precision", "16", "--dad-tol", "0", "--oracle",
+         "--grad-tol", "8e-4", "--oracle-tol", "0.5"]),
+    (2, ["--engine", "powerSGD", "--precision", "32", "--oracle", "--grad-tol", "1e-6",
+         "--oracle-tol", "0.25"]),
+    (3, ["--engine", "powerSGD", "--precision", "32", "--oracle", "--grad-tol", "1e-6",
+         "--oracle-tol", "0.25"]),
+    (2, ["--engine", "powerSGD", "--precision", "16", "--oracle", "--grad-tol", "1e-3",
+         "--oracle-tol", "0.35"]),
+    (2, ["--engine", "powerSGD", "--precision", "32", "--accum", "2", "--oracle",
+         "--grad-tol", "1e-6", "--oracle-tol", "0.25"]),
     # the bench path across sites: HBM-resident batches, split capture, the fused Adam emitting
     # the next step's operands after the all-reduce
     (2, ["--engine", "dSGD", "--precision", "32", "--feed", "device", "--oracle"]),
-    (3, ["--engine", "dSGD", "--precision", "16", "--feed", "device", "--oracle"]),
+    (3, ["--engine", "dSGD", "--precision", "16", "--feed", "device", "--oracle",
+         "--oracle-tol", "0.3"]),
 ]
 
 
@@ -54,6 +78,8 @@ def test_replicas_bit_identical(world, args):
         with open(log, "a") as f:
             f.write(json.dumps({"test": "multirank", "args": args, **res}) + "\n")
     assert res["ok"], res
+    if "--oracle" in args:  # the oracle ran and judged both the gradient and the update
+        assert res.get("oracle_ok") is True and "grad_rel_err" in res, res
     assert res["graph"] and res["world"] == world
     if "device" in args:  # the bench path: the update emits the next step's operands
         assert res["adam_pack"] and res["split"], res

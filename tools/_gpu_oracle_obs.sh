@@ -25,3 +25,4 @@ done <<'CASES'
 2 --engine powerSGD --precision 16
 2 --engine powerSGD --precision 32 --accum 2
 CASES
+exit 0
