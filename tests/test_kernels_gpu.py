@@ -368,8 +368,8 @@ def test_lstm_rows_per_workgroup_variants(br, monkeypatch):
             assert rel(t.grad, tr.grad) < 5e-2
 
 
-@pytest.mark.parametrize("splits", [1, 3, None])
-def test_gemm_grouped_matches_per_problem(splits):
+@pytest.mark.parametrize("splits,tile", [(1, None), (3, None), (None, None), (3, 1)])
+def test_gemm_grouped_matches_per_problem(splits, tile):
     from dinunet_implementations_amd.ops.gemm import mm_grouped
     torch.manual_seed(7)
     shapes = [(768, 256, 3136), (768, 192, 3136), (100, 70, 500), (64, 64, 64)]
@@ -384,7 +384,7 @@ def test_gemm_grouped_matches_per_problem(splits):
         ref[rmap.long()] = 0.5 * (a.float().t() @ b.float()) + bias + ref[rmap.long()]
         probs.append(dict(a=a, b=b, out=out, alpha=0.5, beta=1.0, row_map=rmap, bias=bias))
         refs.append(ref)
-    mm_grouped(probs, trans_a=True, splits=splits)
+    mm_grouped(probs, trans_a=True, splits=splits, tile=tile)
     for q, ref in zip(probs, refs):
         assert rel(q["out"], ref) < 2e-3
 

@@ -78,8 +78,10 @@ def test_replicas_bit_identical(world, args):
         with open(log, "a") as f:
             f.write(json.dumps({"test": "multirank", "args": args, **res}) + "\n")
     assert res["ok"], res
-    if "--oracle" in args:  # the oracle ran and judged both the gradient and the update
-        assert res.get("oracle_ok") is True and "grad_rel_err" in res, res
+    if "--oracle" in args:  # the oracle ran and judged the update (and, host-fed, the gradient)
+        assert res.get("oracle_ok") is True, res
+        if "device" not in args:  # (device-fed: the fused Adam zeroes the gradient it consumes)
+            assert "grad_rel_err" in res, res
     assert res["graph"] and res["world"] == world
     if "device" in args:  # the bench path: the update emits the next step's operands
         assert res["adam_pack"] and res["split"], res

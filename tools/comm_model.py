@@ -20,7 +20,7 @@ measures on ONE MI355X what the N > 1 step is made of and combines it with a sta
 Exposed communication per step = max(0, T(body bucket) - T(graph B)) + T(stem bucket): the body
 bucket's collective starts between the replays, the stem (encoder) bucket after graph B.
 
-    python tools/comm_model.py [--b-link-gbs 64] [--alpha-us 6] [--rings 4]
+    python tools/comm_model.py [--b-link-gbs 64] [--alpha-us 2 6] [--rings 4] [--from-json F]
 """
 from __future__ import annotations
 
@@ -77,7 +77,8 @@ def split_graphs(at: str):
 
 
 def direct_kernels(n: int, world: int, payload: str) -> float:
-    """pack + rowsum + unpack of one DirectMean exchange of ``n`` fp32 elements (us)."""
+    """pack + rowsum + unpack of one DirectMean exchange of ``n`` fp32 elements: (device us as a
+    graph replay, us per exchange issued eagerly from Python)."""
     import torch
     from dinunet_implementations_amd.parallel import collective as C
     code, dt = C.PAYLOAD_TYPES[payload]
@@ -91,64 +92,109 @@ def direct_kernels(n: int, world: int, payload: str) -> float:
         C.to_payload(x, send, world, chunk, amax=amax)
         C.rowsum(send, mine, world, chunk, 1.0 / world)
         C.from_payload(send, x, world, chunk, 1.0, amax=amax)
-    return _time(run)
+    # device time of the kernels (a graph replay), and separately what issuing them from Python
+    # costs per exchange (ctypes launches: the host side of the eager exchange)
+    run()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()
+    torch.cuda.current_stream().wait_stream(s)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        run()
+    return _time(gr.replay), _time(run)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--b-link-gbs", type=float, default=64.0,
-                    help="effective per-link one-direction xGMI bandwidth an RCCL channel gets")
-    ap.add_argument("--alpha-us", type=float, default=6.0, help="per-hop / per-phase latency")
-    ap.add_argument("--rings", type=int, default=4, help="concurrent rings (channels) of RCCL")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4_comm_model.md"))
-    a = ap.parse_args()
-    b = a.b_link_gbs * 1e3  # bytes per us
-    res = {}
-    for at in ("projection", "stem"):
-        res[at] = split_graphs(at)
-    ta, tb, body, stem = res["projection"]
+def measure() -> dict:
+    """The GPU-measured inputs of the model (see the module docstring)."""
+    res = {at: split_graphs(at) for at in ("projection", "stem")}
+    body = res["projection"][2]
+    local, host = {}, {}
+    for N in (2, 4, 8):
+        for w in ("fp32", "fp16", "bf16"):
+            local[f"{N}/{w}"], host[f"{N}/{w}"] = direct_kernels(int(body // 4), N, w)
+    return {"graphs": {k: list(v) for k, v in res.items()}, "local_us": local,
+            "local_eager_us": host}
+
+
+def model(meas: dict, b_gbs: float, alpha: float, rings: int):
+    """Rows of the exposed-communication table for one link-model parameter set."""
+    b = b_gbs * 1e3  # bytes per us
+    g = meas["graphs"]
+    body, stem = g["projection"][2], g["projection"][3]
     rows = []
-    lines = ["# Multi-site dSGD step: exposed-communication model (1 MI355X measured + link model)",
-             "",
-             "Measured on one MI355X (`tools/comm_model.py`): the split step's graphs at the "
-             "headline config (ICA-LSTM B=32, S=98, H=384).  Link model (NOT measured: no multi-GPU "
-             f"run is available to the builder): per-link one-direction bandwidth {a.b_link_gbs} "
-             f"GB/s, per-phase latency {a.alpha_us} us, RCCL ring all-reduce over {a.rings} "
-             "concurrent rings; direct exchange = all-to-all + all-gather with every peer on its "
-             "own link.  No scaling curve is claimed.", "",
-             "| cut | graph A us | graph B us (hides the body bucket) | body bucket MB | stem bucket MB |",
-             "|---|---:|---:|---:|---:|"]
-    for at, (xa, xb, bb, sb) in res.items():
-        lines.append(f"| {at} | {xa:.1f} | {xb:.1f} | {bb / 2**20:.2f} | {sb / 2**20:.2f} |")
-    lines += ["", "| N | wire | collective | T(body) us | T(stem) us | local kernels us | exposed us (cut: projection) | exposed us (cut: stem) |",
-              "|---:|---|---|---:|---:|---:|---:|---:|"]
     for N in (2, 4, 8):
         for wire, coll in (("fp32", "ring all-reduce"), ("fp32", "direct"), ("fp16", "direct"),
                            ("bf16", "direct")):
             es = 4 if wire == "fp32" else 2
             nb, ns = body / 4 * es, stem / 4 * es
             if coll == "ring all-reduce":
-                t = lambda by: 2 * (N - 1) / N * by / (a.rings * b) + 2 * (N - 1) * a.alpha_us
+                def t(by):
+                    return 2 * (N - 1) / N * by / (rings * b) + 2 * (N - 1) * alpha
                 loc = 0.0
             else:
-                t = lambda by: 2 * (by / N / b + a.alpha_us)
-                loc = direct_kernels(int(body // 4), N, wire)
+                def t(by):
+                    return 2 * (by / N / b + alpha)
+                loc = meas["local_us"][f"{N}/{wire}"]
             tbody, tstem = t(nb) + loc, t(ns)
-            exp_p = max(0.0, tbody - res["projection"][1]) + tstem
-            exp_s = max(0.0, tbody - res["stem"][1]) + tstem
             rows.append({"N": N, "wire": wire, "collective": coll, "t_body_us": tbody,
-                         "t_stem_us": tstem, "local_us": loc, "exposed_projection_us": exp_p,
-                         "exposed_stem_us": exp_s})
-            lines.append(f"| {N} | {wire} | {coll} | {tbody:.1f} | {tstem:.1f} | {loc:.1f} | "
-                         f"{exp_p:.1f} | {exp_s:.1f} |")
+                         "t_stem_us": tstem, "local_us": loc,
+                         "exposed_projection_us": max(0.0, tbody - g["projection"][1]) + tstem,
+                         "exposed_stem_us": max(0.0, tbody - g["stem"][1]) + tstem})
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b-link-gbs", type=float, default=64.0,
+                    help="effective per-link one-direction xGMI bandwidth an RCCL channel gets")
+    ap.add_argument("--alpha-us", type=float, nargs="+", default=[2.0, 6.0],
+                    help="per-hop / per-phase latencies to tabulate")
+    ap.add_argument("--rings", type=int, default=4, help="concurrent rings (channels) of RCCL")
+    ap.add_argument("--from-json", default=None,
+                    help="model from a previous run's measurements (the JSON line it printed)")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4_comm_model.md"))
+    a = ap.parse_args()
+    if a.from_json:
+        with open(a.from_json) as f:
+            meas = json.loads(f.read().strip().splitlines()[-1])
+        meas.setdefault("local_us", {f"{r['N']}/{r['wire']}": r["local_us"] for r in meas.get("rows", [])
+                                     if r["collective"] == "direct"})
+    else:
+        meas = measure()
+    g = meas["graphs"]
+    lines = ["# Multi-site dSGD step: exposed-communication model (1 MI355X measured + link model)",
+             "",
+             "Measured on one MI355X (`tools/comm_model.py`): the split step's two graphs at the "
+             "headline config (ICA-LSTM B=32, S=98, H=384) and the direct exchange's local kernels "
+             "(pack + fp32 rowsum + unpack of the body bucket).  The transfers come from a link "
+             "model, NOT a measurement (no multi-GPU run is available to the builder): per-link "
+             f"one-direction bandwidth {a.b_link_gbs} GB/s, RCCL ring all-reduce over {a.rings} "
+             "concurrent rings `2(N-1)/N * bytes / (rings * b) + 2(N-1) * alpha`, direct exchange "
+             "`2 * (bytes / N / b + alpha)` (all-to-all + all-gather, every peer on its own link).  "
+             "No scaling curve is claimed.", "",
+             "| cut | graph A us | graph B us (hides the body bucket) | body bucket MB | stem bucket MB |",
+             "|---|---:|---:|---:|---:|"]
+    for at, (xa, xb, bb, sb) in g.items():
+        lines.append(f"| {at} | {xa:.1f} | {xb:.1f} | {bb / 2**20:.2f} | {sb / 2**20:.2f} |")
+    for alpha in a.alpha_us:
+        lines += ["", f"alpha = {alpha} us:", "",
+                  "| N | wire | collective | T(body) us | T(stem) us | local kernels us | exposed us (cut: projection) | exposed us (cut: stem) |",
+                  "|---:|---|---|---:|---:|---:|---:|---:|"]
+        for r in model(meas, a.b_link_gbs, alpha, a.rings):
+            lines.append(f"| {r['N']} | {r['wire']} | {r['collective']} | {r['t_body_us']:.1f} | "
+                         f"{r['t_stem_us']:.1f} | {r['local_us']:.1f} | "
+                         f"{r['exposed_projection_us']:.1f} | {r['exposed_stem_us']:.1f} |")
     lines += ["", "Exposed = max(0, T(body) - T(graph B)) + T(stem): the body (LSTM + head) bucket's "
               "collective runs between the replays under graph B; the stem (encoder) bucket's after "
-              "it.  Local kernels = the direct exchange's pack + fp32 rowsum + unpack, measured "
-              "(they run on the comm stream, inside T(body))."]
+              "it.  Local kernels (device time of pack + rowsum + unpack, graph replay) run on the "
+              "comm stream inside T(body); issued eagerly from Python the same three launches "
+              "take the `local_eager_us` of the JSON line (host-bound)."]
     with open(a.out, "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
-    print(json.dumps({"graphs": {k: list(v) for k, v in res.items()}, "rows": rows}))
+    print(json.dumps(meas))
 
 
 if __name__ == "__main__":
