@@ -45,6 +45,12 @@ template <typename XT> struct Gate4Raw;
 template <> struct Gate4Raw<float> { typedef f32x4 type; };
 template <> struct Gate4Raw<bf16> { typedef bf16x4 type; };
 
+typedef __attribute__((ext_vector_type(2))) unsigned dn_u32x2;
+__device__ __forceinline__ f32x4 to_f32x4(const f32x4& v) { return v; }
+__device__ __forceinline__ f32x4 to_f32x4(const bf16x4& v) {
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
 // raw (unconverted) 4-gate load: keeps bf16 inputs packed in 2 VGPRs across the MFMA phase
 template <typename XT>
 __device__ __forceinline__ typename Gate4Raw<XT>::type load_raw4(const XT* p, bool ok) {
@@ -212,7 +218,9 @@ __device__ __forceinline__ void fov_wait(const FwdWait& fw, int dir, int chunk) 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load hoisted above the poll
 }
 
-template <int HD, int BR, bool SEQ, int UG, bool OV>
+// PT: element type of the stored gate pre-activations (float, or bf16 with
+// DINUNET_LSTM_PRE_BF16: half the bytes the forward writes and the backward reads per step)
+template <int HD, int BR, bool SEQ, int UG, bool OV, typename PT = float>
 __device__ __forceinline__ void
 fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, no bias (bf16)
           const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
@@ -223,7 +231,7 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
           float* __restrict__ hseq,        // SEQ: [Bp][S][ndir*HD] (processing order)
           float* __restrict__ hmean, float mean_scale,  // [B][ndir*Hd]
           float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
-          float* __restrict__ pre,  // [B*S][ndir][4*HD] fp32 gate pre-activations (+ bias), or null
+          PT* __restrict__ pre,  // [B*S][ndir][4*HD] gate pre-activations (+ bias), or null
           int bsplit,  // > 0: bias holds b_ih at [0] and b_hh at [bsplit], summed here
           const int bx, const int dir, const int gx, const FwdWait fw) {
   constexpr int NW = HD / (16 * UG);
@@ -307,7 +315,8 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
   const int nrow = B - b0 < BR ? B - b0 : BR;     // its valid rows
   const __amdgpu_buffer_rsrc_t x_rs = dn_rsrc(xp + (long)b0 * S * rowXi, (uint32_t)(nrow * S * rowXi * 2));
   const __amdgpu_buffer_rsrc_t pre_rs =
-      dn_rsrc(pre ? pre + (long)b0 * S * rowXi : pre, pre ? (uint32_t)(nrow * S * rowXi * 4) : 0u);
+      dn_rsrc(pre ? pre + (long)b0 * S * rowXi : pre,
+              pre ? (uint32_t)(nrow * S * rowXi * (int)sizeof(PT)) : 0u);
   const long cb0 = ((long)dir * Bp + b0) * S * HD;  // [ndir][Bp][S][HD] images
   const __amdgpu_buffer_rsrc_t c_rs = dn_rsrc(c_save + cb0, (uint32_t)(BR * S * HD * 4));
   const __amdgpu_buffer_rsrc_t hp_rs = dn_rsrc(hprev + cb0, (uint32_t)(BR * S * HD * 2));
@@ -315,12 +324,13 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
     xo[s] = (uint32_t)(((bc - b0) * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 2);
-    po[s] = b < B ? (uint32_t)(((b - b0) * S * rowXi + dir * 4 * HD + 4 * uu[s]) * 4) : DN_OOB;
+    po[s] = b < B ? (uint32_t)(((b - b0) * S * rowXi + dir * 4 * HD + 4 * uu[s]) * (int)sizeof(PT))
+                  : DN_OOB;
     co[s] = (uint32_t)((((b - b0) * S) * HD + uu[s]) * 4);
     ho[s] = (uint32_t)((((b - b0) * S) * HD + uu[s]) * 2);
   }
   const uint32_t xstep = (uint32_t)(rowXi * 2);  // bytes per time index (bf16 projection)
-  const uint32_t pstep = (uint32_t)(rowXi * 4);  // (fp32 pre-activations)
+  const uint32_t pstep = (uint32_t)(rowXi * (int)sizeof(PT));  // (pre-activations)
   // the 4 gate inputs of a slot stay packed (2 VGPRs, unconverted) while the load is in flight
   // (OV: the projection of a chunk is read only after its ready counter, and every 128-B line
   // of it was written whole by ONE producer wave through the write-through path before that
@@ -479,7 +489,13 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
       const float p3 = pa[s][3] + (float)xn[s][3] + bb[3];
       // the gate pre-activations x W_ih^T + h W_hh^T + b, in place of the projection they were
       // built from: the backward reads them instead of re-running a time-parallel GEMM
-      dn_store_f32x4(pre_rs, po[s] + (uint32_t)tau * pstep, f32x4{p0, p1, p2, p3});
+      if constexpr (sizeof(PT) == 4) {
+        dn_store_f32x4(pre_rs, po[s] + (uint32_t)tau * pstep, f32x4{p0, p1, p2, p3});
+      } else {
+        const bf16x4 pe = bf16x4{(bf16)p0, (bf16)p1, (bf16)p2, (bf16)p3};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(dn_u32x2, pe), pre_rs,
+                                              (int)(po[s] + (uint32_t)tau * pstep), 0, 0);
+      }
       if constexpr (!EARLY) xn[s] = load_x(s, tau1);
       const float gi = sigmoid_unit(dn_sigmoid(p0));
       const float gf = sigmoid_unit(dn_sigmoid(p1));
@@ -538,14 +554,14 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
   }
 }
 
-template <int HD, int BR, bool SEQ, int UG>
+template <int HD, int BR, bool SEQ, int UG, typename PT = float>
 __global__ void __launch_bounds__(HD / (16 * UG) * 64)
 lstm_fwd_kernel(const bf16* xp, const float* __restrict__ bias, const bf16* __restrict__ whh,
                 int B, int S, int Hd, int ndir, float* __restrict__ c_save,
                 bf16* __restrict__ hprev, float* __restrict__ hseq, float* __restrict__ hmean,
                 float mean_scale, float* __restrict__ hT, float* __restrict__ cT,
-                float* __restrict__ pre, int bsplit) {
-  fwd_recur<HD, BR, SEQ, UG, false>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
+                PT* __restrict__ pre, int bsplit) {
+  fwd_recur<HD, BR, SEQ, UG, false, PT>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
                                     mean_scale, hT, cT, pre, bsplit, (int)blockIdx.x,
                                     (int)blockIdx.y, (int)gridDim.x, FwdWait{});
 }
@@ -569,9 +585,9 @@ struct BwdPub {
 typedef __attribute__((address_space(1))) unsigned ov_gu32;
 typedef __attribute__((ext_vector_type(2))) unsigned ov_u32x2;
 
-template <int HD, int BR, bool DSEQ, int UG, bool PUB>
+template <int HD, int BR, bool DSEQ, int UG, bool PUB, typename PT = float>
 __device__ __forceinline__ void
-bwd_recur(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time order
+bwd_recur(const PT* __restrict__ pre,        // [B*S][ndir][4*HD] original time order
           const float* __restrict__ c_save,  // [ndir][Bp][S][HD]
           const bf16* __restrict__ whhT,     // [ndir][HD][4*HD]
           const float* __restrict__ dh_ext, long dh_sb, long dh_st, float dh_scale,
@@ -634,7 +650,7 @@ bwd_recur(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time 
     dhx[s] = DSEQ ? 0.f : dh_ext[(long)bc * dh_sb + dir * Hd + uc] * dh_scale * msk[s];
     dcc[s] = dcT ? dcT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s] : 0.f;
   }
-  const float* prow = pre + (long)bc * S * rowX + (long)dir * 4 * HD;
+  const PT* prow = pre + (long)bc * S * rowX + (long)dir * 4 * HD;
   const float* crow = c_save + (long)dir * Bp * S * HD + (long)b * S * HD;
   bf16* drow = dpre + (long)b * S * rowX + (long)dir * 4 * HD;
   // PUB: write-through (sc1) dpre stores through a descriptor based at this workgroup's first
@@ -652,14 +668,14 @@ bwd_recur(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time 
   // loads fly during this step's MFMAs and gate phase, and nothing copies a register that a load
   // is still filling (such a copy is a vmcnt wait at the end of the step)
   float ca[NSL], cb[NSL], dTl[NSL];
-  f32x4 pn[NSL];
+  typename Gate4Raw<PT>::type pn[NSL];  // (bf16 pre-activations stay packed until used)
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
     const int uc = uu[s] < Hd ? uu[s] : Hd - 1;
     dTl[s] = dhT ? dhT[(long)bc * ndir * Hd + dir * Hd + uc] * msk[s] : 0.f;  // dL/dh_T
     ca[s] = crow[(long)tauL * HD + uu[s]];
     cb[s] = crow[(long)tauP * HD + uu[s]];
-    pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tauL * rowX + 4 * uu[s]);
+    pn[s] = load_raw4<PT>(prow + (long)tauL * rowX + 4 * uu[s], true);
   }
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(DN_VMCNT0);  // resident weights landed (see the forward)
@@ -685,13 +701,13 @@ bwd_recur(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time 
     auto activations = [&]() {
 #pragma unroll
       for (int s = 0; s < NSL; ++s) {
-        const f32x4 pc = pn[s];
+        const f32x4 pc = to_f32x4(pn[s]);
         cp[s] = t > 0 ? cprv[s] : 0.f;
         si[s] = dn_sigmoid(pc[0]); sf[s] = dn_sigmoid(pc[1]); so[s] = dn_sigmoid(pc[2]);
         gi[s] = sigmoid_unit(si[s]); gf[s] = sigmoid_unit(sf[s]); go[s] = sigmoid_unit(so[s]);
         gg[s] = dn_tanh(pc[3]);
         tc[s] = dn_tanh(ccur[s]);
-        pn[s] = *reinterpret_cast<const f32x4*>(prow + (long)tau1 * rowX + 4 * uu[s]);
+        pn[s] = load_raw4<PT>(prow + (long)tau1 * rowX + 4 * uu[s], true);
         ccur[s] = crow[(long)tau2 * HD + uu[s]];
       }
     };
@@ -879,14 +895,14 @@ bwd_recur(const float* __restrict__ pre,     // [B*S][ndir][4*HD] original time 
 #endif
 }
 
-template <int HD, int BR, bool DSEQ, int UG>
+template <int HD, int BR, bool DSEQ, int UG, typename PT = float>
 __global__ void __launch_bounds__(HD / (16 * UG) * 64)
-lstm_bwd_kernel(const float* __restrict__ pre, const float* __restrict__ c_save,
+lstm_bwd_kernel(const PT* __restrict__ pre, const float* __restrict__ c_save,
                 const bf16* __restrict__ whhT, const float* __restrict__ dh_ext, long dh_sb,
                 long dh_st, float dh_scale, const float* __restrict__ dhT,
                 const float* __restrict__ dcT, int B, int S, int Hd, int ndir,
                 bf16* __restrict__ dpre) {
-  bwd_recur<HD, BR, DSEQ, UG, false>(pre, c_save, whhT, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT,
+  bwd_recur<HD, BR, DSEQ, UG, false, PT>(pre, c_save, whhT, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT,
                                      B, S, Hd, ndir, dpre, (int)blockIdx.x, (int)blockIdx.y,
                                      (int)gridDim.x, BwdPub{nullptr, 1});
 }
@@ -1461,12 +1477,23 @@ static int lstm_ug() {
 // bias layout of the current dn_lstm_fwd call (0: fused b_ih + b_hh; > 0: split, see the kernel),
 // set by dn_lstm_fwd for the launchers below (host launches are issued from one thread)
 int g_bias_split = 0;
+// the next dn_lstm_fwd / dn_lstm_bwd store / read bf16 gate pre-activations where the kernels
+// offer it (dn_lstm_pre_bf16): set by the caller per launch, so forward and backward agree
+int g_pre_bf16 = 0;
 
 template <int HD, int BR, int UG>
 int launch_fwd_ug(const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
                   float* cT, float* pre, hipStream_t st) {
   dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
+  if constexpr (HD == 192 && UG == 1) {
+    if (g_pre_bf16 && !hseq) {  // bf16 pre-activations (dn_lstm_pre_bf16)
+      hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false, UG, bf16>), grid, block, 0, st, xp, bias,
+                         whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT,
+                         reinterpret_cast<bf16*>(pre), g_bias_split);
+      return dn_launch_status();
+    }
+  }
   if (hseq)
     hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, true, UG>), grid, block, 0, st, xp, bias, whh, B, S,
                        Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, g_bias_split);
@@ -1510,6 +1537,14 @@ int launch_bwd_ug(const float* pre, const float* c_save, const bf16* whhT, const
                   long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
                   int Hd, int ndir, bf16* dpre, hipStream_t st) {
   dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
+  if constexpr (HD == 192 && UG == 1) {
+    if (g_pre_bf16 && st_ == 0) {  // bf16 pre-activations (dn_lstm_pre_bf16)
+      hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, false, UG, bf16>), grid, block, 0, st,
+                         reinterpret_cast<const bf16*>(pre), c_save, whhT, dh_ext, sb, st_, scale,
+                         dhT, dcT, B, S, Hd, ndir, dpre);
+      return dn_launch_status();
+    }
+  }
   if (st_ != 0)
     hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, true, UG>), grid, block, 0, st, pre, c_save, whhT,
                        dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
@@ -1666,7 +1701,7 @@ DN_API int dn_lstm_bwd_ov(const float* pre, const float* c_save, const void* whh
       !grads)
     return DN_UNSUPPORTED;
   const int BR = pick_br(B, HD);
-  if (BR != 4 || (long)B * S * ndir * 4 * HD * 2 >= (1L << 31)) return DN_UNSUPPORTED;
+  if (BR != 4 || (long)B * S * ndir * 4 * HD * 2 >= (1L << 31) || g_pre_bf16) return DN_UNSUPPORTED;
   OvJob J{};
   J.x = (const bf16*)x;
   J.hprev = (const bf16*)hprev;
@@ -1729,7 +1764,7 @@ DN_API int dn_lstm_fwd_ov(const void* x, int CW, const void* enc_w, const float*
       (!enc_in && (!x || !enc_w || !enc_b || CW <= 0 || CW % 8)) || I <= 0 || I % 64)
     return DN_UNSUPPORTED;
   if (bias_split != 0 && bias_split != ndir * 4 * HD) return DN_BAD_SHAPE;
-  if (pick_br(B, HD) != 4) return DN_UNSUPPORTED;
+  if (pick_br(B, HD) != 4 || g_pre_bf16) return DN_UNSUPPORTED;
   const long rows = (long)B * S;
   const long lim = 1L << 31;
   if ((!enc_in && rows * CW * 2 >= lim) || rows * ndir * 4 * HD * 2 >= lim || rows * I * 2 >= lim ||
@@ -1779,6 +1814,17 @@ DN_API int dn_lstm_fwd_ov(const void* x, int CW, const void* enc_w, const float*
   hipLaunchKernelGGL(kern, dim3(grid), dim3(768), 0, st, bias, (const bf16*)whh_p, B, S, Hd, ndir,
                      c_save, (bf16*)hprev, hmean, mean_scale, hT, cT, pre, bias_split, J);
   return dn_launch_status();
+}
+
+// bf16 gate pre-activations for the next forward / backward launches (on != 0), where the kernels
+// offer them: per-direction hidden padded to 192 units, one unit group per wave, temporal-mean
+// output (dn_lstm_pre_bf16_used).  The caller allocates the pre buffer accordingly.
+DN_API int dn_lstm_pre_bf16(int on) {
+  g_pre_bf16 = on != 0;
+  return DN_OK;
+}
+DN_API int dn_lstm_pre_bf16_used(int Hd, int seq) {
+  return dn_lstm_padded_hidden(Hd) == 192 && lstm_ug() == 1 && !seq;
 }
 
 // rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows

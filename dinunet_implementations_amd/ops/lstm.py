@@ -73,6 +73,8 @@ _lib.register("dn_lstm_fwd_ov", [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.
                                  _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                                  _lib.c_int, _lib.c_void_p])
 _lib.register("dn_lstm_fwd_ov_sync_bytes", [])
+_lib.register("dn_lstm_pre_bf16", [_lib.c_int])
+_lib.register("dn_lstm_pre_bf16_used", [_lib.c_int, _lib.c_int])
 _lib.register("dn_lstm_fwd_ov_err_word", [])
 
 # The overlapped backward (dn_lstm_bwd_ov: the LSTM weight / bias gradients accumulate on the
@@ -118,6 +120,23 @@ def _sync_block(table: Dict[str, Tensor], bytes_fn: str, device) -> Optional[Ten
 
 def _ov_sync(device) -> Optional[Tensor]:
     return _sync_block(OV_SYNC, "dn_lstm_ov_sync_bytes", device)
+
+# Gate pre-activations stored for the backward in bf16 instead of fp32 (the forward writes and the
+# backward reads half the bytes per step; the backward then recomputes its gates from the rounded
+# values, an error of the order of the bf16 dpre it already stores).  DINUNET_LSTM_PRE_BF16:
+# "0" never, "1" always where the kernels offer it (192-unit resident-weight geometry, temporal
+# mean), "auto" (default) from PRE_BF16_MIN_BATCH rows on -- the HBM-bound large batches
+PRE_BF16 = os.environ.get("DINUNET_LSTM_PRE_BF16", "0")
+PRE_BF16_MIN_BATCH = int(os.environ.get("DINUNET_LSTM_PRE_BF16_MIN_BATCH", "512"))
+
+
+def pre_dtype(B: int, Hd: int, mode: str) -> torch.dtype:
+    """Element type of the stored gate pre-activations for this forward."""
+    if PRE_BF16 == "0" or (PRE_BF16 == "auto" and B < PRE_BF16_MIN_BATCH):
+        return torch.float32
+    used = _lib.lib().dn_lstm_pre_bf16_used(int(Hd), int(mode != "mean"))
+    return torch.bfloat16 if used else torch.float32
+
 
 _ROWMAP_CACHE: Dict[Tuple[int, int, str], Tensor] = {}
 
@@ -210,10 +229,12 @@ class _BiLSTMFn(torch.autograd.Function):
         else:
             hseq = torch.empty(Bp, S, ndir * HD, dtype=torch.float32, device=dev)
         need_bwd = any(ctx.needs_input_grad)
-        # fp32 gate pre-activations (x W_ih^T + h W_hh^T + b) for the backward
-        pre = torch.empty(B * S, ndir * GP, dtype=torch.float32, device=dev) if need_bwd else None
+        # gate pre-activations (x W_ih^T + h W_hh^T + b) for the backward (fp32, or bf16: pre_dtype)
+        pre = (torch.empty(B * S, ndir * GP, dtype=pre_dtype(B, Hd, mode), device=dev)
+               if need_bwd else None)
         # a persistent pack (PersistentPack) keeps b_ih and b_hh as two images: summed in-kernel
         bsplit = ndir * GP if bias_p.numel() == 2 * ndir * GP else 0
+        _lib.call("dn_lstm_pre_bf16", int(pre is not None and pre.dtype == torch.bfloat16))
         _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
                   ndir, c_save.data_ptr(), hprev.data_ptr(), _lib.ptr(hseq), _lib.ptr(hmean),
                   1.0 / S, hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), bsplit, st)
@@ -266,6 +287,7 @@ def _lstm_backward(ctx, saved, dout: Optional[Tensor], dhT: Optional[Tensor],
     dcT = None if dcT is None else dcT.float().contiguous()
     dpre = torch.empty(Bp * S, ndir * GP, dtype=torch.bfloat16, device=dev)
     dpre_v = dpre[:N]
+    _lib.call("dn_lstm_pre_bf16", int(pre.dtype == torch.bfloat16))
     capturing = _cap.active() is not None and ctx.modules is not None
     done = False
     sync = _ov_sync(dev) if (OVERLAP_BWD and mode == "mean" and HD == 192
@@ -352,8 +374,10 @@ class _EncBiLSTMFn(torch.autograd.Function):
         cT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
         hmean = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
         need_bwd = any(ctx.needs_input_grad)
-        pre = torch.empty(B * S, ndir * GP, dtype=torch.float32, device=dev) if need_bwd else None
+        pre = (torch.empty(B * S, ndir * GP, dtype=pre_dtype(B, Hd, "mean"), device=dev)
+               if need_bwd else None)
         bsplit = ndir * GP if bias_p.numel() == 2 * ndir * GP else 0
+        _lib.call("dn_lstm_pre_bf16", int(pre is not None and pre.dtype == torch.bfloat16))
         sync = _sync_block(FOV_SYNC, "dn_lstm_fwd_ov_sync_bytes", dev)
         rc = 3
         enc_in = FOV_MODE != "full"

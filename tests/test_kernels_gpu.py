@@ -200,6 +200,44 @@ def test_lstm_fwd_bwd_matches_reference(B, S, I, Hd, ndir, mode):
             assert v < 7e-3, (k, v)
 
 
+@pytest.mark.parametrize("B,S,Hd", [(32, 98, 192), (600, 20, 150), (13, 9, 192)])
+def test_lstm_bf16_pre_activations(B, S, Hd, monkeypatch):
+    """DINUNET_LSTM_PRE_BF16: the forward stores its gate pre-activations in bf16 and the backward
+    recomputes its gates from them.  Same forward outputs as the fp32 store (the forward's own
+    gates never see the rounding), and gradients within the bf16 tolerance of the fp32 oracle:
+    bounded at ~2x the fp32-store bound (7e-3) -- the rounding is of the order of the bf16 gate
+    gradients the backward already stores."""
+    from dinunet_implementations_amd.ops import lstm as L
+    from dinunet_implementations_amd.ops import reference as ref
+    torch.manual_seed(3)
+    ps = _lstm_params(128, Hd, 2)
+    x = torch.randn(B, S, 128, device=DEV)
+    g = torch.randn(B, 2 * Hd, device=DEV)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(L, "PRE_BF16", mode)
+        for p in ps:
+            for t in p:
+                t.grad = None
+        xx = x.clone().requires_grad_()
+        out, _ = L.bilstm(xx, ps, reduce="mean")
+        (out * g).sum().backward()
+        res[mode] = (out.detach().clone(), xx.grad.clone(),
+                     [t.grad.clone() for p in ps for t in p])
+    assert L.pre_dtype(B, Hd, "mean") == torch.bfloat16  # (monkeypatched "1" still active)
+    assert torch.equal(res["0"][0], res["1"][0])
+    ps_r = [tuple(bf(t.detach()).requires_grad_() for t in p) for p in ps]
+    xr = bf(x).requires_grad_()
+    hs, _ = ref.bilstm(xr, ps_r, bidirectional=True)
+    (hs.mean(1) * g).sum().backward()
+    errs = {"dx": rel(res["1"][1], xr.grad)}
+    for i, (t, tr) in enumerate(zip(res["1"][2], [t for p in ps_r for t in p])):
+        errs[f"dp{i}"] = rel(t, tr.grad)
+    _record_errs("lstm_pre_bf16", dict(B=B, S=S, Hd=Hd), errs)
+    for k, v in errs.items():
+        assert v < 1.4e-2, (k, v)
+
+
 def test_linear_bias_relu_grad():
     from dinunet_implementations_amd.ops import linear_bias_relu
     x = torch.randn(500, 120, device=DEV)
