@@ -84,19 +84,38 @@ __device__ __forceinline__ int scale_exp(float amax) {
 
 __device__ __forceinline__ float exp2i(int e) { return __builtin_ldexpf(1.f, e); }
 
-// max |x| over n -> *word (float bits of a non-negative value order like unsigned ints)
+// max |x| over n -> *word (float bits of a non-negative value order like unsigned ints).  One
+// atomic per WORKGROUP (LDS across its 4 waves) from at most 64 workgroups: same-address atomics
+// serialise at the L2, and one per wave from 512 workgroups (2,048) cost ~20 us of the fp16
+// exchange (tools/comm_model.py local kernels: fp16 40 us vs bf16 16 us)
 __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, long n, unsigned* word) {
+  __shared__ float wm[4];
   float m = 0.f;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float v = __builtin_fabsf(x[i]);
-    m = v > m || v != v ? v : m;  // a NaN wins (and disables scaling)
+  const long n4 = n >> 2;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = __builtin_fabsf(v[k]);
+      m = a > m || a != a ? a : m;  // a NaN wins (and disables scaling)
+    }
+  }
+  for (long i = 4 * n4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float a = __builtin_fabsf(x[i]);
+    m = a > m || a != a ? a : m;
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     const float t = __shfl_xor(m, o, 64);
     m = t > m || t != t ? t : m;
   }
-  if ((threadIdx.x & 63) == 0) atomicMax(word, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < 4; ++w) m = wm[w] > m || wm[w] != wm[w] ? wm[w] : m;
+    atomicMax(word, __float_as_uint(m));
+  }
 }
 
 // src fp32 [n] -> dst T: W blocks of [HDR | chunk] (zeros past n), scaled by scale * 2^e
@@ -200,8 +219,9 @@ bool aligned(const void* a, const void* b) { return (((uintptr_t)a | (uintptr_t)
 
 DN_API int dn_payload_amax(const float* x, long n, unsigned* word, hipStream_t st) {
   if (n <= 0) return DN_OK;
-  const long b = (n + 255) / 256;
-  hipLaunchKernelGGL(amax_kernel, dim3((int)(b < 512 ? b : 512)), dim3(256), 0, st, x, n, word);
+  if (((uintptr_t)x) & 15) return DN_BAD_SHAPE;
+  const long b = (n + 1023) / 1024;
+  hipLaunchKernelGGL(amax_kernel, dim3((int)(b < 64 ? b : 64)), dim3(256), 0, st, x, n, word);
   return dn_launch_status();
 }
 
