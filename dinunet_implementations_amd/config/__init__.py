@@ -86,6 +86,9 @@ FRAMEWORK_DEFAULTS: Dict[str, Any] = {
     # site loop: train epochs device-fed (runtime.feed: HBM-resident bf16 split, K-step graphs,
     # on-device train records) when the step supports it
     "device_feed": True,
+    # classifier / MLP normalisation: "batch" = the reference's BatchNorm1d, "layer" = the
+    # optional LayerNorm on its own gfx950 kernels (ops.layernorm)
+    "norm_layer": "batch",
     # "fused": gfx950 kernels (bf16 MFMA operands, fp32 accumulation / state);
     # "reference": the fp32 oracle math of ops/reference.py on the same device (fidelity baseline)
     "compute_path": "fused",
@@ -268,6 +271,8 @@ def generate_compspec() -> Dict[str, Any]:
         "validation_epochs": item("Validate every N epochs", "number", 1, conditional=train),
         "precision_bits": item("Payload precision bits", "select", "32", conditional=train,
                                values=["32", "16"]),
+        "norm_layer": item("Classifier normalisation", "select", "batch",
+                           values=["batch", "layer"]),
         "pin_memory": item("Pin memory", "boolean", False, source="member"),
         "num_workers": item("Loader workers", "number", 0, source="member"),
         "patience": item("Early-stopping patience", "number", 35, conditional=train),

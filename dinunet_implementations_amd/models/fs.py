@@ -22,7 +22,7 @@ from .. import ops
 
 class MSANNet(nn.Module):
     def __init__(self, in_size: int, hidden_sizes: Sequence[int], out_size: int,
-                 dropout_in: Sequence[int] = ()):
+                 dropout_in: Sequence[int] = (), norm_layer: str = "batch"):
         super().__init__()
         self.in_size = int(in_size)
         self.out_size = int(out_size)
@@ -30,9 +30,14 @@ class MSANNet(nn.Module):
         self.dropout_in = list(dropout_in or [])
         self.layers = nn.ModuleList()
         d = self.in_size
+        if norm_layer not in ("batch", "layer"):
+            raise ValueError(f"norm_layer {norm_layer!r}: expected 'batch' or 'layer'")
         for i, h in enumerate(self.hidden_sizes):
-            block = [nn.Linear(d, h, bias=False), nn.BatchNorm1d(h, track_running_stats=False),
-                     nn.ReLU()]
+            # "layer": the optional LayerNorm on its gfx950 kernels (ops.layernorm) in place of
+            # the reference's BatchNorm1d
+            norm = (nn.BatchNorm1d(h, track_running_stats=False) if norm_layer == "batch"
+                    else ops.LayerNorm(h))
+            block = [nn.Linear(d, h, bias=False), norm, nn.ReLU()]
             if i in self.dropout_in:
                 block.append(nn.Dropout(p=0.5))
             self.layers.append(nn.Sequential(*block))

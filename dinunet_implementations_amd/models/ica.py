@@ -134,7 +134,7 @@ class ICALstm(nn.Module):
 
     def __init__(self, input_size: int = 256, hidden_size: int = 256, bidirectional: bool = True,
                  num_cls: int = 2, num_comps: int = 53, window_size: int = 20,
-                 num_layers: int = 1):
+                 num_layers: int = 1, norm_layer: str = "batch"):
         super().__init__()
         self.input_size = input_size
         self.hidden_size = hidden_size
@@ -143,10 +143,15 @@ class ICALstm(nn.Module):
         self.encoder = nn.Sequential(nn.Linear(num_comps * window_size, input_size), nn.ReLU())
         self.lstm = LSTM(input_size=input_size, hidden_size=hidden_size,
                          bidirectional=bidirectional, num_layers=num_layers)
+        # norm_layer "batch": the reference's BatchNorm1d (fused head kernels); "layer": the
+        # optional LayerNorm on its own gfx950 kernels (ops.layernorm; the head then runs
+        # module by module)
+        if norm_layer not in ("batch", "layer"):
+            raise ValueError(f"norm_layer {norm_layer!r}: expected 'batch' or 'layer'")
         self.classifier = nn.Sequential(
             nn.Dropout(0.25),
             nn.Linear(hidden_size, 256),
-            nn.BatchNorm1d(256),
+            nn.BatchNorm1d(256) if norm_layer == "batch" else ops.LayerNorm(256),
             nn.ReLU(),
             nn.Linear(256, 64),
             nn.ReLU(),

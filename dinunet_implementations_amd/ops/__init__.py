@@ -9,6 +9,7 @@ from .optim import (DeviceSource, FlatParams, FusedAdam, StepRecorder, cast_bf16
                     cast_f32_to_bf16, step_prologue)
 from .heads import softmax_ce, log_softmax_nll
 from .head import HeadSpec, head_loss
+from .layernorm import LayerNorm, layer_norm
 
 
 def bilstm(x, params, reduce: str = "none", modules=None, packed=None, xp=None,
@@ -18,6 +19,7 @@ def bilstm(x, params, reduce: str = "none", modules=None, packed=None, xp=None,
 
 
 __all__ = [
+    "LayerNorm", "layer_norm",
     "mm", "linear_bias_relu", "bilstm", "lstm_supported", "padded_hidden", "FlatParams",
     "DeviceSource", "StepRecorder", "FusedAdam", "cast_bf16_to_f32", "cast_f32_to_bf16", "step_prologue", "HeadSpec", "head_loss",
     "softmax_ce", "log_softmax_nll", "native_available", "capture", "reference",

@@ -94,7 +94,8 @@ class FreeSurferTrainer(NNTrainer):
         self.nn["fs_net"] = MSANNet(in_size=self.cache["input_size"],
                                     hidden_sizes=self.cache["hidden_sizes"],
                                     out_size=self.cache["num_class"],
-                                    dropout_in=self.cache.get("dropout_in", []))
+                                    dropout_in=self.cache.get("dropout_in", []),
+                                    norm_layer=self.cache.get("norm_layer", "batch"))
 
     def forward_loss(self, x, y):
         return self.nn["fs_net"].forward_loss(x.float(), y)

@@ -97,7 +97,8 @@ class ICATrainer(NNTrainer):
         self.nn["net"] = ICALstm(window_size=c["window_size"], input_size=c["input_size"],
                                  hidden_size=c["hidden_size"], num_comps=c["num_components"],
                                  num_cls=c["num_class"], num_layers=c.setdefault("num_layers", 1),
-                                 bidirectional=c.setdefault("bidirectional", True))
+                                 bidirectional=c.setdefault("bidirectional", True),
+                                 norm_layer=c.get("norm_layer", "batch"))
 
     def forward_loss(self, x, y):
         return self.nn["net"].forward_loss(x.float(), y)
