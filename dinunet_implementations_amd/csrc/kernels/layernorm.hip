@@ -12,12 +12,12 @@
 //             over ITS rows (the rows of a workgroup: a grid-stride loop) into a partial row;
 //   reduce    the workgroup partials summed in a fixed order (deterministic, no float atomics).
 //
-// Rows of up to 64 lanes x 4 x LN_KMAX = 4,096 elements (D % 4 == 0: 16-B vectors), fp32.
+// Rows of up to 64 lanes x 4 x LN_KMAX = 2,048 elements (D % 4 == 0: 16-B vectors), fp32.
 #include "common.h"
 
 namespace {
 
-constexpr int LN_KMAX = 16;   // 16-B vectors per lane: D <= 4096
+constexpr int LN_KMAX = 8;    // 16-B vectors per lane: D <= 2048 (16 spilled in the backward)
 constexpr int LN_WAVES = 4;   // rows in flight per workgroup
 
 __device__ __forceinline__ float ln_wave_sum(float v) {
@@ -174,13 +174,12 @@ int ln_grid(int R) {
     case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(64 * LN_WAVES), 0, ST, __VA_ARGS__); break; \
     case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(64 * LN_WAVES), 0, ST, __VA_ARGS__); break; \
     case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(64 * LN_WAVES), 0, ST, __VA_ARGS__); break; \
-    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(64 * LN_WAVES), 0, ST, __VA_ARGS__); break; \
-    default: hipLaunchKernelGGL(KERNEL<16>, GRID, dim3(64 * LN_WAVES), 0, ST, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(64 * LN_WAVES), 0, ST, __VA_ARGS__); break; \
   }
 
 static int ln_k(int D) {
   const int v = (D / 4 + 63) / 64;  // 16-B vectors per lane
-  return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 8 ? 8 : 16;
+  return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : 8;
 }
 
 static bool ln_ok(const void* a, const void* b, int D) {

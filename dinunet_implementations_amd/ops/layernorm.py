@@ -3,7 +3,7 @@
 An optional classifier norm (config ``norm_layer = "layer"``): the reference normalises with
 ``BatchNorm1d`` only, BASELINE.json's north star lists LayerNorm among the
 hand-written kernels.  :class:`LayerNorm` IS an ``nn.LayerNorm`` (same parameters, ``state_dict``
-keys and CPU math); on a GPU, for a last-dimension norm of ``D % 4 == 0, D <= 4096`` fp32 elements,
+keys and CPU math); on a GPU, for a last-dimension norm of ``D % 4 == 0, D <= 2048`` fp32 elements,
 forward and backward run on the fused kernels (one wave per row, statistics in registers,
 deterministic parameter-gradient reduction).
 """
@@ -22,7 +22,7 @@ _lib.register("dn_layernorm_bwd", [_lib.c_void_p] * 9 + [_lib.c_int, _lib.c_int,
 
 
 def fused_ok(x: torch.Tensor, D: int) -> bool:
-    return (x.is_cuda and x.dtype == torch.float32 and D % 4 == 0 and 0 < D <= 4096
+    return (x.is_cuda and x.dtype == torch.float32 and D % 4 == 0 and 0 < D <= 2048
             and x.shape[-1] == D and _lib.native_available())
 
 

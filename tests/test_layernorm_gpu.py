@@ -9,7 +9,7 @@ def rel(a, b):
     return (a - b).norm().item() / max(b.norm().item(), 1e-12)
 
 
-@pytest.mark.parametrize("R,D", [(32, 256), (1000, 384), (7, 4096), (5, 12), (3000, 64)])
+@pytest.mark.parametrize("R,D", [(32, 256), (1000, 384), (7, 2048), (5, 12), (3000, 64)])
 @pytest.mark.parametrize("affine", [True, False])
 def test_layernorm_matches_torch(R, D, affine):
     from dinunet_implementations_amd.ops import layernorm as L
