@@ -215,6 +215,13 @@ struct Epi {
   long ldm;
   void* C2;  // optional second output (same ldc, its own beta accumulate): the LSTM's b_ih and
              // b_hh gradients are the same column sum of the gate gradient, formed once
+  // >= 0: result column `xcol` is the column sum of op(A) (the LDS-DMA kernel reads a virtual
+  // column of ones as B's column xcol, B holding xcol real columns) and goes to the vectors X1
+  // (and X2) [row_map(m)] instead of C: a bias gradient riding in the spare columns of a weight
+  // gradient's last tile column, so A is not streamed a second time for it
+  int xcol;
+  float* X1;
+  float* X2;
 };
 
 constexpr int GMAX = 12;  // problems per grouped launch (kernarg: ~1.6 KB)
@@ -246,6 +253,10 @@ struct GemmGroup {
   // Adam also packs the next step's weights and batch, optim.hip adam_pack_kernel)
   int* bump_t;
   long long* bump_c;
+  // optional slot -> tile map (a permutation of the launch's tiles): consecutive slots share an
+  // XCD (8 contiguous slot ranges), so the host orders tiles that read the same operand blocks
+  // next to each other (ops.gemm._xcd_order) and each block is fetched into one XCD's L2
+  const int* perm;
 };
 
 // the armed bump rides in the next launch of one group only
@@ -265,6 +276,13 @@ __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int
   if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col] > 0.f)) v = 0.f;
   const long orow = epi.row_map ? epi.row_map[row] : row;
   if (orow < 0) return;  // dropped row (e.g. zero-padded LSTM units)
+  if (col == epi.xcol) {
+    for (int o = 0; o < (epi.X2 ? 2 : 1); ++o) {
+      float* xp = (o ? epi.X2 : epi.X1) + orow;
+      *xp = epi.beta != 0.f ? v + epi.beta * *xp : v;
+    }
+    return;
+  }
   for (int o = 0; o < (epi.C2 ? 2 : 1); ++o) {
     void* Co = o ? epi.C2 : C;
     if (epi.out_bf16) {
@@ -377,9 +395,10 @@ gemm_kernel(GemmGroup g) {
   // gridDim.x is padded to a multiple of 8 by the launcher; surplus blocks exit.
   const int ntiles = g.tile_start[g.n];
   const int bid = (int)blockIdx.x;
-  const int gtile = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
-  if (gtile >= ntiles) return;
+  const int slot = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
+  if (slot >= ntiles) return;
   group_bump(g);
+  const int gtile = g.perm ? g.perm[slot] : slot;
   int pi = 0;
   while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
   const GemmProb& P = g.p[pi];
@@ -503,6 +522,8 @@ gemm_kernel(GemmGroup g) {
 // Out-of-range 16-B chunks (ragged M / N / K, split-K slice ends) read a zero page instead, so the
 // loop carries no masks.  Contract (host-checked): both operands bf16, GemmGroup::vec.
 __device__ const uint4 g_gemm_zero[1] = {};
+// a 16-B chunk of 8 bf16 columns {1, 0, ..., 0}: the virtual ones column (Epi::xcol)
+__device__ const uint4 g_gemm_unit[1] = {{0x3f80u, 0u, 0u, 0u}};
 
 __device__ __forceinline__ int sw_kc(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ int sw_km256(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
@@ -527,10 +548,13 @@ struct DmaStream {
   int kofs[PW];  // the chunk's k offset within the tile
   long kstep;    // elements per unit of k
   int ins0;
+  unsigned unit;  // bit j: chunk j is the virtual ones column (k-major operands only)
+  // unitcol >= 0 (k-major only, a multiple of 8): the 8 columns from unitcol read {1, 0, .., 0}
   __device__ __forceinline__ void init(const bf16* __restrict__ base, long ld, int row0, int nrows,
-                                       int wid, int lane) {
+                                       int wid, int lane, int unitcol = -1) {
     ins0 = wid * PW;
     kstep = KCONTIG ? 1 : ld;
+    unit = 0;
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
       const int ins = ins0 + j;
@@ -548,6 +572,10 @@ struct DmaStream {
         const int gc = row0 + 8 * ch;
         kofs[j] = kr;
         p[j] = gc < nrows ? base + (long)kr * ld + gc : nullptr;
+        if (gc == unitcol) {
+          unit |= 1u << j;
+          p[j] = reinterpret_cast<const bf16*>(g_gemm_unit);
+        }
       }
     }
   }
@@ -555,7 +583,8 @@ struct DmaStream {
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
       const bool ok = p[j] != nullptr && k0 + kofs[j] < K;
-      const bf16* src = ok ? p[j] + (long)k0 * kstep : reinterpret_cast<const bf16*>(g_gemm_zero);
+      const bf16* src = !ok ? reinterpret_cast<const bf16*>(g_gemm_zero)
+                        : ((unit >> j) & 1u) ? p[j] : p[j] + (long)k0 * kstep;
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(img + (ins0 + j) * 1024), 16, 0, 0);
     }
   }
@@ -607,9 +636,10 @@ gemm_dma_kernel(GemmGroup g) {
 
   const int ntiles = g.tile_start[g.n];
   const int bid = (int)blockIdx.x;
-  const int gtile = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);  // XCD-contiguous tiles
-  if (gtile >= ntiles) return;
+  const int slot = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);  // XCD-contiguous slots
+  if (slot >= ntiles) return;
   group_bump(g);
+  const int gtile = g.perm ? g.perm[slot] : slot;
   int pi = 0;
   while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
   const GemmProb& P = g.p[pi];
@@ -635,7 +665,7 @@ gemm_dma_kernel(GemmGroup g) {
   DmaStream<BM, !TA> sa;
   DmaStream<BN, TB> sb;
   sa.init(A, P.lda, row0, M, wid, lane);
-  sb.init(B, P.ldb, col0, N, wid, lane);
+  sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol);
   // S-stage ring, tiles prefetched D = S - 1 ahead: at the top of iteration t this wave waits
   // until only the glds of tiles t+1 .. t+D-1 are outstanding (counted vmcnt, never 0 in the
   // steady state), one raw barrier makes every wave's share of tile t visible and retires the
@@ -831,7 +861,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
     const long mn = (long)P.M * P.N;
     const long idx = idx0 - base;
     if (idx >= mn) continue;
-    const bool vec = P.epi.ncol <= 0 && (P.N & 3) == 0 && (P.ldc & 3) == 0 &&
+    const bool vec = P.epi.ncol <= 0 && P.epi.xcol < 0 && (P.N & 3) == 0 && (P.ldc & 3) == 0 &&
                      ((((uintptr_t)P.C) & 15) == 0) &&
                      ((((uintptr_t)P.slab) & 15) == 0);
     if (vec) {
@@ -952,15 +982,23 @@ static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int t
   g_bump_c = nullptr;
   g.vec = 1;
   g.vepi = 1;
+  bool xcol = false;
   for (int i = 0; i < g.n; ++i) {
     const GemmProb& P = g.p[i];
-    if (!vec_ok(P.A, !ta, P.M, P.K, P.lda) || !vec_ok(P.B, tb, P.N, P.K, P.ldb)) g.vec = 0;
+    const int nb = P.epi.xcol >= 0 ? P.epi.xcol : P.N;  // B's real columns
+    if (!vec_ok(P.A, !ta, P.M, P.K, P.lda) || !vec_ok(P.B, tb, nb, P.K, P.ldb)) g.vec = 0;
+    if (P.epi.xcol >= 0) {
+      g.vepi = 0;
+      xcol = true;
+    }
     // 16-B output vectors: 8 columns (bf16) / 4 (fp32) never straddle N or a misaligned row
     const int cv = P.epi.out_bf16 ? 8 : 4;
     if (P.slab || P.epi.row_map || P.epi.ncol > 0 || P.N % cv || P.ldc % cv || !aligned16(P.C))
       g.vepi = 0;
     if (P.epi.mask && (P.epi.ldm % 8 || !aligned16(P.epi.mask))) g.vepi = 0;
   }
+  // the virtual ones column exists only in the LDS-DMA kernel's k-major B stream
+  if (xcol && (!g.vec || !g_gemm_dma || !a_bf16 || !b_bf16 || tb)) return DN_UNSUPPORTED;
   if (tile == 1) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
   return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, g, st);
 }
@@ -995,6 +1033,9 @@ DN_API int dn_gemm_set_dma(int on) {
   return DN_OK;
 }
 
+// the current dn_gemm_set_dma setting (1: LDS-DMA kernel)
+DN_API int dn_gemm_dma_on() { return g_gemm_dma; }
+
 // Output tiles of a launch (the split-K ticket count `counters` must provide): 64x64 tiles
 // (tile 0) or 128x128 (tile 1) summed over the problems.
 DN_API long dn_gemm_tiles(int n, const int* M, const int* N, int tile) {
@@ -1019,6 +1060,7 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
   g.cnt = splits > 1 && (long)splits * M * N < (1L << 29) ? counters : nullptr;
+  g.perm = nullptr;
   g.n = 1;
   g.splits = splits > 1 ? splits : 1;
   GemmProb& P = g.p[0];
@@ -1028,7 +1070,8 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   P.kchunk = kchunk_for(K, g.splits);
   if (g.splits > 1) g.splits = (K + P.kchunk - 1) / P.kchunk;
   P.slab = g.splits > 1 ? slab : nullptr;
-  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0, (const bf16*)mask, ldm, nullptr};
+  P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0, (const bf16*)mask, ldm, nullptr, -1,
+              nullptr, nullptr};
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }
 
@@ -1040,13 +1083,15 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
                            const long* ldb, void* const* C, const long* ldc, const int* M,
                            const int* N, const int* K, const float* alpha, const float* beta,
                            const void* const* bias, const void* const* row_map,
-                           const int* ncol, void* const* C2, int relu,
+                           const int* ncol, void* const* C2, const int* xcol,
+                           void* const* X1, void* const* X2, const int* perm, int relu,
                            int a_bf16, int b_bf16, int ta, int tb, int c_bf16, int tile,
                            int splits, float* slab, int* counters, hipStream_t st) {
   if (n < 1 || n > GMAX) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
   g.cnt = splits > 1 ? counters : nullptr;
+  g.perm = perm;
   g.n = n;
   g.splits = splits > 1 ? splits : 1;
   long soff = 0;
@@ -1062,8 +1107,12 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
     soff += (long)g.splits * M[i] * N[i];
     if ((long)g.splits * M[i] * N[i] >= (1L << 29)) g.cnt = nullptr;  // 32-bit slab offsets
     P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16,
-                ncol ? ncol[i] : 0, nullptr, 0, C2 ? C2[i] : nullptr};
+                ncol ? ncol[i] : 0, nullptr, 0, C2 ? C2[i] : nullptr,
+                xcol ? xcol[i] : -1, X1 ? (float*)X1[i] : nullptr, X2 ? (float*)X2[i] : nullptr};
     if (P.epi.C2 && !P.epi.ncol) return DN_BAD_SHAPE;  // second outputs: column sums only
+    if (P.epi.xcol >= 0 && (P.epi.xcol != N[i] - 1 || P.epi.xcol % 8 || !P.epi.X1 || c_bf16 ||
+                            P.epi.ncol > 0 || bias[i]))
+      return DN_BAD_SHAPE;  // the ones column is the last one, fp32 outputs
   }
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }

@@ -26,9 +26,10 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_void_p])
 
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
+_lib.register("dn_gemm_dma_on", [])
 _lib.register("dn_gemm_arm_bump", [_lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_gemm_bump_armed", [])
-_lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 15 + [_lib.c_int] * 8
+_lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 19 + [_lib.c_int] * 8
               + [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p])
 
 # DINUNET_SPLITK_INLAUNCH=1: split-K partials are combined inside the GEMM launch by each
@@ -183,6 +184,144 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
     return out
 
 
+_ONES = {}
+
+
+def ones_operand(n: int, device) -> Tensor:
+    """bf16 ones ``[n, 8]`` (8 columns: the 16-B operand path), cached per (n, device): the B
+    operand of a column sum formed as its own GEMM problem."""
+    key = (n, str(device))
+    t = _ONES.get(key)
+    if t is None:
+        t = torch.ones(n, 8, dtype=torch.bfloat16, device=device)
+        _ONES[key] = t
+    return t
+
+
+# DINUNET_COLSUM_FOLD=0: bias gradients always as their own ``a^T @ ones`` problems (A/B switch)
+COLSUM_FOLD = __import__("os").environ.get("DINUNET_COLSUM_FOLD", "1") == "1"
+
+
+def _group_tile(probs, trans_a: bool, tile: Optional[int]) -> Optional[int]:
+    if tile is None and _GROUP_TILE >= 0:
+        tile = _GROUP_TILE
+    maxk = max((q["a"].shape[0] if trans_a else q["a"].shape[1]) for q in probs)
+    if tile is None and maxk >= _LONG_K:
+        # very long K (large-batch weight gradients, K = B*S): 128x128 tiles double the MFMA
+        # work per staged byte.  B = 2048 ICA step on MI355X (tools/_gpu_group_ab.sh): 64x64
+        # 3.88 ms/step, 128x128 3.45 ms at ~8 workgroups per CU (24 splits)
+        tile = 1
+    return tile
+
+
+def _dma_vec_ok(q, trans_a: bool, trans_b: bool) -> bool:
+    """The launch-wide contract of the LDS-DMA kernel (gemm.hip run_group: bf16 operands, 16-B
+    aligned bases, leading dims and contiguous-axis extents % 8), checked for one problem."""
+    A = q["a"].t() if trans_a else q["a"]
+    B = q["b"].t() if trans_b else q["b"]
+    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16:
+        return False
+    (M, K), N = A.shape, B.shape[1]
+    A, ta, lda = _layout(A, True)
+    B, tb, ldb = _layout(B, False)
+
+    def ok(t, kcontig, rows, ld):
+        return t.data_ptr() % 16 == 0 and ld % 8 == 0 and (K if kcontig else rows) % 8 == 0
+    return ok(A, not ta, M, lda) and ok(B, bool(tb), N, ldb)
+
+
+def _place_colsums(probs, trans_a: bool, trans_b: bool, tile: Optional[int]):
+    """Resolve the ``colsum`` requests of a grouped launch; returns ``(problems, tile)``.
+
+    A column sum ``op(a) @ 1`` (a bias gradient: ``dpre^T @ 1``) is folded into its own problem
+    when the launch runs 128x128 tiles on the LDS-DMA kernel with a k-major ``b`` of ``N % 8 ==
+    0`` columns: the kernel reads a virtual ones column as ``b``'s column N and routes result
+    column N to the colsum vectors.  In the ICA step's large-batch weight-gradient launch the
+    LSTM ``dW_hh`` (N = 192) and encoder ``dW`` (N = 1000) tiles have spare columns in their last
+    tile column, so each bias stops costing its own tiles and a third pass over ``dpre`` / the
+    encoder gradient.  Otherwise (CPU, small-batch 64x64 tiles, fp32 or k-contiguous ``b``) the
+    column sum becomes its own ``a^T @ ones[K, 8]`` problem of the launch (one column stored)."""
+    tile = _group_tile(probs, trans_a, tile) if probs[0]["a"].is_cuda else tile
+    if not any(q.get("colsum") for q in probs):
+        return probs, tile
+    fold_ok = (COLSUM_FOLD and tile == 1 and probs[0]["a"].is_cuda and not trans_b
+               and _lib.native_available() and int(_lib.lib().dn_gemm_dma_on()) == 1
+               and all(_dma_vec_ok(q, trans_a, trans_b) for q in probs))
+    out = []
+    extra = []
+    for q in probs:
+        cs = q.get("colsum")
+        if not cs:
+            out.append(q)
+            continue
+        q = {k: v for k, v in q.items() if k != "colsum"}
+        a, b = q["a"], q["b"]
+        x1, x2 = cs[0], (cs[1] if len(cs) > 1 else None)
+        K = a.shape[0] if trans_a else a.shape[1]
+        if (fold_ok and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+                and b.stride(-1) == 1 and b.shape[1] % 8 == 0 and b.stride(0) % 8 == 0
+                and b.data_ptr() % 16 == 0 and q["out"].dtype == torch.float32
+                and q.get("bias") is None and not q.get("ncol")
+                and x1.dtype == torch.float32 and x1.is_contiguous()
+                and (x2 is None or (x2.dtype == torch.float32 and x2.is_contiguous()))):
+            q["colsum_folded"] = (x1, x2)
+            out.append(q)
+        else:
+            out.append(q)
+            extra.append(dict(a=a, b=ones_operand(K, a.device), out=x1.view(-1, 1),
+                              beta=q.get("beta", 0.0), alpha=q.get("alpha", 1.0),
+                              row_map=q.get("row_map"), ncol=1,
+                              out2=x2.view(-1, 1) if x2 is not None else None))
+    return out + extra, tile
+
+
+# DINUNET_XCD_ORDER=0: grouped launches keep the plain problem-major tile order (A/B switch)
+XCD_ORDER = __import__("os").environ.get("DINUNET_XCD_ORDER", "1") == "1"
+_PERMS = {}
+
+
+def _xcd_order(arrs, bt: int, dev) -> Optional[Tensor]:
+    """Slot -> tile permutation of a grouped launch (``GemmGroup::perm``).
+
+    The kernel gives each XCD a contiguous range of slots, and an XCD's L2 serves every re-read
+    of an operand block its own workgroups fetched.  Tiles are therefore ordered by the block of
+    their LARGER operand: an A row block (keyed by A's address, so problems sharing A -- the
+    LSTM's dW_ih and dW_hh of one direction, both ``dpre^T @ .`` -- interleave per row block) or
+    a B column block (the encoder dW: X, 1000 columns, outweighs its 256-row gradient).  In the
+    B = 2048 ICA step's weight-gradient launch this is the difference between fetching dpre
+    twice, the LSTM input 4x and X 2x across XCDs, and once-ish (profiles/r4_dw_xcd_order.md).
+    Cached per permutation (graph capture cannot allocate: a miss there keeps the plain order)."""
+    keys = []
+    t = 0
+    for i in range(len(arrs["M"])):
+        M, N, K = arrs["M"][i], arrs["N"][i], arrs["K"][i]
+        tm, tn = -(-M // bt), -(-N // bt)
+        a_big = M >= N
+        for m in range(tm):
+            for nn in range(tn):
+                keys.append(((0, arrs["A"][i], m, i, nn) if a_big else (1, arrs["B"][i], nn, i, m), t))
+                t += 1
+    order = tuple(j for _, j in sorted(keys))
+    if order == tuple(range(t)):
+        return None
+    p = _PERMS.get((dev, order))
+    if p is None:
+        if torch.device(dev).type == "cuda" and torch.cuda.is_current_stream_capturing():
+            return None
+        p = torch.tensor(order, dtype=torch.int32, device=dev)
+        _PERMS[(dev, order)] = p
+    return p
+
+
+def _launch_class(q, trans_a: bool, trans_b: bool):
+    A = q["a"].t() if trans_a else q["a"]
+    B = q["b"].t() if trans_b else q["b"]
+    _, ta, _ = _layout(A, True)
+    _, tb, _ = _layout(B, False)
+    bf = torch.bfloat16
+    return (ta, tb, A.dtype == bf, B.dtype == bf, q["out"].dtype == bf)
+
+
 def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
                splits: Optional[int] = None, tile: Optional[int] = None):
     """Several independent ``out_i (+)= alpha_i * op(a_i) @ op(b_i)`` in ONE launch.
@@ -190,13 +329,27 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
     ``problems``: sequence of dicts with keys ``a``, ``b``, ``out`` (required, fp32 or bf16 like
     every other ``out`` of the group) and optional ``alpha``, ``beta``, ``bias``, ``row_map``,
     ``ncol`` (store only the first ``ncol`` result columns into ``out``; lets a column sum ride
-    along as ``a^T @ ones[K, 8]`` with the vectorised operand path).
+    along as ``a^T @ ones[K, 8]`` with the vectorised operand path), ``colsum``: a tuple of one
+    or two fp32 vectors ``[M]`` that receive (``beta``-accumulate, ``row_map``-ed) the column
+    sums of ``op(a)``, i.e. ``op(a) @ 1`` -- a bias gradient beside its weight gradient (see
+    :func:`_place_colsums`).
     All ``a`` (and all ``b``) share dtype and memory layout.  On CPU runs :func:`mm` per problem.
     """
     import ctypes
     probs = list(problems)
     if not probs:
         return
+    probs, tile = _place_colsums(probs, trans_a, trans_b, tile)
+    if probs[0]["a"].is_cuda:
+        # a column sum issued as its own problem has a bf16 ones operand: it joins the launch
+        # of the problems sharing its operand dtypes / layouts (one launch per class)
+        classes = {}
+        for q in probs:
+            classes.setdefault(_launch_class(q, trans_a, trans_b), []).append(q)
+        if len(classes) > 1:
+            for grp in classes.values():
+                mm_grouped(grp, trans_a, trans_b, splits, tile)
+            return
     if len(probs) > GMAX:
         for i in range(0, len(probs), GMAX):
             mm_grouped(probs[i:i + GMAX], trans_a, trans_b, splits, tile)
@@ -214,7 +367,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         return
     n = len(probs)
     arrs = {k: [] for k in ("A", "lda", "B", "ldb", "C", "ldc", "M", "N", "K", "alpha", "beta",
-                            "bias", "rmap", "ncol", "C2")}
+                            "bias", "rmap", "ncol", "C2", "xcol", "X1", "X2")}
     keep = []
     ta = tb = None
     a_bf = b_bf = c_bf = None
@@ -247,28 +400,28 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         if rmap is not None:
             rmap = rmap.to(device=out.device, dtype=torch.int32).contiguous()
         keep += [A, B, bias, rmap]
+        xs = q.get("colsum_folded")  # (x1, x2): B's virtual ones column N -> result column N
+        xcol = -1
+        if xs is not None:
+            xcol, N = N, N + 1
         for k, v in (("A", A.data_ptr()), ("lda", lda), ("B", B.data_ptr()), ("ldb", ldb),
                      ("C", out.data_ptr()), ("ldc", out.stride(0)), ("M", M), ("N", N), ("K", K),
                      ("alpha", float(q.get("alpha", 1.0))), ("beta", float(q.get("beta", 0.0))),
                      ("bias", _lib.ptr(bias)), ("rmap", _lib.ptr(rmap)),
-                     ("ncol", int(q.get("ncol", 0) or 0)), ("C2", _lib.ptr(out2))):
+                     ("ncol", int(q.get("ncol", 0) or 0)), ("C2", _lib.ptr(out2)),
+                     ("xcol", xcol), ("X1", _lib.ptr(xs[0]) if xs else None),
+                     ("X2", _lib.ptr(xs[1]) if xs else None)):
             arrs[k].append(v)
         maxk = max(maxk, K)
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
         t128 += ((M + 127) // 128) * ((N + 127) // 128)
     if splits is None and _GROUP_SPLITS:
         splits = _GROUP_SPLITS
-    if tile is None and _GROUP_TILE >= 0:
-        tile = _GROUP_TILE
-    if tile is None and maxk >= _LONG_K:
-        # very long K (large-batch weight gradients, K = B*S): 128x128 tiles double the MFMA
-        # work per staged byte.  B = 2048 ICA step on MI355X (tools/_gpu_group_ab.sh): 64x64
-        # 3.88 ms/step, 128x128 3.45 ms at ~8 workgroups per CU (24 splits)
-        tile = 1
     if splits is None:
         splits = _split_rule(t128, maxk, per_cu=8) if tile == 1 else _split_rule(t64, maxk)
     sp = max(1, int(splits))
     dev = probs[0]["out"].device
+    perm = _xcd_order(arrs, 128 if tile == 1 else 64, dev) if (XCD_ORDER and tile == 1) else None
     slab = cnt = None
     if sp > 1:
         slab = torch.empty(sp * sum(m * nn for m, nn in zip(arrs["M"], arrs["N"])),
@@ -284,7 +437,8 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               (L * n)(*arrs["ldc"]), (I * n)(*arrs["M"]), (I * n)(*arrs["N"]),
               (I * n)(*arrs["K"]), (F * n)(*arrs["alpha"]), (F * n)(*arrs["beta"]),
               (P * n)(*arrs["bias"]), (P * n)(*arrs["rmap"]), (I * n)(*arrs["ncol"]),
-              (P * n)(*arrs["C2"]), 0,
+              (P * n)(*arrs["C2"]), (I * n)(*arrs["xcol"]), (P * n)(*arrs["X1"]),
+              (P * n)(*arrs["X2"]), _lib.ptr(perm), 0,
               int(a_bf), int(b_bf), ta, tb,
               int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.ptr(cnt),
               _lib.stream())

@@ -109,12 +109,8 @@ def defer_linear_grads(x2d: torch.Tensor, dym: torch.Tensor, weight: torch.Tenso
     """Queue ``dW += dym^T x2d`` and ``db += dym^T 1`` (``dym``: the masked output gradient,
     bf16 ``[N, O]``) into the end-of-backward grouped launch (``ops._grad.defer``); record the
     pair for activation capture (rank-dAD) when one is active and ``module`` is given."""
-    N = dym.shape[0]
-    probs = [dict(a=dym, b=x2d, out=_grad.grad_buffer(weight), beta=1.0)]
-    if bias is not None:
-        from .lstm import _ones
-        probs.append(dict(a=dym, b=_ones(N, dym.device), out=_grad.grad_buffer(bias).view(-1, 1),
-                          beta=1.0, ncol=1))
+    probs = [dict(a=dym, b=x2d, out=_grad.grad_buffer(weight), beta=1.0,
+                  colsum=(_grad.grad_buffer(bias),) if bias is not None else None)]
     _grad.defer(probs, [weight] + ([bias] if bias is not None else []))
     if module is not None and _cap.active() is not None:
         _cap.record(module, x2d, dym)

@@ -175,17 +175,9 @@ def _row_map(Hd: int, HD: int, device) -> Tensor:
     return rm
 
 
-_ONES = {}
-
-
 def _ones(n: int, device) -> Tensor:
-    """bf16 ones ``[n, 8]`` (8 columns: the 16-B operand path), cached per (n, device)."""
-    key = (n, str(device))
-    t = _ONES.get(key)
-    if t is None:
-        t = torch.ones(n, 8, dtype=torch.bfloat16, device=device)
-        _ONES[key] = t
-    return t
+    from .gemm import ones_operand
+    return ones_operand(n, device)
 
 
 class _BiLSTMFn(torch.autograd.Function):
@@ -694,21 +686,19 @@ def _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev):
     N = B * S
     Bp = hprev.shape[1]
     rmap = _row_map(Hd, HD, dev)
-    ones = _ones(N, dev)
     probs = []
     for d in range(ndir):
         w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
         dsl = dpre_v[:, d * GP:(d + 1) * GP]
         probs.append(dict(a=dsl, b=x2d, out=_grad.grad_buffer(w_ih), beta=1.0, row_map=rmap))
+        # bias grads = column sums of dpre = dpre^T @ 1, requested with dW_hh (ops.gemm
+        # _place_colsums: a virtual ones column in dW_hh's spare tile columns on large-batch
+        # launches, else its own problem).  d b_ih == d b_hh (both add to the same
+        # pre-activation): ONE column sum, stored twice
+        bs = tuple(_grad.grad_buffer(b) for b in (b_ih, b_hh) if b is not None)
         probs.append(dict(a=dsl, b=hprev[d].view(Bp * S, HD)[:N, :Hd],
-                          out=_grad.grad_buffer(w_hh), beta=1.0, row_map=rmap))
-        # bias grads = column sums of dpre = dpre^T @ ones: an extra problem of the same launch.
-        # d b_ih == d b_hh (both add to the same pre-activation): ONE column sum, stored twice
-        bs = [b for b in (b_ih, b_hh) if b is not None]
-        if bs:
-            probs.append(dict(a=dsl, b=ones, out=_grad.grad_buffer(bs[0]).view(-1, 1), beta=1.0,
-                              row_map=rmap, ncol=1,
-                              out2=_grad.grad_buffer(bs[1]).view(-1, 1) if len(bs) > 1 else None))
+                          out=_grad.grad_buffer(w_hh), beta=1.0, row_map=rmap,
+                          colsum=bs or None))
     return probs
 
 

@@ -382,6 +382,98 @@ def test_gemm_grouped_ncol_stores_only_leading_columns():
         assert torch.allclose(gw, a.float().t() @ w.float(), rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("splits,tile,fold", [(1, 1, True), (3, 1, True), (4, 1, False),
+                                               (3, 0, True), (None, None, True)])
+def test_gemm_grouped_colsum_folded_or_separate(splits, tile, fold, monkeypatch):
+    """A column sum requested beside its weight gradient (``colsum``, the LSTM / encoder bias
+    gradients): with 128x128 tiles on the LDS-DMA kernel it is folded into the problem (B's
+    virtual ones column, result column N routed to the vectors), otherwise issued as its own
+    ``a^T @ ones`` problem.  Both match the fp32 reference, beta-accumulate, honour the row map
+    and the twin output, and leave the weight gradient as without the request.  Shapes cover a
+    spare last tile column (N = 192, 1000, 64) and none (N = 256: the ones column opens one);
+    an operand off the DMA kernel's alignment contract keeps the whole launch unfolded."""
+    from dinunet_implementations_amd.ops import gemm as G
+    monkeypatch.setattr(G, "COLSUM_FOLD", fold)
+    torch.manual_seed(3)
+    K = 2000
+    probs, refs = [], []
+    for i, (M, N) in enumerate([(768, 192), (256, 1000), (304, 64), (200, 256)]):
+        a = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+        b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+        out = torch.randn(M + 5, N, device=DEV)
+        rmap = torch.randperm(M + 5, device=DEV)[:M].to(torch.int32) if i % 2 == 0 else None
+        x1 = torch.randn(M + 5 if rmap is not None else M, device=DEV)
+        x2 = torch.randn_like(x1) if i < 2 else None
+        idx = rmap.long() if rmap is not None else torch.arange(M, device=DEV)
+        ro, r1 = out.clone(), x1.clone()
+        ro[idx] += a.float().t() @ b.float()
+        r1[idx] += a.float().sum(0)
+        r2 = None
+        if x2 is not None:
+            r2 = x2.clone()
+            r2[idx] += a.float().sum(0)
+        q = dict(a=a, b=b, out=out if rmap is not None else out[:M], beta=1.0,
+                 colsum=(x1, x2) if x2 is not None else (x1,))
+        if rmap is not None:
+            q["row_map"] = rmap
+        probs.append(q)
+        refs.append((out, ro, x1, r1, x2, r2))
+    placed, t = G._place_colsums(list(probs), True, False, tile)
+    folded = sum("colsum_folded" in q for q in placed)
+    assert folded == (4 if (fold and t == 1) else 0)
+    assert len(placed) == 4 + (4 - folded)
+    G.mm_grouped(probs, trans_a=True, splits=splits, tile=tile)
+    for out, ro, x1, r1, x2, r2 in refs:
+        assert rel(out, ro) < 2e-3
+        assert rel(x1, r1) < 1e-4
+        if x2 is not None:
+            assert rel(x2, r2) < 1e-4
+
+
+def test_gemm_grouped_colsum_unaligned_launch_stays_separate():
+    """M = 300 (not a multiple of 8) breaks the LDS-DMA contract for the launch: no fold, the
+    column sums run as their own problems and still match."""
+    from dinunet_implementations_amd.ops import gemm as G
+    torch.manual_seed(4)
+    K, probs, refs = 2000, [], []
+    for M, N in [(300, 64), (256, 192)]:
+        a = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+        b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+        out, x1 = torch.zeros(M, N, device=DEV), torch.zeros(M, device=DEV)
+        probs.append(dict(a=a, b=b, out=out, beta=1.0, colsum=(x1,)))
+        refs.append((out, a.float().t() @ b.float(), x1, a.float().sum(0)))
+    placed, t = G._place_colsums(list(probs), True, False, 1)
+    assert t == 1 and not any("colsum_folded" in q for q in placed) and len(placed) == 4
+    G.mm_grouped(probs, trans_a=True, tile=1, splits=2)
+    for out, ro, x1, r1 in refs:
+        assert rel(out, ro) < 2e-3 and rel(x1, r1) < 1e-4
+
+
+def test_gemm_grouped_xcd_order_is_bitwise_neutral(monkeypatch):
+    """The slot -> tile permutation only moves tiles between XCDs: every tile's K loop and the
+    split-K combine order are unchanged, so results are bitwise equal with and without it."""
+    from dinunet_implementations_amd.ops import gemm as G
+    torch.manual_seed(5)
+    K = 4096
+    dpre = torch.randn(K, 1536, device=DEV).to(torch.bfloat16)
+    x = torch.randn(K, 256, device=DEV).to(torch.bfloat16)
+    h = torch.randn(2, K, 192, device=DEV).to(torch.bfloat16)
+    outs = {}
+    for on in (True, False):
+        monkeypatch.setattr(G, "XCD_ORDER", on)
+        gi, gh = torch.zeros(2, 768, 256, device=DEV), torch.zeros(2, 768, 192, device=DEV)
+        gb = torch.zeros(2, 768, device=DEV)
+        G.mm_grouped([p for d in range(2) for p in (
+            dict(a=dpre[:, d * 768:(d + 1) * 768], b=x, out=gi[d], beta=1.0),
+            dict(a=dpre[:, d * 768:(d + 1) * 768], b=h[d], out=gh[d], beta=1.0,
+                 colsum=(gb[d],)))], trans_a=True, tile=1, splits=4)
+        outs[on] = (gi, gh, gb)
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
+    ref = dpre[:, :768].float().t() @ x.float()
+    assert rel(outs[True][0][0], ref) < 2e-3
+
+
 @pytest.mark.parametrize("br", ["4", "8", "16"])
 def test_lstm_rows_per_workgroup_variants(br, monkeypatch):
     """Every rows-per-workgroup instantiation (column redistribution) matches the oracle."""
