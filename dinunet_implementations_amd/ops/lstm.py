@@ -125,8 +125,11 @@ def _ov_sync(device) -> Optional[Tensor]:
 # backward reads half the bytes per step; the backward then recomputes its gates from the rounded
 # values, an error of the order of the bf16 dpre it already stores).  DINUNET_LSTM_PRE_BF16:
 # "0" never, "1" always where the kernels offer it (192-unit resident-weight geometry, temporal
-# mean), "auto" (default) from PRE_BF16_MIN_BATCH rows on -- the HBM-bound large batches
-PRE_BF16 = os.environ.get("DINUNET_LSTM_PRE_BF16", "0")
+# mean), "auto" (default) from PRE_BF16_MIN_BATCH rows on -- the HBM-bound large batches (B=2048
+# step 3.091 -> 2.956 ms, profiles/r4_pre_bf16_b2048.jsonl; B=512 hard-cohort training, 3 seeds x
+# 300 steps: final validation AUC 0.8583 vs 0.8612 with the fp32 store, seed spread 0.009,
+# profiles/r4_pre_bf16_fidelity_b512.jsonl).  The B=32 headline step keeps the fp32 store.
+PRE_BF16 = os.environ.get("DINUNET_LSTM_PRE_BF16", "auto")
 PRE_BF16_MIN_BATCH = int(os.environ.get("DINUNET_LSTM_PRE_BF16_MIN_BATCH", "512"))
 
 
