@@ -218,7 +218,8 @@ struct Epi {
   // >= 0: result column `xcol` is the column sum of op(A) (the LDS-DMA kernel reads a virtual
   // column of ones as B's column xcol, B holding xcol real columns) and goes to the vectors X1
   // (and X2) [row_map(m)] instead of C: a bias gradient riding in the spare columns of a weight
-  // gradient's last tile column, so A is not streamed a second time for it
+  // gradient's last tile column, so A is not streamed a second time for it.  The problem's N is
+  // xcol + 4 (16-B slab rows for the split-K reduce); columns past xcol are zeros, never stored
   int xcol;
   float* X1;
   float* X2;
@@ -276,7 +277,8 @@ __device__ __forceinline__ void epi_store(const Epi& epi, void* C, long ldc, int
   if (epi.mask && !((float)epi.mask[(long)row * epi.ldm + col] > 0.f)) v = 0.f;
   const long orow = epi.row_map ? epi.row_map[row] : row;
   if (orow < 0) return;  // dropped row (e.g. zero-padded LSTM units)
-  if (col == epi.xcol) {
+  if (epi.xcol >= 0 && col >= epi.xcol) {
+    if (col > epi.xcol) return;
     for (int o = 0; o < (epi.X2 ? 2 : 1); ++o) {
       float* xp = (o ? epi.X2 : epi.X1) + orow;
       *xp = epi.beta != 0.f ? v + epi.beta * *xp : v;
@@ -811,6 +813,10 @@ gemm_dma_kernel(GemmGroup g) {
 
 // 4 consecutive outputs of one row: v (already alpha-free split sum) -> epilogue -> vector store
 __device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, int row, int col, f32x4 v) {
+  if (epi.xcol >= 0 && col + 3 >= epi.xcol) {  // the column-sum group (xcol % 4 == 0)
+    epi_store(epi, C, ldc, row, col, v[0]);
+    return;
+  }
   const long orow = epi.row_map ? epi.row_map[row] : row;
   if (orow < 0) return;
 #pragma unroll
@@ -861,7 +867,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
     const long mn = (long)P.M * P.N;
     const long idx = idx0 - base;
     if (idx >= mn) continue;
-    const bool vec = P.epi.ncol <= 0 && P.epi.xcol < 0 && (P.N & 3) == 0 && (P.ldc & 3) == 0 &&
+    const bool vec = P.epi.ncol <= 0 && (P.N & 3) == 0 && (P.ldc & 3) == 0 &&
                      ((((uintptr_t)P.C) & 15) == 0) &&
                      ((((uintptr_t)P.slab) & 15) == 0);
     if (vec) {
@@ -1110,7 +1116,7 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
                 ncol ? ncol[i] : 0, nullptr, 0, C2 ? C2[i] : nullptr,
                 xcol ? xcol[i] : -1, X1 ? (float*)X1[i] : nullptr, X2 ? (float*)X2[i] : nullptr};
     if (P.epi.C2 && !P.epi.ncol) return DN_BAD_SHAPE;  // second outputs: column sums only
-    if (P.epi.xcol >= 0 && (P.epi.xcol != N[i] - 1 || P.epi.xcol % 8 || !P.epi.X1 || c_bf16 ||
+    if (P.epi.xcol >= 0 && (N[i] != P.epi.xcol + 4 || P.epi.xcol % 8 || !P.epi.X1 || c_bf16 ||
                             P.epi.ncol > 0 || bias[i]))
       return DN_BAD_SHAPE;  // the ones column is the last one, fp32 outputs
   }

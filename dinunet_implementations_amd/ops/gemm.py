@@ -403,7 +403,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         xs = q.get("colsum_folded")  # (x1, x2): B's virtual ones column N -> result column N
         xcol = -1
         if xs is not None:
-            xcol, N = N, N + 1
+            xcol, N = N, N + 4  # N % 4 == 0: the split-K reduce keeps its 16-B slab rows
         for k, v in (("A", A.data_ptr()), ("lda", lda), ("B", B.data_ptr()), ("ldb", ldb),
                      ("C", out.data_ptr()), ("ldc", out.stride(0)), ("M", M), ("N", N), ("K", K),
                      ("alpha", float(q.get("alpha", 1.0))), ("beta", float(q.get("beta", 0.0))),
