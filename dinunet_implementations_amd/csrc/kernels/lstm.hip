@@ -1455,9 +1455,11 @@ static inline int pick_br(int B, int HD) {
     const int v = atoi(e);
     if (v == 4 || v == 8 || v == 16) return v;
   }
-  // measured per step (bench.py, MI355X): B = 512: 4 rows 1.059 ms vs 8 rows 1.292;
-  // B = 2048: 8 rows 3.79 vs 4 rows 3.88 vs 16 rows 3.98
-  return B <= 1024 ? 4 : 8;
+  // measured per step (bench.py, MI355X, round 4 with bf16 stored pre-activations from 512 rows,
+  // profiles/r4_lstm_rows_per_wg_ab.jsonl): B = 512: 4 rows 0.838 ms vs 8 rows 1.029; B = 1024:
+  // 1.506 vs 1.522; B = 2048: 2.726 vs 2.784 / 2.807 (16 rows 2.907); B = 4096: 5.31 / 5.34 vs
+  // 5.37 / 5.51; B = 8192: 10.61 vs 10.52
+  return B <= 4096 ? 4 : 8;
 }
 
 // unit groups per wave for (HD, BR) = (192, 4): 1 (12 waves, 3 per SIMD) unless
