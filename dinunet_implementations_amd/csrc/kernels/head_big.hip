@@ -130,14 +130,23 @@ __device__ __forceinline__ void bn_affine(const BArgs& a, const BLayer& P, const
     const F2* part = reinterpret_cast<const F2*>(ws + P.part_off);
     float cnt = 0.f, m2 = 0.f;
     mean = 0.f;
-    for (int rb = 0; rb < a.nrb; ++rb) {
-      const float nb = (float)min(RB, a.B - rb * RB);
-      const F2 q = part[(long)rb * P.out + k];
-      const float tot = cnt + nb;
-      const float d = q.x - mean;
-      mean += d * (nb / tot);
-      m2 += q.y + d * d * (cnt * nb / tot);
-      cnt = tot;
+    for (int r8 = 0; r8 < a.nrb; r8 += 8) {  // 8 partial loads in flight, merged in order
+      F2 qs[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qs[i] = part[(long)min(r8 + i, a.nrb - 1) * P.out + k];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int rb = r8 + i;
+        if (rb < a.nrb) {
+          const float nb = (float)min(RB, a.B - rb * RB);
+          const F2 q = qs[i];
+          const float tot = cnt + nb;
+          const float d = q.x - mean;
+          mean += d * (nb / tot);
+          m2 += q.y + d * d * (cnt * nb / tot);
+          cnt = tot;
+        }
+      }
     }
     const float var = m2 / (float)a.B;
     rstd = rsqrtf(var + P.eps);
@@ -367,10 +376,16 @@ headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws) {
   F2* cs = reinterpret_cast<F2*>(cf + 3 * N);
   for (int c = tid; c < N; c += BNT) {
     float s1 = 0.f, s2 = 0.f;
-    for (int rb = 0; rb < a.nrb; ++rb) {
-      const F2 q = part2[(long)rb * N + c];
-      s1 += q.x;
-      s2 += q.y;
+    for (int r8 = 0; r8 < a.nrb; r8 += 8) {  // 8 partial loads in flight, summed in order
+      F2 qs[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qs[i] = part2[(long)min(r8 + i, a.nrb - 1) * N + c];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (r8 + i < a.nrb) {
+          s1 += qs[i].x;
+          s2 += qs[i].y;
+        }
     }
     if (blockIdx.x == 0) {
       L.ggamma[c] += s2;
@@ -394,12 +409,27 @@ headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws) {
     const float A = cA[cc], m = cm[cc], rs = cr[cc];
     const F2 q = cs[cc];
     float sum = 0.f;
-    for (int r = 0; r < cnt; ++r) {
-      const long o = (long)(r0 + r) * N + cc;
-      const float xh = (Z[o] - m) * rs;
-      const float dz = cv ? A * (dy[o] - q.x - xh * q.y) : 0.f;
-      img[(long)(r0 + r) * L.S_z + c] = (bf16)dz;
-      sum += dz;
+    // rows in groups of 16 with every load of a group issued before its first use: a thread
+    // walks 64 rows of one column, and one dependent L2 round trip per row made this launch
+    // ~30 us at B = 2048
+    constexpr int RG = 16;
+    for (int rg = 0; rg < cnt; rg += RG) {
+      float zv[RG], dv[RG];
+#pragma unroll
+      for (int i = 0; i < RG; ++i) {
+        const long o = (long)(r0 + min(rg + i, cnt - 1)) * N + cc;
+        zv[i] = Z[o];
+        dv[i] = dy[o];
+      }
+#pragma unroll
+      for (int i = 0; i < RG; ++i) {
+        if (rg + i < cnt) {
+          const float xh = (zv[i] - m) * rs;
+          const float dz = cv ? A * (dv[i] - q.x - xh * q.y) : 0.f;
+          img[(long)(r0 + rg + i) * L.S_z + c] = (bf16)dz;
+          sum += dz;
+        }
+      }
     }
     if (cv) dbp[(long)blockIdx.x * N + c] = sum;
   }
@@ -584,7 +614,14 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
     } else {
       const float* dbp = reinterpret_cast<const float*>(ws + L.dbp_off);
       db = 0.f;
-      for (int rb = 0; rb < a.nrb; ++rb) db += dbp[(long)rb * N + n];
+      for (int r8 = 0; r8 < a.nrb; r8 += 8) {  // 8 loads in flight, summed in order
+        float qs[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qs[i] = dbp[(long)min(r8 + i, a.nrb - 1) * N + n];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (r8 + i < a.nrb) db += qs[i];
+      }
     }
     L.gb[n] += db;
   }
@@ -598,7 +635,14 @@ headb_dw_reduce_kernel(BArgs a, int l, const char* __restrict__ ws, int RS) {
   const float* part = reinterpret_cast<const float*>(ws + a.dwp_off);
   for (long e = blockIdx.x * 256L + threadIdx.x; e < NK; e += (long)gridDim.x * 256) {
     float v = 0.f;
-    for (int sp = 0; sp < RS; ++sp) v += part[sp * NK + e];
+    for (int s8 = 0; s8 < RS; s8 += 8) {  // 8 split loads in flight, added in split order
+      float qs[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qs[i] = part[min(s8 + i, RS - 1) * NK + e];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (s8 + i < RS) v += qs[i];
+    }
     L.gW[e] += v;
   }
 }
