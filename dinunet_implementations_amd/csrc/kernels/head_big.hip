@@ -206,12 +206,22 @@ headb_fwd_kernel(BArgs a, int l, const float* __restrict__ x, long ldx,
   const bool wimg = train && blockIdx.y == 0;
   const int sr = tid >> 4, sq = (tid & 15) * 4;  // staging: 16 rows x 16 column quads per pass
   f32x4 acc[4] = {};
+  // chunk kc+TB's raw input / weight values are loaded into registers before chunk kc's MFMAs
+  // (one chunk of prefetch): the loop is a chain of global round trips otherwise
+  float va[4][4], vw[4][4];
+  auto load_chunk = [&](int kc) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      load4<VX>(src, ld, r0 + sr + 16 * p, kc + sq, B, K, va[p]);
+      load4<VW>(L.W, K, n0 + sr + 16 * p, kc + sq, N, K, vw[p]);
+    }
+  };
+  load_chunk(0);
   for (int kc = 0; kc < K; kc += TB) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int row = sr + 16 * p, gr = r0 + row, k = kc + sq;
-      float v[4];
-      load4<VX>(src, ld, gr, k, B, K, v);
+      float v[4] = {va[p][0], va[p][1], va[p][2], va[p][3]};
       if (l > 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -229,15 +239,10 @@ headb_fwd_kernel(BArgs a, int l, const float* __restrict__ x, long ldx,
       const bf16x4 b4 = to_bf4(v);
       *reinterpret_cast<bf16x4*>(At + row * LS + sq) = b4;
       if (wimg && gr < B && k < L.S_a) *reinterpret_cast<bf16x4*>(aimg + (long)gr * L.S_a + k) = b4;
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int nl_ = sr + 16 * p, k = kc + sq;
-      float v[4];
-      load4<VW>(L.W, K, n0 + nl_, k, N, K, v);
-      *reinterpret_cast<bf16x4*>(Wt + nl_ * LS + sq) = to_bf4(v);
+      *reinterpret_cast<bf16x4*>(Wt + row * LS + sq) = to_bf4(vw[p]);
     }
     __syncthreads();
+    if (kc + TB < K) load_chunk(kc + TB);
 #pragma unroll
     for (int ks = 0; ks < TB; ks += 32) {
       const int kk = ks + 8 * (lane >> 4);
