@@ -1462,6 +1462,17 @@ static inline int pick_br(int B, int HD) {
   return B <= 4096 ? 4 : 8;
 }
 
+// rows per workgroup of the BACKWARD recurrence: the forward's, except at large batches of the
+// resident 192-unit geometry, where 8 rows win for the backward alone (B = 2048 kernel trace:
+// backward 462 us at 8 rows vs 513 at 4, forward 606 vs 450; profiles/r4_b2048_timeline.txt).
+// The buffers are row-major over the batch, so the two launches may tile the rows differently
+// as long as both tilings cover the padded batch exactly (B % 8 == 0).
+static inline int pick_br_bwd(int B, int HD) {
+  const int br = pick_br(B, HD);
+  if (getenv("DN_LSTM_BR") || getenv("DN_LSTM_BR_BWD_SAME")) return br;
+  return (HD == 192 && br == 4 && B >= 2048 && B % 8 == 0) ? 8 : br;
+}
+
 // unit groups per wave for (HD, BR) = (192, 4): 1 (12 waves, 3 per SIMD) unless
 // DINUNET_LSTM_UG=3 asks for one wave per SIMD.  Measured on MI355X (tools/lstm_stamps.py): the
 // one-wave layout runs 2.06 us/step fwd and bwd vs 1.19 / 1.46 -- a lone wave issues its 72
@@ -1863,7 +1874,7 @@ DN_API int dn_lstm_bwd(const float* pre, const float* c_save, const void* whhT_p
                        void* dpre, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
-  const int BR = pick_br(B, HD);
+  const int BR = pick_br_bwd(B, HD);
   if (!lstm_fits_32bit(B, S, HD, ndir, BR)) return DN_BAD_SHAPE;
   switch (HD) {
     case 64: return launch_bwd<64>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
