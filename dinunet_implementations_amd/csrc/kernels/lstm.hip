@@ -1458,7 +1458,10 @@ static inline int pick_br(int B, int HD) {
   // measured per step (bench.py, MI355X, round 4 with bf16 stored pre-activations from 512 rows,
   // profiles/r4_lstm_rows_per_wg_ab.jsonl): B = 512: 4 rows 0.838 ms vs 8 rows 1.029; B = 1024:
   // 1.506 vs 1.522; B = 2048: 2.726 vs 2.784 / 2.807 (16 rows 2.907); B = 4096: 5.31 / 5.34 vs
-  // 5.37 / 5.51; B = 8192: 10.61 vs 10.52
+  // 5.37 / 5.51; B = 8192: 10.61 vs 10.52 (both recurrences at one size).  With the backward at
+  // 8 rows from B = 2048 (pick_br_bwd), a 4-row forward also wins at B = 8192: 10.21 / 10.20 vs
+  // 10.41 / 10.44 ms (profiles/r4_lstm_bwd_rows_ab.jsonl)
+  if (HD == 192) return 4;
   return B <= 4096 ? 4 : 8;
 }
 
