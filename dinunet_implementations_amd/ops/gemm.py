@@ -418,7 +418,10 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
     if splits is None and _GROUP_SPLITS:
         splits = _GROUP_SPLITS
     if splits is None:
-        splits = _split_rule(t128, maxk, per_cu=8) if tile == 1 else _split_rule(t64, maxk)
+        # 128x128 tiles: ~4 workgroups per CU (B = 2048 ICA step, 64 tiles: 16 splits 2.631 /
+        # 2.634 ms vs 32 splits 2.651 / 2.650, 20 splits 2.679; B = 4096 5.179 / 5.161 vs
+        # 5.195 / 5.171 -- profiles/r4_group_splits_ab.jsonl)
+        splits = _split_rule(t128, maxk, per_cu=4) if tile == 1 else _split_rule(t64, maxk)
     sp = max(1, int(splits))
     dev = probs[0]["out"].device
     perm = _xcd_order(arrs, 128 if tile == 1 else 64, dev) if (XCD_ORDER and tile == 1) else None
