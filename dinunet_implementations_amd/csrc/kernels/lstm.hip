@@ -1845,6 +1845,11 @@ DN_API int dn_lstm_pre_bf16_used(int Hd, int seq) {
 
 // rows per workgroup the kernels use for batch B; internal buffers need Bp = ceil(B/BR)*BR rows
 DN_API int dn_lstm_rows_per_wg(int B, int Hd) { return pick_br(B, dn_lstm_padded_hidden(Hd)); }
+// rows per workgroup of the backward recurrence (pick_br_bwd; the buffers are padded to the
+// forward's dn_lstm_rows_per_wg)
+DN_API int dn_lstm_rows_per_wg_bwd(int B, int Hd) {
+  return pick_br_bwd(B, dn_lstm_padded_hidden(Hd));
+}
 
 // xp: the bf16 input projection [B*S][ndir][4*HD]; pre (fp32, same layout, or null when no
 // backward follows) receives the gate pre-activations (+ bias) the backward consumes

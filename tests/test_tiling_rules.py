@@ -31,3 +31,24 @@ def test_split_rule_long_k_targets_workgroups_per_cu():
     assert gemm._split_rule(284, 3136) >= 1
     assert gemm._split_rule(284, 256) == 1
     assert gemm._LONG_K == 16384
+
+
+def test_lstm_backward_rows_tile_the_forward_padding():
+    """The backward recurrence may tile the batch with more rows per workgroup than the forward
+    (8 vs 4 from B = 2048 at 192 units); its grid must never reach rows past the forward's padded
+    buffers, at any batch and hidden size."""
+    from dinunet_implementations_amd.ops import _lib
+    if not _lib.native_available():
+        import pytest
+        pytest.skip("kernel library not built")
+    L = _lib.lib()
+    for hd in (64, 128, 174, 192, 256, 384):
+        for B in list(range(1, 70)) + [511, 512, 1023, 1024, 2040, 2044, 2048, 2052, 4096, 4100,
+                                       8192, 16384]:
+            bf = int(L.dn_lstm_rows_per_wg(B, hd))
+            bb = int(L.dn_lstm_rows_per_wg_bwd(B, hd))
+            padded = -(-B // bf) * bf
+            assert -(-B // bb) * bb <= padded, (hd, B, bf, bb)
+    assert int(L.dn_lstm_rows_per_wg(2048, 192)) == 4 and int(L.dn_lstm_rows_per_wg_bwd(2048, 192)) == 8
+    assert int(L.dn_lstm_rows_per_wg_bwd(2044, 192)) == 4  # not a multiple of 8: same as forward
+    assert int(L.dn_lstm_rows_per_wg_bwd(32, 192)) == 4
