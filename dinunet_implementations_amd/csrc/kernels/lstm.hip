@@ -1467,13 +1467,19 @@ static inline int pick_br(int B, int HD) {
 
 // rows per workgroup of the BACKWARD recurrence: the forward's, except at large batches of the
 // resident 192-unit geometry, where 8 rows win for the backward alone (B = 2048 kernel trace:
-// backward 462 us at 8 rows vs 513 at 4, forward 606 vs 450; profiles/r4_b2048_timeline.txt).
+// backward 462 us at 8 rows vs 513 at 4, forward 606 vs 450; profiles/r4_b2048_timeline.txt;
+// step A/B in profiles/r4_lstm_bwd_rows_ab.jsonl: from B = 1024 on, 1.404 vs 1.433 ms there,
+// while B = 512 loses, 0.869 vs 0.802, and B = 128 0.554 vs 0.466).
 // The buffers are row-major over the batch, so the two launches may tile the rows differently
 // as long as both tilings cover the padded batch exactly (B % 8 == 0).
 static inline int pick_br_bwd(int B, int HD) {
   const int br = pick_br(B, HD);
   if (getenv("DN_LSTM_BR") || getenv("DN_LSTM_BR_BWD_SAME")) return br;
-  return (HD == 192 && br == 4 && B >= 2048 && B % 8 == 0) ? 8 : br;
+  static const int minb = [] {  // probe knob: smallest batch with the 8-row backward
+    const char* e = getenv("DN_LSTM_BWD8_MINB");
+    return e ? atoi(e) : 1024;
+  }();
+  return (HD == 192 && br == 4 && B >= minb && B % 8 == 0) ? 8 : br;
 }
 
 // unit groups per wave for (HD, BR) = (192, 4): 1 (12 waves, 3 per SIMD) unless
