@@ -125,6 +125,25 @@ TASK_DEFAULTS: Dict[str, Dict[str, Any]] = {
 # compspec ICA names -> names the ICA code reads (SURVEY.md §2.7 mismatch row).
 ICA_KEY_ALIASES = {"full_comp_size": "num_components"}
 
+# The reference compspec's input keys (``/root/reference/compspec.json:14-282``), with the keys of
+# each task's args object; ``tests/test_config_data.py`` pins the generated compspec to these
+# modulo the documented extras below.
+REFERENCE_INPUT_KEYS = (
+    "covariates", "data", "task_id", "mode", "agg_engine", "num_reducers", "batch_size",
+    "local_iterations", "learning_rate", "epochs", "pretrain", "pretrain_args",
+    "validation_epochs", "precision_bits", "pin_memory", "num_workers", "patience", "split_ratio",
+    "num_folds", f"{TASK_FS}_args", f"{TASK_ICA}_args")
+REFERENCE_TASK_ARG_KEYS = {
+    TASK_FS: ("labels_column", "input_size", "hidden_sizes", "num_class", "dad_reduction_rank",
+              "dad_num_pow_iters", "dad_tol", "split_files"),
+    TASK_ICA: ("num_class", "monitor_metric", "metric_direction", "log_header", "full_comp_size",
+               "spatial_dim", "window_size", "window_stride", "seq_len", "data_file",
+               "labels_file", "components_file", "split_files", "input_size", "hidden_size",
+               "dad_reduction_rank", "dad_num_pow_iters", "dad_tol"),
+}
+# inputs this framework adds to the GUI contract (documented in README "Configuration")
+EXTRA_INPUT_KEYS = ("norm_layer",)
+
 
 def unwrap_values(site_input: Dict[str, Any]) -> Dict[str, Any]:
     """Turn ``{key: {"value": v}}`` (inputspec / COINSTAC form) into ``{key: v}``.
@@ -164,8 +183,16 @@ def compspec_defaults(compspec: Optional[Dict[str, Any]] = None) -> Dict[str, An
     return out
 
 
-def _flatten_task_args(cfg: Dict[str, Any]) -> Dict[str, Any]:
-    """Merge ``<task_id>_args`` of the *selected* task into the top level (E2(b))."""
+def _flatten_task_args(cfg: Dict[str, Any], user: Optional[set] = None) -> Dict[str, Any]:
+    """Merge ``<task_id>_args`` of the *selected* task into the top level (E2(b)).
+
+    ``user``: the keys the site input / overrides set (top level or inside the task args).  The
+    compspec's ICA names map onto the names the ICA code reads: ``full_comp_size`` ->
+    ``num_components`` and ``seq_len`` (windows per subject) -> ``temporal_size = seq_len *
+    window_size`` -- when the user set the compspec name and not the code name.  ``covariates``
+    (the member's covariate CSV, reference ``compspec.json:15-17``) names the FS labels file
+    unless ``labels_file`` is set."""
+    user = set() if user is None else user
     task = cfg.get("task_id", TASK_FS)
     flat = dict(cfg)
     args = cfg.get(f"{task}_args")
@@ -177,11 +204,14 @@ def _flatten_task_args(cfg: Dict[str, Any]) -> Dict[str, Any]:
         flat.pop(f"{t}_args", None)
     if task == TASK_ICA:
         for src, dst in ICA_KEY_ALIASES.items():
-            if src in flat and dst not in cfg:
+            if src in flat and (dst not in flat or (src in user and dst not in user)):
                 flat[dst] = flat[src]
-        # compspec names temporal length "seq_len" only as number of windows; keep temporal_size
-        if "temporal_size" not in flat and "seq_len" in flat and "window_size" in flat:
+        # the compspec names the temporal length only as a number of windows ("seq_len")
+        if "seq_len" in flat and "window_size" in flat and (
+                "temporal_size" not in flat or ("seq_len" in user and "temporal_size" not in user)):
             flat["temporal_size"] = int(flat["seq_len"]) * int(flat["window_size"])
+    if task == TASK_FS and "covariates" in user and "labels_file" not in user:
+        flat["labels_file"] = flat["covariates"]
     return flat
 
 
@@ -198,16 +228,24 @@ def build_config(*, site_input: Optional[Dict[str, Any]] = None,
         cfg.update(compspec_defaults())
     cfg.update(copy.deepcopy(code_defaults))
     site = unwrap_values(site_input or {})
-    task = site.get("task_id", cfg.get("task_id", TASK_FS))
+    ov = dict(overrides or {})
+    task = ov.get("task_id", site.get("task_id", cfg.get("task_id", TASK_FS)))
+    key = f"{task}_args"
     base = copy.deepcopy(TASK_DEFAULTS.get(task, {}))
-    nested = cfg.get(f"{task}_args") or {}
-    base.update(nested)
-    cfg[f"{task}_args"] = base
+    base.update(cfg.get(key) or {})
+    # a task-args object from the site / overrides refines the defaults key by key (it does not
+    # drop the keys it leaves out)
+    user = set()
+    for src in (site, ov):
+        if isinstance(src.get(key), dict):
+            base.update(copy.deepcopy(src[key]))
+            user.update(src[key])
+        user.update(k for k in src if not k.endswith("_args"))
     cfg.update(site)
-    if overrides:
-        cfg.update(overrides)
-    cfg["task_id"] = task if not (overrides and "task_id" in overrides) else overrides["task_id"]
-    flat = _flatten_task_args(cfg)
+    cfg.update(ov)
+    cfg[key] = base
+    cfg["task_id"] = task
+    flat = _flatten_task_args(cfg, user)
     # anything still explicitly present in site input / overrides wins over task args
     for src in (site, overrides or {}):
         for k, v in src.items():
@@ -253,6 +291,9 @@ def generate_compspec() -> Dict[str, Any]:
 
     train = {"variable": "mode", "value": "train"}
     inputs = {
+        # the member's covariate CSV (FS: the labels file unless labels_file is set)
+        "covariates": {"value": "site0_covariates.csv", "label": "Covariates", "type": "csv",
+                       "source": "member", "group": "Data", "order": next(order)},
         "data": item("Data", "files", None, source="member", group="Data",
                      items=["Files"], extensions=[["csv", "txt", "h5", "npy", "npz"]]),
         "task_id": item("Task", "select", TASK_FS, values=[TASK_FS, TASK_ICA]),
@@ -283,13 +324,16 @@ def generate_compspec() -> Dict[str, Any]:
             "num_class": 2, "dad_reduction_rank": 10, "dad_num_pow_iters": 5, "dad_tol": 1e-3,
             "split_files": []}, group="Computation",
             conditional={"variable": "task_id", "value": TASK_FS}),
+        # the reference's ICA key set (compspec names: full_comp_size -> num_components,
+        # seq_len windows -> temporal_size = seq_len * window_size) on the inputspec geometry
+        # (datasets/icalstm/inputspec.json: 100 components, W = stride = 10, T = 980)
         f"{TASK_ICA}_args": item("ICA args", "object", {
             "num_class": 2, "monitor_metric": "auc", "metric_direction": "maximize",
-            "log_header": "Loss|AUC", "num_components": 100, "window_size": 10,
-            "window_stride": 10, "temporal_size": 980, "data_file": "<Required!>",
-            "labels_file": "<Required!>", "split_files": [], "input_size": 256,
-            "hidden_size": 384, "dad_reduction_rank": 10, "dad_num_pow_iters": 5,
-            "dad_tol": 1e-3}, group="Computation",
+            "log_header": "Loss|AUC", "full_comp_size": 100, "spatial_dim": 140,
+            "window_size": 10, "window_stride": 10, "seq_len": 98,
+            "data_file": "<Required!>", "labels_file": "<Required!>", "components_file": "",
+            "split_files": [], "input_size": 256, "hidden_size": 384, "dad_reduction_rank": 10,
+            "dad_num_pow_iters": 5, "dad_tol": 1e-3}, group="Computation",
             conditional={"variable": "task_id", "value": TASK_ICA}),
     }
     return {
@@ -319,7 +363,8 @@ def site_seed(cfg: Dict[str, Any], rank: int) -> int:
 
 
 __all__ = [
-    "TASK_FS", "TASK_ICA", "FRAMEWORK_DEFAULTS", "TASK_DEFAULTS", "build_config",
+    "TASK_FS", "TASK_ICA", "FRAMEWORK_DEFAULTS", "TASK_DEFAULTS", "REFERENCE_INPUT_KEYS",
+    "REFERENCE_TASK_ARG_KEYS", "EXTRA_INPUT_KEYS", "build_config",
     "load_inputspec", "load_compspec", "compspec_defaults", "unwrap_values", "validate",
     "generate_compspec", "write_compspec", "site_seed",
 ]

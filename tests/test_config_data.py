@@ -39,16 +39,47 @@ def test_validation_errors():
         build_config(site_input={"split_ratio": [0.5, 0.2]})
 
 
-def test_compspec_roundtrip_has_reference_keys():
+def test_compspec_key_set_matches_reference():
+    """The generated compspec declares exactly the reference's inputs (a checked-in copy of
+    /root/reference/compspec.json's key names, tests/fixtures/reference_compspec_keys.json), plus
+    the documented extras; every task-args object carries the reference's keys."""
+    from dinunet_implementations_amd.config import (EXTRA_INPUT_KEYS, REFERENCE_INPUT_KEYS,
+                                                    REFERENCE_TASK_ARG_KEYS)
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "fixtures",
+                                      "reference_compspec_keys.json")))
+    assert sorted(REFERENCE_INPUT_KEYS) == ref["input"]
+    assert {k: sorted(v) for k, v in REFERENCE_TASK_ARG_KEYS.items()} == {
+        k[:-len("_args")]: v for k, v in ref["task_args"].items()}
     spec = generate_compspec()
-    keys = set(spec["computation"]["input"])
-    for k in ["task_id", "mode", "agg_engine", "num_reducers", "batch_size", "local_iterations",
-              "learning_rate", "epochs", "pretrain", "pretrain_args", "validation_epochs",
-              "precision_bits", "pin_memory", "num_workers", "patience", "split_ratio",
-              "num_folds", "FS-Classification_args", "ICA-Classification_args"]:
-        assert k in keys, k
+    inputs = spec["computation"]["input"]
+    assert set(inputs) == set(ref["input"]) | set(EXTRA_INPUT_KEYS)
+    for k, want in ref["task_args"].items():
+        assert sorted(inputs[k]["default"]) == want, k
+    assert sorted(inputs["pretrain_args"]["default"]) == ref["pretrain_args"]
+    assert inputs["covariates"]["value"] == "site0_covariates.csv"
+    # the checked-in compspec.json is the generated one
+    from dinunet_implementations_amd.config import load_compspec
+    assert load_compspec() == json.loads(json.dumps(spec))
     d = compspec_defaults(spec)
     assert d["agg_engine"] == "dSGD" and d["precision_bits"] == "32"
+
+
+def test_compspec_names_map_to_code_names():
+    """Reference compspec names the ICA code does not read map onto the ones it reads, a
+    task-args object refines the defaults key by key, and ``covariates`` names the FS labels
+    file unless labels_file is set."""
+    c = build_config(site_input={"task_id": "ICA-Classification"})
+    assert (c["num_components"], c["temporal_size"], c["window_size"]) == (100, 980, 10)
+    c = build_config(site_input={"task_id": "ICA-Classification",
+                                 "ICA-Classification_args": {"seq_len": 49, "full_comp_size": 53}})
+    assert (c["num_components"], c["temporal_size"], c["hidden_size"]) == (53, 490, 384)
+    c = build_config(site_input={"task_id": "ICA-Classification", "temporal_size": 600,
+                                 "ICA-Classification_args": {"seq_len": 49}})
+    assert c["temporal_size"] == 600  # the code name set by the user wins
+    assert build_config(site_input={"covariates": "site1_Covariate.csv"})["labels_file"] == \
+        "site1_Covariate.csv"
+    assert build_config(site_input={"covariates": "a.csv", "labels_file": "b.csv"})["labels_file"] == "b.csv"
+    assert build_config()["labels_file"] == "site_covariates.csv"
 
 
 def test_reference_inputspec(fs_data_root):
