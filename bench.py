@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--tta-subjects", type=int, default=2560,
                     help="site-loop cohort size (split 0.8/0.1/0.1)")
     ap.add_argument("--tta-epochs", type=int, default=30)
+    ap.add_argument("--loopback-rccl", action="store_true",
+                    help="one GPU, but through a one-rank RCCL group marked distributed: the "
+                         "N > 1 step (split backward, bucketed all-reduce, captured collectives) "
+                         "timed on one GPU")
     return ap.parse_args()
 
 
@@ -140,7 +144,7 @@ def main():
     from dinunet_implementations_amd.models import ICALstm
     from dinunet_implementations_amd.ops import FlatParams, FusedAdam
 
-    grp = init_sites()
+    grp = init_sites(loopback=args.loopback_rccl)
     dev = grp.device
     if dev.type != "cuda":
         print("bench.py needs a GPU", file=sys.stderr)
@@ -207,7 +211,7 @@ def main():
     total = n * args.batch * args.steps / dt
     peak = torch.cuda.max_memory_allocated(dev)
     tta = None
-    if args.site_loop == "1" or (args.site_loop == "auto" and n == 1):
+    if args.site_loop == "1" or (args.site_loop == "auto" and n == 1 and not grp.loopback):
         try:
             tta = site_loop(grp, args)
         except Exception as e:  # never lose the throughput line to the study
@@ -234,7 +238,8 @@ def main():
             "config": {"model": f"ICA-LSTM (C={args.comps}, W={args.window}, S={S}, "
                                 f"I={args.input_size}, H={args.hidden}, bi-dir)",
                        "global_batch": args.batch * n, "seq_len": S,
-                       "parallelism": f"dp{n}", "engine": args.engine,
+                       "parallelism": f"dp{n}" + ("-loopback-rccl" if grp.loopback else ""),
+                       "engine": args.engine,
                        "precision_bits": args.precision_bits, "hip_graph": bool(args.graph),
                        "feed": args.feed},
             "per_site": round(total / n, 2),
@@ -243,6 +248,9 @@ def main():
                              "model's step, B=32, H=384, measured on CPU; the reference publishes "
                              "no throughput); per-site rate in per_site",
             "final_loss": round(loss, 5),
+            # N > 1 code path: collectives captured inside the K-step graphs (runtime.step)
+            "comm_graph": bool(getattr(step, "comm_graph", False)),
+            "split_backward": bool(getattr(step, "split", False)),
             **({"dad_iters_per_step": iters} if iters is not None else {}),
             # HBM high-water mark of the run (allocator view: model, optimizer state, activations,
             # graph pools and the resident synthetic dataset of --pool batches)

@@ -191,36 +191,9 @@ template <> struct LdsSplit<192, 16> { static constexpr int FWD_MT = 1, BWD_KS =
 // UG = 3 is ONE wave per SIMD owning 12 m-tiles -- the 72 MFMAs of a SIMD come from 12
 // independent accumulator chains of one wave (no issue arbitration between waves) and the h
 // tile is read once per k-step for 12 MFMAs instead of 4.
-// Chunk hand-off of the overlapped forward (lstm_fwd_ov_kernel): the input projection of time
-// chunk c (original times [c tc, (c+1) tc)) is ready for direction d when the counter at
-// ready + 32 (d FOV_MAXCH + c) reaches `need`; the recurrence waits on it before its first load of
-// that chunk and reads the projection with device-scope (sc1) loads.
-constexpr int FOV_MAXCH = 64;
-struct FwdWait {
-  const unsigned* ready;
-  unsigned* err;
-  int tc, need, spin;
-};
-typedef __attribute__((address_space(1))) unsigned fov_gu32;
-
-__device__ __forceinline__ void fov_wait(const FwdWait& fw, int dir, int chunk) {
-  const fov_gu32* c = (const fov_gu32*)(fw.ready + 32 * (dir * FOV_MAXCH + chunk));
-  int it = 0;
-  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
-         (unsigned)fw.need) {
-    if (++it >= fw.spin) {  // gives up: error word (runtime.health), the data read is wrong
-      __hip_atomic_store((fov_gu32*)fw.err, 0x400u + (unsigned)chunk, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load hoisted above the poll
-}
-
 // PT: element type of the stored gate pre-activations (float, or bf16 with
 // DINUNET_LSTM_PRE_BF16: half the bytes the forward writes and the backward reads per step)
-template <int HD, int BR, bool SEQ, int UG, bool OV, typename PT = float>
+template <int HD, int BR, bool SEQ, int UG, typename PT = float>
 __device__ __forceinline__ void
 fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, no bias (bf16)
           const float* __restrict__ bias,  // [ndir][4*HD] permuted + padded, b_ih + b_hh
@@ -233,7 +206,7 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
           float* __restrict__ hT, float* __restrict__ cT,  // [B][ndir*Hd]
           PT* __restrict__ pre,  // [B*S][ndir][4*HD] gate pre-activations (+ bias), or null
           int bsplit,  // > 0: bias holds b_ih at [0] and b_hh at [bsplit], summed here
-          const int bx, const int dir, const int gx, const FwdWait fw) {
+          const int bx, const int dir, const int gx) {
   constexpr int NW = HD / (16 * UG);
   constexpr int NT = NW * 64;
   constexpr int MT = 4 * UG;   // m-tiles per wave
@@ -332,10 +305,6 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
   const uint32_t xstep = (uint32_t)(rowXi * 2);  // bytes per time index (bf16 projection)
   const uint32_t pstep = (uint32_t)(rowXi * (int)sizeof(PT));  // (pre-activations)
   // the 4 gate inputs of a slot stay packed (2 VGPRs, unconverted) while the load is in flight
-  // (OV: the projection of a chunk is read only after its ready counter, and every 128-B line
-  // of it was written whole by ONE producer wave through the write-through path before that
-  // counter moved, so no cache on the way holds an older copy: plain loads, no device-scope
-  // (sc1) round trip on the recurrence's critical path)
   auto load_x = [&](int s, int tau) {  // time index -1 / S wraps out of range: reads 0
     return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
         x_rs, (int)(xo[s] + (uint32_t)tau * xstep), 0, 0));
@@ -350,20 +319,6 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
                                             (int)(ho[s] + (uint32_t)(tau0 * HD * 2)), 0, 0);
   }
 
-  // OV: the ready count of the NEXT chunk is read one chunk ahead (a device-scope load lands long
-  // before the boundary), so a boundary whose chunk is already projected costs no round trip
-  unsigned fv_pend = 0u;
-  auto fov_peek = [&](int chunk) -> unsigned {
-    const bool ok = chunk >= 0 && chunk * fw.tc < S;
-    return ok ? __hip_atomic_load((const fov_gu32*)(fw.ready + 32 * (dir * FOV_MAXCH + chunk)),
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-              : 0u;
-  };
-  if constexpr (OV) {
-    const int c0 = (dir == 0 ? 0 : S - 1) / fw.tc;
-    fov_wait(fw, dir, c0);
-    fv_pend = fov_peek(dir == 0 ? c0 + 1 : c0 - 1);
-  }
   float c[NSL], hs[NSL], hl[NSL];
   // xa / xb: the input projection of the current / next step, ping-ponged over a 2-step
   // unrolled loop so that no register copy (and no vmcnt wait) sits between a prefetch and its
@@ -395,15 +350,6 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
 #endif
     const int tau = dir == 0 ? t : S - 1 - t;
     const int tau1 = dir == 0 ? t + 1 : S - 2 - t;  // past the end at the last step: reads 0
-    if constexpr (OV) {
-      static_assert(EARLY, "the overlapped forward prefetches one step ahead");
-      if (t + 1 < S && tau1 / fw.tc != tau / fw.tc) {
-        const int c1 = tau1 / fw.tc;
-        if (__builtin_amdgcn_readfirstlane(fv_pend) < (unsigned)fw.need) fov_wait(fw, dir, c1);
-        fv_pend = fov_peek(dir == 0 ? c1 + 1 : c1 - 1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load hoisted above the check
-    }
     if constexpr (EARLY) {
 #pragma unroll
       for (int s = 0; s < NSL; ++s) xnn[s] = load_x(s, tau1);
@@ -561,9 +507,9 @@ lstm_fwd_kernel(const bf16* xp, const float* __restrict__ bias, const bf16* __re
                 bf16* __restrict__ hprev, float* __restrict__ hseq, float* __restrict__ hmean,
                 float mean_scale, float* __restrict__ hT, float* __restrict__ cT,
                 PT* __restrict__ pre, int bsplit) {
-  fwd_recur<HD, BR, SEQ, UG, false, PT>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
-                                    mean_scale, hT, cT, pre, bsplit, (int)blockIdx.x,
-                                    (int)blockIdx.y, (int)gridDim.x, FwdWait{});
+  fwd_recur<HD, BR, SEQ, UG, PT>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
+                                 mean_scale, hT, cT, pre, bsplit, (int)blockIdx.x,
+                                 (int)blockIdx.y, (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -573,19 +519,7 @@ lstm_fwd_kernel(const bf16* xp, const float* __restrict__ bias, const bf16* __re
 // (pre = x W_ih^T + h_{t-1} W_hh^T + b) instead of being stored per step by the forward kernel.
 // MFMA output: lane (q, n) holds dh for units u0 + j (u0 = 16w + 4q, j = 0..3) of column n; as in
 // the forward, the BR valid columns are redistributed: lane (q, r, b) owns units u0 + r + s*(16/BR).
-// Chunk publication of the overlapped backward (lstm_bwd_ov_kernel): after every `tc` steps a
-// recurrence workgroup makes its dpre stores of those steps visible (write-through stores, every
-// wave drained, a workgroup barrier) and ONE lane adds 1 to the block's ready counter
-// (one 128-B line per counter: ready + 32 * (dir * OV_MAXBLK + k)).
-constexpr int OV_MAXBLK = 64;
-struct BwdPub {
-  unsigned* ready;
-  int tc;
-};
-typedef __attribute__((address_space(1))) unsigned ov_gu32;
-typedef __attribute__((ext_vector_type(2))) unsigned ov_u32x2;
-
-template <int HD, int BR, bool DSEQ, int UG, bool PUB, typename PT = float>
+template <int HD, int BR, bool DSEQ, int UG, typename PT = float>
 __device__ __forceinline__ void
 bwd_recur(const PT* __restrict__ pre,        // [B*S][ndir][4*HD] original time order
           const float* __restrict__ c_save,  // [ndir][Bp][S][HD]
@@ -594,7 +528,8 @@ bwd_recur(const PT* __restrict__ pre,        // [B*S][ndir][4*HD] original time 
           const float* __restrict__ dhT, const float* __restrict__ dcT,  // optional [B][ndir*Hd]
           int B, int S, int Hd, int ndir,
           bf16* __restrict__ dpre,            // [Bp*S][ndir][4*HD] permuted, original time
-          const int bx, const int dir, const int gx, const BwdPub pub) {
+          const int Bp,                       // rows of the forward's padded buffers (c_save)
+          const int bx, const int dir) {
   constexpr int KS = 4 * HD / 32;
   constexpr int LDD = 4 * HD + 32;  // 16 dwords mod 64 banks: see LDH in the forward
   constexpr bool STREAM = HD > 192;  // W_hh^T streamed from L2 every step (see the forward)
@@ -607,7 +542,6 @@ bwd_recur(const PT* __restrict__ pre,        // [B*S][ndir][4*HD] original time 
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane >> 4, n = lane & 15, r = n / BR, bl = n % BR;
-  const int Bp = gx * BR;
   const int b = bx * BR + bl;
   const bool vb = b < B;
   const int bc = vb ? b : B - 1;
@@ -653,11 +587,6 @@ bwd_recur(const PT* __restrict__ pre,        // [B*S][ndir][4*HD] original time 
   const PT* prow = pre + (long)bc * S * rowX + (long)dir * 4 * HD;
   const float* crow = c_save + (long)dir * Bp * S * HD + (long)b * S * HD;
   bf16* drow = dpre + (long)b * S * rowX + (long)dir * 4 * HD;
-  // PUB: write-through (sc1) dpre stores through a descriptor based at this workgroup's first
-  // row (the overlapped weight-gradient workgroups read them during this launch)
-  const __amdgpu_buffer_rsrc_t d_rs =
-      dn_rsrc(dpre + (long)bx * BR * S * rowX, PUB ? (uint32_t)(BR * S * rowX * 2) : 0u);
-  const uint32_t d_off = (uint32_t)((bl * S * rowX + dir * 4 * HD) * 2);
   const float* dhrow = dh_ext + (long)bc * dh_sb + dir * Hd;
   const int tauL = dir == 0 ? S - 1 : 0;
   const int tp0 = S >= 2 ? S - 2 : 0;
@@ -837,44 +766,12 @@ bwd_recur(const PT* __restrict__ pre,        // [B*S][ndir][4*HD] original time 
       e[2] = (bf16)(m * d_o * go[s] * (1.f - go[s]) * so[s] * (1.f - so[s]));
       e[3] = (bf16)(m * d_g * (1.f - gg[s] * gg[s]));
       *reinterpret_cast<bf16x4*>(&dbuf[nxt][bl][4 * uu[s]]) = e;
-      if constexpr (PUB)
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(ov_u32x2, e), d_rs,
-            (int)(d_off + (uint32_t)((tau * rowX + 4 * uu[s]) * 2)), 0, 16);
-      else
-        *reinterpret_cast<bf16x4*>(drow + (long)tau * rowX + 4 * uu[s]) = e;
+      *reinterpret_cast<bf16x4*>(drow + (long)tau * rowX + 4 * uu[s]) = e;
     }
 #ifdef DN_STAMPS
     STAMP(ts2);
 #endif
-    if constexpr (PUB) {
-      // A block of `tc` steps is published one block LATE: at the end of block k, block k-1's
-      // stores were issued >= tc steps ago, so waiting until at most 6 vector-memory ops are
-      // outstanding (every step issues >= 1 store and tc >= 7: all of block k-1 is older than
-      // the newest 6) costs nothing, where a drain (vmcnt 0) right after the stores waited a
-      // write-through round trip every block on the critical path.  The last step drains and
-      // publishes what is left.
-      const int done = S - t;
-      const int k = (done - 1) / pub.tc;
-      ov_gu32* rb = (ov_gu32*)(pub.ready + 32 * dir * OV_MAXBLK);
-      if (t == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-          if (k >= 1) __hip_atomic_fetch_add(rb + 32 * (k - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(rb + 32 * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else if (done % pub.tc == 0 && k >= 1) {
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        __syncthreads();
-        if (tid == 0)
-          __hip_atomic_fetch_add(rb + 32 * (k - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        __syncthreads();
-      }
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
 #ifdef DN_STAMPS
     STAMP(ts3);
     st_a += ts1 - ts0; st_b += ts2 - ts1; st_c += ts3 - ts2;
@@ -901,444 +798,9 @@ lstm_bwd_kernel(const PT* __restrict__ pre, const float* __restrict__ c_save,
                 const bf16* __restrict__ whhT, const float* __restrict__ dh_ext, long dh_sb,
                 long dh_st, float dh_scale, const float* __restrict__ dhT,
                 const float* __restrict__ dcT, int B, int S, int Hd, int ndir,
-                bf16* __restrict__ dpre) {
-  bwd_recur<HD, BR, DSEQ, UG, false, PT>(pre, c_save, whhT, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT,
-                                     B, S, Hd, ndir, dpre, (int)blockIdx.x, (int)blockIdx.y,
-                                     (int)gridDim.x, BwdPub{nullptr, 1});
-}
-
-// ---------------------------------------------------------------------------------------------
-// Overlapped backward: the LSTM weight / bias gradients accumulate WHILE the
-// reverse-time recurrence runs, on the CUs the recurrence leaves idle (it holds 2 * ceil(B/BR)
-// of 256).  One launch, two roles:
-//   * recurrence workgroups (the first 2 * ceil(B/BR)): bwd_recur<..., PUB = true>; every `tc`
-//     steps they publish that block of dpre rows (write-through stores, drained, one agent-scope
-//     add per workgroup on the block's ready counter);
-//   * weight-gradient workgroups: three 64 x 64 output tiles each (one per 4-wave quarter... a
-//     third: waves 4j .. 4j+3), all of one direction, of dW_ih = dpre^T x and dW_hh = dpre^T
-//     h_{t-1} (gate rows m = 4u + g; the tiles with the first input columns also form the bias
-//     column sums).  They take the direction's blocks in the order the recurrence publishes them
-//     (fwd: last times first; rev: first times first), each block as 64-row stages through
-//     k-major LDS images (rows = batch rows, read back by the hardware transpose), and keep the
-//     sums in registers: one fixed summation order, no atomics, no split-K slabs, no reduce launch.
-//     At the end they ADD their tiles into the reference-layout .grad buffers.
-// The weight-gradient workgroups wait only on the recurrence, which never waits on them, and the
-// launcher checks that the whole grid is resident at once: no dependency cycle, no unscheduled
-// producer.  A wait that gives up (bounded polls) sets the error word (runtime.health).  The last
-// workgroup to finish zeroes the counters for the next launch.
-constexpr int OV_C = 64 + 16;            // k-major image row length (elements)
-constexpr int OV_IMG = 64 * OV_C;        // one 64-row stage of one operand
-constexpr int OV_W_READY = 32 * 4;       // word offsets in the sync block
-constexpr int OV_W_DONE = 0, OV_W_ERR = 32;
-constexpr int OV_SYNC_WORDS = OV_W_READY + 32 * 2 * OV_MAXBLK;
-constexpr int OV_SPIN = 1 << 22;
-
-typedef short ov_s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) ov_s16x4 ov_lds_s16x4;
-typedef __attribute__((ext_vector_type(4))) unsigned ov_u32x4;
-
-struct OvJob {
-  const bf16* x;      // [B*S][I] LSTM input (bf16)
-  const bf16* hprev;  // [ndir][Bp][S][HD] h_{t-1}
-  float* gwih[2];     // .grad of W_ih / W_hh / b_ih / b_hh per direction (reference layout)
-  float* gwhh[2];
-  float* gbih[2];
-  float* gbhh[2];
-  unsigned* sync;
-  int I, tc, nblk, nbc, ntile, wpd, spin, probe;
-};
-
-// 16x32 MFMA operand fragment from a k-major image [64 k][OV_C] (operand rows = image columns
-// r0 .. r0+15, k = 32 ks ..): two hardware-transposed reads (ds_read_b64_tr_b16).  k-row k is
-// stored at image row k ^ 4 * ((k >> 3) & 1) so each 32-lane half reads rows 8 apart mod 8
-// (distinct banks; the layout of gemm.hip's register-staged images).
-__device__ __forceinline__ bf16x8 ov_frag(const bf16* img, int r0, int ks, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int kb = 32 * ks + 8 * g + q;
-  const int h0 = (g & 1) ? 4 : 0;
-  const bf16* a0 = img + (kb + h0) * OV_C + r0 + 4 * p;
-  const bf16* a1 = img + (kb + (4 - h0)) * OV_C + r0 + 4 * p;
-  const ov_s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ov_lds_s16x4*)(a0));
-  const ov_s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ov_lds_s16x4*)(a1));
-  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
-// original times of block k of direction d: the forward direction's backward runs t = S-1 .. 0,
-// the reverse direction's runs its input times 0 .. S-1
-__device__ __forceinline__ void ov_block(int d, int k, int S, int tc, int& t0, int& nt) {
-  const int lo = k * tc, hi = min(S, lo + tc);
-  nt = hi - lo;
-  t0 = d == 0 ? S - hi : lo;
-}
-
-template <int HD>
-__device__ void bwd_wgrad_role(const OvJob& J, const bf16* __restrict__ dpre, int B, int S,
-                               int Hd, int ndir, int Bp, int wgi) {
-  __shared__ __attribute__((aligned(16))) bf16 img[3][2][OV_IMG];
-  constexpr int GP = 4 * HD;
-  const int tid = threadIdx.x, sub = tid >> 8, st = tid & 255, lane = st & 63, wv = st >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int d = wgi / J.wpd;
-  const int tile0 = (wgi % J.wpd) * 3 + sub;
-  const bool live = tile0 < J.ntile;
-  const int tile = live ? tile0 : 0;  // an idle third runs tile 0's loop (same barriers), stores nothing
-  const int NI = (J.I + 63) / 64, NH = HD / 64;
-  const int MT = GP / 64;
-  const bool ih = tile < MT * NI;
-  const int mt = ih ? tile / NI : (tile - MT * NI) / NH;
-  const int nt = ih ? tile % NI : (tile - MT * NI) % NH;
-  const int m0 = 64 * mt, n0 = 64 * nt;
-  const int N = ih ? J.I : HD;
-  const bool bias = ih && nt == 0;
-  bf16* As = img[sub][0];
-  bf16* Bs = img[sub][1];
-  const long rowX = (long)ndir * GP;
-  const __amdgpu_buffer_rsrc_t a_rs = dn_rsrc(dpre, (uint32_t)min((long)Bp * S * rowX * 2, 0x7fffffffL));
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
-  // this thread's two 16-B chunks of each 64-row stage: rows ir, ir + 32, columns ic .. ic+7
-  const int ir = st >> 3, ic = (st & 7) * 8;
-  bf16x8 ra[2], rb[2];
-  bool ok[2];
-  auto load = [&](int t0, int ntt, int s) {  // stage s of the block starting at time t0
-    const int rows = B * ntt;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int i = 64 * s + ir + 32 * c;
-      ok[c] = i < rows;
-      const int ic_ = ok[c] ? i : 0;
-      const int tt = ic_ / B, b = ic_ - tt * B, t = t0 + tt;
-      const uint32_t ao = (uint32_t)((((long)b * S + t) * rowX + (long)d * GP + m0 + ic) * 2);
-      ra[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(a_rs, (int)ao, 0, 16));
-      const bool okb = n0 + ic < N;
-      const bf16* bp = ih ? J.x + ((long)b * S + t) * J.I + (okb ? n0 + ic : 0)
-                          : J.hprev + (((long)d * Bp + b) * S + t) * HD + n0 + ic;
-      rb[c] = *reinterpret_cast<const bf16x8*>(bp);
-      if (!okb) ok[c] = false;  // (B only: a zero A row already zeroes the product)
-      if (!(i < rows)) { ra[c] = bf16x8{}; }
-      if (!ok[c]) rb[c] = bf16x8{};
-    }
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int k = ir + 32 * c;
-      const int r = k ^ ((k >> 1) & 4);
-      *reinterpret_cast<bf16x8*>(As + r * OV_C + ic) = ra[c];
-      *reinterpret_cast<bf16x8*>(Bs + r * OV_C + ic) = rb[c];
-    }
-  };
-  for (int k = 0; k < J.nblk; ++k) {
-    int t0, ntt;
-    ov_block(d, k, S, J.tc, t0, ntt);
-    if (tid == 0) {  // ONE lane polls the block's ready counter (sc1), the workgroup follows
-      ov_gu32* c = (ov_gu32*)(J.sync + OV_W_READY + 32 * (d * OV_MAXBLK + k));
-      int it = 0;
-      for (; it < J.spin; ++it) {
-        if (J.probe == 1 ||
-            __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)J.nbc) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (it >= J.spin)
-        __hip_atomic_store((ov_gu32*)(J.sync + OV_W_ERR), 0x300u + (unsigned)k, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    const int nst = (B * ntt + 63) / 64;
-    load(t0, ntt, 0);
-    for (int s = 0; s < nst; ++s) {
-      store();
-      __syncthreads();
-      if (s + 1 < nst) load(t0, ntt, s + 1);  // lands under this stage's MFMAs
-      if (bias && st < 64) {
-#pragma unroll 8
-        for (int r = 0; r < 64; ++r) bsum += (float)As[r * OV_C + st];
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[2], bfr[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = ov_frag(As, wm * 32 + 16 * i, ks, lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bfr[j] = ov_frag(Bs, wn * 32 + 16 * j, ks, lane);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      }
-      __syncthreads();
-    }
-  }
-  if (!live) return;
-  // epilogue: gate row m = 4u + g -> reference row g * Hd + u; added to .grad
-  float* out = ih ? J.gwih[d] : J.gwhh[d];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn * 32 + 16 * j + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + 16 * i + 4 * (lane >> 4) + r;
-        const int u = m >> 2, g = m & 3;
-        if (u < Hd && col < (ih ? N : Hd)) out[(long)(g * Hd + u) * (ih ? N : Hd) + col] += acc[i][j][r];
-      }
-    }
-  if (bias && st < 64) {
-    const int m = m0 + st, u = m >> 2, g = m & 3;
-    if (u < Hd) {
-      if (J.gbih[d]) J.gbih[d][g * Hd + u] += bsum;
-      if (J.gbhh[d]) J.gbhh[d][g * Hd + u] += bsum;
-    }
-  }
-}
-
-template <int HD, int BR>
-__global__ void __launch_bounds__(HD / 16 * 64)
-lstm_bwd_ov_kernel(const float* __restrict__ pre, const float* __restrict__ c_save,
-                   const bf16* __restrict__ whhT, const float* __restrict__ dh_ext, long dh_sb,
-                   float dh_scale, const float* __restrict__ dhT, const float* __restrict__ dcT,
-                   int B, int S, int Hd, int ndir, bf16* __restrict__ dpre, OvJob J) {
-  static_assert(HD / 16 * 64 == 768, "three 256-thread weight-gradient tiles per workgroup");
-  const int nrec = ndir * J.nbc;
-  const int wg = blockIdx.x;
-  if (wg < nrec) {
-    bwd_recur<HD, BR, false, 1, true>(pre, c_save, whhT, dh_ext, dh_sb, 0, dh_scale, dhT, dcT, B,
-                                      S, Hd, ndir, dpre, wg % J.nbc, wg / J.nbc, J.nbc,
-                                      BwdPub{J.sync + OV_W_READY, J.tc});
-  } else if (J.probe != 2) {
-    bwd_wgrad_role<HD>(J, dpre, B, S, Hd, ndir, J.nbc * BR, wg - nrec);
-  }
-  // the last workgroup to finish resets the counters for the next launch (nobody polls anymore)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ov_gu32* done = (ov_gu32*)(J.sync + OV_W_DONE);
-    const unsigned old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == gridDim.x) {
-      for (int i = 0; i < ndir * J.nblk; ++i)
-        __hip_atomic_store((ov_gu32*)(J.sync + OV_W_READY + 32 * ((i / J.nblk) * OV_MAXBLK + i % J.nblk)),
-                           0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Overlapped forward: the encoder GEMM and the input projection run INSIDE the
-// recurrence's launch, on the CUs the recurrence leaves idle, so the recurrence starts after the
-// first time chunk is projected instead of after both whole GEMMs.  One launch, two roles:
-//   * recurrence workgroups (the first ndir * ceil(B/4)): fwd_recur<..., OV = true>, which waits on
-//     a chunk's ready counter before its first (device-scope) load of that chunk's projection;
-//   * producer workgroups: every wave runs independent 32 x 64 output tiles (jobs), operands
-//     loaded straight from global memory in MFMA fragment layout (k-contiguous rows: one 16-B load
-//     per lane and fragment, 2 k-steps in flight), no LDS images and no workgroup barrier.  Jobs
-//     are enumerated chunk by chunk in the order the recurrence needs them (ndir = 2: first chunk,
-//     last chunk, second, second-to-last, ...); within a chunk the encoder tiles
-//     enc = ReLU(x W_e^T + b_e) come first, then the projection tiles xp = enc W_ih^T (the columns
-//     of the direction that needs the chunk first, then the other's).  A projection job waits on
-//     its row tile's encoder counter; a finished job stores through the write-through (sc1) path,
-//     drains, and adds 1 to its counter.
-// Waves take jobs j = wave, wave + nwaves, ... in increasing order, and a job waits only on jobs
-// earlier in that order, so the earliest unfinished job is always runnable; the launcher checks
-// that the whole grid is resident.  Waits are bounded (error word, runtime.health).  The sums
-// are the same k-order MFMA chains as the standalone GEMMs (ops.gemm): same enc / xp values.
-constexpr int FOV_W_DONE = 0, FOV_W_ERR = 32, FOV_W_READY = 64;
-constexpr int FOV_MAXRT = 64;  // 32-row tiles per chunk
-constexpr int FOV_W_ENC = FOV_W_READY + 32 * 2 * FOV_MAXCH;
-constexpr int FOV_SYNC_WORDS = FOV_W_ENC + FOV_MAXCH * FOV_MAXRT;
-constexpr int FOV_SPIN = 1 << 22;
-constexpr int FOV_LDE = 72;  // per-wave epilogue tile row (bf16): 64 + 8, 144-B rows
-
-struct FovJob {
-  const bf16* x;    // [B*S][CW] encoder input
-  const bf16* we;   // [I][CW] encoder weight (bf16 image)
-  const float* be;  // [I] encoder bias
-  bf16* enc;        // [B*S][I] ReLU(x W_e^T + b_e), kept for the backward
-  const bf16* wih;  // [ndir*GP][I] packed input weights
-  bf16* xp;         // [B*S][ndir*GP] input projection (no bias: the recurrence adds it)
-  unsigned* sync;
-  int* bump_t;
-  long long* bump_c;
-  int CW, I, GP, GPN, B, S, tc, nch, nrt, ndir, nbc, jpc, njobs, nwaves, need, spin, probe;
-  int enc_in;  // 1: enc was produced before the launch (projection jobs only, no encoder wait)
-};
-
-// one 32 x 64 tile of enc (ENC) or xp for rows [32 rt, 32 rt + 32) of chunk `chunk` and columns
-// [col0, col0 + 64), by one wave.  64 columns = one whole 128-B line of every output row, so each
-// line has ONE writer (the consumers then read it with plain loads: see fwd_recur's load_x)
-template <bool ENC>
-__device__ __forceinline__ void fov_tile(const FovJob& J, int chunk, int rt, int col0, int lane,
-                                         bf16* __restrict__ lds) {
-  const int t0 = chunk * J.tc, ntc = min(J.tc, J.S - t0), rows = J.B * ntc;
-  const int K = ENC ? J.CW : J.I;
-  const int N = ENC ? J.I : J.GPN;
-  auto grow = [&](int i) { return (i % J.B) * J.S + t0 + i / J.B; };  // chunk row -> batch row
-  const __amdgpu_buffer_rsrc_t a_rs =
-      dn_rsrc(ENC ? (const void*)J.x : (const void*)J.enc, (uint32_t)((long)J.B * J.S * K * 2));
-  const __amdgpu_buffer_rsrc_t b_rs =
-      dn_rsrc(ENC ? (const void*)J.we : (const void*)J.wih, (uint32_t)((long)N * K * 2));
-  const int kq = 8 * (lane >> 4);
-  uint32_t ao[2], bo[4];
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int i = 32 * rt + 16 * f + (lane & 15);
-    ao[f] = i < rows ? (uint32_t)(((long)grow(i) * K + kq) * 2) : DN_OOB;
-  }
-#pragma unroll
-  for (int f = 0; f < 4; ++f) bo[f] = (uint32_t)(((long)(col0 + 16 * f + (lane & 15)) * K + kq) * 2);
-  auto ld = [&](int ks, bf16x8 (&a)[2], bf16x8 (&b)[4]) {
-    const bool kin = 32 * ks + kq < K;
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-      a[f] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-          a_rs, (int)(kin && ao[f] != DN_OOB ? ao[f] + 64u * ks : DN_OOB), 0, 0));
-#pragma unroll
-    for (int f = 0; f < 4; ++f)
-      b[f] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-          b_rs, (int)(kin ? bo[f] + 64u * ks : DN_OOB), 0, 0));
-  };
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mm = [&](const bf16x8 (&a)[2], const bf16x8 (&b)[4]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-  };
-  // two k-steps in flight (a k-step is 8 MFMAs; the operands come from L2; a third register
-  // stage spilled beside the recurrence role's 168 VGPRs)
-  const int nks = (K + 31) / 32;
-  bf16x8 a0[2], b0[4], a1[2], b1[4];
-  ld(0, a0, b0);
-  ld(1, a1, b1);
-  for (int ks = 0; ks < nks; ks += 2) {
-    mm(a0, b0);
-    if (ks + 2 < nks) ld(ks + 2, a0, b0);
-    if (ks + 1 >= nks) break;
-    mm(a1, b1);
-    if (ks + 3 < nks) ld(ks + 3, a1, b1);
-  }
-  // epilogue: (bias + ReLU) -> bf16 -> the wave's LDS tile -> 16-B rows, write-through stores
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int lc = 16 * j + (lane & 15);
-    const float bb = ENC ? J.be[col0 + lc] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = acc[i][j][r];
-        if constexpr (ENC) v = fmaxf(v + bb, 0.f);
-        lds[(16 * i + 4 * (lane >> 4) + r) * FOV_LDE + lc] = (bf16)v;
-      }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  const __amdgpu_buffer_rsrc_t o_rs =
-      dn_rsrc(ENC ? (void*)J.enc : (void*)J.xp, (uint32_t)((long)J.B * J.S * N * 2));
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int c = lane + 64 * p, row = c >> 3, cc = (c & 7) * 8;
-    const int i = 32 * rt + row;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * FOV_LDE + cc);
-    const uint32_t off = i < rows ? (uint32_t)(((long)grow(i) * N + col0 + cc) * 2) : DN_OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ov_u32x4, v), o_rs, (int)off, 0, 16);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-__device__ __forceinline__ void fov_produce(const FovJob& J, int gw, int lane, bf16* lds) {
-  const int nct_e = J.I / 64, nct_p = J.GP / 64;
-  const int ne = J.enc_in ? 0 : J.nrt * nct_e, npd = J.nrt * nct_p;
-  for (int j = gw; j < J.njobs; j += J.nwaves) {
-    const int ci = j / J.jpc;
-    int r = j - ci * J.jpc;
-    const bool back = J.ndir == 2 && (ci & 1);
-    const int chunk = J.ndir == 2 ? (back ? J.nch - 1 - (ci >> 1) : (ci >> 1)) : ci;
-    if (r < ne) {
-      const int rt = r / nct_e, ct = r - rt * nct_e;
-      fov_tile<true>(J, chunk, rt, 64 * ct, lane, lds);
-      if (lane == 0)
-        __hip_atomic_fetch_add((fov_gu32*)(J.sync + FOV_W_ENC + chunk * FOV_MAXRT + rt), 1u,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      r -= ne;
-      const int dd = r / npd, r2 = r - dd * npd;
-      const int rt = r2 / nct_p, ct = r2 - rt * nct_p;
-      const int d = dd == 0 ? (back ? 1 : 0) : (back ? 0 : 1);
-      // this row tile's encoder output (all its column tiles)
-      const fov_gu32* ec = (const fov_gu32*)(J.sync + FOV_W_ENC + chunk * FOV_MAXRT + rt);
-      int it = 0;
-      while (!J.enc_in && __builtin_amdgcn_readfirstlane(
-                 __hip_atomic_load(ec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < (unsigned)nct_e) {
-        if (++it >= J.spin) {
-          __hip_atomic_store((fov_gu32*)(J.sync + FOV_W_ERR), 0x500u + (unsigned)chunk,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      fov_tile<false>(J, chunk, rt, d * J.GP + 64 * ct, lane, lds);
-      if (lane == 0)
-        __hip_atomic_fetch_add((fov_gu32*)(J.sync + FOV_W_READY + 32 * (d * FOV_MAXCH + chunk)), 1u,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <int HD, int BR>
-__global__ void __launch_bounds__(HD / 16 * 64)
-lstm_fwd_ov_kernel(const float* __restrict__ bias, const bf16* __restrict__ whh, int B, int S,
-                   int Hd, int ndir, float* __restrict__ c_save, bf16* __restrict__ hprev,
-                   float* __restrict__ hmean, float mean_scale, float* __restrict__ hT,
-                   float* __restrict__ cT, float* __restrict__ pre, int bsplit, FovJob J) {
-  __shared__ __attribute__((aligned(16))) bf16 fov_lds[HD / 16][32 * FOV_LDE];
-  const int nrec = ndir * J.nbc;
-  const int wg = blockIdx.x;
-  if (wg == 0 && threadIdx.x == 0 && J.bump_t) {  // the encoder GEMM's step-counter bump
-    *J.bump_t += 1;
-    if (J.bump_c) *J.bump_c += 1;
-  }
-  if (wg < nrec) {
-    if (J.probe != 2)
-    fwd_recur<HD, BR, false, 1, true>(J.xp, bias, whh, B, S, Hd, ndir, c_save, hprev, nullptr,
-                                      hmean, mean_scale, hT, cT, pre, bsplit, wg % J.nbc,
-                                      wg / J.nbc, J.nbc,
-                                      FwdWait{J.sync + FOV_W_READY, J.sync + FOV_W_ERR, J.tc,
-                                              J.need, J.spin});
-  } else if (J.probe != 3) {
-    const int wave = threadIdx.x >> 6;
-    fov_produce(J, (wg - nrec) * (HD / 16) + wave, threadIdx.x & 63, fov_lds[wave]);
-  }
-  // the last workgroup to finish resets the counters for the next launch (nobody polls anymore)
-  __syncthreads();
-  __shared__ int fov_last;
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add((fov_gu32*)(J.sync + FOV_W_DONE), 1u,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fov_last = old + 1 == gridDim.x;
-  }
-  __syncthreads();
-  if (fov_last) {
-    const int nr = 2 * FOV_MAXCH, nen = J.nch * FOV_MAXRT;
-    for (int i = threadIdx.x; i < nr + nen; i += blockDim.x) {
-      const int w = i < nr ? FOV_W_READY + 32 * i : FOV_W_ENC + (i - nr);
-      __hip_atomic_store((fov_gu32*)(J.sync + w), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store((fov_gu32*)(J.sync + FOV_W_DONE), 0u, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-  }
+                bf16* __restrict__ dpre, int Bp) {
+  bwd_recur<HD, BR, DSEQ, UG, PT>(pre, c_save, whhT, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT,
+                                  B, S, Hd, ndir, dpre, Bp, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1499,17 +961,14 @@ static int lstm_ug() {
 // bias layout of the current dn_lstm_fwd call (0: fused b_ih + b_hh; > 0: split, see the kernel),
 // set by dn_lstm_fwd for the launchers below (host launches are issued from one thread)
 int g_bias_split = 0;
-// the next dn_lstm_fwd / dn_lstm_bwd store / read bf16 gate pre-activations where the kernels
-// offer it (dn_lstm_pre_bf16): set by the caller per launch, so forward and backward agree
-int g_pre_bf16 = 0;
 
 template <int HD, int BR, int UG>
 int launch_fwd_ug(const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
-                  float* cT, float* pre, hipStream_t st) {
+                  float* cT, float* pre, int pre_bf16, hipStream_t st) {
   dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
   if constexpr (HD == 192 && UG == 1) {
-    if (g_pre_bf16 && !hseq) {  // bf16 pre-activations (dn_lstm_pre_bf16)
+    if (pre_bf16 && !hseq) {  // bf16 pre-activations (dn_lstm_pre_bf16_used)
       hipLaunchKernelGGL((lstm_fwd_kernel<HD, BR, false, UG, bf16>), grid, block, 0, st, xp, bias,
                          whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT,
                          reinterpret_cast<bf16*>(pre), g_bias_split);
@@ -1529,78 +988,78 @@ int launch_fwd_ug(const bf16* xp, const float* bias, const bf16* whh, int B, int
 template <int HD, int BR>
 int launch_fwd_br(const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd, int ndir,
                   float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale, float* hT,
-                  float* cT, float* pre, hipStream_t st) {
+                  float* cT, float* pre, int pre_bf16, hipStream_t st) {
   if constexpr (HD == 192 && BR == 4) {
     if (lstm_ug() == 3)
       return launch_fwd_ug<HD, BR, 3>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
-                                      mean_scale, hT, cT, pre, st);
+                                      mean_scale, hT, cT, pre, pre_bf16, st);
   }
   if constexpr (HD > 256)  // streamed weights: 2 unit groups per wave keep the block <= 16 waves
     return launch_fwd_ug<HD, BR, 2>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
-                                    mean_scale, hT, cT, pre, st);
+                                    mean_scale, hT, cT, pre, pre_bf16, st);
   else return launch_fwd_ug<HD, BR, 1>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean,
-                                  mean_scale, hT, cT, pre, st);
+                                  mean_scale, hT, cT, pre, pre_bf16, st);
 }
 
 template <int HD>
 int launch_fwd(int BR, const bf16* xp, const float* bias, const bf16* whh, int B, int S, int Hd,
                int ndir, float* c_save, bf16* hprev, float* hseq, float* hmean, float mean_scale,
-               float* hT, float* cT, float* pre, hipStream_t st) {
-  if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+               float* hT, float* cT, float* pre, int pre_bf16, hipStream_t st) {
+  if (BR == 4) return launch_fwd_br<HD, 4>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
   if constexpr (HD > 192) return DN_UNSUPPORTED;  // streamed variants: 4 rows only (pick_br)
   else {
-  if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
-  return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+  if (BR == 8) return launch_fwd_br<HD, 8>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
+  return launch_fwd_br<HD, 16>(xp, bias, whh, B, S, Hd, ndir, c_save, hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
   }
 }
 
 template <int HD, int BR, int UG>
 int launch_bwd_ug(const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
                   long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
-                  int Hd, int ndir, bf16* dpre, hipStream_t st) {
+                  int Hd, int ndir, bf16* dpre, int Bp, int pre_bf16, hipStream_t st) {
   dim3 grid((B + BR - 1) / BR, ndir), block(HD / (16 * UG) * 64);
   if constexpr (HD == 192 && UG == 1) {
-    if (g_pre_bf16 && st_ == 0) {  // bf16 pre-activations (dn_lstm_pre_bf16)
+    if (pre_bf16 && st_ == 0) {  // bf16 pre-activations (dn_lstm_pre_bf16_used)
       hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, false, UG, bf16>), grid, block, 0, st,
                          reinterpret_cast<const bf16*>(pre), c_save, whhT, dh_ext, sb, st_, scale,
-                         dhT, dcT, B, S, Hd, ndir, dpre);
+                         dhT, dcT, B, S, Hd, ndir, dpre, Bp);
       return dn_launch_status();
     }
   }
   if (st_ != 0)
     hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, true, UG>), grid, block, 0, st, pre, c_save, whhT,
-                       dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
+                       dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, Bp);
   else
     hipLaunchKernelGGL((lstm_bwd_kernel<HD, BR, false, UG>), grid, block, 0, st, pre, c_save, whhT,
-                       dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre);
+                       dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, Bp);
   return dn_launch_status();
 }
 
 template <int HD, int BR>
 int launch_bwd_br(const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
                   long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
-                  int Hd, int ndir, bf16* dpre, hipStream_t st) {
+                  int Hd, int ndir, bf16* dpre, int Bp, int pre_bf16, hipStream_t st) {
   if constexpr (HD == 192 && BR == 4) {
     if (lstm_ug() == 3)
       return launch_bwd_ug<HD, BR, 3>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S,
-                                      Hd, ndir, dpre, st);
+                                      Hd, ndir, dpre, Bp, pre_bf16, st);
   }
   if constexpr (HD > 256)
     return launch_bwd_ug<HD, BR, 2>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd,
-                                    ndir, dpre, st);
+                                    ndir, dpre, Bp, pre_bf16, st);
   else return launch_bwd_ug<HD, BR, 1>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd,
-                                  ndir, dpre, st);
+                                  ndir, dpre, Bp, pre_bf16, st);
 }
 
 template <int HD>
 int launch_bwd(int BR, const float* pre, const float* c_save, const bf16* whhT, const float* dh_ext,
                long sb, long st_, float scale, const float* dhT, const float* dcT, int B, int S,
-               int Hd, int ndir, bf16* dpre, hipStream_t st) {
-  if (BR == 4) return launch_bwd_br<HD, 4>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
+               int Hd, int ndir, bf16* dpre, int Bp, int pre_bf16, hipStream_t st) {
+  if (BR == 4) return launch_bwd_br<HD, 4>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, Bp, pre_bf16, st);
   if constexpr (HD > 192) return DN_UNSUPPORTED;
   else {
-  if (BR == 8) return launch_bwd_br<HD, 8>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
-  return launch_bwd_br<HD, 16>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, st);
+  if (BR == 8) return launch_bwd_br<HD, 8>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, Bp, pre_bf16, st);
+  return launch_bwd_br<HD, 16>(pre, c_save, whhT, dh_ext, sb, st_, scale, dhT, dcT, B, S, Hd, ndir, dpre, Bp, pre_bf16, st);
   }
 }
 
@@ -1705,56 +1164,6 @@ DN_API int dn_lstm_pack_gather(const float* wih0, const float* bih0, const float
 }
 
 
-// The overlapped backward (lstm_bwd_ov_kernel): recurrence + the LSTM weight / bias gradients in
-// ONE launch.  Taken for the resident-weight geometry it is built for (HD = 192, 4 rows per
-// workgroup, temporal-mean output) and batches whose operand offsets fit 32 bits; DN_UNSUPPORTED
-// otherwise (the caller then runs dn_lstm_bwd + the grouped weight-gradient GEMM).
-// grads: [8] = W_ih, W_hh, b_ih, b_hh .grad (fp32, reference layout) of direction 0 then 1.
-// sync: dn_lstm_ov_sync_bytes() bytes, zeroed once before the first launch.
-DN_API long dn_lstm_ov_sync_bytes() { return 4L * OV_SYNC_WORDS; }
-DN_API long dn_lstm_ov_err_word() { return OV_W_ERR; }
-DN_API int dn_lstm_bwd_ov(const float* pre, const float* c_save, const void* whhT_p,
-                          const float* dh_ext, long dh_sb, float dh_scale, const float* dhT,
-                          const float* dcT, int B, int S, int Hd, int ndir, void* dpre,
-                          const void* x, int I, const void* hprev, float* const* grads,
-                          void* sync, hipStream_t st) {
-  const int HD = dn_lstm_padded_hidden(Hd);
-  if (HD != 192 || B <= 0 || S <= 0 || ndir < 1 || ndir > 2 || I <= 0 || I % 8 || !sync ||
-      !grads)
-    return DN_UNSUPPORTED;
-  const int BR = pick_br(B, HD);
-  if (BR != 4 || (long)B * S * ndir * 4 * HD * 2 >= (1L << 31) || g_pre_bf16) return DN_UNSUPPORTED;
-  OvJob J{};
-  J.x = (const bf16*)x;
-  J.hprev = (const bf16*)hprev;
-  for (int d = 0; d < 2; ++d) {
-    J.gwih[d] = d < ndir ? grads[4 * d + 0] : nullptr;
-    J.gwhh[d] = d < ndir ? grads[4 * d + 1] : nullptr;
-    J.gbih[d] = d < ndir ? grads[4 * d + 2] : nullptr;
-    J.gbhh[d] = d < ndir ? grads[4 * d + 3] : nullptr;
-    if (d < ndir && (!J.gwih[d] || !J.gwhh[d])) return DN_BAD_SHAPE;
-  }
-  J.sync = (unsigned*)sync;
-  J.I = I;
-  J.tc = S <= 7 * OV_MAXBLK ? 7 : (S + OV_MAXBLK - 1) / OV_MAXBLK;
-  J.nblk = (S + J.tc - 1) / J.tc;
-  J.nbc = (B + BR - 1) / BR;
-  J.ntile = (4 * HD / 64) * ((I + 63) / 64 + HD / 64);
-  J.wpd = (J.ntile + 2) / 3;
-  J.spin = dn_spin_limit(OV_SPIN);
-  // diagnostic knobs (tools/fov_probe.py): DN_BOV_PROBE=1 the weight-gradient workgroups do not
-  // wait (wrong results; interference), =2 they exit at once (the recurrence role alone)
-  J.probe = 0;
-  if (const char* e = getenv("DN_BOV_PROBE")) J.probe = atoi(e);
-  const int grid = ndir * (J.nbc + J.wpd);
-  const auto kern = lstm_bwd_ov_kernel<192, 4>;
-  // the weight-gradient workgroups wait on the recurrence ones: all must be resident at once
-  if (!dn_fits_resident(reinterpret_cast<const void*>(kern), grid, 768, 0)) return DN_UNSUPPORTED;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(768), 0, st, pre, c_save, (const bf16*)whhT_p, dh_ext,
-                     dh_sb, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, J);
-  return dn_launch_status();
-}
-
 // the forward's per-workgroup buffer descriptors span BR rows (32-bit offsets); the backward
 // addresses with 64-bit pointers.  Only a single sequence longer than the descriptors can hold
 // (BR * S * ndir * 4 * HD * 4 >= 2 GiB, S in the millions) is refused.
@@ -1763,88 +1172,9 @@ static bool lstm_fits_32bit(int B, int S, int HD, int ndir, int BR) {
   return (long)BR * S * ndir * 4 * HD * 4 < (1L << 31);
 }
 
-// The overlapped forward (lstm_fwd_ov_kernel): encoder GEMM (bias + ReLU) + input projection +
-// recurrence in ONE launch.  Taken for the geometry it is built for (HD = 192, 4 rows per
-// workgroup, temporal-mean output, encoder widths CW % 8 == 0 and I % 64 == 0) when the whole grid
-// can be resident; DN_UNSUPPORTED otherwise (the caller then runs the encoder GEMM, the projection
-// GEMM and dn_lstm_fwd).  x [B*S][CW], enc_w [I][CW] and wih_p [ndir*4HD][I] bf16; enc_b fp32.
-// Outputs enc [B*S][I] and xp [B*S][ndir*4HD] (bf16) besides dn_lstm_fwd's.  tc: time steps per
-// chunk (<= 0: 4); nprod: producer workgroups (<= 0: 64); enc_in: enc is an input computed before
-// the launch (the producers run the projection only).  sync: dn_lstm_fwd_ov_sync_bytes()
-// bytes, zeroed once before the first launch.  An armed GEMM bump (dn_gemm_arm_bump) is consumed.
-DN_API long dn_lstm_fwd_ov_sync_bytes() { return 4L * FOV_SYNC_WORDS; }
-DN_API long dn_lstm_fwd_ov_err_word() { return FOV_W_ERR; }
-extern "C" int dn_gemm_take_bump(int** t, long long** c);
-DN_API int dn_lstm_fwd_ov(const void* x, int CW, const void* enc_w, const float* enc_b, void* enc,
-                          int I, const void* wih_p, void* xp, const float* bias, int bias_split,
-                          const void* whh_p, int B, int S, int Hd, int ndir, float* c_save,
-                          void* hprev, float* hmean, float mean_scale, float* hT, float* cT,
-                          float* pre, void* sync, int tc, int nprod, int enc_in,
-                          hipStream_t st) {
-  const int HD = dn_lstm_padded_hidden(Hd);
-  if (HD != 192 || B <= 0 || S <= 0 || ndir < 1 || ndir > 2 || !sync || !hmean || !enc ||
-      (!enc_in && (!x || !enc_w || !enc_b || CW <= 0 || CW % 8)) || I <= 0 || I % 64)
-    return DN_UNSUPPORTED;
-  if (bias_split != 0 && bias_split != ndir * 4 * HD) return DN_BAD_SHAPE;
-  if (pick_br(B, HD) != 4 || g_pre_bf16) return DN_UNSUPPORTED;
-  const long rows = (long)B * S;
-  const long lim = 1L << 31;
-  if ((!enc_in && rows * CW * 2 >= lim) || rows * ndir * 4 * HD * 2 >= lim || rows * I * 2 >= lim ||
-      !lstm_fits_32bit(B, S, HD, ndir, 4))
-    return DN_UNSUPPORTED;
-  if (tc <= 0) tc = 4;
-  if ((S + tc - 1) / tc > FOV_MAXCH) tc = (S + FOV_MAXCH - 1) / FOV_MAXCH;
-  FovJob J{};
-  J.x = (const bf16*)x;
-  J.we = (const bf16*)enc_w;
-  J.be = enc_b;
-  J.enc = (bf16*)enc;
-  J.wih = (const bf16*)wih_p;
-  J.xp = (bf16*)xp;
-  J.sync = (unsigned*)sync;
-  J.CW = CW;
-  J.I = I;
-  J.GP = 4 * HD;
-  J.GPN = ndir * 4 * HD;
-  J.B = B;
-  J.S = S;
-  J.tc = tc;
-  J.nch = (S + tc - 1) / tc;
-  J.nrt = (B * tc + 31) / 32;
-  if (J.nrt > FOV_MAXRT) return DN_UNSUPPORTED;
-  J.ndir = ndir;
-  J.nbc = (B + 3) / 4;
-  J.enc_in = enc_in != 0;
-  J.jpc = (J.enc_in ? 0 : J.nrt * (I / 64)) + ndir * J.nrt * (J.GP / 64);
-  J.njobs = J.nch * J.jpc;
-  J.need = J.nrt * (J.GP / 64);
-  J.spin = dn_spin_limit(FOV_SPIN);
-  if (nprod <= 0) nprod = 64;
-  // diagnostic knobs (tools/fov_probe.py): DN_FOV_PROBE=1 the recurrence does not wait for the
-  // producers (wrong results; measures the interference of the two roles), =2 the recurrence
-  // workgroups exit at once (producer time), =3 the producers exit at once and nothing waits
-  // (the recurrence role alone)
-  J.probe = 0;
-  if (const char* e = getenv("DN_FOV_PROBE")) J.probe = atoi(e);
-  if (J.probe == 1 || J.probe == 3) J.need = 0;
-  const int grid = ndir * J.nbc + nprod;
-  J.nwaves = nprod * (HD / 16);
-  const auto kern = lstm_fwd_ov_kernel<192, 4>;
-  // the recurrence waits on the producers: all workgroups must be resident at once
-  if (!dn_fits_resident(reinterpret_cast<const void*>(kern), grid, 768, 0)) return DN_UNSUPPORTED;
-  dn_gemm_take_bump(&J.bump_t, &J.bump_c);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(768), 0, st, bias, (const bf16*)whh_p, B, S, Hd, ndir,
-                     c_save, (bf16*)hprev, hmean, mean_scale, hT, cT, pre, bias_split, J);
-  return dn_launch_status();
-}
-
-// bf16 gate pre-activations for the next forward / backward launches (on != 0), where the kernels
-// offer them: per-direction hidden padded to 192 units, one unit group per wave, temporal-mean
-// output (dn_lstm_pre_bf16_used).  The caller allocates the pre buffer accordingly.
-DN_API int dn_lstm_pre_bf16(int on) {
-  g_pre_bf16 = on != 0;
-  return DN_OK;
-}
+// Can dn_lstm_fwd / dn_lstm_bwd keep the gate pre-activations in bf16 (their pre_bf16 argument)?
+// Where the kernels offer it: per-direction hidden padded to 192 units, one unit group per wave,
+// temporal-mean output.  The caller allocates the pre buffer accordingly.
 DN_API int dn_lstm_pre_bf16_used(int Hd, int seq) {
   return dn_lstm_padded_hidden(Hd) == 192 && lstm_ug() == 1 && !seq;
 }
@@ -1864,20 +1194,23 @@ DN_API int dn_lstm_rows_per_wg_bwd(int B, int Hd) {
 DN_API int dn_lstm_fwd(const void* xp, const float* bias, const void* whh_p, int B, int S, int Hd,
                        int ndir, float* c_save, void* hprev, float* hseq, float* hmean,
                        float mean_scale, float* hT, float* cT, float* pre, int bias_split,
-                       hipStream_t st) {
+                       int pre_bf16, hipStream_t st) {
   const int HD = dn_lstm_padded_hidden(Hd);
   if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
   if (bias_split != 0 && bias_split != ndir * 4 * HD) return DN_BAD_SHAPE;
+  // pre_bf16: `pre` is bf16 -- allowed only where dn_lstm_pre_bf16_used (a bf16 buffer the kernel
+  // would fill in fp32 is refused, not overrun)
+  if (pre_bf16 && !dn_lstm_pre_bf16_used(Hd, hseq != nullptr)) return DN_BAD_SHAPE;
   g_bias_split = bias_split;
   const int BR = pick_br(B, HD);
   if (!lstm_fits_32bit(B, S, HD, ndir, BR)) return DN_BAD_SHAPE;
   switch (HD) {
-    case 64: return launch_fwd<64>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
-    case 128: return launch_fwd<128>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
-    case 192: return launch_fwd<192>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
-    case 256: return launch_fwd<256>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
-    case 384: return launch_fwd<384>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
-    case 512: return launch_fwd<512>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, st);
+    case 64: return launch_fwd<64>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
+    case 128: return launch_fwd<128>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
+    case 192: return launch_fwd<192>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
+    case 256: return launch_fwd<256>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
+    case 384: return launch_fwd<384>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
+    case 512: return launch_fwd<512>(BR, (const bf16*)xp, bias, (const bf16*)whh_p, B, S, Hd, ndir, c_save, (bf16*)hprev, hseq, hmean, mean_scale, hT, cT, pre, pre_bf16, st);
   }
   return DN_UNSUPPORTED;
 }
@@ -1885,18 +1218,24 @@ DN_API int dn_lstm_fwd(const void* xp, const float* bias, const void* whh_p, int
 DN_API int dn_lstm_bwd(const float* pre, const float* c_save, const void* whhT_p,
                        const float* dh_ext, long dh_sb, long dh_st, float dh_scale,
                        const float* dhT, const float* dcT, int B, int S, int Hd, int ndir,
-                       void* dpre, hipStream_t st) {
+                       void* dpre, int Bp, int pre_bf16, hipStream_t st) {
+  // Bp: padded rows of the FORWARD's buffers (c_save [ndir][Bp][S][HD], dpre [Bp*S][...]): the
+  // backward may tile the batch with other rows per workgroup (pick_br_bwd) but addresses the
+  // forward's layout; pre_bf16 as in dn_lstm_fwd
   const int HD = dn_lstm_padded_hidden(Hd);
-  if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2) return DN_BAD_SHAPE;
-  const int BR = pick_br_bwd(B, HD);
+  if (!HD || B <= 0 || S <= 0 || ndir < 1 || ndir > 2 || Bp < B) return DN_BAD_SHAPE;
+  if (pre_bf16 && !dn_lstm_pre_bf16_used(Hd, dh_st != 0)) return DN_BAD_SHAPE;
+  int BR = pick_br_bwd(B, HD);
+  if ((B + BR - 1) / BR * BR > Bp) BR = pick_br(B, HD);  // past the buffers: the forward's tiling
+  if ((B + BR - 1) / BR * BR > Bp) return DN_BAD_SHAPE;
   if (!lstm_fits_32bit(B, S, HD, ndir, BR)) return DN_BAD_SHAPE;
   switch (HD) {
-    case 64: return launch_bwd<64>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
-    case 128: return launch_bwd<128>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
-    case 192: return launch_bwd<192>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
-    case 256: return launch_bwd<256>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
-    case 384: return launch_bwd<384>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
-    case 512: return launch_bwd<512>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, st);
+    case 64: return launch_bwd<64>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, Bp, pre_bf16, st);
+    case 128: return launch_bwd<128>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, Bp, pre_bf16, st);
+    case 192: return launch_bwd<192>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, Bp, pre_bf16, st);
+    case 256: return launch_bwd<256>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, Bp, pre_bf16, st);
+    case 384: return launch_bwd<384>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, Bp, pre_bf16, st);
+    case 512: return launch_bwd<512>(BR, pre, c_save, (const bf16*)whhT_p, dh_ext, dh_sb, dh_st, dh_scale, dhT, dcT, B, S, Hd, ndir, (bf16*)dpre, Bp, pre_bf16, st);
   }
   return DN_UNSUPPORTED;
 }

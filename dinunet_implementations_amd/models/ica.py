@@ -184,33 +184,7 @@ class ICALstm(nn.Module):
     def forward_loss(self, x: torch.Tensor, y: torch.Tensor):
         """``(probs, ce_loss, argmax)`` (reference ``comps/icalstm/__init__.py:59-63``); on a GPU
         the classifier, softmax and cross-entropy are one fused launch each way."""
-        if self._overlapped_forward_ok(x):
-            return self._overlapped_forward_loss(x, y)
         return self.body_loss(self.stem(x), y)
-
-    def _overlapped_forward_ok(self, x: torch.Tensor) -> bool:
-        """Encoder + bi-LSTM as one overlapped launch (``ops.lstm.enc_bilstm``): the fused GPU
-        path at the resident-weight hidden size (per direction <= 192), biased encoder / LSTM,
-        no activation capture (rank-dAD's module recording takes the module-by-module path)."""
-        from ..ops import lstm as L
-        return bool(L.OVERLAP_FWD and self.use_fused and x.is_cuda and x.dim() == 4
-                    and x.dtype in (torch.float32, torch.bfloat16)
-                    and self.lstm.fused_ok(x) and ops.capture.active() is None
-                    and self.encoder[0].bias is not None
-                    and L.padded_hidden(self.lstm.hidden_size) == 192)
-
-    def _overlapped_forward_loss(self, x: torch.Tensor, y: torch.Tensor):
-        from ..ops.lstm import enc_bilstm
-        lin = self.encoder[0]
-        if x.dtype == torch.float32:
-            x = x.to(torch.bfloat16)  # as stem(): every GEMM rounds its operands to bf16
-        casts: list = []
-        packed = self.lstm.prepack(x.device, side=False, casts=(lin.weight, lin.bias),
-                                   cast_out=casts)
-        B, S = x.shape[:2]
-        o = enc_bilstm(x.reshape(B * S, -1), lin, casts[0], packed, self.lstm, B, S)
-        o = o.flatten(1).to(self.classifier[1].weight.dtype)
-        return ops.head_loss(o, self.head_spec(), y, log_out=False)
 
     def stem(self, x: torch.Tensor) -> torch.Tensor:
         """First half of :meth:`forward_loss`: the encoder (``[B,S,C,W] -> [B,S,I]``).

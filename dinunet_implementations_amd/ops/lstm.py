@@ -52,75 +52,13 @@ _lib.register("dn_lstm_pack_gather", [_lib.c_void_p] * 8 + [_lib.c_int] * 3
 _lib.register("dn_lstm_fwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
                               _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
-                              _lib.c_void_p, _lib.c_int, _lib.c_void_p])
+                              _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p])
 _lib.register("dn_lstm_bwd", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                               _lib.c_long, _lib.c_long, _lib.c_float, _lib.c_void_p,
                               _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
-                              _lib.c_void_p, _lib.c_void_p])
+                              _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p])
 _lib.register("dn_lstm_rows_per_wg", [_lib.c_int, _lib.c_int])
-_lib.register("dn_lstm_bwd_ov", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_long, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_void_p])
-_lib.register("dn_lstm_ov_sync_bytes", [])
-_lib.register("dn_lstm_ov_err_word", [])
-_lib.register("dn_lstm_fwd_ov", [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_int,
-                                 _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_float, _lib.c_void_p, _lib.c_void_p,
-                                 _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
-                                 _lib.c_int, _lib.c_void_p])
-_lib.register("dn_lstm_fwd_ov_sync_bytes", [])
-_lib.register("dn_lstm_pre_bf16", [_lib.c_int])
 _lib.register("dn_lstm_pre_bf16_used", [_lib.c_int, _lib.c_int])
-_lib.register("dn_lstm_fwd_ov_err_word", [])
-
-# The overlapped backward (dn_lstm_bwd_ov: the LSTM weight / bias gradients accumulate on the
-# CUs the recurrence leaves idle, in the same launch) is opt-in (DINUNET_LSTM_OV=1): measured on
-# MI355X at the headline step (tools/_gpu_probe.sh, profiles/r4_overlap_probe.jsonl) it costs
-# 26 us per step -- the grouped weight-gradient GEMM it replaces took ~5 us, and the dpre
-# publication (write-through drains, block waits, the tail of the last blocks) takes more
-OVERLAP_BWD = os.environ.get("DINUNET_LSTM_OV", "0") == "1"
-# per-device control block of the overlapped launch (counters + error word, runtime.health)
-OV_SYNC: Dict[str, Tensor] = {}
-
-
-# The overlapped forward (dn_lstm_fwd_ov: the input projection -- and with FOV_MODE "full" the
-# encoder GEMM too -- produced time chunk by time chunk on the CUs the recurrence leaves idle, in
-# the recurrence's launch) is opt-in (DINUNET_LSTM_FOV=1).  Measured on MI355X at the headline
-# step (profiles/r4_overlap_probe.jsonl): 0.348 ms/step vs 0.3115 for the three launches.  The
-# producer waves load MFMA fragments straight from global memory (16 half-used cache lines per
-# load instruction: address-bound, 66 us for what the LDS-DMA GEMM does in 10 us) and the
-# recurrence role alone runs ~10 us slower than the standalone kernel, so the 10-19 us of GEMM it
-# hides never pays.  DINUNET_LSTM_FOV_TC: time steps per chunk; DINUNET_LSTM_FOV_WG: producer
-# workgroups
-OVERLAP_FWD = os.environ.get("DINUNET_LSTM_FOV", "0") == "1"
-# "proj": the encoder stays a standalone GEMM before the launch, only the projection overlaps;
-# "full": encoder tiles are produced in the launch too
-FOV_MODE = os.environ.get("DINUNET_LSTM_FOV_MODE", "proj")
-FOV_TC = int(os.environ.get("DINUNET_LSTM_FOV_TC", "4"))
-FOV_WG = int(os.environ.get("DINUNET_LSTM_FOV_WG", "64"))
-FOV_SYNC: Dict[str, Tensor] = {}
-
-
-def _sync_block(table: Dict[str, Tensor], bytes_fn: str, device) -> Optional[Tensor]:
-    key = str(device)
-    t = table.get(key)
-    if t is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None  # created by an eager step first (never as a node of a graph)
-        L = _lib.lib()
-        getattr(L, bytes_fn).restype = ctypes.c_long
-        t = torch.zeros(int(getattr(L, bytes_fn)()) // 4, dtype=torch.int32, device=device)
-        table[key] = t
-    return t
-
-
-def _ov_sync(device) -> Optional[Tensor]:
-    return _sync_block(OV_SYNC, "dn_lstm_ov_sync_bytes", device)
-
 # Gate pre-activations stored for the backward in bf16 instead of fp32 (the forward writes and the
 # backward reads half the bytes per step; the backward then recomputes its gates from the rounded
 # values, an error of the order of the bf16 dpre it already stores).  DINUNET_LSTM_PRE_BF16:
@@ -229,10 +167,10 @@ class _BiLSTMFn(torch.autograd.Function):
                if need_bwd else None)
         # a persistent pack (PersistentPack) keeps b_ih and b_hh as two images: summed in-kernel
         bsplit = ndir * GP if bias_p.numel() == 2 * ndir * GP else 0
-        _lib.call("dn_lstm_pre_bf16", int(pre is not None and pre.dtype == torch.bfloat16))
         _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
                   ndir, c_save.data_ptr(), hprev.data_ptr(), _lib.ptr(hseq), _lib.ptr(hmean),
-                  1.0 / S, hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), bsplit, st)
+                  1.0 / S, hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), bsplit,
+                  int(pre is not None and pre.dtype == torch.bfloat16), st)
         if mode == "mean":
             out = hmean
         else:
@@ -282,37 +220,16 @@ def _lstm_backward(ctx, saved, dout: Optional[Tensor], dhT: Optional[Tensor],
     dcT = None if dcT is None else dcT.float().contiguous()
     dpre = torch.empty(Bp * S, ndir * GP, dtype=torch.bfloat16, device=dev)
     dpre_v = dpre[:N]
-    _lib.call("dn_lstm_pre_bf16", int(pre.dtype == torch.bfloat16))
     capturing = _cap.active() is not None and ctx.modules is not None
-    done = False
-    sync = _ov_sync(dev) if (OVERLAP_BWD and mode == "mean" and HD == 192
-                             and all(p is not None for p in params)) else None
-    if sync is not None:
-        # (5)+(6) in ONE launch: the LSTM weight / bias gradients accumulate into .grad on
-        # the CUs the recurrence leaves idle, block by block as it publishes dpre
-        gl = []
-        for d in range(ndir):
-            w_ih, b_ih, w_hh, b_hh = params[4 * d:4 * d + 4]
-            gl += [_grad.grad_buffer(w_ih), _grad.grad_buffer(w_hh), _grad.grad_buffer(b_ih),
-                   _grad.grad_buffer(b_hh)]
-        gp = (ctypes.c_void_p * 8)(*([g.data_ptr() for g in gl] + [None] * (8 - len(gl))))
-        rc = _lib.lib().dn_lstm_bwd_ov(
-            pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(), dout.data_ptr(), sb, scale,
-            _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd, ndir, dpre.data_ptr(), x2d.data_ptr(), I,
-            hprev.data_ptr(), gp, sync.data_ptr(), st)
-        if rc == 0:
-            done = True
-            _grad.notify([p for p in params if p is not None])
-        elif rc != 3:  # 3 = outside the overlapped kernel's envelope
-            raise RuntimeError(f"dn_lstm_bwd_ov failed with status {rc}")
-    if not done:
-        _lib.call("dn_lstm_bwd", pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
-                  dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd,
-                  ndir, dpre.data_ptr(), st)
-        # (6) parameter grads accumulated into .grad (reference layout via row map): queued
-        # for the end-of-backward grouped launch together with the encoder's (ops._grad.defer)
-        probs = _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
-        _grad.defer(probs, [p for p in params if p is not None])
+    # the backward addresses the forward's padded buffers (Bp rows) whatever rows per workgroup
+    # it tiles with
+    _lib.call("dn_lstm_bwd", pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(),
+              dout.data_ptr(), sb, stt, scale, _lib.ptr(dhT), _lib.ptr(dcT), B, S, Hd,
+              ndir, dpre.data_ptr(), Bp, int(pre.dtype == torch.bfloat16), st)
+    # (6) parameter grads accumulated into .grad (reference layout via row map): queued
+    # for the end-of-backward grouped launch together with the encoder's (ops._grad.defer)
+    probs = _param_grad_problems(params, dpre_v, x2d, hprev, B, S, Hd, HD, ndir, dev)
+    _grad.defer(probs, [p for p in params if p is not None])
     # (7) input grad
     dx = None
     if need_dx:
@@ -334,87 +251,6 @@ def _lstm_backward(ctx, saved, dout: Optional[Tensor], dhT: Optional[Tensor],
             _cap.record(cell.i2h, x2d, dref[:, d])
             _cap.record(cell.h2h, hprev[d].view(Bp * S, HD)[:N, :Hd], dref[:, d])
     return dx, dpre_v
-
-
-class _EncBiLSTMFn(torch.autograd.Function):
-    """The ICA encoder ``ReLU(x W_e^T + b_e)`` and the bi-LSTM (temporal mean) in ONE forward
-    launch (``dn_lstm_fwd_ov``: encoder and input-projection tiles produced time chunk by time
-    chunk on the CUs the recurrence leaves idle, the recurrence waiting per chunk).  Outside that
-    kernel's envelope the same values come from the three-launch form (encoder GEMM, projection
-    GEMM, ``dn_lstm_fwd``).  Backward: the LSTM backward (``_lstm_backward``, its input gradient
-    masked by the ReLU in the GEMM epilogue), then the encoder's weight / bias gradients deferred
-    into the end-of-backward grouped launch -- the same launches as encoder + ``_BiLSTMFn``."""
-
-    @staticmethod
-    def forward(ctx, x2d: Tensor, enc_w: Tensor, enc_b: Tensor, enc_wb: Tensor, enc_module,
-                modules, packed, B: int, S: int, *params: Tensor):
-        ctx.set_materialize_grads(False)
-        ndir = len(params) // 4
-        Hd = params[2].shape[1]
-        HD = padded_hidden(Hd)
-        GP = 4 * HD
-        I, CW = enc_w.shape
-        BR = int(_lib.lib().dn_lstm_rows_per_wg(B, Hd))
-        Bp = (B + BR - 1) // BR * BR
-        dev = x2d.device
-        st = _lib.stream()
-        wih_p, bias_p, whh_p, whhT_p, ev = packed
-        if ev is not None:
-            torch.cuda.current_stream(dev).wait_event(ev)
-        enc = torch.empty(B * S, I, dtype=torch.bfloat16, device=dev)
-        xp = torch.empty(B * S, ndir * GP, dtype=torch.bfloat16, device=dev)
-        c_save = torch.empty(ndir, Bp, S, HD, dtype=torch.float32, device=dev)
-        hprev = torch.empty(ndir, Bp, S, HD, dtype=torch.bfloat16, device=dev)
-        hT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
-        cT = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
-        hmean = torch.empty(B, ndir * Hd, dtype=torch.float32, device=dev)
-        need_bwd = any(ctx.needs_input_grad)
-        pre = (torch.empty(B * S, ndir * GP, dtype=pre_dtype(B, Hd, "mean"), device=dev)
-               if need_bwd else None)
-        bsplit = ndir * GP if bias_p.numel() == 2 * ndir * GP else 0
-        _lib.call("dn_lstm_pre_bf16", int(pre is not None and pre.dtype == torch.bfloat16))
-        sync = _sync_block(FOV_SYNC, "dn_lstm_fwd_ov_sync_bytes", dev)
-        rc = 3
-        enc_in = FOV_MODE != "full"
-        if enc_in:
-            enc = mm(x2d, enc_wb, trans_b=True, bias=enc_b, relu=True, out_dtype=torch.bfloat16)
-        if sync is not None:
-            rc = _lib.lib().dn_lstm_fwd_ov(
-                x2d.data_ptr(), CW, enc_wb.data_ptr(), enc_b.data_ptr(), enc.data_ptr(), I,
-                wih_p.data_ptr(), xp.data_ptr(), bias_p.data_ptr(), bsplit, whh_p.data_ptr(), B, S,
-                Hd, ndir, c_save.data_ptr(), hprev.data_ptr(), hmean.data_ptr(), 1.0 / S,
-                hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), sync.data_ptr(), FOV_TC, FOV_WG,
-                int(enc_in), st)
-        if rc == 3:  # outside the overlapped kernel's envelope: the three-launch form
-            if not enc_in:
-                enc = mm(x2d, enc_wb, trans_b=True, bias=enc_b, relu=True,
-                         out_dtype=torch.bfloat16)
-            xp = mm_plain(enc, wih_p, trans_b=True, out_dtype=torch.bfloat16)
-            _lib.call("dn_lstm_fwd", xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd,
-                      ndir, c_save.data_ptr(), hprev.data_ptr(), None, hmean.data_ptr(), 1.0 / S,
-                      hT.data_ptr(), cT.data_ptr(), _lib.ptr(pre), bsplit, st)
-        elif rc != 0:
-            raise RuntimeError(f"dn_lstm_fwd_ov failed with status {rc}")
-        ctx.save_for_backward(enc, wih_p, whh_p, whhT_p, bias_p, pre, c_save, hprev, x2d)
-        ctx.params = params
-        ctx.relu_in = True
-        ctx.meta = (B, S, I, Hd, HD, ndir, "mean", torch.bfloat16)
-        ctx.modules = modules
-        ctx.enc = (enc_w, enc_b, enc_module)
-        ctx.overlapped = rc == 0
-        return hmean, hT, cT
-
-    @staticmethod
-    def backward(ctx, dout: Optional[Tensor], dhT: Optional[Tensor], dcT: Optional[Tensor]):
-        saved = ctx.saved_tensors
-        B, S, I = ctx.meta[:3]
-        dx, _ = _lstm_backward(ctx, saved[:8], dout, dhT, dcT, True)
-        from .linear import _take_premasked, defer_linear_grads
-        dym = dx.view(B * S, I)
-        _take_premasked(dym)  # masked in the input-gradient GEMM's epilogue
-        enc_w, enc_b, enc_module = ctx.enc
-        defer_linear_grads(saved[8], dym, enc_w, enc_b, enc_module)
-        return (None,) * 9 + (None,) * len(ctx.params)
 
 
 class _ProjFn(torch.autograd.Function):
@@ -458,18 +294,6 @@ def project(enc: Tensor, packed, relu_input: bool = False) -> Tensor:
     if ev is not None:
         torch.cuda.current_stream(enc.device).wait_event(ev)
     return _ProjFn.apply(enc, wih_p, bool(relu_input))
-
-
-def enc_bilstm(x2d: Tensor, lin, w_bf16: Tensor, packed, lstm_module, B: int, S: int) -> Tensor:
-    """``mean_t biLSTM(ReLU(x W^T + b))`` for ``x2d = [B*S, C*W]`` (bf16) through
-    :class:`_EncBiLSTMFn`; ``lin`` is the encoder ``nn.Linear``, ``w_bf16`` its bf16 image and
-    ``packed`` the LSTM's packed operands (``pack_params``).  Returns ``hmean [B, ndir*Hd]``."""
-    if not _lib.native_available():
-        raise RuntimeError("fused encoder + LSTM requested but the gfx950 kernel library is not built")
-    params = [t for cell in lstm_module.lstms for t in cell.params()]
-    hmean, _, _ = _EncBiLSTMFn.apply(x2d.contiguous(), lin.weight, lin.bias, w_bf16, lin,
-                                     list(lstm_module.lstms), packed, B, S, *params)
-    return hmean
 
 
 def pack_params(params: Sequence[Tensor], input_size: int, device, side: bool = False,

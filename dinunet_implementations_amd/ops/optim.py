@@ -335,6 +335,27 @@ class DeviceSource:
                 _lib.ptr(bump)]
 
 
+_STEP_RECORD = None
+
+
+def _step_record_type():
+    """The ctypes layout of ``optim.hip StepRecord``, checked against the library once."""
+    global _STEP_RECORD
+    if _STEP_RECORD is None:
+        import ctypes
+
+        class _Rec(ctypes.Structure):
+            _fields_ = [("out", ctypes.c_void_p), ("ld", ctypes.c_long), ("col", ctypes.c_int),
+                        ("B", ctypes.c_int), ("loss", ctypes.c_void_p), ("rs", ctypes.c_void_p),
+                        ("rl", ctypes.c_void_p), ("n", ctypes.c_long), ("cursor", ctypes.c_void_p)]
+        L = _lib.lib()
+        L.dn_step_record_size.restype = ctypes.c_long
+        if ctypes.sizeof(_Rec) != L.dn_step_record_size():
+            raise RuntimeError("step record layout mismatch with the kernel library")
+        _STEP_RECORD = _Rec
+    return _STEP_RECORD
+
+
 class StepRecorder:
     """Per-step train records of device-fed steps (``runtime.feed.DeviceFeed``): ring slot
     ``c mod n`` of batch cursor ``c`` holds the step's score column ``out[:, col]`` (``[B]``; ICA:
@@ -350,24 +371,26 @@ class StepRecorder:
         self.scores = torch.zeros(self.n, self.B, dtype=torch.float32, device=dev)
         self.losses = torch.zeros(self.n, dtype=torch.float32, device=dev)
         self.cursor = cursor
+        self._cache: Dict[tuple, object] = {}
 
     def args(self, out: torch.Tensor, loss: torch.Tensor):
-        """The ``StepRecord`` struct for a step whose outputs are ``out`` [B, C] / ``loss`` []."""
-        import ctypes
-
-        class _Rec(ctypes.Structure):
-            _fields_ = [("out", ctypes.c_void_p), ("ld", ctypes.c_long), ("col", ctypes.c_int),
-                        ("B", ctypes.c_int), ("loss", ctypes.c_void_p), ("rs", ctypes.c_void_p),
-                        ("rl", ctypes.c_void_p), ("n", ctypes.c_long), ("cursor", ctypes.c_void_p)]
-        L = _lib.lib()
-        L.dn_step_record_size.restype = ctypes.c_long
-        if ctypes.sizeof(_Rec) != L.dn_step_record_size():
-            raise RuntimeError("step record layout mismatch with the kernel library")
+        """The ``StepRecord`` struct for a step whose outputs are ``out`` [B, C] / ``loss`` [].
+        Cached per output pair: a multi-site step issued from the host every step asks for the
+        same static buffers' struct each time (no per-step class or library query)."""
+        key = (out.data_ptr(), loss.data_ptr(), tuple(out.shape))
+        rec = self._cache.get(key)
+        if rec is not None:
+            return rec
         if (out.dim() != 2 or out.shape[0] != self.B or out.dtype != torch.float32
                 or not out.is_contiguous() or loss.dtype != torch.float32 or loss.numel() != 1):
             raise ValueError("StepRecorder: out must be contiguous fp32 [B, C], loss fp32 scalar")
-        return _Rec(out.data_ptr(), out.shape[1], self.col, self.B, loss.data_ptr(),
-                    self.scores.data_ptr(), self.losses.data_ptr(), self.n, self.cursor.data_ptr())
+        rec = _step_record_type()(out.data_ptr(), out.shape[1], self.col, self.B, loss.data_ptr(),
+                                  self.scores.data_ptr(), self.losses.data_ptr(), self.n,
+                                  self.cursor.data_ptr())
+        if len(self._cache) > 64:
+            self._cache.clear()
+        self._cache[key] = rec
+        return rec
 
     def record(self, out: torch.Tensor, loss: torch.Tensor, cofs: int = -1):
         """Standalone record into slot ``(cursor + cofs) mod n``."""

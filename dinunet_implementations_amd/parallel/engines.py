@@ -57,6 +57,15 @@ class Engine:
         self._means: Dict[Tuple[int, int], DirectMean] = {}
 
     # collective path -------------------------------------------------------------------------
+    @property
+    def capturable(self) -> bool:
+        """Can the step capture this engine's collectives in its HIP graph
+        (``runtime.step.TrainStep.comm_graph``)?  Not when a site-mean goes through the direct
+        exchange (16-bit wires, ``collective.DirectMean``): RCCL's all-to-all captured from the
+        exchange's own stream crashes at capture end (``tools/diag/capture_collectives.py``
+        a2a_side, RCCL 2.26.6), so those steps keep host-issued collectives."""
+        return not self.half
+
     def step_context(self):
         return contextlib.nullcontext()
 
@@ -179,6 +188,10 @@ class DSGDEngine(Engine):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulated))
             _gradreg.register(self._on_grad)  # fused ops write .grad directly and notify
         self._reset()
+
+    @property
+    def capturable(self) -> bool:
+        return not self.direct  # all-reduce buckets (fp32, or the 16-bit all-reduce) capture
 
     def _marker(self, pid: int):
         def hook(g):

@@ -29,10 +29,13 @@ class SiteGroup:
     # does another site process use this rank's GPU? (init_sites: all-gathered (host, device);
     # None = unknown).  Launches whose workgroups wait on each other are only safe when not.
     gpu_shared: Optional[bool] = None
+    # a one-rank RCCL group that still takes every collective code path (``init_sites(loopback=
+    # True)``, ``bench.py --loopback-rccl``): times the N > 1 step on one GPU
+    loopback: bool = False
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.loopback
 
     @property
     def is_master(self) -> bool:
@@ -148,8 +151,12 @@ def resolve_device(gpus=None, local_rank: int = 0, world: int = 1, backend: Opti
 
 
 def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
-               timeout_s: Optional[int] = None, gpus=None) -> SiteGroup:
+               timeout_s: Optional[int] = None, gpus=None, loopback: bool = False) -> SiteGroup:
     """Initialise from torchrun-style env vars; world 1 when they are absent.
+
+    ``loopback`` (world 1 only): build a one-rank process group anyway (RCCL on a GPU) and mark
+    the group distributed, so every collective of the multi-site step runs -- and is captured --
+    exactly as at N > 1 (``bench.py --loopback-rccl``).
 
     ``timeout_s`` (default ``DINUNET_PG_TIMEOUT``, else 1800 s) bounds every collective: a site
     that dies or hangs makes the survivors' next collective fail (gloo: at once when the peer's
@@ -176,7 +183,10 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
     # (RCCL needs one device per rank); production multi-GPU runs use nccl (= RCCL)
     be = backend or os.environ.get("DINUNET_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
     pg = None
-    if world > 1:
+    loopback = bool(loopback and world == 1)
+    if loopback:
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    if world > 1 or loopback:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = dict(backend=be, rank=rank, world_size=world,
@@ -186,9 +196,18 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
             dist.init_process_group(**kw)
         pg = dist.group.WORLD
     _GROUP = SiteGroup(rank=rank, world=world, local_rank=local, device=dev,
-                       backend=be if world > 1 else None, pg=pg)
+                       backend=be if (world > 1 or loopback) else None, pg=pg, loopback=loopback)
     _GROUP.gpu_shared = _gpu_shared(_GROUP)
     return _GROUP
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def _gpu_shared(g: SiteGroup) -> Optional[bool]:
@@ -198,7 +217,7 @@ def _gpu_shared(g: SiteGroup) -> Optional[bool]:
     multi-node run has more ranks than local devices without sharing any."""
     if g.device.type != "cuda":
         return False
-    if not g.distributed:
+    if g.world == 1:
         return False
     import socket
     me = (socket.gethostname(), int(g.device.index or 0))

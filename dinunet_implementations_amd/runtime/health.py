@@ -1,12 +1,10 @@
 """Hand-off health of the persistent kernels: a timed-out in-kernel wait is an error, not data.
 
-Three launches of a training step hand data between their own workgroups and wait with a
+Two launches of a training step hand data between their own workgroups and wait with a
 bounded poll (so a wedged launch cannot hang the GPU): the one-launch fused head
-(``head_step.hip``: A1 / dZ1 / dZ0 hand-offs between the column workgroups and the tail), the
-one-launch rank-dAD power iteration (``lowrank.hip lr_persist_kernel``: per-layer barriers) and
-the overlapped LSTM backward (``lstm.hip lstm_bwd_ov_kernel``: weight-gradient workgroups wait
-for the recurrence's dpre blocks) and the overlapped LSTM forward (``lstm_fwd_ov_kernel``: the
-recurrence waits for a time chunk's input projection, projection tiles for their encoder rows).  A wait that gives up
+(``head_step.hip``: A1 / dZ1 / dZ0 hand-offs between the column workgroups and the tail) and the
+one-launch rank-dAD power iteration (``lowrank.hip lr_persist_kernel``: per-layer barriers).  A
+wait that gives up
 records which one in a sticky error word and lets the launch finish; the data it then used is
 whatever was there.  This module reads those words -- one small device-to-host copy per check --
 and raises, so the site loop (``runtime.site.FederatedSite``, after every validation pass and at
@@ -65,31 +63,6 @@ def handoff_errors(modules: Iterable[torch.nn.Module], engine=None,
             found.append(("head_step", code, HEAD_WAITS.get(code, "unknown wait")))
             if reset:
                 w.zero_()
-    from ..ops import lstm as _lstm
-    if _lstm.OV_SYNC:
-        L = _lib.lib()
-        L.dn_lstm_ov_err_word.restype = ctypes.c_long
-        ew = int(L.dn_lstm_ov_err_word())
-        for sync in _lstm.OV_SYNC.values():
-            w = sync[ew:ew + 1]
-            code = int(w.item())
-            if code:
-                found.append(("lstm_bwd_ov", code, f"dpre block {code & 0xff} ready wait"))
-                if reset:
-                    w.zero_()
-    if _lstm.FOV_SYNC:
-        L = _lib.lib()
-        L.dn_lstm_fwd_ov_err_word.restype = ctypes.c_long
-        ew = int(L.dn_lstm_fwd_ov_err_word())
-        for sync in _lstm.FOV_SYNC.values():
-            w = sync[ew:ew + 1]
-            code = int(w.item())
-            if code:
-                what = {4: "projection ready wait (recurrence)",
-                        5: "encoder rows ready wait (projection)"}.get(code >> 8, "wait")
-                found.append(("lstm_fwd_ov", code, f"time chunk {code & 0xff} {what}"))
-                if reset:
-                    w.zero_()
     table = getattr(engine, "_table", None) if engine is not None else None
     sync = getattr(table, "_persist", None)
     if sync is not None:

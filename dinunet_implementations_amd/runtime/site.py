@@ -371,7 +371,17 @@ class FederatedSite:
                 or not isinstance(trainer.optimizer, FusedAdam)
                 or not (engine.name.startswith("dSGD") or getattr(engine, "fast", False))):
             return None
-        return DeviceFeed(step, tr.inputs, tr.labels, bs, steps, col=col)
+        X = tr.inputs
+        if X.dtype != torch.bfloat16:
+            # the feed keeps a bf16 copy of the split in HBM next to the loader's: fall back to
+            # the host-fed loop (same trajectory) when it would not fit
+            need = X.numel() * 2 + tr.labels.numel() * 8
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if need > 0.9 * free:
+                self.log(f"device feed off: its bf16 copy of the train split ({need / 2**30:.2f} "
+                         f"GiB) does not fit the free HBM ({free / 2**30:.2f} GiB)")
+                return None
+        return DeviceFeed(step, X, tr.labels, bs, steps, col=col)
 
     def _pretrain(self, trainer: NNTrainer, data, fold_dir: str, seed: int, logs: Dict[str, Any]):
         sizes = self.group.all_gather_object(int(data["train"][0].shape[0]))

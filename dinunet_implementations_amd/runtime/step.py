@@ -11,14 +11,21 @@ Before each replay ONE prologue launch converts the batch into the graph's stati
 copies the labels and zeroes the flat gradient.  With a single site the fused Adam update is
 captured too (its step number lives on the device), so a step is prologue + one replay.
 
-Split capture (dSGD across sites): the model's ``stem`` (ICA: the encoder) produces the LAST
-gradients of the backward, so the step is captured as TWO graphs cut inside the backward —
-A = zero-grad + forward + backward of everything after the cut, B = the rest.  The cut is the
-LSTM input projection when the model provides ``proj_stem`` (A then ends with every LSTM and head
-gradient final; B = the input-gradient GEMM + the encoder's weight gradients), else the stem
-output (B = the encoder's weight gradients).  Between the replays the all-reduce of every
-non-stem gradient starts on RCCL's stream and runs under graph B; only the small stem bucket's
-all-reduce is exposed.
+Split backward (dSGD across sites): the model's ``stem`` (ICA: the encoder) produces the LAST
+gradients of the backward, so the backward is issued in two parts cut at the LSTM input
+projection when the model provides ``proj_stem`` (part A ends with every LSTM and head gradient
+final; part B = the input-gradient GEMM + the encoder's weight gradients), else at the stem
+output.  The all-reduce of every non-stem gradient starts on RCCL's stream between the parts and
+runs under part B; only the small stem bucket's all-reduce is exposed.
+
+Multi-site steps over RCCL capture their collectives (``comm_graph``, default; RCCL supports
+stream capture): the two backward parts, the bucket all-reduces on RCCL's stream (a forked
+branch of the graph, joined before the update), the engine's reduction and the fused Adam are
+ONE captured step, and device-fed runs replay graphs of K whole steps exactly as at one site --
+no host work, no graph boundary and no eager launch between steps.  Without it
+(``DINUNET_CAPTURE_COMM=0``, or the gloo backend, whose collectives are host calls) the parts
+are two graphs A / B with the collectives and the update issued from the host between and
+after the replays.
 """
 from __future__ import annotations
 
@@ -63,6 +70,10 @@ SPLIT_AT_PROJECTION = os.environ.get("DINUNET_SPLIT_AT", "projection") != "stem"
 # from the parameters it updates, zeroes the gradient and gathers the next batch (one launch
 # instead of Adam + a pack/gather launch per step); DINUNET_ADAM_PACK=0 keeps the pack launch
 ADAM_PACK = os.environ.get("DINUNET_ADAM_PACK", "1") != "0"
+
+# Multi-site steps over RCCL capture the engine's collectives inside the step graph
+# (DINUNET_CAPTURE_COMM=0 keeps host-issued collectives between two graph replays)
+CAPTURE_COMM = os.environ.get("DINUNET_CAPTURE_COMM", "1") != "0"
 
 
 class _NoDefer:
@@ -115,6 +126,11 @@ class TrainStep:
             env = os.environ.get("DINUNET_SPLIT_GRAPH", "")
             split = can_split and (engine.group.distributed if env == "" else env == "1")
         self.split = bool(split and can_split)
+        # collectives inside the captured step: RCCL only (gloo collectives are host calls)
+        grp = engine.group
+        self.comm_graph = bool(CAPTURE_COMM and self.use_graph and grp.distributed
+                               and grp.backend == "nccl" and self.accum == 1
+                               and getattr(engine, "capturable", True))
         self.split_at = None  # "projection" | "stem", set at capture
         self._first_buckets = engine.split_buckets(list(model.stem_parameters())) if self.split else []
         self.graph_b = None
@@ -202,10 +218,11 @@ class TrainStep:
                 self.flat.grad.zero_()
 
     def _graph_opt_ok(self) -> bool:
-        # the optimizer joins the graph when no collective sits between backward and update
-        # (and every replay is a whole step: no accumulation)
-        return (not self.engine.group.distributed and isinstance(self.opt, ops.FusedAdam)
-                and self.flat.data.is_cuda and self.accum == 1)
+        # the optimizer joins the graph when every collective between backward and update is
+        # captured too (one site: none) and every replay is a whole step (no accumulation)
+        return ((not self.engine.group.distributed or self.comm_graph)
+                and isinstance(self.opt, ops.FusedAdam) and self.flat.data.is_cuda
+                and self.accum == 1)
 
     def _reduce_after_replay(self):
         if self._pre_reduce is not None:
@@ -228,7 +245,10 @@ class TrainStep:
             self._cap_lr = self.opt.lr
         try:
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE), self._defer_pack() as dp:
-                out, loss, pred = self._fwd_bwd(sx, sy)
+                if self.split:  # comm_graph: both backward parts, the buckets launched between
+                    out, loss, pred = self._split_backward(sx, sy)
+                else:
+                    out, loss, pred = self._fwd_bwd(sx, sy)
                 if self._pre_reduce is not None:
                     self._pre_reduce()
                 if self.graph_opt:
@@ -263,6 +283,21 @@ class TrainStep:
             self._backward(loss)
         return h, hd, out, loss, pred
 
+    def _split_backward(self, sx, sy, fwd_ctx=None):
+        """Both parts of a split step issued into the current stream, the non-stem buckets'
+        collectives launched between them (captured: a branch on RCCL's stream).  ``fwd_ctx``:
+        the context the forward runs in (device-fed prologue / Adam-emitted pack)."""
+        with (fwd_ctx if fwd_ctx is not None else _NoDefer()) as rp:
+            h, hd, out, loss, pred = self._split_fwd_bwd(sx, sy)
+        if isinstance(rp, ride_pack) and not rp.consumed:
+            raise RuntimeError("device-fed prologue was not absorbed by the model's weight pack")
+        for b in self._first_buckets:  # all-reduce under the stem backward
+            self.engine.launch_bucket(b)
+        if h.requires_grad:
+            torch.autograd.backward(h, hd.grad)
+        self._keep = (h, hd)
+        return out, loss, pred
+
     def _capture_split(self, x, y):
         sx, sy = self._static_inputs(x, y)
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -296,7 +331,7 @@ class TrainStep:
                     loss = self._eager(x, y, first, last)
                 torch.cuda.current_stream().wait_stream(s)
                 return loss
-            (self._capture_split if self.split else self._capture)(x, y)
+            (self._capture_split if (self.split and not self.comm_graph) else self._capture)(x, y)
         sx, sy, out, loss, pred = self.static
         if sx.shape != x.shape or sy.shape != y.shape:  # e.g. a ragged last batch
             loss = self._eager(x, y, first, last)
@@ -438,8 +473,28 @@ class TrainStep:
         # after the last replay: the cursor names the NEXT batch again (the eager convention)
         self.src.cursor.add_(1)
 
+    def _dev_body_split(self):
+        """One whole multi-site device-fed step with its collectives (``comm_graph``): prologue
+        (or the Adam-emitted pack's forward), the split backward with the non-stem buckets'
+        all-reduce between its parts, the reduction, and the update that also emits the next
+        step's operands -- everything a replay needs, so K such steps form one graph."""
+        if self._apack is not None:
+            out, loss, pred = self._split_backward(self._dsx, self._dsy, self._apack_forward())
+        else:
+            out, loss, pred = self._split_backward(self._dsx, self._dsy,
+                                                   self._dev_prologue(self.opt.device_step()))
+        scale = self._reduce_after_replay()
+        if self._apack is not None:
+            self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss))
+        else:
+            self.opt.step_graphable(grad_scale=scale, prebumped=True)
+            self._record(out, loss)
+        return out, loss, pred
+
     def _dev_body(self, graph_opt: bool):
         """One whole device-fed step as issued into the current stream (eager or captured)."""
+        if self.split and self.comm_graph and graph_opt:
+            return self._dev_body_split()
         if self._apack is not None and graph_opt:
             return self._dev_body_apack()
         bump = self.opt.device_step() if graph_opt else None
@@ -546,7 +601,7 @@ class TrainStep:
         if self._dgraphs and self.opt.lr != self._cap_lr and any(
                 v[2] is True for v in self._dgraphs.values()):
             self._dgraphs = {}  # the learning rate is baked into the captured update
-        if self.split:
+        if self.split and not self.comm_graph:
             if "split" not in self._dgraphs:
                 self._dev_capture_split()
             ga, gb, (out, loss, pred), _ = self._dgraphs["split"]
@@ -584,7 +639,9 @@ class TrainStep:
             self.opt.step_count += k
         else:
             with self.timers.phase("reduce"):
-                scale = self._reduce_after_replay()
+                # the replay holds no local factorisation here (_dev_body captures pre_reduce
+                # only with the update): the engine's full reduction runs it
+                scale = self.engine.reduce()
             with self.timers.phase("optim"):
                 self.opt.step(grad_scale=scale)
                 self._record(out, loss)
@@ -596,7 +653,7 @@ class TrainStep:
         region never includes a capture.  Call after the eager warm-up steps."""
         if self.src is None or not self.use_graph or self._dcalls < self.eager_warmup:
             return
-        if self.split:
+        if self.split and not self.comm_graph:
             if "split" not in self._dgraphs:
                 self._dev_capture_split()
             return

@@ -59,55 +59,3 @@ def test_site_loop_fails_on_timed_out_handoff(tmp_path, spin_zero):
     root = _ica_root(tmp_path)
     with pytest.raises(spin_zero.HandoffError):
         _run_site(root, str(tmp_path / "out"), {"epochs": 2, "batch_size": 8})
-
-
-def test_overlapped_backward_wait_timeout_raises(spin_zero, monkeypatch):
-    """The overlapped LSTM backward's weight-gradient workgroups give up waiting for the dpre
-    blocks at once with a zero poll limit: its error word must make the check raise."""
-    health = spin_zero
-    from dinunet_implementations_amd.models import ICALstm
-    from dinunet_implementations_amd.ops import lstm as L
-    monkeypatch.setattr(L, "OVERLAP_BWD", True)
-    torch.manual_seed(0)
-    m = ICALstm(input_size=64, hidden_size=384, num_comps=20, window_size=10).cuda().train()
-    x = torch.randn(32, 14, 20, 10, device="cuda")
-    y = torch.randint(0, 2, (32,), device="cuda")
-    _, loss, _ = m.forward_loss(x, y)
-    loss.backward()
-    torch.cuda.synchronize()
-    with pytest.raises(health.HandoffError, match="lstm_bwd_ov"):
-        health.check([m])
-    health.set_spin_limit(-1)
-    _, loss, _ = m.forward_loss(x, y)
-    loss.backward()
-    torch.cuda.synchronize()
-    health.check([m])
-
-
-@pytest.mark.parametrize("mode", ["proj", "full"])
-def test_overlapped_forward_wait_timeout_raises(spin_zero, monkeypatch, mode):
-    """The overlapped LSTM forward's recurrence gives up waiting for the first projected time
-    chunk at once with a zero poll limit: its error word must make the check raise."""
-    health = spin_zero
-    from dinunet_implementations_amd.models import ICALstm
-    from dinunet_implementations_amd.ops import lstm as L
-    monkeypatch.setattr(L, "OVERLAP_FWD", True)
-    monkeypatch.setattr(L, "FOV_MODE", mode)
-    # one producer workgroup for a 98-step sequence: the recurrence outruns the projection and
-    # must wait (the first chunk alone can be ready before the recurrence's first poll)
-    monkeypatch.setattr(L, "FOV_WG", 1)
-    torch.manual_seed(0)
-    m = ICALstm(input_size=64, hidden_size=384, num_comps=20, window_size=10).cuda().eval()
-    x = torch.randn(32, 98, 20, 10, device="cuda")
-    y = torch.randint(0, 2, (32,), device="cuda")
-    with torch.no_grad():
-        m.forward_loss(x, y)
-    torch.cuda.synchronize()
-    assert L.FOV_SYNC, "the overlapped forward did not run"
-    with pytest.raises(health.HandoffError, match="lstm_fwd_ov"):
-        health.check([m])
-    health.set_spin_limit(-1)
-    with torch.no_grad():
-        m.forward_loss(x, y)
-    torch.cuda.synchronize()
-    health.check([m])

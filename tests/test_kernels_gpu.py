@@ -616,109 +616,3 @@ def test_payload_kernels_match_torch_layout(payload, n, W):
     else:
         r = ((out - x).abs() / x.abs()).max().item()
         assert r <= (2.0 ** -11 if payload == "fp16" else 2.0 ** -8) * 1.01, r
-
-
-@pytest.mark.parametrize("B,S,hidden", [(32, 98, 384), (13, 12, 384), (8, 30, 300)])
-def test_overlapped_lstm_backward_matches_grouped(B, S, hidden, monkeypatch):
-    """dn_lstm_bwd_ov (recurrence + the LSTM weight / bias gradients accumulated block by block
-    on the idle CUs, one launch) gives the gradients of dn_lstm_bwd + the grouped weight-gradient
-    GEMM: same dpre, the sums in another order.  Ragged batches (padded rows), sequences that are
-    not a multiple of the 7-step publication block, and a padded hidden (300 -> 2 x 150 in the
-    192-unit kernel) included."""
-    from dinunet_implementations_amd.models import ICALstm
-    from dinunet_implementations_amd.ops import lstm as L
-    torch.manual_seed(0)
-    m = ICALstm(input_size=256, hidden_size=hidden, num_comps=20, window_size=10).cuda().train()
-    m.classifier[0].p = 0.0
-    g = torch.Generator(device="cuda").manual_seed(4)
-    x = torch.randn(B, S, 20, 10, device="cuda", generator=g)
-    y = torch.randint(0, 2, (B,), device="cuda", generator=g)
-    grads = {}
-    for ov in (False, True):
-        monkeypatch.setattr(L, "OVERLAP_BWD", ov)
-        m.zero_grad(set_to_none=True)
-        _, loss, _ = m.forward_loss(x, y)
-        loss.backward()
-        torch.cuda.synchronize()
-        grads[ov] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
-    assert L.OV_SYNC, "the overlapped launch did not run"
-    sync = next(iter(L.OV_SYNC.values()))
-    assert int(sync[32].item()) == 0, "a weight-gradient wait timed out"
-    for n in grads[False]:
-        a, b = grads[True][n], grads[False][n]
-        rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
-        assert rel < 2e-3, (n, rel)
-
-
-@pytest.mark.parametrize("mode", ["proj", "full"])
-@pytest.mark.parametrize("B,S,hidden,tc,nwg", [(32, 98, 384, 4, 64), (13, 12, 384, 4, 64),
-                                              (8, 30, 300, 7, 64), (32, 98, 384, 1, 3),
-                                              (5, 9, 384, 4, 1)])
-def test_overlapped_forward_matches_three_launches(B, S, hidden, tc, nwg, mode, monkeypatch):
-    """dn_lstm_fwd_ov (encoder GEMM + input projection produced chunk by chunk by producer waves
-    inside the recurrence's launch) against the three-launch form (encoder GEMM, projection GEMM,
-    dn_lstm_fwd): the tiles accumulate in the same k order, so loss and output agree to fp32
-    rounding and every gradient matches.  Ragged batches, sequences that are not a multiple of the
-    chunk, a padded hidden (300 -> 2 x 150 in the 192-unit kernel), one-step chunks, and a
-    single producer workgroup (12 waves serialising every job: the in-order job argument) are
-    included."""
-    from dinunet_implementations_amd.models import ICALstm
-    from dinunet_implementations_amd.ops import lstm as L
-    from dinunet_implementations_amd.runtime import health
-    torch.manual_seed(0)
-    m = ICALstm(input_size=256, hidden_size=hidden, num_comps=20, window_size=10).cuda().train()
-    m.classifier[0].p = 0.0
-    g = torch.Generator(device="cuda").manual_seed(4)
-    x = torch.randn(B, S, 20, 10, device="cuda", generator=g)
-    y = torch.randint(0, 2, (B,), device="cuda", generator=g)
-    monkeypatch.setattr(L, "FOV_TC", tc)
-    monkeypatch.setattr(L, "FOV_WG", nwg)
-    monkeypatch.setattr(L, "FOV_MODE", mode)
-    res = {}
-    for ov in (False, True):
-        monkeypatch.setattr(L, "OVERLAP_FWD", ov)
-        m.zero_grad(set_to_none=True)
-        probs, loss, _ = m.forward_loss(x, y)
-        loss.backward()
-        torch.cuda.synchronize()
-        res[ov] = (probs.detach().clone(), float(loss),
-                   {n: p.grad.detach().clone() for n, p in m.named_parameters()})
-    assert L.FOV_SYNC, "the overlapped forward did not run"
-    health.check([m])  # no wait gave up
-    assert abs(res[True][1] - res[False][1]) <= 1e-6 * max(1.0, abs(res[False][1])), \
-        (res[True][1], res[False][1])
-    assert (res[True][0] - res[False][0]).abs().max().item() <= 1e-6
-    for n in res[False][2]:
-        a, b = res[True][2][n], res[False][2][n]
-        rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
-        assert rel < 1e-5, (n, rel)
-
-
-@pytest.mark.parametrize("mode", ["proj", "full"])
-def test_overlapped_forward_in_graph_replay(mode, monkeypatch):
-    """The overlapped forward captured in a HIP graph and replayed: its control block resets
-    itself at the end of every launch (the last workgroup zeroes the counters), so replays
-    agree with an eager step on the same batch."""
-    from dinunet_implementations_amd.models import ICALstm
-    from dinunet_implementations_amd.ops import lstm as L
-    monkeypatch.setattr(L, "OVERLAP_FWD", True)
-    monkeypatch.setattr(L, "FOV_MODE", mode)
-    torch.manual_seed(0)
-    m = ICALstm(input_size=256, hidden_size=384, num_comps=20, window_size=10).cuda().eval()
-    x = torch.randn(32, 40, 20, 10, device="cuda").to(torch.bfloat16)
-    y = torch.randint(0, 2, (32,), device="cuda")
-    with torch.no_grad():
-        ref = m.forward_loss(x, y)[0].clone()
-        assert L.FOV_SYNC
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            m.forward_loss(x, y)
-        torch.cuda.current_stream().wait_stream(s)
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr):
-            out = m.forward_loss(x, y)[0]
-        for _ in range(5):
-            gr.replay()
-        torch.cuda.synchronize()
-    assert torch.equal(out, ref)

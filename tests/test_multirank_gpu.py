@@ -56,6 +56,12 @@ CASES = [
     (2, ["--engine", "dSGD", "--precision", "32", "--feed", "device", "--oracle"]),
     (3, ["--engine", "dSGD", "--precision", "16", "--feed", "device", "--oracle",
          "--oracle-tol", "0.3"]),
+    # device-fed low-rank engines across sites (host-issued collectives: each replay's local
+    # factorisation must run in the engine's reduction -- it once did not)
+    (2, ["--engine", "rankDAD", "--precision", "32", "--dad-tol", "0", "--feed", "device",
+         "--oracle", "--grad-tol", "1e-6", "--oracle-tol", "0.4"]),
+    (2, ["--engine", "powerSGD", "--precision", "32", "--feed", "device", "--oracle",
+         "--grad-tol", "1e-6", "--oracle-tol", "0.25"]),
 ]
 
 
@@ -83,6 +89,6 @@ def test_replicas_bit_identical(world, args):
         if "device" not in args:  # (device-fed: the fused Adam zeroes the gradient it consumes)
             assert "grad_rel_err" in res, res
     assert res["graph"] and res["world"] == world
-    if "device" in args:  # the bench path: the update emits the next step's operands
-        assert res["adam_pack"] and res["split"], res
+    if "device" in args and "dSGD" in args:  # the bench path: the update emits the next
+        assert res["adam_pack"] and res["split"], res  # step's operands
     assert r.returncode == 0, r.stderr[-3000:]

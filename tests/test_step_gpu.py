@@ -123,6 +123,117 @@ def test_split_capture_overlapped_allreduce_over_rccl():
         dist.destroy_process_group()
 
 
+@pytest.fixture
+def rccl1():
+    """A one-rank RCCL process group the multi-site code paths run on (``_OneRankGroup``)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        yield _OneRankGroup(dist.group.WORLD)
+    finally:
+        dist.destroy_process_group()
+
+
+def _trainer_cfg(seed, engine, group, cfg, **kw):
+    from dinunet_implementations_amd.ops import FlatParams, FusedAdam
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.runtime.step import TrainStep
+    m = _model(seed, kw.pop("hidden", 128))
+    flat = FlatParams(m.parameters())
+    opt = FusedAdam(flat, lr=1e-3)
+    eng = make_engine(engine, m, flat, group, {"precision_bits": "32", **cfg})
+    return m, flat, TrainStep(m, flat, opt, eng, task="ica", **kw)
+
+
+def _device_fed(step, xs, ys, n, K=4):
+    from dinunet_implementations_amd.runtime.feed import DeviceFeed
+    B = xs.shape[1]
+    X = xs.reshape(-1, *xs.shape[2:]).to(torch.bfloat16)
+    Y = ys.reshape(-1)
+    feed = DeviceFeed(step, X, Y, B, xs.shape[0], col=1, steps_per_graph=K)
+    feed.run(3)
+    feed.prepare(n - 3)
+    feed.run(n - 3)
+    torch.cuda.synchronize()
+    return feed
+
+
+@pytest.mark.parametrize("apack", [True, False])
+def test_comm_graph_device_fed_matches_single_site(rccl1, apack, monkeypatch):
+    """The multi-site device-fed step with its RCCL collectives captured (split backward, the
+    body bucket's all-reduce on RCCL's stream between the parts, the stem bucket, the update and
+    the next operands) replays in K-step graphs like one site and, over a one-rank RCCL group
+    (sum over one site = identity), trains bit-identically to the single-site step."""
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    from dinunet_implementations_amd.runtime import step as step_mod
+    monkeypatch.setattr(step_mod, "ADAM_PACK", apack)
+    xs, ys = _batches(n=8)
+    n = 16
+    _, f1, s1 = _trainer_cfg(0, "dSGD", SiteGroup(device=torch.device("cuda")), {}, use_graph=True)
+    _, f2, s2 = _trainer_cfg(0, "dSGD", rccl1, {}, use_graph=True)
+    assert s2.split and s2.comm_graph and not s1.comm_graph
+    _device_fed(s1, xs, ys, n)
+    _device_fed(s2, xs, ys, n)
+    assert set(s2._dgraphs) == {4, 1}, "K-step graphs, not the two-graph split replay"
+    assert (s2._apack is not None) == apack
+    assert s2.opt.step_count == s1.opt.step_count == n
+    assert s2.engine.comm_bytes == f2.numel * 4
+    assert torch.equal(f1.data, f2.data), (f1.data - f2.data).abs().max()
+    assert abs(float(s1.last_loss) - float(s2.last_loss)) == 0.0
+
+
+@pytest.mark.parametrize("engine,cfg,captured", [
+    ("dSGD", {}, True),
+    ("dSGD", {"precision_bits": "16"}, False),          # direct fp16 exchange: host-issued
+    ("dSGD", {"precision_bits": "16", "dsgd_collective": "allreduce", "payload_dtype": "bf16"},
+     True),
+    ("rankDAD", {}, True),
+    ("powerSGD", {}, True),
+])
+def test_comm_graph_matches_host_issued_collectives(rccl1, engine, cfg, captured, monkeypatch):
+    """Every engine with a capturable wire: the step with its collectives captured in the K-step
+    graph gives the trajectory of the uncaptured multi-site step (DINUNET_CAPTURE_COMM=0:
+    host-issued collectives between / after the replays, eager update).  The direct 16-bit
+    exchange (RCCL all-to-all) keeps host-issued collectives (Engine.capturable)."""
+    from dinunet_implementations_amd.runtime import step as step_mod
+    xs, ys = _batches(n=8)
+    n = 12
+    monkeypatch.setattr(step_mod, "CAPTURE_COMM", False)
+    _, fh, sh = _trainer_cfg(0, engine, rccl1, cfg, use_graph=True)
+    monkeypatch.setattr(step_mod, "CAPTURE_COMM", True)
+    _, fc, sc = _trainer_cfg(0, engine, rccl1, cfg, use_graph=True)
+    assert sc.comm_graph == captured and not sh.comm_graph
+    if not captured:
+        return
+    _device_fed(sh, xs, ys, n)
+    _device_fed(sc, xs, ys, n)
+    assert 4 in sc._dgraphs and sc._dK == 4
+    assert sc.opt.step_count == sh.opt.step_count == n
+    assert torch.allclose(fh.data, fc.data, rtol=1e-5, atol=1e-6), (fh.data - fc.data).abs().max()
+    eng = sc.engine
+    if hasattr(eng, "_table") and getattr(eng._table, "_persist", None) is not None:
+        assert eng._table.persist_error() == 0
+
+
+def test_comm_graph_host_fed_matches_uncaptured(rccl1, monkeypatch):
+    """Host-fed steps (``TrainStep.__call__``) across sites: one captured graph per step with
+    the split backward, the bucket collectives and the fused Adam inside == the two-graph
+    replay with host-issued collectives and an eager update."""
+    from dinunet_implementations_amd.runtime import step as step_mod
+    xs, ys = _batches()
+    monkeypatch.setattr(step_mod, "CAPTURE_COMM", False)
+    _, fh, sh = _trainer_cfg(0, "dSGD", rccl1, {}, use_graph=True)
+    monkeypatch.setattr(step_mod, "CAPTURE_COMM", True)
+    _, fc, sc = _trainer_cfg(0, "dSGD", rccl1, {}, use_graph=True)
+    _run(sh, xs, ys)
+    _run(sc, xs, ys)
+    assert sc.graph_opt and sc.graph_b is None and sh.graph_b is not None
+    assert sc.opt.step_count == sh.opt.step_count == xs.shape[0]
+    assert int(sc.opt.device_step().item()) == sc.opt.step_count
+    assert torch.allclose(fh.data, fc.data, rtol=1e-6, atol=1e-7), (fh.data - fc.data).abs().max()
+
+
 def test_rankdad_capture_reconstructs_fused_gradients():
     """Every Linear's (A, Delta) captured from the fused encoder / LSTM / head kernels must
     rebuild that Linear's weight gradient: dW = Delta^T A."""

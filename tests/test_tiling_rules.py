@@ -35,8 +35,9 @@ def test_split_rule_long_k_targets_workgroups_per_cu():
 
 def test_lstm_backward_rows_tile_the_forward_padding():
     """The backward recurrence may tile the batch with more rows per workgroup than the forward
-    (8 vs 4 from B = 2048 at 192 units); its grid must never reach rows past the forward's padded
-    buffers, at any batch and hidden size."""
+    (8 vs 4 from B = 1024 at 192 units).  It addresses the forward's padded buffers with the
+    forward's row count, passed explicitly (``dn_lstm_bwd``'s ``Bp``), so a tiling only has to
+    stay inside them: never a row past the forward's padding, at any batch and hidden size."""
     from dinunet_implementations_amd.ops import _lib
     if not _lib.native_available():
         import pytest
@@ -50,5 +51,34 @@ def test_lstm_backward_rows_tile_the_forward_padding():
             padded = -(-B // bf) * bf
             assert -(-B // bb) * bb <= padded, (hd, B, bf, bb)
     assert int(L.dn_lstm_rows_per_wg(2048, 192)) == 4 and int(L.dn_lstm_rows_per_wg_bwd(2048, 192)) == 8
+    assert int(L.dn_lstm_rows_per_wg_bwd(1024, 192)) == 8
     assert int(L.dn_lstm_rows_per_wg_bwd(2044, 192)) == 4  # not a multiple of 8: same as forward
     assert int(L.dn_lstm_rows_per_wg_bwd(32, 192)) == 4
+
+
+def test_lstm_launchers_refuse_inconsistent_buffers():
+    """The host launchers check what the kernels would otherwise read silently wrong, before any
+    launch (so this runs without a GPU): a backward given fewer padded rows than the batch, and a
+    bf16 pre-activation buffer where the kernels only offer fp32 (the element type
+    travels as an explicit argument, not a process-global flag)."""
+    import ctypes
+    from dinunet_implementations_amd.ops import _lib
+    if not _lib.native_available():
+        import pytest
+        pytest.skip("kernel library not built")
+    L = _lib.lib()
+    V, I_, Lg, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
+    L.dn_lstm_bwd.argtypes = [V, V, V, V, Lg, Lg, F, V, V, I_, I_, I_, I_, V, I_, I_, V]
+    L.dn_lstm_fwd.argtypes = [V, V, V, I_, I_, I_, I_, V, V, V, V, F, V, V, V, I_, I_, V]
+    BAD = 1  # common.h DN_BAD_SHAPE
+    # Bp < B
+    assert L.dn_lstm_bwd(None, None, None, None, 384, 0, 1.0, None, None, 32, 98, 192, 2, None,
+                         16, 0, None) == BAD
+    # bf16 pre at 64 units (only the 192-unit resident geometry offers it), and with a sequence
+    # output
+    assert L.dn_lstm_bwd(None, None, None, None, 128, 0, 1.0, None, None, 32, 98, 64, 2, None,
+                         32, 1, None) == BAD
+    assert L.dn_lstm_fwd(None, None, None, 32, 98, 64, 2, None, None, None, None, 1.0, None, None,
+                         None, 0, 1, None) == BAD
+    assert L.dn_lstm_fwd(None, None, None, 32, 98, 192, 2, None, None, ctypes.c_void_p(16),
+                         None, 1.0, None, None, None, 0, 1, None) == BAD

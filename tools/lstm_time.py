@@ -23,8 +23,8 @@ def time_lib(path, B=32, S=98, I=256, H=384, reps=50):
     lib = ctypes.CDLL(path)
     V, I_, F, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
     lib.dn_lstm_pack.argtypes = [V] * 8 + [I_] * 3 + [V] * 4 + [I_, V, V, V, V]
-    lib.dn_lstm_fwd.argtypes = [V, V, V, I_, I_, I_, I_, V, V, V, V, F, V, V, V, I_, V]
-    lib.dn_lstm_bwd.argtypes = [V, V, V, V, L, L, F, V, V, I_, I_, I_, I_, V, V]
+    lib.dn_lstm_fwd.argtypes = [V, V, V, I_, I_, I_, I_, V, V, V, V, F, V, V, V, I_, I_, V]
+    lib.dn_lstm_bwd.argtypes = [V, V, V, V, L, L, F, V, V, I_, I_, I_, I_, V, I_, I_, V]
     lib.dn_lstm_rows_per_wg.argtypes = [I_, I_]
     lib.dn_lstm_padded_hidden.argtypes = [I_]
     dev = "cuda"
@@ -65,12 +65,12 @@ def time_lib(path, B=32, S=98, I=256, H=384, reps=50):
         ev[0].record()
         rc = lib.dn_lstm_fwd(xp.data_ptr(), bias_p.data_ptr(), whh_p.data_ptr(), B, S, Hd, ndir,
                              c_save.data_ptr(), hprev.data_ptr(), None, hmean.data_ptr(), 1.0 / S,
-                             hT.data_ptr(), cT.data_ptr(), pre.data_ptr(), 0, st)
+                             hT.data_ptr(), cT.data_ptr(), pre.data_ptr(), 0, 0, st)
         ev[1].record()
         assert rc == 0, rc
         ev[2].record()
         rc = lib.dn_lstm_bwd(pre.data_ptr(), c_save.data_ptr(), whhT_p.data_ptr(), dout.data_ptr(),
-                             ndir * Hd, 0, 1.0 / S, None, None, B, S, Hd, ndir, dpre.data_ptr(), st)
+                             ndir * Hd, 0, 1.0 / S, None, None, B, S, Hd, ndir, dpre.data_ptr(), Bp, 0, st)
         ev[3].record()
         assert rc == 0, rc
         torch.cuda.synchronize()
