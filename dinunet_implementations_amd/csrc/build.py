@@ -96,8 +96,14 @@ def build_kernels(force: bool = False, jobs: int = 4, verbose: bool = True) -> s
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
-        _run([HIPCC, *HIP_FLAGS, *FILE_FLAGS.get(os.path.basename(src), []),
-              "-I", os.path.join(HERE, "kernels"), "-c", src, "-o", obj])
+        flags = [*HIP_FLAGS, *FILE_FLAGS.get(os.path.basename(src), [])]
+        # per-object stamp (source + every header + flags): an edit recompiles only its file
+        od = _digest([src], " ".join(flags) + ARCH)
+        if not force and _stamp_ok(obj, od):
+            return obj
+        _run([HIPCC, *flags, "-I", os.path.join(HERE, "kernels"), "-c", src, "-o", obj])
+        with open(obj + ".sha256", "w") as f:
+            f.write(od)
         if verbose:
             print(f"[build] {os.path.relpath(src, PKG)}", flush=True)
         return obj

@@ -60,6 +60,8 @@ _lib.register("dn_head_step_layout", [_lib.c_int, _P, _P, _lib.c_int, _P])
 _lib.register("dn_head_step_sync_bytes", [])
 _lib.register("dn_head_step", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int, _P, _P,
                                _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
+_lib.register("dn_head_rep", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int, _P, _P,
+                              _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
 
 # d(loss) tensor of the running training step, when the step will backpropagate exactly that
 # tensor (runtime.step.TrainStep's persistent 1): the forward then runs the head's output-gradient
@@ -70,6 +72,9 @@ _FUSED_HEAD = _os.environ.get("DINUNET_FUSED_HEAD", "1") == "1"
 # the whole training step of the head in ONE launch (csrc/kernels/head_step.hip) when the d loss
 # is known at forward time; DINUNET_HEAD_STEP=0 keeps the three-launch path
 _HEAD_STEP = _os.environ.get("DINUNET_HEAD_STEP", "1") == "1"
+# ... with the forward REPLICATED in every workgroup (csrc/kernels/head_rep.hip: no cross-workgroup
+# hand-off; head_step.hip where it does not apply); DINUNET_HEAD_REP=0 keeps head_step
+_HEAD_REP = _os.environ.get("DINUNET_HEAD_REP", "0") == "1"
 
 
 class loss_grad_hint:
@@ -274,6 +279,24 @@ class _HeadFn(torch.autograd.Function):
         ctx.hint_ptr = None
         ctx.step_dx = None
         ctx.one_launch = False
+        if train and hint is not None and _HEAD_STEP and _HEAD_REP and _cap.active() is None:
+            dx = (torch.empty(B, x.shape[1], dtype=torch.float32, device=x.device)
+                  if ctx.needs_input_grad[0] else None)
+            rc = _lib.lib().dn_head_rep(
+                spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True),
+                x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(), loss.data_ptr(),
+                pred.data_ptr(), rng.data_ptr(), spec.sync(x.device).data_ptr(), int(log_out),
+                hint.data_ptr(), _lib.ptr(dx), x.shape[1], _lib.stream())
+            if rc == 0:
+                ctx.one_launch = True
+                ctx.hint_ptr = hint.data_ptr()
+                ctx.step_dx = dx
+                ctx.spec, ctx.B, ctx.D0, ctx.train = spec, B, x.shape[1], train
+                ctx.ws = None
+                ctx.mark_non_differentiable(out, pred)
+                return out, loss, pred
+            if rc != 3:
+                raise RuntimeError(f"dn_head_rep failed with status {rc}")
         if train and hint is not None and _HEAD_STEP and _cap.active() is None:
             sw = spec.step_ws(B)
             if sw is not None:

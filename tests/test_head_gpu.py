@@ -301,17 +301,19 @@ def test_hinted_backward_with_other_dloss():
         torch.autograd.backward(loss, torch.full((), 2.5, device=DEV))
 
 
-def _step_vs_classic(mods, x, y, log_out, reps=1):
-    """Run the head with the one-launch step and the three-launch path from identical state;
-    return both results (outputs, dx, grads, buffers)."""
+def _step_vs_classic(mods, x, y, log_out, reps=1, rep=False):
+    """Run the head with the one-launch step (``rep``: the replicated-forward kernel
+    head_rep.hip, else head_step.hip) and the three-launch path from identical state; return both
+    results (outputs, dx, grads, buffers)."""
     from dinunet_implementations_amd.ops import head as H
     ref_mods = [copy.deepcopy(m) for m in mods]
     one = torch.ones((), device=DEV)
     res = []
     seed0 = None
     for flag, ms in ((True, mods), (False, ref_mods)):
-        old = H._HEAD_STEP
+        old, old_rep = H._HEAD_STEP, H._HEAD_REP
         H._HEAD_STEP = flag
+        H._HEAD_REP = rep
         try:
             spec = H.HeadSpec(ms)
             r = spec.rng(x.device)  # both paths draw the same dropout masks
@@ -330,7 +332,7 @@ def _step_vs_classic(mods, x, y, log_out, reps=1):
             res.append((out.clone(), loss.clone(), pred.clone(), xi.grad.clone(),
                         [p.grad.clone() for p in params], [b.clone() for b in bufs], spec))
         finally:
-            H._HEAD_STEP = old
+            H._HEAD_STEP, H._HEAD_REP = old, old_rep
     return res
 
 
@@ -365,11 +367,77 @@ def test_head_step_one_launch_fs_bitwise(B, dropout_in):
         assert torch.equal(u, v)
 
 
-def test_head_step_one_launch_graph_replay_and_epochs():
+@pytest.mark.parametrize("B,p", [(32, 0.0), (17, 0.0), (32, 0.25), (2, 0.0), (32, 0.5)])
+def test_head_rep_one_launch_ica_bitwise(B, p):
+    """The replicated-forward head (head_rep.hip: every workgroup runs the whole forward and
+    output-gradient chain, no hand-off) equals the three-launch path bitwise: outputs, loss,
+    argmax, d input, every parameter gradient; running statistics to an ulp."""
+    from dinunet_implementations_amd.ops import head as H
+    torch.manual_seed(11)
+    mods = list(_ica_head(p=p).to(DEV).train())
+    spec = H.HeadSpec(mods)
+    assert int(_lib_call_rep_supported(spec, B)) == 1
+    x = torch.randn(B, 384, device=DEV)
+    y = torch.randint(0, 2, (B,), device=DEV)
+    a, b = _step_vs_classic(mods, x, y, log_out=False, reps=3, rep=True)
+    for u, v in zip(a[:4], b[:4]):
+        assert torch.equal(u, v)
+    for u, v in zip(a[4], b[4]):
+        assert torch.equal(u, v)
+    for u, v in zip(a[5], b[5]):
+        assert torch.allclose(u.double(), v.double(), rtol=1e-6, atol=0)
+
+
+def _lib_call_rep_supported(spec, B):
+    from dinunet_implementations_amd.ops import _lib
+    return _lib.lib().dn_head_rep_supported(spec.nl, spec._dims, spec._flags, B)
+
+
+def test_head_rep_graph_replay_fresh_masks():
+    """The replicated head captured in a HIP graph: every replay draws a fresh dropout seed (the
+    last workgroup advances it once per launch, after all read it) and a replay equals the eager
+    launch from the same state."""
+    from dinunet_implementations_amd.ops import head as H
+    torch.manual_seed(14)
+    mods = list(_ica_head(p=0.25).to(DEV).train())
+    spec = H.HeadSpec(mods)
+    x = torch.randn(32, 384, device=DEV, requires_grad=True)
+    y = torch.randint(0, 2, (32,), device=DEV)
+    one = torch.ones((), device=DEV)
+
+    def run():
+        with H.loss_grad_hint(one):
+            _, loss, _ = H.head_loss(x, spec, y, log_out=False)
+        torch.autograd.backward(loss, one)
+        return loss
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            run()
+    torch.cuda.current_stream().wait_stream(s)
+    seed0 = int(spec.rng(x.device).item())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        sl = run()
+    losses = []
+    for i in range(50):
+        g.replay()
+        losses.append(float(sl))
+    torch.cuda.synchronize()
+    assert int(spec.rng(x.device).item()) == seed0 + 50
+    assert int(spec.sync(x.device)[192].item()) == 0  # the done counter resets every launch
+    assert len(set(losses)) > 10  # fresh masks: the loss moves with every draw
+    assert torch.isfinite(x.grad).all()
+
+
+def test_head_step_one_launch_graph_replay_and_epochs(monkeypatch):
     """Captured in a HIP graph and replayed 200 times (with eager launches in between): the
     monotonic-epoch hand-offs stay consistent (no timeout, epoch == launches) and the replayed
     result equals the eager one from the same state."""
     from dinunet_implementations_amd.ops import head as H
+    monkeypatch.setattr(H, "_HEAD_REP", False)
     torch.manual_seed(13)
     mods = list(_ica_head(p=0.25).to(DEV).train())
     spec = H.HeadSpec(mods)

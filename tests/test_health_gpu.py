@@ -25,7 +25,9 @@ def _step(engine="dSGD"):
     return m, st, x, y
 
 
-def test_head_step_timeout_raises(spin_zero):
+def test_head_step_timeout_raises(spin_zero, monkeypatch):
+    from dinunet_implementations_amd.ops import head as H
+    monkeypatch.setattr(H, "_HEAD_REP", False)  # head_step.hip: the head with hand-offs
     health = spin_zero
     m, st, x, y = _step()
     st(x, y)
@@ -54,7 +56,9 @@ def test_rankdad_barrier_timeout_raises(spin_zero):
     health.check([m], eng)
 
 
-def test_site_loop_fails_on_timed_out_handoff(tmp_path, spin_zero):
+def test_site_loop_fails_on_timed_out_handoff(tmp_path, spin_zero, monkeypatch):
+    from dinunet_implementations_amd.ops import head as H
+    monkeypatch.setattr(H, "_HEAD_REP", False)  # head_step.hip: the head with hand-offs
     from test_runtime_gpu import _ica_root, _run_site
     root = _ica_root(tmp_path)
     with pytest.raises(spin_zero.HandoffError):
