@@ -262,7 +262,10 @@ class ICALstm(nn.Module):
             return None
         from ..ops.lstm import PersistentPack
         flat = [t for cell in self.lstm.lstms for t in cell.params()]
-        return PersistentPack(flat, self.lstm.input_size, device, casts=(lin.weight, lin.bias))
+        # + bf16 images of the classifier weights for the replicated head (ops.head, head_rep.hip)
+        extra = [m.weight for m in self.classifier if isinstance(m, nn.Linear)]
+        return PersistentPack(flat, self.lstm.input_size, device, casts=(lin.weight, lin.bias),
+                              extra=extra)
 
     def body_loss(self, enc: torch.Tensor, y: torch.Tensor):
         """Second half of :meth:`forward_loss`: bi-LSTM, classifier, softmax-CE on ``enc``."""

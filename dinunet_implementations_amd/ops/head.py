@@ -60,8 +60,9 @@ _lib.register("dn_head_step_layout", [_lib.c_int, _P, _P, _lib.c_int, _P])
 _lib.register("dn_head_step_sync_bytes", [])
 _lib.register("dn_head_step", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int, _P, _P,
                                _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
-_lib.register("dn_head_rep", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int, _P, _P,
-                              _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
+_lib.register("dn_head_rep", [_lib.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int,
+                              _P, _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
+_lib.register("dn_head_rep_jobs", [_lib.c_int, _P, _P, _lib.c_int, _P, _lib.c_int])
 
 # d(loss) tensor of the running training step, when the step will backpropagate exactly that
 # tensor (runtime.step.TrainStep's persistent 1): the forward then runs the head's output-gradient
@@ -73,8 +74,26 @@ _FUSED_HEAD = _os.environ.get("DINUNET_FUSED_HEAD", "1") == "1"
 # is known at forward time; DINUNET_HEAD_STEP=0 keeps the three-launch path
 _HEAD_STEP = _os.environ.get("DINUNET_HEAD_STEP", "1") == "1"
 # ... with the forward REPLICATED in every workgroup (csrc/kernels/head_rep.hip: no cross-workgroup
-# hand-off; head_step.hip where it does not apply); DINUNET_HEAD_REP=0 keeps head_step
-_HEAD_REP = _os.environ.get("DINUNET_HEAD_REP", "0") == "1"
+# hand-off), reading the bf16 weight images the fused Adam keeps current (ops.lstm.PersistentPack,
+# device-fed steps); head_step.hip where it does not apply.  DINUNET_HEAD_REP=0 keeps head_step
+_HEAD_REP = _os.environ.get("DINUNET_HEAD_REP", "1") == "1"
+
+
+REP_LAUNCHES = 0  # head_rep.hip launches issued (tests: the replicated head really ran)
+
+
+def _bf16_images(spec: "HeadSpec"):
+    """The bf16 weight images of every head layer from the active persistent operand pack
+    (``ops.lstm.use_persistent``), or None when any is missing."""
+    from . import lstm as _lstm
+    pp = _lstm._PERSIST
+    if pp is None or not hasattr(pp, "bf16_of"):
+        return None
+    imgs = [pp.bf16_of(L.linear.weight) for L in spec.layers]
+    if any(t is None for t in imgs):
+        return None
+    pp.used = True
+    return (ctypes.c_void_p * len(imgs))(*[t.data_ptr() for t in imgs])
 
 
 class loss_grad_hint:
@@ -157,6 +176,7 @@ class HeadSpec:
         self._layout = {}
         self._step_layout = {}
         self._rng: Optional[Tensor] = None
+        self._rep_jobs = {}
         self._sync: Optional[Tensor] = None
 
     @staticmethod
@@ -211,6 +231,20 @@ class HeadSpec:
             rc = _lib.lib().dn_head_step_layout(self.nl, self._dims, self._flags, B, buf)
             self._step_layout[B] = int(buf[0]) if rc == 0 else None
         return self._step_layout[B]
+
+    def rep_jobs(self, B: int, device) -> Optional[Tensor]:
+        """head_rep.hip's dW job table of batch B on ``device`` (host-decoded once, so the kernel
+        does no integer division), or None outside that kernel's envelope."""
+        key = (B, str(device))
+        if key not in self._rep_jobs:
+            cap = 1 << 14
+            buf = (ctypes.c_int * cap)()
+            n = int(_lib.lib().dn_head_rep_jobs(self.nl, self._dims, self._flags, B, buf, cap))
+            if n < 0:
+                raise RuntimeError("dn_head_rep_jobs: job table larger than its buffer")
+            self._rep_jobs[key] = (torch.tensor(list(buf[:n]), dtype=torch.int32, device=device)
+                                   if n > 0 else None)
+        return self._rep_jobs[key]
 
     def sync(self, device) -> Tensor:
         """The one-launch kernel's persistent hand-off counters (zeroed once; the kernel keeps
@@ -279,15 +313,21 @@ class _HeadFn(torch.autograd.Function):
         ctx.hint_ptr = None
         ctx.step_dx = None
         ctx.one_launch = False
+        wbf = jt = None
         if train and hint is not None and _HEAD_STEP and _HEAD_REP and _cap.active() is None:
+            jt = spec.rep_jobs(B, x.device)
+            wbf = _bf16_images(spec) if jt is not None else None
+        if wbf is not None:
             dx = (torch.empty(B, x.shape[1], dtype=torch.float32, device=x.device)
                   if ctx.needs_input_grad[0] else None)
             rc = _lib.lib().dn_head_rep(
-                spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True),
-                x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(), loss.data_ptr(),
+                spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True), wbf,
+                jt.data_ptr(), x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(), loss.data_ptr(),
                 pred.data_ptr(), rng.data_ptr(), spec.sync(x.device).data_ptr(), int(log_out),
                 hint.data_ptr(), _lib.ptr(dx), x.shape[1], _lib.stream())
             if rc == 0:
+                global REP_LAUNCHES
+                REP_LAUNCHES += 1
                 ctx.one_launch = True
                 ctx.hint_ptr = hint.data_ptr()
                 ctx.step_dx = dx

@@ -389,7 +389,7 @@ class PersistentPack:
     buffers without a launch."""
 
     def __init__(self, params: Sequence[Tensor], input_size: int, device,
-                 casts: Sequence[Tensor] = ()):
+                 casts: Sequence[Tensor] = (), extra: Sequence[Tensor] = ()):
         self.params = list(params)
         if len(self.params) % 4 or any(p is None for p in self.params):
             raise ValueError("PersistentPack: every direction needs W_ih, b_ih, W_hh, b_hh")
@@ -405,7 +405,18 @@ class PersistentPack:
         self.whhT_p = torch.zeros(self.ndir, self.HD, GP, dtype=torch.bfloat16, **z)
         self.cast_src = list(casts)
         self.casts = [torch.zeros(c.shape, dtype=torch.bfloat16, **z) for c in casts]
+        # further bf16 copies kept current by the same Adam launch, looked up by parameter
+        # (bf16_of): the classifier weights the replicated head kernel reads (head_rep.hip)
+        self.extra_src = list(extra)
+        self.extra = [torch.zeros(c.shape, dtype=torch.bfloat16, **z) for c in extra]
         self.used = False
+
+    def bf16_of(self, t: Tensor) -> Optional[Tensor]:
+        """The bf16 image of parameter ``t`` this pack keeps current, or None."""
+        for src, dst in zip(self.cast_src + self.extra_src, self.casts + self.extra):
+            if src is t:
+                return dst
+        return None
 
     def matches(self, params, casts) -> bool:
         return (len(params) == len(self.params)
@@ -427,7 +438,7 @@ class PersistentPack:
             out.append((offs[id(b_ih)], b_ih.numel(), PK_BIAS, d, self.bias_p.data_ptr(), 0))
             out.append((offs[id(b_hh)], b_hh.numel(), PK_BIAS, d,
                         self.bias_p.data_ptr() + 4 * self.ndir * GP, 0))
-        for src, dst in zip(self.cast_src, self.casts):
+        for src, dst in zip(self.cast_src + self.extra_src, self.casts + self.extra):
             out.append((offs[id(src)], src.numel(), PK_CAST, 0, dst.data_ptr(), 0))
         return sorted(out)
 

@@ -301,6 +301,19 @@ def test_hinted_backward_with_other_dloss():
         torch.autograd.backward(loss, torch.full((), 2.5, device=DEV))
 
 
+class _Imgs:
+    """bf16 weight images of a head's Linear layers in the role of the fused Adam's persistent
+    operand pack (ops.lstm.PersistentPack.bf16_of), for the replicated head kernel."""
+
+    def __init__(self, mods):
+        self.m = {id(mm.weight): mm.weight.detach().to(torch.bfloat16).contiguous()
+                  for mm in mods if isinstance(mm, nn.Linear)}
+        self.used = False
+
+    def bf16_of(self, t):
+        return self.m.get(id(t))
+
+
 def _step_vs_classic(mods, x, y, log_out, reps=1, rep=False):
     """Run the head with the one-launch step (``rep``: the replicated-forward kernel
     head_rep.hip, else head_step.hip) and the three-launch path from identical state; return both
@@ -321,9 +334,11 @@ def _step_vs_classic(mods, x, y, log_out, reps=1, rep=False):
                 seed0 = r.clone()
             else:
                 r.copy_(seed0)
+            from dinunet_implementations_amd.ops.lstm import use_persistent
+            imgs = _Imgs(ms) if (rep and flag) else None
             for _ in range(reps):
                 xi = x.clone().requires_grad_()
-                with H.loss_grad_hint(one):
+                with H.loss_grad_hint(one), use_persistent(imgs):
                     out, loss, pred = H.head_loss(xi, spec, y, log_out=log_out)
                 torch.autograd.backward(loss, one)
             torch.cuda.synchronize()
@@ -379,7 +394,9 @@ def test_head_rep_one_launch_ica_bitwise(B, p):
     assert int(_lib_call_rep_supported(spec, B)) == 1
     x = torch.randn(B, 384, device=DEV)
     y = torch.randint(0, 2, (B,), device=DEV)
+    n0 = H.REP_LAUNCHES
     a, b = _step_vs_classic(mods, x, y, log_out=False, reps=3, rep=True)
+    assert H.REP_LAUNCHES == n0 + 3, "the replicated head did not run"
     for u, v in zip(a[:4], b[:4]):
         assert torch.equal(u, v)
     for u, v in zip(a[4], b[4]):
@@ -405,18 +422,23 @@ def test_head_rep_graph_replay_fresh_masks():
     y = torch.randint(0, 2, (32,), device=DEV)
     one = torch.ones((), device=DEV)
 
+    from dinunet_implementations_amd.ops.lstm import use_persistent
+    imgs = _Imgs(mods)
+
     def run():
-        with H.loss_grad_hint(one):
+        with H.loss_grad_hint(one), use_persistent(imgs):
             _, loss, _ = H.head_loss(x, spec, y, log_out=False)
         torch.autograd.backward(loss, one)
         return loss
 
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
+    n0 = H.REP_LAUNCHES
     with torch.cuda.stream(s):
         for _ in range(3):
             run()
     torch.cuda.current_stream().wait_stream(s)
+    assert H.REP_LAUNCHES == n0 + 3
     seed0 = int(spec.rng(x.device).item())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):

@@ -29,8 +29,20 @@ def main():
     y = torch.randint(0, 2, (B,), device=dev)
     one = torch.ones((), device=dev)
 
+    from dinunet_implementations_amd.ops.lstm import use_persistent
+
+    class Imgs:  # the fused Adam's bf16 weight images (ops.lstm.PersistentPack.bf16_of)
+        used = False
+        m = {id(mm.weight): mm.weight.detach().to(torch.bfloat16).contiguous()
+             for mm in mods if isinstance(mm, nn.Linear)}
+
+        def bf16_of(self, t):
+            return self.m.get(id(t))
+
+    imgs = Imgs()
+
     def run():
-        with H.loss_grad_hint(one):
+        with H.loss_grad_hint(one), use_persistent(imgs):
             _, loss, _ = H.head_loss(x, spec, y, log_out=False)
         torch.autograd.backward(loss, one)
 
