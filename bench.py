@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--tta-subjects", type=int, default=2560,
                     help="site-loop cohort size (split 0.8/0.1/0.1)")
     ap.add_argument("--tta-epochs", type=int, default=30)
+    ap.add_argument("--collective", default="auto",
+                    choices=["auto", "allreduce", "direct", "calibrate"],
+                    help="dSGD site-mean form (dsgd_collective); calibrate = time both, keep the "
+                         "faster")
     ap.add_argument("--loopback-rccl", action="store_true",
                     help="one GPU, but through a one-rank RCCL group marked distributed: the "
                          "N > 1 step (split backward, bucketed all-reduce, captured collectives) "
@@ -156,7 +160,7 @@ def main():
     flat = FlatParams(model.parameters())
     grp.broadcast(flat.data, 0)
     opt = FusedAdam(flat, lr=1e-3)
-    cfg = {"precision_bits": args.precision_bits, "seed": 0}
+    cfg = {"precision_bits": args.precision_bits, "seed": 0, "dsgd_collective": args.collective}
     engine = make_engine(args.engine, model, flat, grp, cfg)
     step = TrainStep(model, flat, opt, engine, task="ica", use_graph=bool(args.graph))
 
@@ -250,6 +254,9 @@ def main():
             "final_loss": round(loss, 5),
             # N > 1 code path: collectives captured inside the K-step graphs (runtime.step)
             "comm_graph": bool(getattr(step, "comm_graph", False)),
+            "collective": ((getattr(engine, "calibration", None)
+                            or ("direct" if engine.direct else "allreduce"))
+                           if args.engine == "dSGD" else None),
             "split_backward": bool(getattr(step, "split", False)),
             **({"dad_iters_per_step": iters} if iters is not None else {}),
             # HBM high-water mark of the run (allocator view: model, optimizer state, activations,

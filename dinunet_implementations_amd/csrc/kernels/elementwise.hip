@@ -164,3 +164,19 @@ DN_API int dn_set_spin_limit(int polls) {
   g_dn_spin_limit = polls < 0 ? -1 : polls;
   return DN_OK;
 }
+
+// CU-occupancy probe for tests of the persistent kernels beside collectives: `blocks` workgroups
+// of `threads` that each spin (s_sleep between polls) until `us` microseconds have passed on the
+// 100 MHz real-time counter -- the footprint of RCCL's channel kernels while a collective is in
+// flight (one workgroup per channel, resident for the whole transfer).  Bounded to 100 ms.
+__global__ void busy_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+DN_API int dn_busy(int blocks, int threads, int us, hipStream_t st) {
+  if (blocks < 1 || blocks > 4096 || threads < 64 || threads > 1024 || us < 0 || us > 100000)
+    return DN_BAD_SHAPE;
+  hipLaunchKernelGGL(busy_kernel, dim3(blocks), dim3(threads), 0, st, (unsigned long long)us * 100);
+  return dn_launch_status();
+}

@@ -158,10 +158,15 @@ class DSGDEngine(Engine):
         self._half_bufs: Dict[int, Tensor] = {}
         # ``dsgd_collective``: "direct" = all_to_all + fp32 sum + all_gather (collective.py) on a
         # comm stream of its own; "allreduce" = one RCCL all-reduce per bucket (a 16-bit payload
-        # is then SUMMED in 16 bits inside RCCL); "auto" = direct for 16-bit payloads
+        # is then SUMMED in 16 bits inside RCCL); "auto" = direct for 16-bit payloads;
+        # "calibrate" = whichever of the two measures faster on this job's buckets and links
         coll = str(self.cfg.get("dsgd_collective", "auto"))
-        if coll not in ("auto", "direct", "allreduce"):
-            raise ValueError(f"dsgd_collective {coll!r}: expected auto, direct or allreduce")
+        if coll not in ("auto", "direct", "allreduce", "calibrate"):
+            raise ValueError(f"dsgd_collective {coll!r}: expected auto, direct, allreduce or "
+                             "calibrate")
+        self.calibration: Optional[dict] = None
+        if coll == "calibrate":
+            coll = self._calibrate()
         self.direct = coll == "direct" or (coll == "auto" and self.half)
         if self.half and not self.direct and self.wire == "fp16":
             # RCCL sums an all-reduce buffer in its own type: unscaled fp16 would flush
@@ -192,6 +197,75 @@ class DSGDEngine(Engine):
     @property
     def capturable(self) -> bool:
         return not self.direct  # all-reduce buckets (fp32, or the 16-bit all-reduce) capture
+
+    def _calibrate(self) -> str:
+        """``dsgd_collective="calibrate"``: time both site-mean forms on THIS job's buckets and
+        links and keep the faster -- the choice the link model of ``profiles/r4_comm_model.md``
+        could only predict (it depends on per-hop latency and link rates nobody had measured).
+
+        Both forms are timed host-issued over every bucket: the RCCL all-reduce and the direct
+        exchange (all-to-all + fp32 sum + all-gather, ``collective.DirectMean``).  The step then
+        captures the all-reduce in its HIP graph (``TrainStep.comm_graph``), which only removes
+        host time from it, so a tie or a near-tie still favours the all-reduce.  (A capture here,
+        at process-group start, aborted RCCL's watchdog on an event recorded in the capturing
+        stream, ``hipErrorCapturedEvent``.)  The per-form times are max-reduced over the sites, so every site takes the same decision
+        from the same numbers; the record lands in ``self.calibration`` (``logs.json``
+        ``dsgd_collective``).  ``dsgd_calibrate_reps`` (default 10) timed repetitions."""
+        import time as _time
+        g = self.group
+        sizes = [e - s for s, e in self.buckets]
+        if not g.distributed:
+            self.calibration = {"choice": "allreduce", "reason": "one site: no collective"}
+            return "allreduce"
+        if self.half and self.wire == "fp16":
+            self.calibration = {"choice": "direct",
+                                "reason": "fp16 wire: only the direct exchange sums in fp32"}
+            return "direct"
+        dev = self.flat.grad.device
+        cuda = dev.type == "cuda"
+        reps = max(1, int(self.cfg.get("dsgd_calibrate_reps", 10)))
+        sync = torch.cuda.synchronize if cuda else (lambda: None)
+        wdt = PAYLOAD_TYPES[self.wire][1] if self.half else torch.float32
+        ar_bufs = [torch.zeros(n, dtype=wdt, device=dev) for n in sizes]
+        dm_bufs = [torch.zeros(n, dtype=torch.float32, device=dev) for n in sizes]
+        means = [self._direct((s, e), e - s, dev) for s, e in self.buckets]
+
+        def allreduce():
+            for b in ar_bufs:
+                g.all_reduce(b)
+
+        def direct():
+            for dm, b in zip(means, dm_bufs):
+                dm.run_(b)
+
+        def timed(fn):
+            for _ in range(2):
+                fn()
+            sync()
+            g.barrier()
+            t0 = _time.perf_counter()
+            for _ in range(reps):
+                fn()
+            sync()
+            return (_time.perf_counter() - t0) / reps * 1e6
+
+        t = torch.tensor([timed(allreduce), timed(direct)], dtype=torch.float64,
+                         device=dev if g.backend == "nccl" else "cpu")
+        g.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_ar, t_dm = (float(v) for v in t.cpu())
+        if g.backend == "nccl":
+            # let RCCL's watchdog retire the calibration's finished collectives before anything
+            # captures: it polls their (pooled) events every ~100 ms, and a pooled event reused
+            # by a captured collective while the watchdog still holds the old work aborts the
+            # process (hipErrorCapturedEvent, seen on the bench's first capture after this)
+            sync()
+            _time.sleep(0.5)
+        choice = "direct" if t_dm < t_ar else "allreduce"
+        self.calibration = {"choice": choice, "allreduce_us": round(t_ar, 2),
+                            "direct_us": round(t_dm, 2), "form": "host-issued",
+                            "bucket_elems": sizes, "sites": g.world, "reps": reps,
+                            "wire": self.wire}
+        return choice
 
     def _marker(self, pid: int):
         def hook(g):

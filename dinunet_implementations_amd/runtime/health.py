@@ -26,6 +26,7 @@ import torch
 from ..ops import _lib
 
 _lib.register("dn_set_spin_limit", [_lib.c_int])
+_lib.register("dn_busy", [_lib.c_int, _lib.c_int, _lib.c_int, _lib.c_void_p])
 
 # head_step.hip sync block: u32 word index of the error word (Y_ERR), codes 1 dZ1 / 2 dZ0 / 3 A1
 HEAD_ERR_WORD = 160
@@ -42,6 +43,14 @@ def set_spin_limit(polls: int):
     """Poll limit of every in-kernel wait (< 0: the kernels' defaults; 0: give up at once, the
     negative control of :func:`check`)."""
     _lib.call("dn_set_spin_limit", int(polls))
+
+
+def occupy_cus(blocks: int = 64, us: int = 2000, threads: int = 256):
+    """Hold ``blocks`` CUs (one spinning workgroup each, ``us`` microseconds, at most 100 ms) on
+    the CURRENT stream: the footprint of RCCL's channel kernels during a collective.  Tests launch
+    it on a side stream beside the persistent kernels, which reserve ``DN_RESERVE_CUS`` (64) CUs
+    for exactly these (csrc/kernels/common.h)."""
+    _lib.call("dn_busy", int(blocks), int(threads), int(us), _lib.stream())
 
 
 def _heads(modules: Iterable[torch.nn.Module]):

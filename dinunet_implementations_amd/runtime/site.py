@@ -491,6 +491,10 @@ class FederatedSite:
                 self._pretrain(trainer, data, fdir, seed, logs)
             engine = make_engine(str(cfg.get("agg_engine", "dSGD")), trainer.modules(), trainer.flat,
                                  self.group, cfg)
+            cal = getattr(engine, "calibration", None)
+            if cal:  # dsgd_collective="calibrate": what was measured and chosen
+                logs["dsgd_collective"] = cal
+                self.log(f"dsgd_collective calibrated: {cal}")
             if resume is not None:
                 if resume.get("engine"):
                     engine.load_state_dict(resume["engine"])

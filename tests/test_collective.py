@@ -141,3 +141,32 @@ def test_fp16_wire_never_summed_by_a_16bit_allreduce():
     assert wire == "bf16" and not direct and any("bf16" in m for m in warns)
     wire, direct, warns = run_world(w_engine_wire, 2, {"precision_bits": "16"})[0]
     assert wire == "fp16" and direct and not warns
+
+
+def w_calibrate(grp, cfg):
+    import torch.nn as nn
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import make_engine
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(64, 64), nn.Linear(64, 8))
+    flat = FlatParams(m.parameters())
+    e = make_engine("dSGD", m, flat, grp, cfg)
+    # the chosen form still computes the site mean
+    flat.grad.fill_(float(grp.rank + 1))
+    e.reduce()
+    return e.calibration, e.direct, flat.grad.clone() * e.last_scale
+
+
+def test_dsgd_collective_calibrate_agrees_across_sites():
+    """dsgd_collective='calibrate': both forms timed on the job's buckets, timings max-reduced
+    so every site takes the same choice; the record says which and why; the mean is right."""
+    outs = run_world(w_calibrate, 2, {"dsgd_collective": "calibrate", "dsgd_calibrate_reps": 3})
+    (c0, d0, g0), (c1, d1, g1) = outs
+    assert c0 == c1 and d0 == d1
+    assert c0["choice"] in ("allreduce", "direct") and d0 == (c0["choice"] == "direct")
+    assert c0["allreduce_us"] > 0 and c0["direct_us"] > 0 and c0["form"] == "host-issued"
+    assert c0["choice"] == ("direct" if c0["direct_us"] < c0["allreduce_us"] else "allreduce")
+    assert torch.allclose(g0, torch.full_like(g0, 1.5)) and torch.equal(g0, g1)
+    # the fp16 wire has one admissible form; one site has no collective
+    c16 = run_world(w_calibrate, 2, {"dsgd_collective": "calibrate", "precision_bits": "16"})[0][0]
+    assert c16["choice"] == "direct" and "fp16" in c16["reason"]
