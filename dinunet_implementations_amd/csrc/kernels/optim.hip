@@ -133,12 +133,14 @@ struct StepRecord {
   float* rl;  // [n] losses
   long n;
   const long long* cursor;
+  const long long* pred;  // col < 0: the score is the predicted class (FS: hard labels)
 };
 
 __device__ __forceinline__ void record_step(const StepRecord& r, int cofs) {
   long c = (*r.cursor + cofs) % r.n;
   if (c < 0) c += r.n;
-  for (int b = threadIdx.x; b < r.B; b += blockDim.x) r.rs[c * r.B + b] = r.out[b * r.ld + r.col];
+  for (int b = threadIdx.x; b < r.B; b += blockDim.x)
+    r.rs[c * r.B + b] = r.col < 0 ? (float)r.pred[b] : r.out[b * r.ld + r.col];
   if (threadIdx.x == 0) r.rl[c] = *r.loss;
 }
 
@@ -279,7 +281,7 @@ DN_API int dn_adam_pack(float* p, float* g, float* m, float* v, long n, float lr
   if (record && update) {
     rec = *reinterpret_cast<const StepRecord*>(record);
     if (!rec.out || !rec.loss || !rec.rs || !rec.rl || !rec.cursor || rec.n <= 0 || rec.B <= 0 ||
-        rec.col < 0 || rec.ld <= rec.col)
+        (rec.col < 0 ? !rec.pred : rec.ld <= rec.col))
       return DN_BAD_SHAPE;
   }
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return DN_BAD_SHAPE;
@@ -321,8 +323,8 @@ DN_API long dn_step_record_size() { return (long)sizeof(StepRecord); }
 DN_API int dn_step_record(const void* record, int cofs, hipStream_t st) {
   if (!record) return DN_BAD_SHAPE;
   const StepRecord r = *reinterpret_cast<const StepRecord*>(record);
-  if (!r.out || !r.loss || !r.rs || !r.rl || !r.cursor || r.n <= 0 || r.B <= 0 || r.col < 0 ||
-      r.ld <= r.col)
+  if (!r.out || !r.loss || !r.rs || !r.rl || !r.cursor || r.n <= 0 || r.B <= 0 ||
+      (r.col < 0 ? !r.pred : r.ld <= r.col))
     return DN_BAD_SHAPE;
   hipLaunchKernelGGL(record_kernel, dim3(1), dim3(256), 0, st, r, cofs);
   return dn_launch_status();

@@ -6,7 +6,8 @@
 // Two batch sources:
 //   host-fed  (gx == null): x fp32 [ux * 8] -> xb, y [ny] -> yd (the caller's batch tensors);
 //   device-fed (gx != null): the batch is gathered from a dataset RESIDENT in HBM, gx [N][f8 * 8]
-//       (bf16, or fp32 when gx_bf16 == 0), labels gy [N]; sample b of this step is row
+//       (bf16, or fp32 when gx_bf16 == 0; gx_bf16 == 2: fp32 copied to an fp32 static input
+//       unrounded -- the FS features), labels gy [N]; sample b of this step is row
 //       order[c * B + b] (or c * B + b without an order) where c = *cursor mod nb.  Nothing in
 //       the step reads the host, so K steps can be captured in one HIP graph.  The cursor is
 //       advanced by the step's Adam launch (optim.hip), never here: every workgroup of this
@@ -43,6 +44,13 @@ __device__ __forceinline__ void prologue_item(const StepPrologue& sp, long i, lo
     if (sp.gx) {
       const int ii = (int)i, b = ii / sp.f8, e = ii - b * sp.f8;  // ux < 2^31 (host-checked)
       const long r = prologue_row(sp, c, b);
+      if (sp.gx_bf16 == 2) {
+        const f32x4* s = reinterpret_cast<const f32x4*>(sp.gx) + 2 * (r * sp.f8 + e);
+        f32x4* d = reinterpret_cast<f32x4*>(sp.xb) + 2 * i;
+        d[0] = s[0];
+        d[1] = s[1];
+        return;
+      }
       if (sp.gx_bf16) {
         o = reinterpret_cast<const bf16x8*>(sp.gx)[r * sp.f8 + e];
       } else {

@@ -299,7 +299,9 @@ class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y, spec: HeadSpec, log_out: bool, hint, *params):
         ctx.set_materialize_grads(False)  # no zero-filled grads for out / pred
-        x = x.float().contiguous()
+        x = x.float()
+        if x.stride(1) != 1:  # rows may be strided (a device-fed padded feature buffer)
+            x = x.contiguous()
         y = y.long().contiguous()
         B = x.shape[0]
         C = spec.dims[-1]

@@ -199,7 +199,7 @@ class FusedAdam:
             self.sync_device_step()
         b1, b2 = self.betas
         if src is not None:
-            gx = [src.X.data_ptr(), int(src.X.dtype == torch.bfloat16), src.row,
+            gx = [src.X.data_ptr(), src._mode(xb), src.row,
                   src.Y.data_ptr(), _lib.ptr(src.order), src.nb, src.cursor.data_ptr(), src.B,
                   xb.data_ptr(), yd.data_ptr()]
         else:
@@ -274,6 +274,15 @@ class DeviceSource:
                  order: Optional[torch.Tensor] = None):
         if not X.is_cuda or X.dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("DeviceSource: X must be a bf16 / fp32 GPU tensor")
+        self.width = None  # the real feature count of a padded fp32 feature matrix
+        if X.dtype == torch.float32 and X.dim() == 2 and X.shape[1] % 8:
+            # fp32 feature rows (FS: 66 features) padded with zero columns to whole 16-B chunks
+            # once; the step's static input keeps the padded width and the model reads the
+            # first `width` columns (``view``)
+            self.width = int(X.shape[1])
+            Xp = torch.zeros(X.shape[0], -(-X.shape[1] // 8) * 8, dtype=X.dtype, device=X.device)
+            Xp[:, :self.width] = X
+            X = Xp
         self.X = X.contiguous()
         self.Y = Y.to(device=X.device, dtype=torch.int64).contiguous()
         self.B = int(batch)
@@ -312,10 +321,24 @@ class DeviceSource:
                 else torch.arange(j, j + self.B, device=self.X.device))
         return self.X[rows], self.Y[rows]
 
+    def view(self, xb: torch.Tensor) -> torch.Tensor:
+        """What the model reads of a static input ``xb`` this source gathers into (the real
+        columns of padded feature rows)."""
+        return xb if self.width is None else xb[:, :self.width]
+
+    def _mode(self, xb: torch.Tensor) -> int:
+        # dn_step_gather's source / destination mode (prologue.h): 1 bf16 -> bf16, 0 fp32 ->
+        # bf16 (rounded), 2 fp32 -> fp32 (exact)
+        if self.X.dtype == torch.bfloat16:
+            if xb.dtype != torch.bfloat16:
+                raise ValueError("DeviceSource: a bf16 dataset gathers into a bf16 static input")
+            return 1
+        return 2 if xb.dtype == torch.float32 else 0
+
     def gather(self, xb: torch.Tensor, yd: torch.Tensor, grad: torch.Tensor,
                bump: Optional[torch.Tensor] = None):
         """The standalone device-fed prologue launch (``dn_step_gather``)."""
-        _lib.call("dn_step_gather", self.X.data_ptr(), int(self.X.dtype == torch.bfloat16),
+        _lib.call("dn_step_gather", self.X.data_ptr(), self._mode(xb),
                   self.row, self.Y.data_ptr(), _lib.ptr(self.order), self.nb,
                   self.cursor.data_ptr(), self.B, xb.data_ptr(), yd.data_ptr(), grad.data_ptr(),
                   grad.numel(), _lib.ptr(bump), _lib.stream())
@@ -329,7 +352,7 @@ class DeviceSource:
 
     def prologue_args(self, xb, yd, grad, bump=None):
         """Argument tail of ``dn_lstm_pack_gather`` (the prologue riding in the weight pack)."""
-        return [self.X.data_ptr(), int(self.X.dtype == torch.bfloat16), self.row,
+        return [self.X.data_ptr(), self._mode(xb), self.row,
                 self.Y.data_ptr(), _lib.ptr(self.order), self.nb, self.cursor.data_ptr(),
                 self.B, xb.data_ptr(), yd.data_ptr(), grad.data_ptr(), grad.numel(),
                 _lib.ptr(bump)]
@@ -347,7 +370,8 @@ def _step_record_type():
         class _Rec(ctypes.Structure):
             _fields_ = [("out", ctypes.c_void_p), ("ld", ctypes.c_long), ("col", ctypes.c_int),
                         ("B", ctypes.c_int), ("loss", ctypes.c_void_p), ("rs", ctypes.c_void_p),
-                        ("rl", ctypes.c_void_p), ("n", ctypes.c_long), ("cursor", ctypes.c_void_p)]
+                        ("rl", ctypes.c_void_p), ("n", ctypes.c_long), ("cursor", ctypes.c_void_p),
+                        ("pred", ctypes.c_void_p)]
         L = _lib.lib()
         L.dn_step_record_size.restype = ctypes.c_long
         if ctypes.sizeof(_Rec) != L.dn_step_record_size():
@@ -359,7 +383,8 @@ def _step_record_type():
 class StepRecorder:
     """Per-step train records of device-fed steps (``runtime.feed.DeviceFeed``): ring slot
     ``c mod n`` of batch cursor ``c`` holds the step's score column ``out[:, col]`` (``[B]``; ICA:
-    ``prob[:, 1]``, the reference's train-AUC input, ``comps/icalstm/__init__.py:64-65``) and its
+    ``prob[:, 1]``, the reference's train-AUC input, ``comps/icalstm/__init__.py:64-65``; ``col``
+    < 0: the predicted class, FS's hard-label scores, ``comps/fs/__init__.py:57-59``) and its
     loss (``:67-68``).  The write rides in the packing Adam launch (one more workgroup,
     ``optim.hip adam_pack_kernel``) or is a one-workgroup launch of its own (``dn_step_record``)
     after an update that already advanced the cursor; either way K-step graph replays keep exact
@@ -373,11 +398,16 @@ class StepRecorder:
         self.cursor = cursor
         self._cache: Dict[tuple, object] = {}
 
-    def args(self, out: torch.Tensor, loss: torch.Tensor):
-        """The ``StepRecord`` struct for a step whose outputs are ``out`` [B, C] / ``loss`` [].
-        Cached per output pair: a multi-site step issued from the host every step asks for the
-        same static buffers' struct each time (no per-step class or library query)."""
-        key = (out.data_ptr(), loss.data_ptr(), tuple(out.shape))
+    def args(self, out: torch.Tensor, loss: torch.Tensor, pred: Optional[torch.Tensor] = None):
+        """The ``StepRecord`` struct for a step whose outputs are ``out`` [B, C] / ``loss`` []
+        (/ ``pred`` [B] int64, needed when ``col`` < 0).  Cached per output set: a multi-site
+        step issued from the host every step asks for the same static buffers' struct each time
+        (no per-step class or library query)."""
+        if self.col < 0 and (pred is None or pred.dtype != torch.int64 or pred.numel() != self.B
+                             or not pred.is_contiguous()):
+            raise ValueError("StepRecorder(col < 0) records the predicted class: pass pred [B] int64")
+        pp = pred.data_ptr() if (self.col < 0 and pred is not None) else None
+        key = (out.data_ptr(), loss.data_ptr(), tuple(out.shape), pp)
         rec = self._cache.get(key)
         if rec is not None:
             return rec
@@ -386,20 +416,21 @@ class StepRecorder:
             raise ValueError("StepRecorder: out must be contiguous fp32 [B, C], loss fp32 scalar")
         rec = _step_record_type()(out.data_ptr(), out.shape[1], self.col, self.B, loss.data_ptr(),
                                   self.scores.data_ptr(), self.losses.data_ptr(), self.n,
-                                  self.cursor.data_ptr())
+                                  self.cursor.data_ptr(), pp)
         if len(self._cache) > 64:
             self._cache.clear()
         self._cache[key] = rec
         return rec
 
-    def record(self, out: torch.Tensor, loss: torch.Tensor, cofs: int = -1):
+    def record(self, out: torch.Tensor, loss: torch.Tensor, cofs: int = -1,
+               pred: Optional[torch.Tensor] = None):
         """Standalone record into slot ``(cursor + cofs) mod n``."""
         if out.is_cuda:
-            rec = self.args(out, loss)  # (held: the launcher reads it through its address)
+            rec = self.args(out, loss, pred)  # (held: the launcher reads it through its address)
             _lib.call("dn_step_record", ctypes_addr(rec), int(cofs), _lib.stream())
             return
         c = (int(self.cursor.item()) + cofs) % self.n
-        self.scores[c].copy_(out[:, self.col].float())
+        self.scores[c].copy_((pred if self.col < 0 else out[:, self.col]).float())
         self.losses[c] = loss.detach().float()
 
     def reset(self):

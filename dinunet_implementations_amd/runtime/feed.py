@@ -41,8 +41,11 @@ class DeviceFeed:
 
     ``step``: a :class:`runtime.step.TrainStep` (bound here); ``X`` ``[N, *sample]`` (any float
     dtype, converted once to bf16 in HBM), ``Y`` ``[N]`` labels; ``batch`` samples per step;
-    ``nb`` steps per pass (an epoch's step count; the order buffer holds ``nb * batch`` rows);
-    ``col``: the score column of the step's output the train metric ranks (ICA: 1)."""
+    ``nb`` steps per pass (an epoch's step count); with gradient accumulation
+    (``step.accum`` = ``local_iterations`` > 1) a step takes ``accum`` batches, so the order
+    buffer holds ``nb * accum * batch`` rows and the records are per batch (micro-batch);
+    ``col``: the score column of the step's output the train metric ranks (ICA: 1; -1: the
+    predicted class, FS's hard-label scores)."""
 
     def __init__(self, step, X: torch.Tensor, Y: torch.Tensor, batch: int, nb: int,
                  col: int = 1, steps_per_graph: Optional[int] = None):
@@ -53,25 +56,32 @@ class DeviceFeed:
         self.nb = int(nb)
         if self.nb < 1 or X.shape[0] < 1:
             raise ValueError("DeviceFeed: no steps")
-        Xb = X if X.dtype == torch.bfloat16 else X.to(torch.bfloat16)
-        rows = torch.arange(self.nb * self.B, device=X.device) % X.shape[0]
+        self.A = max(1, int(getattr(step, "accum", 1)))
+        self.nbb = self.nb * self.A  # batches per pass
+        # bf16 in HBM for models that take a bf16 batch (ICA: the encoder GEMM rounds its operand
+        # anyway); fp32 otherwise (FS features, gathered exactly into an fp32 static input)
+        if getattr(step.model, "accepts_bf16_input", False):
+            Xb = X if X.dtype == torch.bfloat16 else X.to(torch.bfloat16)
+        else:
+            Xb = X.float()
+        rows = torch.arange(self.nbb * self.B, device=X.device) % X.shape[0]
         self.src = DeviceSource(Xb, Y, self.B, order=rows)
-        self.rec = StepRecorder(self.nb, self.B, self.src.cursor, col=col)
+        self.rec = StepRecorder(self.nbb, self.B, self.src.cursor, col=col)
         K = steps_per_graph or default_graph_steps(self.nb)
         step.bind(self.src, steps_per_graph=K, recorder=self.rec)
 
     # ---- epochs of the site loop --------------------------------------------------------------
     def run_epoch(self, order: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """Train ``nb`` steps on the batches ``order`` (``[nb * batch]`` row indices, the
-        epoch's batch sequence); returns the device tensors ``(losses [nb], scores [nb*B],
-        labels [nb*B])`` of the epoch's train records."""
-        if order.numel() != self.nb * self.B:
+        """Train ``nb`` steps on the batches ``order`` (``[nb * accum * batch]`` row indices, the
+        epoch's batch sequence); returns the device tensors ``(losses [nb * accum], scores
+        [nb * accum * B], labels [nb * accum * B])`` of the epoch's per-batch train records."""
+        if order.numel() != self.nbb * self.B:
             raise ValueError(f"DeviceFeed.run_epoch: order of {order.numel()} rows, want "
-                             f"{self.nb * self.B}")
+                             f"{self.nbb * self.B}")
         self.src.set_order(order)
         self.src.cursor.zero_()
         self.step.run(self.nb)
-        return self.rec.losses, self.rec.scores.view(-1), self.src.labels_of(self.nb)
+        return self.rec.losses, self.rec.scores.view(-1), self.src.labels_of(self.nbb)
 
     # ---- free-running steps (bench.py) --------------------------------------------------------
     def run(self, n: int):

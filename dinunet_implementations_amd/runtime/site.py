@@ -251,16 +251,16 @@ class FederatedSite:
                 # ONE host call per epoch: the epoch's batch order (the loader's own passes),
                 # then K-step graph replays with the train records kept on the device
                 order = []
-                for _ in range(steps):
+                for _ in range(steps * li):  # li batches per step (local_iterations)
                     try:
                         order.append(next(it))
                     except StopIteration:
                         it = tr.iter_indices()
                         order.append(next(it))
                 losses, scores, labels = feed.run_epoch(torch.cat(order))
-                avg.add(losses.mean(), steps * bs)
+                avg.add(losses.mean(), steps * li * bs)
                 met.add(scores.clone(), labels)
-                nsamp += steps * bs
+                nsamp += steps * li * bs
             for _ in range(steps if feed is None else 0):
                 if fault_at is not None:  # failure-path tests (DINUNET_FAULT=<rank>:<step>)
                     fault_at -= 1
@@ -361,24 +361,28 @@ class FederatedSite:
                      steps: int, cfg: Dict[str, Any], fault_at) -> Optional[DeviceFeed]:
         """The device-fed epoch (``runtime.feed``) when this site's step can take it: a captured
         step on the GPU, a model that takes a bf16 batch, a plugin with a score column, full
-        batches, no accumulation, an engine that runs inside the captured step.  ``device_feed``
+        batches, an engine that runs inside the captured step (``local_iterations`` > 1: whole
+        accumulated steps per replay, ``TrainStep._dev_body_accum``).  ``device_feed``
         (default on) turns it off; the fault-injection hook keeps the per-step host loop."""
         col = getattr(trainer, "score_column", None)
-        if (step is None or not step.use_graph or self.device.type != "cuda" or li != 1
+        if (step is None or not step.use_graph or self.device.type != "cuda" or step.accum != li
                 or not cfg.get("device_feed", True) or fault_at is not None or col is None
                 or not tr.full_batches or steps < 1
-                or not getattr(step.model, "accepts_bf16_input", False)
                 or not isinstance(trainer.optimizer, FusedAdam)
                 or not (engine.name.startswith("dSGD") or getattr(engine, "fast", False))):
             return None
         X = tr.inputs
-        if X.dtype != torch.bfloat16:
-            # the feed keeps a bf16 copy of the split in HBM next to the loader's: fall back to
-            # the host-fed loop (same trajectory) when it would not fit (ADVICE r4)
-            need = X.numel() * 2 + tr.labels.numel() * 8
+        bf = bool(getattr(step.model, "accepts_bf16_input", False))
+        row = X[0].numel() if X.shape[0] else 0
+        copies = (X.dtype != torch.bfloat16) if bf else (X.dtype != torch.float32 or row % 8 != 0)
+        if copies:
+            # the feed keeps its own copy of the split in HBM next to the loader's (bf16, or
+            # fp32 rows padded to 8 features): fall back to the host-fed loop (same trajectory)
+            # when it would not fit (ADVICE r4)
+            need = X.shape[0] * (2 * row if bf else 4 * (-(-row // 8) * 8)) + tr.labels.numel() * 8
             free, _ = torch.cuda.mem_get_info(self.device)
             if need > 0.9 * free:
-                self.log(f"device feed off: its bf16 copy of the train split ({need / 2**30:.2f} "
+                self.log(f"device feed off: its copy of the train split ({need / 2**30:.2f} "
                          f"GiB) does not fit the free HBM ({free / 2**30:.2f} GiB)")
                 return None
         return DeviceFeed(step, X, tr.labels, bs, steps, col=col)

@@ -110,6 +110,7 @@ class TrainStep:
         # every partial gradient), so it then runs eagerly inside engine.reduce()
         pre = getattr(engine, "pre_reduce", None) if engine.name != "dSGD" else None
         self._pre_reduce = pre if self.accum == 1 else None
+        self._pre_any = pre  # device-fed accumulated steps capture it after the last micro-batch
         self.eager_warmup = eager_warmup
         self.calls = 0
         self.graph = None
@@ -216,6 +217,17 @@ class TrainStep:
                 sy.copy_(y, non_blocking=True)
             if zero:
                 self.flat.grad.zero_()
+
+    def _dev_graph_opt_ok(self) -> bool:
+        """Can a device-fed replay hold whole steps (update inside)?  With accumulation a
+        device-fed body is a whole step of ``accum`` micro-batches (:meth:`_dev_body_accum`),
+        so unlike a host-fed replay it may hold the reduction and the update too."""
+        if self.accum == 1:
+            return self._graph_opt_ok()
+        g = self.engine.group
+        comm = (not g.distributed) or (CAPTURE_COMM and g.backend == "nccl"
+                                       and getattr(self.engine, "capturable", True))
+        return comm and isinstance(self.opt, ops.FusedAdam) and self.flat.data.is_cuda
 
     def _graph_opt_ok(self) -> bool:
         # the optimizer joins the graph when every collective between backward and update is
@@ -377,10 +389,9 @@ class TrainStep:
         every step also writes its score column and loss into the recorder's rings (inside the
         packing Adam launch when there is one), so the train metrics of an epoch are exact without
         a host round trip per step (``runtime.feed.DeviceFeed``)."""
-        if self.accum != 1:
-            raise ValueError("TrainStep.bind: device-fed steps need local_iterations == 1")
-        if not getattr(self.model, "accepts_bf16_input", False):
-            raise ValueError("TrainStep.bind: the model must take a bf16 batch")
+        bf = src.X.dtype == torch.bfloat16
+        if bf and not getattr(self.model, "accepts_bf16_input", False):
+            raise ValueError("TrainStep.bind: a bf16 dataset needs a model that takes a bf16 batch")
         if not isinstance(self.opt, ops.FusedAdam):
             raise ValueError("TrainStep.bind: device-fed steps need the fused Adam")
         self.src = src
@@ -389,9 +400,14 @@ class TrainStep:
             raise ValueError("TrainStep.bind: the recorder must index by the source's cursor")
         self.opt.cursor = src.cursor
         dev = src.X.device
-        self._dsx = torch.empty((src.B,) + src.sample_shape, dtype=torch.bfloat16, device=dev)
+        # the static input the prologue gathers into (bf16, or the fp32 rows of an fp32
+        # dataset such as FS features: exact), and what the model reads of it
+        self._dsx = torch.empty((src.B,) + src.sample_shape,
+                                dtype=torch.bfloat16 if bf else torch.float32, device=dev)
+        self._dsxf = src.view(self._dsx)
         self._dsy = torch.empty(src.B, dtype=torch.int64, device=dev)
-        self._dK = max(1, int(steps_per_graph)) if (self.use_graph and self._graph_opt_ok()) else 1
+        self._dK = (max(1, int(steps_per_graph)) if (self.use_graph and self._dev_graph_opt_ok())
+                    else 1)
         self._dgraphs = {}
         self._dcalls = 0
         # the Adam-emitted operand pack (ADAM_PACK): every replayed step then runs encoder GEMM
@@ -400,7 +416,8 @@ class TrainStep:
         self._apack = None
         from ..ops.gemm import PLAIN_BLAS
         # (across sites the update runs after the replays, eagerly: the same launch then)
-        if (ADAM_PACK and self.use_graph and (self._graph_opt_ok() or self.split)
+        # (one gather per step: not with accumulation, whose micro-batches gather each)
+        if (ADAM_PACK and self.accum == 1 and self.use_graph and (self._graph_opt_ok() or self.split)
                 and not PLAIN_BLAS and self._rides() and hasattr(self.model, "persistent_pack")):
             pp = self.model.persistent_pack(dev)
             if pp is not None:
@@ -415,14 +432,50 @@ class TrainStep:
         fn = getattr(self.model, "prologue_rides_pack", None)
         return bool(fn is not None and fn(self._dsx))
 
-    def _dev_prologue(self, bump):
+    def _dev_prologue(self, bump, grad: Optional[torch.Tensor] = None):
         """The device-fed prologue of one step: riding in the model's first launch when it can
-        (returns the context to run the forward in), else as a launch of its own."""
+        (returns the context to run the forward in), else as a launch of its own.  ``grad``:
+        the gradient range it zeroes (default all; empty for the later micro-batches of an
+        accumulated step)."""
+        grad = self.flat.grad if grad is None else grad
         if self._rides():
-            tail = self.src.prologue_args(self._dsx, self._dsy, self.flat.grad, bump)
+            tail = self.src.prologue_args(self._dsx, self._dsy, grad, bump)
             return ride_pack(tail)
-        self.src.gather(self._dsx, self._dsy, self.flat.grad, bump)
+        self.src.gather(self._dsx, self._dsy, grad, bump)
         return _NoDefer()
+
+    def _dev_body_accum(self, graph_opt: bool):
+        """One whole device-fed step of ``accum`` micro-batches (``local_iterations``; the
+        reference's ``(loss / local_iterations).backward()`` per micro-batch and one update,
+        ``/root/reference/compspec.json:88-95``): each micro-batch gathers its batch at the
+        cursor and backpropagates d(loss)/accum into the gradient the first one zeroed; the
+        cursor advances per micro-batch (the last one through the update) and every micro-batch
+        is recorded; then, once, the local factorisation (rank-dAD / PowerSGD), the reduction and
+        the update.  Eager (``graph_opt`` false), the collectives ride the last micro-batch's
+        backward and the caller reduces and updates."""
+        sx, sy = self._dsxf, self._dsy
+        A = self.accum
+        sync = getattr(self.engine, "sync_enabled", None)
+        for k in range(A):
+            bump = self.opt.device_step() if (graph_opt and k == 0) else None
+            grad = self.flat.grad if k == 0 else self.flat.grad[:0]
+            if sync is not None and not graph_opt:
+                self.engine.sync_enabled = k == A - 1
+            with self._dev_prologue(bump, grad) as rp:
+                out, loss, pred = self._fwd_bwd(sx, sy)
+            if isinstance(rp, ride_pack) and not rp.consumed:
+                raise RuntimeError("device-fed prologue was not absorbed by the model's weight pack")
+            if k < A - 1:
+                self.src.cursor.add_(1)
+                self._record(out, loss, pred)
+        if graph_opt:
+            if self._pre_any is not None:
+                self._pre_any()
+            scale = (self.engine.reduce(factorized=True) if self._pre_any is not None
+                     else self.engine.reduce())
+            self.opt.step_graphable(grad_scale=scale, prebumped=True)
+            self._record(out, loss, pred)
+        return out, loss, pred
 
     @contextlib.contextmanager
     def _apack_forward(self):
@@ -443,23 +496,23 @@ class TrainStep:
 
     def _dev_body_apack(self):
         """One whole device-fed step in the Adam-emitted-pack form (single site)."""
-        sx, sy = self._dsx, self._dsy
+        sx, sy = self._dsxf, self._dsy
         with self._apack_forward():
             out, loss, pred = self._fwd_bwd(sx, sy)
         if self._pre_reduce is not None:
             self._pre_reduce()
         scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
                  else self.engine.reduce())
-        self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss))
+        self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss, pred))
         return out, loss, pred
 
-    def _rec_args(self, out, loss):
-        return self.rec.args(out, loss) if self.rec is not None else None
+    def _rec_args(self, out, loss, pred=None):
+        return self.rec.args(out, loss, pred) if self.rec is not None else None
 
-    def _record(self, out, loss):
+    def _record(self, out, loss, pred=None):
         """The standalone record of a step whose update already advanced the cursor."""
         if self.rec is not None:
-            self.rec.record(out, loss, cofs=-1)
+            self.rec.record(out, loss, cofs=-1, pred=pred)
 
     def _apack_prime(self):
         """Before the first replay of a run: the persistent images from the current parameters,
@@ -479,26 +532,28 @@ class TrainStep:
         all-reduce between its parts, the reduction, and the update that also emits the next
         step's operands -- everything a replay needs, so K such steps form one graph."""
         if self._apack is not None:
-            out, loss, pred = self._split_backward(self._dsx, self._dsy, self._apack_forward())
+            out, loss, pred = self._split_backward(self._dsxf, self._dsy, self._apack_forward())
         else:
-            out, loss, pred = self._split_backward(self._dsx, self._dsy,
+            out, loss, pred = self._split_backward(self._dsxf, self._dsy,
                                                    self._dev_prologue(self.opt.device_step()))
         scale = self._reduce_after_replay()
         if self._apack is not None:
-            self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss))
+            self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss, pred))
         else:
             self.opt.step_graphable(grad_scale=scale, prebumped=True)
-            self._record(out, loss)
+            self._record(out, loss, pred)
         return out, loss, pred
 
     def _dev_body(self, graph_opt: bool):
         """One whole device-fed step as issued into the current stream (eager or captured)."""
+        if self.accum > 1:
+            return self._dev_body_accum(graph_opt)
         if self.split and self.comm_graph and graph_opt:
             return self._dev_body_split()
         if self._apack is not None and graph_opt:
             return self._dev_body_apack()
         bump = self.opt.device_step() if graph_opt else None
-        sx, sy = self._dsx, self._dsy
+        sx, sy = self._dsxf, self._dsy
         with self._dev_prologue(bump) as rp:
             out, loss, pred = self._fwd_bwd(sx, sy)
         if isinstance(rp, ride_pack) and not rp.consumed:
@@ -509,7 +564,7 @@ class TrainStep:
             scale = (self.engine.reduce(factorized=True) if self._pre_reduce is not None
                      else self.engine.reduce())
             self.opt.step_graphable(grad_scale=scale, prebumped=True)
-            self._record(out, loss)
+            self._record(out, loss, pred)
         return out, loss, pred
 
     def _dev_capture(self, k: int):
@@ -517,7 +572,7 @@ class TrainStep:
         prev = getattr(self.engine, "sync_enabled", None)
         if prev is not None:
             self.engine.sync_enabled = False
-        graph_opt = self._dK > 1 or self._graph_opt_ok()
+        graph_opt = self._dK > 1 or self._dev_graph_opt_ok()
         if graph_opt:
             self.opt.sync_device_step()
             self._cap_lr = self.opt.lr
@@ -535,7 +590,7 @@ class TrainStep:
         down to the cut (:meth:`_split_fwd_bwd`), graph B = the rest (the all-reduce of every
         non-stem gradient runs between the two replays)."""
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        sx, sy = self._dsx, self._dsy
+        sx, sy = self._dsxf, self._dsy
         self.engine.sync_enabled = False
         try:
             with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
@@ -562,7 +617,7 @@ class TrainStep:
             scale = self.engine.reduce()
         with T.phase("optim"):
             self.opt.step(grad_scale=scale)  # advances the source cursor too
-            self._record(out, loss)
+            self._record(out, loss, pred)
         self.last_out, self.last_loss, self.last_pred = out.detach(), loss.detach(), pred
         return loss
 
@@ -601,7 +656,7 @@ class TrainStep:
         if self._dgraphs and self.opt.lr != self._cap_lr and any(
                 v[2] is True for v in self._dgraphs.values()):
             self._dgraphs = {}  # the learning rate is baked into the captured update
-        if self.split and not self.comm_graph:
+        if self.split and not self.comm_graph and self.accum == 1:
             if "split" not in self._dgraphs:
                 self._dev_capture_split()
             ga, gb, (out, loss, pred), _ = self._dgraphs["split"]
@@ -619,11 +674,11 @@ class TrainStep:
             with self.timers.phase("optim"):
                 if self._apack is not None:
                     # + next operands and batch (+ this step's train record)
-                    self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss))
+                    self.opt.step_pack(grad_scale=scale, record=self._rec_args(out, loss, pred))
                     self.opt.step_count += 1
                 else:
                     self.opt.step(grad_scale=scale)
-                    self._record(out, loss)
+                    self._record(out, loss, pred)
             self.last_out, self.last_loss, self.last_pred = out, loss, pred
             return loss, done + 1, primed
         k = min(self._dK, n - done)
@@ -644,7 +699,7 @@ class TrainStep:
                 scale = self.engine.reduce()
             with self.timers.phase("optim"):
                 self.opt.step(grad_scale=scale)
-                self._record(out, loss)
+                self._record(out, loss, pred)
         self.last_out, self.last_loss, self.last_pred = out, loss, pred
         return loss, done + k, primed
 
@@ -653,7 +708,7 @@ class TrainStep:
         region never includes a capture.  Call after the eager warm-up steps."""
         if self.src is None or not self.use_graph or self._dcalls < self.eager_warmup:
             return
-        if self.split and not self.comm_graph:
+        if self.split and not self.comm_graph and self.accum == 1:
             if "split" not in self._dgraphs:
                 self._dev_capture_split()
             return

@@ -103,6 +103,8 @@ class FreeSurferTrainer(NNTrainer):
     def score(self, out, pred):
         return pred  # metrics on hard argmax labels (comps/fs/__init__.py:57-59, quirk A10)
 
+    score_column = -1  # device-fed epochs record the predicted class (ops.StepRecorder)
+
 
 class FSVDataHandle(SiteDataHandle):
     def list_files(self):

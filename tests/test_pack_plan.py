@@ -24,12 +24,16 @@ def test_persistent_pack_rows_cover_lstm_and_encoder():
     kinds = [r[2] for r in rows]
     ndir = 2
     assert kinds.count(PK_WIH) == ndir and kinds.count(PK_WHH) == ndir
-    assert kinds.count(PK_BIAS) == 2 * ndir and kinds.count(PK_CAST) == 2
+    # casts: the encoder's weight and bias, and the bf16 image of every classifier weight the
+    # replicated head reads (ops.head._bf16_images)
+    heads = [L.linear.weight for L in m.head_spec().layers]
+    assert kinds.count(PK_BIAS) == 2 * ndir and kinds.count(PK_CAST) == 2 + len(heads)
     seg = {id(p): (o, n) for p, o, n in flat.segments()}
     lin = m.encoder[0]
-    for p, kind in ((lin.weight, PK_CAST), (lin.bias, PK_CAST)):
+    for p, kind in [(lin.weight, PK_CAST), (lin.bias, PK_CAST)] + [(w, PK_CAST) for w in heads]:
         o, n = seg[id(p)]
         assert (o, n, kind) in [(r[0], r[1], r[2]) for r in rows]
+    assert all(pp.bf16_of(w) is not None and pp.bf16_of(w).shape == w.shape for w in heads)
     # b_hh images start ndir * 4 HD floats after the b_ih images (the kernel's bias_split)
     GP = 4 * pp.HD
     bias_rows = [r for r in rows if r[2] == PK_BIAS]

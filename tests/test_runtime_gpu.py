@@ -78,12 +78,14 @@ def test_ica_site_collective_paths_over_rccl(tmp_path):
         dist.destroy_process_group()
 
 
-def test_ica_site_device_feed_matches_host_feed(tmp_path):
+@pytest.mark.parametrize("li", [1, 2])
+def test_ica_site_device_feed_matches_host_feed(tmp_path, li):
     """The production site loop trains its epochs device-fed (runtime.feed: HBM-resident bf16
     split, K-step graphs, train records on the device) and logs what the per-step host loop
-    logs: same train loss / AUC per epoch, same validation curve, same test metrics."""
+    logs: same train loss / AUC per epoch, same validation curve, same test metrics; also with
+    gradient accumulation (local_iterations = 2: whole accumulated steps per replay)."""
     root = _ica_root(tmp_path)
-    ov = {"epochs": 3, "batch_size": 8, "seed": 3}
+    ov = {"epochs": 3, "batch_size": 8, "seed": 3, "local_iterations": li}
     dev = _run_site(root, str(tmp_path / "dev"), dict(ov, device_feed=True))[0]
     host = _run_site(root, str(tmp_path / "host"), dict(ov, device_feed=False))[0]
     assert dev.get("feed") == "device" and "feed" not in host
@@ -92,3 +94,16 @@ def test_ica_site_device_feed_matches_host_feed(tmp_path):
     for a, b in zip(dev["validation_log"], host["validation_log"]):
         assert abs(a[0] - b[0]) < 2e-4 and abs(a[1] - b[1]) < 2e-3
     assert len(dev["samples_per_sec"]) == 3
+
+
+def test_fs_site_device_feed_matches_host_feed(fs_data_root, tmp_path):
+    """The FS task trains device-fed too (fp32 features resident, hard-label train scores from
+    the predicted class): the same logs as the per-step host loop."""
+    ov = {"epochs": 3, "batch_size": 16, "seed": 3}
+    dev = _run_site(fs_data_root, str(tmp_path / "dev"), dict(ov, device_feed=True))[0]
+    host = _run_site(fs_data_root, str(tmp_path / "host"), dict(ov, device_feed=False))[0]
+    assert dev.get("feed") == "device" and "feed" not in host
+    for a, b in zip(dev["train_log"], host["train_log"]):
+        assert abs(a[0] - b[0]) < 2e-4 and abs(a[1] - b[1]) < 2e-3, (dev["train_log"], host["train_log"])
+    for a, b in zip(dev["validation_log"], host["validation_log"]):
+        assert abs(a[0] - b[0]) < 2e-4 and abs(a[1] - b[1]) < 2e-3

@@ -614,3 +614,83 @@ def test_device_feed_epoch_matches_host_loop(apack, monkeypatch):
         assert torch.allclose(scores, hs, rtol=1e-4, atol=1e-6), (scores - hs).abs().max()
     assert sd.opt.step_count == sh.opt.step_count == 2 * nb
     assert torch.allclose(fh.data, fd.data, rtol=1e-6, atol=1e-7), (fh.data - fd.data).abs().max()
+
+
+def _feed_vs_host(sh, sd, X, Y, B, nb, accum, col, epochs=2, seed=5):
+    """One DeviceFeed epoch per loop over a random batch order vs the host-fed TrainStep on the
+    same batches (``accum`` micro-batches per step); returns the two flat parameter sets."""
+    from dinunet_implementations_amd.runtime.feed import DeviceFeed
+    feed = DeviceFeed(sd, X, Y, B, nb, col=col, steps_per_graph=4)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    nbb = nb * accum
+    host_loss, host_score = [], []
+    for _ in range(epochs):
+        order = torch.randint(0, X.shape[0], (nbb * B,), device="cuda", generator=g)
+        for c in range(nbb):
+            rows = order[c * B:(c + 1) * B]
+            loss = sh(X[rows].float(), Y[rows], first=c % accum == 0, last=c % accum == accum - 1)
+            host_loss.append(float(loss))
+            host_score.append((sh.last_pred.float() if col < 0 else sh.last_out[:, col]).clone())
+        losses, scores, labels = feed.run_epoch(order)
+        torch.cuda.synchronize()
+        assert torch.equal(labels, Y[order])
+        hl = torch.tensor(host_loss[-nbb:], device="cuda")
+        assert torch.allclose(losses, hl, rtol=1e-5, atol=1e-6), (losses, hl)
+        hs = torch.cat(host_score[-nbb:])
+        assert torch.allclose(scores, hs, rtol=1e-4, atol=1e-6), (scores - hs).abs().max()
+    assert sd.opt.step_count == sh.opt.step_count == epochs * nb
+    return feed
+
+
+@pytest.mark.parametrize("engine,sites", [("dSGD", 1), ("dSGD", "rccl1"), ("rankDAD", 1),
+                                          ("powerSGD", "rccl1")])
+def test_device_feed_accumulation_matches_host_loop(engine, sites, request):
+    """local_iterations > 1 on the device-fed epoch -- every replay holds
+    whole accumulated steps (2 micro-batches each gathered at the cursor, d(loss)/2 into one
+    gradient, one reduction and one update), giving the host-fed accumulation's trajectory and
+    per-micro-batch train records; across sites the collectives are captured with the update."""
+    grp = request.getfixturevalue("rccl1") if sites == "rccl1" else None
+    xs, ys = _batches(n=6)
+    B = xs.shape[1]
+    X = xs.reshape(-1, *xs.shape[2:]).to(torch.bfloat16)
+    Y = ys.reshape(-1)
+    mk = (lambda: _trainer_cfg(0, engine, grp, {"dad_reduction_rank": 4}, use_graph=True,
+                               accum=2)) if grp is not None else (
+        lambda: _trainer(0, engine=engine, use_graph=True, accum=2))
+    _, fh, sh = mk()
+    _, fd, sd = mk()
+    feed = _feed_vs_host(sh, sd, X, Y, B, nb=5, accum=2, col=1)
+    assert sd._dK == 4 and sd._apack is None and feed.nbb == 10
+    assert all(v[2] for v in sd._dgraphs.values()), "the update must be inside the replays"
+    tol = dict(rtol=1e-6, atol=1e-7) if engine == "dSGD" else dict(rtol=1e-4, atol=1e-5)
+    assert torch.allclose(fh.data, fd.data, **tol), (fh.data - fd.data).abs().max()
+
+
+@pytest.mark.parametrize("accum", [1, 2])
+def test_fs_device_feed_matches_host_loop(accum):
+    """the FS task on the device-fed epoch -- 66 fp32 features resident in
+    HBM (padded to 72 columns once, gathered exactly into an fp32 static input the head reads
+    through its row stride) and hard-label train scores recorded from the predicted class
+    (comps/fs/__init__.py:57-59)."""
+    from dinunet_implementations_amd.models import MSANNet
+    from dinunet_implementations_amd.ops import FlatParams, FusedAdam
+    from dinunet_implementations_amd.parallel import make_engine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    from dinunet_implementations_amd.runtime.step import TrainStep
+
+    def mk():
+        torch.manual_seed(0)
+        m = MSANNet(66, [64, 32], 2).cuda().train()
+        flat = FlatParams(m.parameters())
+        opt = FusedAdam(flat, lr=1e-3)
+        eng = make_engine("dSGD", m, flat, SiteGroup(device=torch.device("cuda")), {})
+        return flat, TrainStep(m, flat, opt, eng, task="fs", use_graph=True, accum=accum)
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.randn(96, 66, device="cuda", generator=g)
+    Y = torch.randint(0, 2, (96,), device="cuda", generator=g)
+    fh, sh = mk()
+    fd, sd = mk()
+    feed = _feed_vs_host(sh, sd, X, Y, 16, nb=5, accum=accum, col=-1)
+    assert feed.src.width == 66 and sd._dsx.shape == (16, 72) and sd._dsx.dtype == torch.float32
+    assert torch.allclose(fh.data, fd.data, rtol=1e-6, atol=1e-7), (fh.data - fd.data).abs().max()
