@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--work", default="/tmp/dinunet_runpy_rate")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4_runpy_rate.json"))
     ap.add_argument("--bench", type=int, default=1, help="also run bench.py for the comparison")
+    ap.add_argument("--li", type=int, default=1, help="local_iterations (gradient accumulation)")
     a = ap.parse_args()
     from dinunet_implementations_amd.data.synthetic import make_ica_sites
     from dinunet_implementations_amd.utils import analysis
@@ -40,7 +41,8 @@ def main():
                    hidden_size=384, input_size=256, cohort="hard", signal=0.35, label_noise=0.1)
     out = os.path.join(a.work, "out")
     sets = ["agg_engine=dSGD", "batch_size=32", f"epochs={a.epochs}", f"patience={a.epochs}",
-            "split_ratio=[0.8, 0.1, 0.1]", "learning_rate=0.001", "seed=11"]
+            "split_ratio=[0.8, 0.1, 0.1]", "learning_rate=0.001", "seed=11",
+            f"local_iterations={a.li}"]
     cmd = [sys.executable, "-m", "dinunet_implementations_amd.run", "--data-path", data,
            "--out", out, "--device", "cuda"]
     for s in sets:
@@ -59,7 +61,7 @@ def main():
     rec = {"what": "python -m dinunet_implementations_amd.run, 1 site, synthetic hard ICA cohort "
                    f"({a.subjects} subjects, C=100, T=980 -> S=98, split 0.8/0.1/0.1), B=32, "
                    "H=384, I=256, dSGD, bf16, 1 MI355X",
-           "feed": logs.get("feed", "host"), "epochs": a.epochs,
+           "feed": logs.get("feed", "host"), "epochs": a.epochs, "local_iterations": a.li,
            "samples_per_sec_per_epoch": [round(v, 1) for v in sps],
            "runpy_samples_per_sec": round(statistics.median(sps[1:] or sps), 1) if sps else None,
            "runpy_wall_s": round(wall, 1),
