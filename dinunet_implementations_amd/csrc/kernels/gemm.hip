@@ -533,19 +533,19 @@ __device__ __forceinline__ int sw_km128(int k) { return (((k >> 1) & 1) | (((k >
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <int ROWS, bool KCONTIG>
+template <int ROWS, bool KCONTIG, int NW = 4>
 struct DmaImg {
   static constexpr int BYTES = ROWS * 64 * 2;    // one 64-deep K tile
-  static constexpr int PER_WAVE = BYTES / 1024 / 4;
+  static constexpr int PER_WAVE = BYTES / 1024 / NW;  // 1 KB DMA instructions per wave
 };
 
 // This wave's share of the DMA of operand rows [row0, row0 + ROWS) x k [k, k + 64), as per-lane
 // source pointers fixed for the whole K loop (row / column part and swizzle folded in once; a K
 // tile only adds its k offset).  A lane whose row (column) is out of range keeps a null pointer
 // and reads the zero page; the k range is checked per tile (K % 8 == 0: chunks are all in or out).
-template <int ROWS, bool KCONTIG>
+template <int ROWS, bool KCONTIG, int NW = 4>
 struct DmaStream {
-  static constexpr int PW = DmaImg<ROWS, KCONTIG>::PER_WAVE;
+  static constexpr int PW = DmaImg<ROWS, KCONTIG, NW>::PER_WAVE;
   const bf16* p[PW];
   int kofs[PW];  // the chunk's k offset within the tile
   long kstep;    // elements per unit of k
@@ -811,6 +811,164 @@ gemm_dma_kernel(GemmGroup g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large-M GEMMs (the ICA step at B >= 1024: M = B*S rows, N = 256 / 1536): 256 x 256 tiles, 8
+// waves (2 x 4, 128 x 64 outputs and 32 accumulator fragments each), BK = 64, both operands
+// k-contiguous (A [M][K], B [N][K]), staged by LDS-DMA into two 64 KB stages of dynamic LDS: one
+// workgroup per CU at two waves per SIMD, tile t+1's DMA in flight under tile t's 64 MFMAs per
+// wave.  Against the 128 x 128 kernel a tile reads half the operand bytes per MFMA, and at N = 256
+// one workgroup streams its A rows exactly once (cdna_hip_programming §5: the 256^2 tile with a
+// glds pipeline).  Epilogue: the LDS-staged vector path in four passes of 32 rows per wave (the
+// ring's 128 KB cannot hold eight 128 x 64 fp32 blocks at once); problems that need another
+// epilogue (row maps, column sums, split-K) take the 128 x 128 kernel.
+constexpr int G256_SMEM = 2 * (256 * 64 * 2) * 2;  // two stages of A + B images
+
+template <bool TA, bool TB>
+__global__ void __launch_bounds__(512)
+gemm256_kernel(GemmGroup g) {
+  static_assert(!TA && TB, "gemm256_kernel: k-contiguous operands only");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  constexpr int BM = 256, BN = 256, NW = 8, WM = 128, WN = 64, FM = WM / 16, FN = WN / 16;
+  typedef DmaImg<BM, true, NW> IA;
+  typedef DmaImg<BN, true, NW> IB;
+  constexpr int STAGE = IA::BYTES + IB::BYTES;
+
+  const int ntiles = g.tile_start[g.n];
+  const int bid = (int)blockIdx.x;
+  const int slot = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);  // XCD-contiguous slots
+  if (slot >= ntiles) return;
+  group_bump(g);
+  const int gtile = g.perm ? g.perm[slot] : slot;
+  int pi = 0;
+  while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
+  const GemmProb& P = g.p[pi];
+  const bf16* __restrict__ A = reinterpret_cast<const bf16*>(P.A);
+  const bf16* __restrict__ B = reinterpret_cast<const bf16*>(P.B);
+  const int M = P.M, N = P.N, K = P.K;
+  const int tile = gtile - g.tile_start[pi];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int row0 = (tile / tiles_n) * BM, col0 = (tile % tiles_n) * BN;
+  const int nk = (K + 63) / 64;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  DmaStream<BM, true, NW> sa;
+  DmaStream<BN, true, NW> sb;
+  sa.init(A, P.lda, row0, M, wid, lane);
+  sb.init(B, P.ldb, col0, N, wid, lane);
+  sa.issue(0, K, smem);
+  sb.issue(0, K, smem + IA::BYTES);
+  for (int t = 0; t < nk; ++t) {
+    __builtin_amdgcn_s_waitcnt(DN_VMCNT0);  // this wave's share of tile t has landed
+    __builtin_amdgcn_s_barrier();           // ... every wave's; stage (t+1)&1 is free again
+    if (t + 1 < nk) {
+      char* nxt = smem + ((t + 1) & 1) * STAGE;
+      sa.issue(64 * (t + 1), K, nxt);
+      sb.issue(64 * (t + 1), K, nxt + IA::BYTES);
+    }
+    const char* cur = smem + (t & 1) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = dma_frag<BN, true>(cur + IA::BYTES, wn * WN + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const bf16x8 af = dma_frag<BM, true>(cur, wm * WM + 16 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af, bfr[j], acc[i][j]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the ring
+
+  const Epi& ep = P.epi;
+  {  // (host contract: g.vepi -- bias / ReLU / mask / beta, no row map, 16-B output rows)
+    constexpr int ES = WN + 4;  // fp32 staging row stride
+    float* E = reinterpret_cast<float*>(smem) + wid * 32 * ES;
+#pragma unroll
+    for (int pass = 0; pass < FM / 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int lc = 16 * j + (lane & 15);
+        const int col = col0 + wn * WN + lc;
+        const float bias = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[2 * pass + i][j][r] * ep.alpha + bias;
+            if (ep.relu) v = fmaxf(v, 0.f);
+            E[(16 * i + 4 * (lane >> 4) + r) * ES + lc] = v;
+          }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      const int gr0 = row0 + wm * WM + 32 * pass, gc0 = col0 + wn * WN;
+      if (ep.out_bf16) {
+        constexpr int CPR = WN / 8, RPI = 64 / CPR;  // 8 vectors per row, 8 rows per round
+#pragma unroll
+        for (int it = 0; it < 32 / RPI; ++it) {
+          const int lr = it * RPI + lane / CPR, lc = 8 * (lane % CPR);
+          const int row = gr0 + lr, col = gc0 + lc;
+          if (row >= M || col >= N) continue;
+          const f32x4 a = *reinterpret_cast<const f32x4*>(E + lr * ES + lc);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(E + lr * ES + lc + 4);
+          bf16x8* cp = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(P.C) + (long)row * P.ldc + col);
+          float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+          if (ep.mask) {
+            const bf16x8 m = *reinterpret_cast<const bf16x8*>(ep.mask + (long)row * ep.ldm + col);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (float)m[e] > 0.f ? v[e] : 0.f;
+          }
+          if (ep.beta != 0.f) {
+            const bf16x8 o = *cp;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += ep.beta * (float)o[e];
+          }
+          bf16x8 w;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] = (bf16)v[e];
+          *cp = w;
+        }
+      } else {
+        constexpr int CPR = WN / 4, RPI = 64 / CPR;
+#pragma unroll
+        for (int it = 0; it < 32 / RPI; ++it) {
+          const int lr = it * RPI + lane / CPR, lc = 4 * (lane % CPR);
+          const int row = gr0 + lr, col = gc0 + lc;
+          if (row >= M || col >= N) continue;
+          f32x4 v = *reinterpret_cast<const f32x4*>(E + lr * ES + lc);
+          f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + (long)row * P.ldc + col);
+          if (ep.mask) {
+            const bf16x4 m = *reinterpret_cast<const bf16x4*>(ep.mask + (long)row * ep.ldm + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (float)m[e] > 0.f ? v[e] : 0.f;
+          }
+          if (ep.beta != 0.f) {
+            const f32x4 o = *cp;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += ep.beta * o[e];
+          }
+          *cp = v;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();  // the next pass rewrites this wave's staging rows
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+  }
+}
+
 // 4 consecutive outputs of one row: v (already alpha-free split sum) -> epilogue -> vector store
 __device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, int row, int col, f32x4 v) {
   if (epi.xcol >= 0 && col + 3 >= epi.xcol) {  // the column-sum group (xcol % 4 == 0)
@@ -954,6 +1112,30 @@ int launch(GemmGroup& g, hipStream_t st) {
   return dn_launch_status();
 }
 
+static bool g_g256_init = false;
+
+// 256 x 256 tiles (tile 2): bf16 k-contiguous operands, no split-K, no virtual ones column
+static int launch256(GemmGroup& g, hipStream_t st) {
+  int tiles = 0;
+  long elems = 0;
+  for (int i = 0; i < g.n; ++i) {
+    g.tile_start[i] = tiles;
+    g.elem_start[i] = elems;
+    tiles += ((g.p[i].M + 255) / 256) * ((g.p[i].N + 255) / 256);
+    elems += ((long)g.p[i].M * g.p[i].N + 3) / 4 * 4;
+  }
+  g.tile_start[g.n] = tiles;
+  g.elem_start[g.n] = elems;
+  if (!g_g256_init) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm256_kernel<false, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G256_SMEM);
+    g_g256_init = true;
+  }
+  hipLaunchKernelGGL((gemm256_kernel<false, true>), dim3((tiles + 7) / 8 * 8), dim3(512),
+                     G256_SMEM, st, g);
+  return dn_launch_status();
+}
+
 template <int BM, int BN, typename TAe, typename TBe>
 int dispatch_t(int ta, int tb, GemmGroup& g, hipStream_t st) {
   if (!ta && !tb) return launch<BM, BN, false, false, TAe, TBe>(g, st);
@@ -970,7 +1152,8 @@ int dispatch_tile(int a_bf16, int b_bf16, int ta, int tb, GemmGroup& g, hipStrea
   return dispatch_t<BM, BN, float, float>(ta, tb, g, st);
 }
 
-// tile: 0 -> 64x64, 1 -> 128x128 (BM x BN)
+// tile: 0 -> 64x64, 1 -> 128x128 (BM x BN), 2 -> 256x256 (k-contiguous bf16 operands, no split;
+// other problems fall back to 128x128)
 static bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 // stage_load_vec's contract for one operand: contiguous-axis extent and leading dim % 8 == 0
@@ -1005,7 +1188,10 @@ static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int t
   }
   // the virtual ones column exists only in the LDS-DMA kernel's k-major B stream
   if (xcol && (!g.vec || !g_gemm_dma || !a_bf16 || !b_bf16 || tb)) return DN_UNSUPPORTED;
-  if (tile == 1) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
+  if (tile == 2 && g.vec && g.vepi && g_gemm_dma && a_bf16 && b_bf16 && !ta && tb && !xcol &&
+      g.splits == 1)
+    return launch256(g, st);
+  if (tile == 1 || tile == 2) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
   return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, g, st);
 }
 

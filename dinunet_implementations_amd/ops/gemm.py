@@ -78,6 +78,10 @@ def _layout(t: Tensor, rows_first: bool):
     return t, 0, t.stride(0)
 
 
+# 256 x 256 tiles for large-M GEMMs with k-contiguous operands (csrc/kernels/gemm.hip
+# gemm256_kernel); DINUNET_GEMM256=0 keeps 128 x 128 (A/B switch)
+GEMM256 = __import__("os").environ.get("DINUNET_GEMM256", "1") != "0"
+
 # tuning override of the grouped launches' split-K (0 = heuristic); tools/gpu sweeps
 _GROUP_SPLITS = int(__import__("os").environ.get("DINUNET_GROUP_SPLITS", "0"))
 _GROUP_TILE = int(__import__("os").environ.get("DINUNET_GROUP_TILE", "-1"))
@@ -91,7 +95,10 @@ def choose_tiling(M: int, N: int, K: int):
     t128 = ((M + 127) // 128) * ((N + 127) // 128)
     t64 = ((M + 63) // 64) * ((N + 63) // 64)
     if t128 >= 2 * _NCU:
-        return 1, 1
+        # >= a chip of 256 x 256 tiles: tile 2 (the kernel library takes it for k-contiguous
+        # bf16 operands with a vector epilogue, 128 x 128 otherwise)
+        t256 = ((M + 255) // 256) * ((N + 255) // 256)
+        return (2 if (GEMM256 and t256 >= _NCU) else 1), 1
     return 0, _split_rule(t64, K)
 
 
@@ -166,7 +173,7 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
     slab = cnt = None
     if sp > 1:
         slab = torch.empty(sp * M * N, dtype=torch.float32, device=a.device)
-        b_ = 128 if tile == 1 else 64
+        b_ = 128 if tile in (1, 2) else 64
         cnt = _tickets(a.device, -(-M // b_) * -(-N // b_))
     if bias is not None:
         bias = bias.float().contiguous()
@@ -429,7 +436,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
     if sp > 1:
         slab = torch.empty(sp * sum(m * nn for m, nn in zip(arrs["M"], arrs["N"])),
                            dtype=torch.float32, device=dev)
-        b_ = 128 if tile == 1 else 64
+        b_ = 128 if tile in (1, 2) else 64
         cnt = _tickets(dev, sum(-(-m // b_) * -(-nn // b_) for m, nn in zip(arrs["M"], arrs["N"])))
     P = ctypes.c_void_p
     L = ctypes.c_long

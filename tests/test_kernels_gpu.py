@@ -76,7 +76,7 @@ def test_gemm_lds_dma_bf16(tile, splits, ta, tb, M, N, K):
     assert torch.equal(out, old)
 
 
-@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("tile", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K", [(300, 200, 128), (3136, 1536, 256)])
 def test_gemm_lds_dma_vector_epilogue(tile, M, N, K):
     """The DMA kernel's LDS-staged 16-B epilogue: bias + ReLU into bf16, alpha + beta
@@ -92,6 +92,29 @@ def test_gemm_lds_dma_vector_epilogue(tile, M, N, K):
     c0 = c.clone()
     mm(a, w, trans_b=True, out=c, beta=1.0, alpha=0.5, tile=tile)
     assert rel(c, c0 + 0.5 * (a.float() @ w.float().t())) < 2e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(3136, 256, 1000), (600, 1536, 256), (1000, 264, 72),
+                                   (16384, 256, 1000)])
+def test_gemm256_matches_128_tile(M, N, K):
+    """The 256 x 256 LDS-DMA kernel (tile 2: eight waves, two 64 KB stages of dynamic LDS,
+    four-pass staged epilogue) on k-contiguous operands: the fp32 reference of the same bf16
+    operands, and bit-identical to the 128 x 128 kernel (same k order per output) -- ragged M / N,
+    K not a multiple of the 64-deep tile, bias + ReLU into bf16 and beta accumulation."""
+    from dinunet_implementations_amd.ops import mm
+    g = torch.Generator(device=DEV).manual_seed(0)
+    a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, generator=g).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV, generator=g)
+    y2 = mm(a, w, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16, tile=2)
+    y1 = mm(a, w, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16, tile=1)
+    ref = torch.relu(a.float() @ w.float().t() + bias)
+    assert rel(y2, ref) < 1e-2 and torch.equal(y2, y1)
+    c = torch.randn(M, N, device=DEV, generator=g)
+    c2, c1 = c.clone(), c.clone()
+    mm(a, w, trans_b=True, out=c2, beta=1.0, alpha=0.5, tile=2)
+    mm(a, w, trans_b=True, out=c1, beta=1.0, alpha=0.5, tile=1)
+    assert rel(c2, c + 0.5 * (a.float() @ w.float().t())) < 2e-3 and torch.equal(c2, c1)
 
 
 @pytest.mark.parametrize("bf16_ops", [True, False])
