@@ -570,7 +570,9 @@ struct DmaStream {
         constexpr int CPR = ROWS / 8;
         constexpr int RPI = 64 / CPR;
         const int kr = ins * RPI + lane / CPR;
-        const int ch = (lane % CPR) ^ (ROWS == 128 ? sw_km256(kr) : sw_km128(kr));
+        // (512-B rows of a 256-column image take the 256-B rule: the bank of a chunk only sees
+        // the row offset mod 256 B, which is 0 for both)
+        const int ch = (lane % CPR) ^ (ROWS >= 128 ? sw_km256(kr) : sw_km128(kr));
         const int gc = row0 + 8 * ch;
         kofs[j] = kr;
         p[j] = gc < nrows ? base + (long)kr * ld + gc : nullptr;
@@ -615,8 +617,8 @@ __device__ __forceinline__ bf16x8 dma_frag(const char* img, int r0, int ks, int 
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int k0 = 32 * ks + 8 * g + q, k1 = k0 + 4;
     const int ch = (r0 >> 3) + (p >> 1);
-    const int s0 = ROWS == 128 ? sw_km256(k0) : sw_km128(k0);
-    const int s1 = ROWS == 128 ? sw_km256(k1) : sw_km128(k1);
+    const int s0 = ROWS >= 128 ? sw_km256(k0) : sw_km128(k0);
+    const int s1 = ROWS >= 128 ? sw_km256(k1) : sw_km128(k1);
     const s16x4 x0 = tr16_asm(img + k0 * RB + 16 * (ch ^ s0) + 8 * (p & 1));
     const s16x4 x1 = tr16_asm(img + k1 * RB + 16 * (ch ^ s1) + 8 * (p & 1));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -812,25 +814,25 @@ gemm_dma_kernel(GemmGroup g) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Large-M GEMMs (the ICA step at B >= 1024: M = B*S rows, N = 256 / 1536): 256 x 256 tiles, 8
-// waves (2 x 4, 128 x 64 outputs and 32 accumulator fragments each), BK = 64, both operands
-// k-contiguous (A [M][K], B [N][K]), staged by LDS-DMA into two 64 KB stages of dynamic LDS: one
-// workgroup per CU at two waves per SIMD, tile t+1's DMA in flight under tile t's 64 MFMAs per
-// wave.  Against the 128 x 128 kernel a tile reads half the operand bytes per MFMA, and at N = 256
-// one workgroup streams its A rows exactly once (cdna_hip_programming §5: the 256^2 tile with a
-// glds pipeline).  Epilogue: the LDS-staged vector path in four passes of 32 rows per wave (the
-// ring's 128 KB cannot hold eight 128 x 64 fp32 blocks at once); problems that need another
-// epilogue (row maps, column sums, split-K) take the 128 x 128 kernel.
+// Large GEMMs of the ICA step at B >= 1024 (M = B*S rows; the weight gradients' K = B*S):
+// 256 x 256 tiles, 8 waves (2 x 4, 128 x 64 outputs and 32 accumulator fragments each), BK = 64,
+// every operand layout (k-major images read with ds_read_b64_tr_b16), staged by LDS-DMA into two
+// 64 KB stages of dynamic LDS: one workgroup per CU at two waves per SIMD, tile t+1's DMA in
+// flight under tile t's 64 MFMAs per wave.  Against the 128 x 128 kernel a tile reads half the
+// operand bytes per MFMA, and at N = 256 one workgroup streams its A rows exactly once
+// (cdna_hip_programming §5: the 256^2 tile with a glds pipeline).  Epilogue: the LDS-staged vector
+// path in four passes of 32 rows per wave (the ring's 128 KB cannot hold eight 128 x 64 fp32
+// blocks at once), into C (bias / ReLU / mask / beta) or, split-K, raw into the fp32 slab that
+// gemm_splitk_reduce combines (which also applies row maps and the virtual ones column).
 constexpr int G256_SMEM = 2 * (256 * 64 * 2) * 2;  // two stages of A + B images
 
 template <bool TA, bool TB>
 __global__ void __launch_bounds__(512)
 gemm256_kernel(GemmGroup g) {
-  static_assert(!TA && TB, "gemm256_kernel: k-contiguous operands only");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr int BM = 256, BN = 256, NW = 8, WM = 128, WN = 64, FM = WM / 16, FN = WN / 16;
-  typedef DmaImg<BM, true, NW> IA;
-  typedef DmaImg<BN, true, NW> IB;
+  typedef DmaImg<BM, !TA, NW> IA;
+  typedef DmaImg<BN, TB, NW> IB;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
 
   const int ntiles = g.tile_start[g.n];
@@ -851,7 +853,9 @@ gemm256_kernel(GemmGroup g) {
   const int wm = wid >> 2, wn = wid & 3;
   const int tiles_n = (N + BN - 1) / BN;
   const int row0 = (tile / tiles_n) * BM, col0 = (tile % tiles_n) * BN;
-  const int nk = (K + 63) / 64;
+  const int kbeg = blockIdx.z * P.kchunk;
+  const int kend = min(K, kbeg + P.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -859,39 +863,54 @@ gemm256_kernel(GemmGroup g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  DmaStream<BM, true, NW> sa;
-  DmaStream<BN, true, NW> sb;
+  DmaStream<BM, !TA, NW> sa;
+  DmaStream<BN, TB, NW> sb;
   sa.init(A, P.lda, row0, M, wid, lane);
-  sb.init(B, P.ldb, col0, N, wid, lane);
-  sa.issue(0, K, smem);
-  sb.issue(0, K, smem + IA::BYTES);
+  sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol);
+  if (nk > 0) {
+    sa.issue(kbeg, kend, smem);
+    sb.issue(kbeg, kend, smem + IA::BYTES);
+  }
   for (int t = 0; t < nk; ++t) {
     __builtin_amdgcn_s_waitcnt(DN_VMCNT0);  // this wave's share of tile t has landed
     __builtin_amdgcn_s_barrier();           // ... every wave's; stage (t+1)&1 is free again
     if (t + 1 < nk) {
       char* nxt = smem + ((t + 1) & 1) * STAGE;
-      sa.issue(64 * (t + 1), K, nxt);
-      sb.issue(64 * (t + 1), K, nxt + IA::BYTES);
+      sa.issue(kbeg + 64 * (t + 1), kend, nxt);
+      sb.issue(kbeg + 64 * (t + 1), kend, nxt + IA::BYTES);
     }
     const char* cur = smem + (t & 1) * STAGE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 bfr[FN];
+      bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = dma_frag<BN, true>(cur + IA::BYTES, wn * WN + 16 * j, ks, lane);
+      for (int j = 0; j < FN; ++j) bfr[j] = dma_frag<BN, TB>(cur + IA::BYTES, wn * WN + 16 * j, ks, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8 af = dma_frag<BM, true>(cur, wm * WM + 16 * i, ks, lane);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af, bfr[j], acc[i][j]);
+      for (int i = 0; i < FM; ++i) af[i] = dma_frag<BM, !TA>(cur, wm * WM + 16 * i, ks, lane);
+      if constexpr (TA || !TB) {  // asm transposed reads: retire them before the MFMAs
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
       }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
 
   const Epi& ep = P.epi;
-  {  // (host contract: g.vepi -- bias / ReLU / mask / beta, no row map, 16-B output rows)
+  // split-K: raw partials into this split's fp32 slab [M][N] (the reduce kernel applies Epi);
+  // else (host contract: g.vepi) bias / ReLU / mask / beta into C, no row map, 16-B rows
+  const bool raw = P.slab != nullptr;
+  void* const Cd = raw ? (void*)(P.slab + (long)blockIdx.z * M * N) : P.C;
+  const long ldc = raw ? (long)N : P.ldc;
+  const float alpha = raw ? 1.f : ep.alpha, beta = raw ? 0.f : ep.beta;
+  const float* const ebias = raw ? nullptr : ep.bias;
+  const bf16* const emask = raw ? nullptr : ep.mask;
+  const int relu = raw ? 0 : ep.relu, obf = raw ? 0 : ep.out_bf16;
+  {
     constexpr int ES = WN + 4;  // fp32 staging row stride
     float* E = reinterpret_cast<float*>(smem) + wid * 32 * ES;
 #pragma unroll
@@ -900,13 +919,13 @@ gemm256_kernel(GemmGroup g) {
       for (int j = 0; j < FN; ++j) {
         const int lc = 16 * j + (lane & 15);
         const int col = col0 + wn * WN + lc;
-        const float bias = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+        const float bias = (ebias && col < N) ? ebias[col] : 0.f;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float v = acc[2 * pass + i][j][r] * ep.alpha + bias;
-            if (ep.relu) v = fmaxf(v, 0.f);
+            float v = acc[2 * pass + i][j][r] * alpha + bias;
+            if (relu) v = fmaxf(v, 0.f);
             E[(16 * i + 4 * (lane >> 4) + r) * ES + lc] = v;
           }
       }
@@ -914,7 +933,7 @@ gemm256_kernel(GemmGroup g) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
       const int gr0 = row0 + wm * WM + 32 * pass, gc0 = col0 + wn * WN;
-      if (ep.out_bf16) {
+      if (obf) {
         constexpr int CPR = WN / 8, RPI = 64 / CPR;  // 8 vectors per row, 8 rows per round
 #pragma unroll
         for (int it = 0; it < 32 / RPI; ++it) {
@@ -923,17 +942,17 @@ gemm256_kernel(GemmGroup g) {
           if (row >= M || col >= N) continue;
           const f32x4 a = *reinterpret_cast<const f32x4*>(E + lr * ES + lc);
           const f32x4 b = *reinterpret_cast<const f32x4*>(E + lr * ES + lc + 4);
-          bf16x8* cp = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(P.C) + (long)row * P.ldc + col);
+          bf16x8* cp = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(Cd) + (long)row * ldc + col);
           float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-          if (ep.mask) {
-            const bf16x8 m = *reinterpret_cast<const bf16x8*>(ep.mask + (long)row * ep.ldm + col);
+          if (emask) {
+            const bf16x8 m = *reinterpret_cast<const bf16x8*>(emask + (long)row * ep.ldm + col);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = (float)m[e] > 0.f ? v[e] : 0.f;
           }
-          if (ep.beta != 0.f) {
+          if (beta != 0.f) {
             const bf16x8 o = *cp;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += ep.beta * (float)o[e];
+            for (int e = 0; e < 8; ++e) v[e] += beta * (float)o[e];
           }
           bf16x8 w;
 #pragma unroll
@@ -948,16 +967,16 @@ gemm256_kernel(GemmGroup g) {
           const int row = gr0 + lr, col = gc0 + lc;
           if (row >= M || col >= N) continue;
           f32x4 v = *reinterpret_cast<const f32x4*>(E + lr * ES + lc);
-          f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + (long)row * P.ldc + col);
-          if (ep.mask) {
-            const bf16x4 m = *reinterpret_cast<const bf16x4*>(ep.mask + (long)row * ep.ldm + col);
+          f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cd) + (long)row * ldc + col);
+          if (emask) {
+            const bf16x4 m = *reinterpret_cast<const bf16x4*>(emask + (long)row * ep.ldm + col);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = (float)m[e] > 0.f ? v[e] : 0.f;
           }
-          if (ep.beta != 0.f) {
+          if (beta != 0.f) {
             const f32x4 o = *cp;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += ep.beta * o[e];
+            for (int e = 0; e < 4; ++e) v[e] += beta * o[e];
           }
           *cp = v;
         }
@@ -1112,10 +1131,22 @@ int launch(GemmGroup& g, hipStream_t st) {
   return dn_launch_status();
 }
 
-static bool g_g256_init = false;
+template <bool TA, bool TB>
+static void launch256_t(GemmGroup& g, int tiles, hipStream_t st) {
+  static bool init = false;
+  if (!init) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm256_kernel<TA, TB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G256_SMEM);
+    init = true;
+  }
+  hipLaunchKernelGGL((gemm256_kernel<TA, TB>), dim3((tiles + 7) / 8 * 8, 1, g.splits), dim3(512),
+                     G256_SMEM, st, g);
+}
 
-// 256 x 256 tiles (tile 2): bf16 k-contiguous operands, no split-K, no virtual ones column
-static int launch256(GemmGroup& g, hipStream_t st) {
+// 256 x 256 tiles (tile 2): bf16 operands on the LDS-DMA contract, split-K through the reduce
+// kernel (no in-launch combine)
+static int launch256(GemmGroup& g, int ta, int tb, hipStream_t st) {
+  g.cnt = nullptr;
   int tiles = 0;
   long elems = 0;
   for (int i = 0; i < g.n; ++i) {
@@ -1126,13 +1157,15 @@ static int launch256(GemmGroup& g, hipStream_t st) {
   }
   g.tile_start[g.n] = tiles;
   g.elem_start[g.n] = elems;
-  if (!g_g256_init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm256_kernel<false, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, G256_SMEM);
-    g_g256_init = true;
+  if (!ta && !tb) launch256_t<false, false>(g, tiles, st);
+  else if (!ta && tb) launch256_t<false, true>(g, tiles, st);
+  else if (ta && !tb) launch256_t<true, false>(g, tiles, st);
+  else launch256_t<true, true>(g, tiles, st);
+  if (g.splits > 1) {
+    const long t4 = elems / 4;
+    const int blocks = (int)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g);
   }
-  hipLaunchKernelGGL((gemm256_kernel<false, true>), dim3((tiles + 7) / 8 * 8), dim3(512),
-                     G256_SMEM, st, g);
   return dn_launch_status();
 }
 
@@ -1152,8 +1185,8 @@ int dispatch_tile(int a_bf16, int b_bf16, int ta, int tb, GemmGroup& g, hipStrea
   return dispatch_t<BM, BN, float, float>(ta, tb, g, st);
 }
 
-// tile: 0 -> 64x64, 1 -> 128x128 (BM x BN), 2 -> 256x256 (k-contiguous bf16 operands, no split;
-// other problems fall back to 128x128)
+// tile: 0 -> 64x64, 1 -> 128x128 (BM x BN), 2 -> 256x256 (bf16 operands on the LDS-DMA
+// contract; other problems fall back to 128x128)
 static bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 // stage_load_vec's contract for one operand: contiguous-axis extent and leading dim % 8 == 0
@@ -1188,9 +1221,13 @@ static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int t
   }
   // the virtual ones column exists only in the LDS-DMA kernel's k-major B stream
   if (xcol && (!g.vec || !g_gemm_dma || !a_bf16 || !b_bf16 || tb)) return DN_UNSUPPORTED;
-  if (tile == 2 && g.vec && g.vepi && g_gemm_dma && a_bf16 && b_bf16 && !ta && tb && !xcol &&
-      g.splits == 1)
-    return launch256(g, st);
+  if (tile == 2 && g.vec && g_gemm_dma && a_bf16 && b_bf16) {
+    // the staged epilogue's contract: 16-B rows into C (vepi), or fp32 slabs of N % 4 == 0
+    bool ok = g.splits > 1 || g.vepi;
+    for (int i = 0; i < g.n && ok; ++i)
+      if (g.splits > 1 && (g.p[i].N % 4 || (((uintptr_t)g.p[i].slab) & 15))) ok = false;
+    if (ok) return launch256(g, ta, tb, st);
+  }
   if (tile == 1 || tile == 2) return dispatch_tile<128, 128>(a_bf16, b_bf16, ta, tb, g, st);
   return dispatch_tile<64, 64>(a_bf16, b_bf16, ta, tb, g, st);
 }

@@ -216,8 +216,9 @@ def _group_tile(probs, trans_a: bool, tile: Optional[int]) -> Optional[int]:
     if tile is None and maxk >= _LONG_K:
         # very long K (large-batch weight gradients, K = B*S): 128x128 tiles double the MFMA
         # work per staged byte.  B = 2048 ICA step on MI355X (tools/_gpu_group_ab.sh): 64x64
-        # 3.88 ms/step, 128x128 3.45 ms at ~8 workgroups per CU (24 splits)
-        tile = 1
+        # 3.88 ms/step, 128x128 3.45 ms at ~8 workgroups per CU (24 splits); 256 x 256 (tile 2,
+        # one workgroup per CU) halves the staged bytes per MFMA again
+        tile = 2 if GEMM256 else 1
     return tile
 
 
@@ -251,7 +252,7 @@ def _place_colsums(probs, trans_a: bool, trans_b: bool, tile: Optional[int]):
     tile = _group_tile(probs, trans_a, tile) if probs[0]["a"].is_cuda else tile
     if not any(q.get("colsum") for q in probs):
         return probs, tile
-    fold_ok = (COLSUM_FOLD and tile == 1 and probs[0]["a"].is_cuda and not trans_b
+    fold_ok = (COLSUM_FOLD and tile in (1, 2) and probs[0]["a"].is_cuda and not trans_b
                and _lib.native_available() and int(_lib.lib().dn_gemm_dma_on()) == 1
                and all(_dma_vec_ok(q, trans_a, trans_b) for q in probs))
     out = []
@@ -379,7 +380,7 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
     ta = tb = None
     a_bf = b_bf = c_bf = None
     maxk = 0
-    t64 = t128 = 0
+    t64 = t128 = t256 = 0
     for q in probs:
         A = q["a"].t() if trans_a else q["a"]
         B = q["b"].t() if trans_b else q["b"]
@@ -422,13 +423,15 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         maxk = max(maxk, K)
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
         t128 += ((M + 127) // 128) * ((N + 127) // 128)
+        t256 += ((M + 255) // 256) * ((N + 255) // 256)
     if splits is None and _GROUP_SPLITS:
         splits = _GROUP_SPLITS
     if splits is None:
         # 128x128 tiles: ~4 workgroups per CU (B = 2048 ICA step, 64 tiles: 16 splits 2.631 /
         # 2.634 ms vs 32 splits 2.651 / 2.650, 20 splits 2.679; B = 4096 5.179 / 5.161 vs
         # 5.195 / 5.171 -- profiles/r4_group_splits_ab.jsonl)
-        splits = _split_rule(t128, maxk, per_cu=4) if tile == 1 else _split_rule(t64, maxk)
+        splits = (_split_rule(t256, maxk, per_cu=1) if tile == 2 else
+                  _split_rule(t128, maxk, per_cu=4) if tile == 1 else _split_rule(t64, maxk))
     sp = max(1, int(splits))
     dev = probs[0]["out"].device
     perm = _xcd_order(arrs, 128 if tile == 1 else 64, dev) if (XCD_ORDER and tile == 1) else None

@@ -117,6 +117,25 @@ def test_gemm256_matches_128_tile(M, N, K):
     assert rel(c2, c + 0.5 * (a.float() @ w.float().t())) < 2e-3 and torch.equal(c2, c1)
 
 
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(600, 264, 1000), (768, 256, 4096)])
+def test_gemm256_layouts_and_split(ta, tb, splits, M, N, K):
+    """The 256 x 256 kernel on every operand layout (k-major images through transposed LDS
+    reads, 512-B image rows) and split-K into fp32 slabs + the reduce kernel: the fp32 reference
+    and bit-identical to the 128 x 128 kernel at the same split."""
+    from dinunet_implementations_amd.ops import mm
+    g = torch.Generator(device=DEV).manual_seed(1)
+    a = (torch.randn(K, M, device=DEV, generator=g) if ta
+         else torch.randn(M, K, device=DEV, generator=g)).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV, generator=g) if tb
+         else torch.randn(K, N, device=DEV, generator=g)).to(torch.bfloat16)
+    ref = (a.t() if ta else a).float() @ (b.t() if tb else b).float()
+    o2 = mm(a, b, trans_a=ta, trans_b=tb, tile=2, splits=splits)
+    o1 = mm(a, b, trans_a=ta, trans_b=tb, tile=1, splits=splits)
+    assert rel(o2, ref) < 2e-3 and torch.equal(o2, o1)
+
+
 @pytest.mark.parametrize("bf16_ops", [True, False])
 def test_gemm_relu_mask_epilogue(bf16_ops):
     """mm(..., mask=y): outputs where y <= 0 are zeroed in the epilogue (the ICA encoder's ReLU
@@ -406,7 +425,8 @@ def test_gemm_grouped_ncol_stores_only_leading_columns():
 
 
 @pytest.mark.parametrize("splits,tile,fold", [(1, 1, True), (3, 1, True), (4, 1, False),
-                                               (3, 0, True), (None, None, True)])
+                                               (3, 0, True), (None, None, True), (1, 2, True),
+                                               (3, 2, True)])
 def test_gemm_grouped_colsum_folded_or_separate(splits, tile, fold, monkeypatch):
     """A column sum requested beside its weight gradient (``colsum``, the LSTM / encoder bias
     gradients): with 128x128 tiles on the LDS-DMA kernel it is folded into the problem (B's
@@ -443,7 +463,7 @@ def test_gemm_grouped_colsum_folded_or_separate(splits, tile, fold, monkeypatch)
         refs.append((out, ro, x1, r1, x2, r2))
     placed, t = G._place_colsums(list(probs), True, False, tile)
     folded = sum("colsum_folded" in q for q in placed)
-    assert folded == (4 if (fold and t == 1) else 0)
+    assert folded == (4 if (fold and t in (1, 2)) else 0)
     assert len(placed) == 4 + (4 - folded)
     G.mm_grouped(probs, trans_a=True, splits=splits, tile=tile)
     for out, ro, x1, r1, x2, r2 in refs:
