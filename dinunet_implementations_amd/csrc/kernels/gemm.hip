@@ -227,6 +227,18 @@ struct Epi {
 
 constexpr int GMAX = 12;  // problems per grouped launch (kernarg: ~1.6 KB)
 
+// Rows of one operand gathered from a dataset resident in HBM instead of a batch copy (the
+// device-fed step at large batch): logical row r of the operand is dataset row
+// subj[r / gs] * gs + r % gs of gx (row stride = the operand's ld) -- the ICA batch of B
+// subjects x S windows, read in place through the step's subject indices (prologue.h sd).  The
+// LDS-DMA kernels only: A's rows (k-contiguous A) or B's k rows (k-major B); gs >= 64.
+struct RowGather {
+  const bf16* gx;            // null: no gather
+  const long long* subj;     // [rows / gs + 1] dataset subject indices
+  int gs;                    // rows per subject
+  int op;                    // 1: operand A, 2: operand B
+};
+
 // One GEMM problem of a (possibly grouped) launch.
 struct GemmProb {
   const void* A;
@@ -236,6 +248,7 @@ struct GemmProb {
   long lda, ldb, ldc;
   int M, N, K, kchunk;
   Epi epi;
+  RowGather rg;
 };
 
 // A launch: problems sharing layouts / element types / tile shape.  blockIdx.x enumerates the
@@ -551,12 +564,27 @@ struct DmaStream {
   long kstep;    // elements per unit of k
   int ins0;
   unsigned unit;  // bit j: chunk j is the virtual ones column (k-major operands only)
+  // k-major row gather (RowGather on this operand): p[j] holds the column part only, the row
+  // part comes from the subjects of each K tile (two scalar loads per tile: gs >= 64)
+  const long long* subj;
+  int gs;
+  long ldr;
   // unitcol >= 0 (k-major only, a multiple of 8): the 8 columns from unitcol read {1, 0, .., 0}
   __device__ __forceinline__ void init(const bf16* __restrict__ base, long ld, int row0, int nrows,
-                                       int wid, int lane, int unitcol = -1) {
+                                       int wid, int lane, int unitcol = -1,
+                                       const bf16* ggx = nullptr,
+                                       const long long* gsubj = nullptr, int ggs = 1) {
     ins0 = wid * PW;
     kstep = KCONTIG ? 1 : ld;
     unit = 0;
+    subj = nullptr;
+    gs = 1;
+    ldr = ld;
+    if (ggx) {  // gathered rows (RowGather): read the dataset, not the operand pointer
+      base = ggx;
+      subj = gsubj;
+      gs = ggs;
+    }
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
       const int ins = ins0 + j;
@@ -565,7 +593,12 @@ struct DmaStream {
         const int ch = (lane & 7) ^ sw_kc(r);
         const int gr = row0 + r;
         kofs[j] = 8 * ch;
-        p[j] = gr < nrows ? base + (long)gr * ld + 8 * ch : nullptr;
+        long row = gr;
+        if (subj && gr < nrows) {  // operand row gr -> dataset row (once per workgroup)
+          const int b = gr / gs;
+          row = subj[b] * gs + (gr - b * gs);
+        }
+        p[j] = gr < nrows ? base + row * ld + 8 * ch : nullptr;
       } else {
         constexpr int CPR = ROWS / 8;
         constexpr int RPI = 64 / CPR;
@@ -575,7 +608,7 @@ struct DmaStream {
         const int ch = (lane % CPR) ^ (ROWS >= 128 ? sw_km256(kr) : sw_km128(kr));
         const int gc = row0 + 8 * ch;
         kofs[j] = kr;
-        p[j] = gc < nrows ? base + (long)kr * ld + gc : nullptr;
+        p[j] = gc < nrows ? base + (subj ? 0L : (long)kr * ld) + gc : nullptr;
         if (gc == unitcol) {
           unit |= 1u << j;
           p[j] = reinterpret_cast<const bf16*>(g_gemm_unit);
@@ -584,6 +617,22 @@ struct DmaStream {
     }
   }
   __device__ __forceinline__ void issue(int k0, int K, char* img) const {
+    if (!KCONTIG && subj) {  // k rows k0 .. k0 + 63 span at most two subjects (gs >= 64)
+      typedef const __attribute__((address_space(4))) long long csubj;
+      const int b0 = __builtin_amdgcn_readfirstlane(k0 / gs);
+      const long long s0 = ((csubj*)subj)[b0], s1 = ((csubj*)subj)[b0 + 1];
+      const int kb = (b0 + 1) * gs;
+#pragma unroll
+      for (int j = 0; j < PW; ++j) {
+        const int k = k0 + kofs[j];
+        const bool ok = p[j] != nullptr && k < K;
+        const long row = k < kb ? s0 * gs + (k - b0 * gs) : s1 * gs + (k - kb);
+        const bf16* src = !ok ? reinterpret_cast<const bf16*>(g_gemm_zero)
+                          : ((unit >> j) & 1u) ? p[j] : p[j] + row * ldr;
+        __builtin_amdgcn_global_load_lds(src, (lds_void*)(img + (ins0 + j) * 1024), 16, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
       const bool ok = p[j] != nullptr && k0 + kofs[j] < K;
@@ -668,8 +717,9 @@ gemm_dma_kernel(GemmGroup g) {
 
   DmaStream<BM, !TA> sa;
   DmaStream<BN, TB> sb;
-  sa.init(A, P.lda, row0, M, wid, lane);
-  sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol);
+  sa.init(A, P.lda, row0, M, wid, lane, -1, P.rg.op == 1 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
+  sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol,
+          P.rg.op == 2 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
   // S-stage ring, tiles prefetched D = S - 1 ahead: at the top of iteration t this wave waits
   // until only the glds of tiles t+1 .. t+D-1 are outstanding (counted vmcnt, never 0 in the
   // steady state), one raw barrier makes every wave's share of tile t visible and retires the
@@ -865,8 +915,9 @@ gemm256_kernel(GemmGroup g) {
 
   DmaStream<BM, !TA, NW> sa;
   DmaStream<BN, TB, NW> sb;
-  sa.init(A, P.lda, row0, M, wid, lane);
-  sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol);
+  sa.init(A, P.lda, row0, M, wid, lane, -1, P.rg.op == 1 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
+  sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol,
+          P.rg.op == 2 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
   if (nk > 0) {
     sa.issue(kbeg, kend, smem);
     sb.issue(kbeg, kend, smem + IA::BYTES);
@@ -1221,6 +1272,15 @@ static int run_group(GemmGroup& g, int a_bf16, int b_bf16, int ta, int tb, int t
   }
   // the virtual ones column exists only in the LDS-DMA kernel's k-major B stream
   if (xcol && (!g.vec || !g_gemm_dma || !a_bf16 || !b_bf16 || tb)) return DN_UNSUPPORTED;
+  // gathered rows: the LDS-DMA kernels' streams only (A rows of a k-contiguous A, k rows of a
+  // k-major B), whole 16-B chunks of an aligned dataset, at most two subjects per K tile
+  for (int i = 0; i < g.n; ++i) {
+    const RowGather& r = g.p[i].rg;
+    if (!r.op) continue;
+    if (!g.vec || !g_gemm_dma || !a_bf16 || !b_bf16 || !r.gx || !r.subj || r.gs < 64 ||
+        !aligned16(r.gx) || (r.op == 1 && ta) || (r.op == 2 && tb) || r.op > 2)
+      return DN_BAD_SHAPE;
+  }
   if (tile == 2 && g.vec && g_gemm_dma && a_bf16 && b_bf16) {
     // the staged epilogue's contract: 16-B rows into C (vepi), or fp32 slabs of N % 4 == 0
     bool ok = g.splits > 1 || g.vepi;
@@ -1284,7 +1344,7 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
                    long ldb, void* C, int c_bf16, long ldc, int M, int N, int K, float alpha,
                    float beta, const float* bias, int relu, const int* row_map, int tile,
                    int splits, float* slab, const void* mask, long ldm, int* counters,
-                   hipStream_t st) {
+                   const void* gx, const long long* subj, int gs, int gop, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
@@ -1301,6 +1361,7 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   P.slab = g.splits > 1 ? slab : nullptr;
   P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0, (const bf16*)mask, ldm, nullptr, -1,
               nullptr, nullptr};
+  P.rg = RowGather{(const bf16*)gx, subj, gs, gx ? gop : 0};
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }
 
@@ -1315,7 +1376,8 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
                            const int* ncol, void* const* C2, const int* xcol,
                            void* const* X1, void* const* X2, const int* perm, int relu,
                            int a_bf16, int b_bf16, int ta, int tb, int c_bf16, int tile,
-                           int splits, float* slab, int* counters, hipStream_t st) {
+                           int splits, float* slab, int* counters, void* const* GX,
+                           void* const* SUBJ, const int* GS, const int* GOP, hipStream_t st) {
   if (n < 1 || n > GMAX) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
@@ -1338,6 +1400,9 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
     P.epi = Epi{(const float*)bias[i], (const int*)row_map[i], alpha[i], beta[i], relu, c_bf16,
                 ncol ? ncol[i] : 0, nullptr, 0, C2 ? C2[i] : nullptr,
                 xcol ? xcol[i] : -1, X1 ? (float*)X1[i] : nullptr, X2 ? (float*)X2[i] : nullptr};
+    P.rg = RowGather{};
+    if (GX && GX[i])
+      P.rg = RowGather{(const bf16*)GX[i], (const long long*)SUBJ[i], GS[i], GOP[i]};
     if (P.epi.C2 && !P.epi.ncol) return DN_BAD_SHAPE;  // second outputs: column sums only
     if (P.epi.xcol >= 0 && (N[i] != P.epi.xcol + 4 || P.epi.xcol % 8 || !P.epi.X1 || c_bf16 ||
                             P.epi.ncol > 0 || bias[i]))

@@ -275,7 +275,8 @@ DN_API int dn_adam_pack(float* p, float* g, float* m, float* v, long n, float lr
                         int update, int zero_grad, const void* segs, int cnt, int I, int Hd,
                         int HD, const void* gx, int gx_bf16, long row_elems, const long long* gy,
                         const long long* order, long nb, const long long* cursor, int B,
-                        void* xb, long long* yd, int gofs, const void* record, hipStream_t st) {
+                        void* xb, long long* yd, long long* sd, int gofs, const void* record,
+                        hipStream_t st) {
   if (n <= 0 || n % 4 || cnt < 0 || cnt > PACK_SEGS) return DN_BAD_SHAPE;
   StepRecord rec{};
   if (record && update) {
@@ -304,7 +305,7 @@ DN_API int dn_adam_pack(float* p, float* g, float* m, float* v, long n, float lr
   StepPrologue sp{};
   if (gx) {
     const int rc = prologue_gather(sp, gx, gx_bf16, row_elems, gy, order, nb, cursor, B, xb, yd,
-                                   g, 0, nullptr);
+                                   g, 0, nullptr, sd);
     if (rc != DN_OK) return rc;
   }
   // one item per thread up to 4096 workgroups per part (the chip holds ~2048 at a time; the

@@ -21,6 +21,19 @@
 // precision.  The mean block uses the smallest of the W exponents (|mean| <= max |g_w|, so it
 // cannot overflow).  bf16 / fp32 blocks carry e = 0 (their exponent range is fp32's).
 //
+// fp16 data carry power-of-two scales 2^e PER SUB-BLOCK of SB = 2,048 elements (an 8-element
+// header ahead of every sub-block, element 0 = e): the pack launch computes each sub-block's
+// max |x| in the workgroup that packs it (one workgroup = one sub-block, 8 elements per lane) and
+// scales it so that max|g| * 2^e < 2^15, which keeps gradients that are tiny against fp16's fixed
+// range (|g| < 2^-14 would be subnormal, < 2^-24 zero) at full 11-bit precision -- with no
+// separate max launch, no atomic and no host sync (a per-site scale needed a grid-wide max
+// first: amax launch + pack, 40 us of local kernels against 16 for bf16, profiles/r4_comm_model).
+// The mean sub-block uses the smallest of its W exponents (|mean| <= max |g_w|, so it cannot
+// overflow).  bf16 / fp32 sub-blocks carry e = 0 (their exponent range is fp32's).
+//
+// Layout: a rank-block of `chunk` elements (a multiple of SB) is chunk / SB sub-blocks of
+// [HDR | SB]; the payload of W ranks is W rank-blocks back to back.
+//
 // Element type codes: 0 = bf16, 1 = fp16 (IEEE binary16), 2 = fp32.  Every kernel moves 8
 // elements (16/32 bytes) per lane; chunk is a multiple of 8 (host-checked), the fp32 gradient
 // range need not be (a scalar tail).
@@ -71,7 +84,9 @@ __device__ __forceinline__ float load1(const void* p, long i) {
   else return (float)reinterpret_cast<const typename Pay<T>::s*>(p)[i];
 }
 
-constexpr int HDR = 8;  // header elements per block (16 B at 16 bits)
+constexpr int HDR = 8;     // header elements per sub-block (16 B at 16 bits)
+constexpr int SB = 2048;   // elements per scaled sub-block: 256 lanes x 8
+constexpr int SBS = HDR + SB;
 
 // block exponent of a range with max |x| = amax: max |x| * 2^e < 2^15
 __device__ __forceinline__ int scale_exp(float amax) {
@@ -84,26 +99,8 @@ __device__ __forceinline__ int scale_exp(float amax) {
 
 __device__ __forceinline__ float exp2i(int e) { return __builtin_ldexpf(1.f, e); }
 
-// max |x| over n -> *word (float bits of a non-negative value order like unsigned ints).  One
-// atomic per WORKGROUP (LDS across its 4 waves) from at most 64 workgroups: same-address atomics
-// serialise at the L2, and one per wave from 512 workgroups (2,048) cost ~20 us of the fp16
-// exchange (tools/comm_model.py local kernels: fp16 40 us vs bf16 16 us)
-__global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, long n, unsigned* word) {
-  __shared__ float wm[4];
-  float m = 0.f;
-  const long n4 = n >> 2;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float a = __builtin_fabsf(v[k]);
-      m = a > m || a != a ? a : m;  // a NaN wins (and disables scaling)
-    }
-  }
-  for (long i = 4 * n4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float a = __builtin_fabsf(x[i]);
-    m = a > m || a != a ? a : m;
-  }
+// max |v| over the workgroup (256 lanes); a NaN wins (and disables scaling)
+__device__ __forceinline__ float wg_amax(float m, float* wm) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     const float t = __shfl_xor(m, o, 64);
@@ -111,99 +108,101 @@ __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, 
   }
   if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  m = wm[0];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) m = wm[w] > m || wm[w] != wm[w] ? wm[w] : m;
-    atomicMax(word, __float_as_uint(m));
-  }
+  for (int w = 1; w < 4; ++w) m = wm[w] > m || wm[w] != wm[w] ? wm[w] : m;
+  return m;
 }
 
-// src fp32 [n] -> dst T: W blocks of [HDR | chunk] (zeros past n), scaled by scale * 2^e
+// src fp32 [n] -> dst T: nsb_total sub-blocks of [HDR | SB] (zeros past n), each scaled by
+// scale * 2^e with its own e (fp16: from the sub-block's max |x|, `scaled`)
 template <int T>
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src, void* __restrict__ dst,
-                                                   long n, int W, long chunk, float scale,
-                                                   const unsigned* __restrict__ amax) {
-  const int e = (T == PT_F16 && amax) ? scale_exp(__uint_as_float(*amax)) : 0;
-  const float sc = scale * exp2i(e);
-  const long c8 = chunk / 8, m8 = W * c8;
-  if (blockIdx.x == 0 && threadIdx.x < W) {
-    float h[8] = {(float)e, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    store8<T>(dst, threadIdx.x * (c8 + 1), h);
-  }
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < m8; i += (long)gridDim.x * 256) {
+                                                   long n, long nsb, float scale, int scaled) {
+  __shared__ float wm[4];
+  for (long g = blockIdx.x; g < nsb; g += gridDim.x) {
+    const long e0 = g * SB + 8 * threadIdx.x;
     float o[8];
-    if (8 * i + 8 <= n) {
-      load8<PT_F32>(src, i, o);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] *= sc;
+    if (e0 + 8 <= n) {
+      load8<PT_F32>(src, e0 / 8, o);
     } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = 8 * i + k < n ? src[8 * i + k] * sc : 0.f;
+      for (int k = 0; k < 8; ++k) o[k] = e0 + k < n ? src[e0 + k] : 0.f;
     }
-    const long b = i / c8;
-    store8<T>(dst, i + b + 1, o);  // past the headers of blocks 0..b
+    int e = 0;
+    if (T == PT_F16 && scaled) {
+      float m = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float a = __builtin_fabsf(o[k]);
+        m = a > m || a != a ? a : m;
+      }
+      e = scale_exp(wg_amax(m, wm));
+    }
+    const float sc = scale * exp2i(e);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] *= sc;
+    const long base8 = g * (SBS / 8);
+    store8<T>(dst, base8 + 1 + threadIdx.x, o);
+    if (threadIdx.x == 0) {
+      float h[8] = {(float)e, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      store8<T>(dst, base8, h);
+    }
+    if (T == PT_F16 && scaled) __syncthreads();  // wm is reused by the next sub-block
   }
 }
 
-// src T: W blocks of [HDR | chunk] -> dst fp32 [n], each block unscaled by its 2^-e, * scale;
-// resets the amax word for the next exchange
+// src T: sub-blocks of [HDR | SB] -> dst fp32 [n], each unscaled by its 2^-e, * scale
 template <int T>
 __global__ void __launch_bounds__(256) unpack_kernel(const void* __restrict__ src, float* __restrict__ dst,
-                                                     long n, long chunk, float scale, unsigned* amax) {
-  const long n8 = (n + 7) / 8, c8 = chunk / 8;
-  if (amax && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
-    const long b = i / c8;
-    float h[8];
-    load8<T>(src, b * (c8 + 1), h);
-    const float sc = scale * exp2i(-(int)h[0]);
-    if (8 * i + 8 <= n) {
-      float o[8];
-      load8<T>(src, i + b + 1, o);
+                                                     long n, long nsb, float scale) {
+  for (long g = blockIdx.x; g < nsb; g += gridDim.x) {
+    const long base8 = g * (SBS / 8);
+    const float e = load1<T>(src, g * SBS);
+    const float sc = scale * exp2i(-(int)e);
+    const long e0 = g * SB + 8 * threadIdx.x;
+    if (e0 >= n) continue;
+    float o[8];
+    load8<T>(src, base8 + 1 + threadIdx.x, o);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] *= sc;
-      store8<PT_F32>(dst, i, o);
+    for (int k = 0; k < 8; ++k) o[k] *= sc;
+    if (e0 + 8 <= n) {
+      store8<PT_F32>(dst, e0 / 8, o);
     } else {
-      for (long k = 8 * i; k < n; ++k) dst[k] = load1<T>(src, (b + 1) * HDR + k) * sc;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (e0 + k < n) dst[e0 + k] = o[k];
     }
   }
 }
 
-// src T: W blocks of [HDR | chunk] -> dst T one block = scale * sum_w unscaled src[w] (fp32
-// accumulation in rank order), rescaled by the smallest block exponent
+// src T: W rank-blocks of nsb sub-blocks -> dst T one rank-block: sub-block s = scale * sum_w
+// unscaled src[w][s] (fp32 accumulation in rank order), rescaled by the smallest exponent
 template <int T>
 __global__ void __launch_bounds__(256) rowsum_kernel(const void* __restrict__ src, void* __restrict__ dst,
-                                                     int W, long c8, float scale) {
-  int emin = 1 << 20;
-  for (int w = 0; w < W; ++w) {
-    float h[8];
-    load8<T>(src, w * (c8 + 1), h);
-    emin = min(emin, (int)h[0]);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float h[8] = {(float)emin, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    store8<T>(dst, 0, h);
-  }
-  const float out_sc = scale * exp2i(emin);
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < c8; i += (long)gridDim.x * 256) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v[8], h[8];
+                                                     int W, long nsb, float scale) {
+  for (long s = blockIdx.x; s < nsb; s += gridDim.x) {
+    int emin = 1 << 20;
+    for (int w = 0; w < W; ++w) emin = min(emin, (int)load1<T>(src, (w * nsb + s) * SBS));
+    const float out_sc = scale * exp2i(emin);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v[8];
     for (int w = 0; w < W; ++w) {
-      load8<T>(src, w * (c8 + 1), h);
-      const float un = exp2i(-(int)h[0]);
-      load8<T>(src, w * (c8 + 1) + 1 + i, v);
+      const long base8 = (w * nsb + s) * (SBS / 8);
+      const float un = exp2i(-(int)load1<T>(src, (w * nsb + s) * SBS));
+      load8<T>(src, base8 + 1 + threadIdx.x, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += v[k] * un;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] *= out_sc;
-    store8<T>(dst, 1 + i, acc);
+    store8<T>(dst, s * (SBS / 8) + 1 + threadIdx.x, acc);
+    if (threadIdx.x == 0) {
+      float h[8] = {(float)emin, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      store8<T>(dst, s * (SBS / 8), h);
+    }
   }
 }
 
-int grid8(long n8) {
-  const long b = (n8 + 255) / 256;
-  return (int)(b < 1024 ? (b > 0 ? b : 1) : 1024);
-}
 
 bool aligned(const void* a, const void* b) { return (((uintptr_t)a | (uintptr_t)b) & 15) == 0; }
 
@@ -217,36 +216,39 @@ bool aligned(const void* a, const void* b) { return (((uintptr_t)a | (uintptr_t)
     default: return DN_BAD_SHAPE;                                                                  \
   }
 
-DN_API int dn_payload_amax(const float* x, long n, unsigned* word, hipStream_t st) {
-  if (n <= 0) return DN_OK;
-  if (((uintptr_t)x) & 15) return DN_BAD_SHAPE;
-  const long b = (n + 1023) / 1024;
-  hipLaunchKernelGGL(amax_kernel, dim3((int)(b < 64 ? b : 64)), dim3(256), 0, st, x, n, word);
-  return dn_launch_status();
-}
+static int grid_sb(long nsb) { return (int)(nsb < 8192 ? (nsb > 0 ? nsb : 1) : 8192); }
 
+// fp32 src [n] -> world * chunk elements of payload (chunk % SB == 0, world * chunk >= n)
 DN_API int dn_payload_pack(const float* src, void* dst, long n, int world, long chunk, float scale,
-                           const unsigned* amax, int type, hipStream_t st) {
-  if (n < 0 || world < 1 || chunk <= 0 || chunk % 8 || world * chunk < n || world > 256 || !aligned(src, dst))
+                           int scaled, int type, hipStream_t st) {
+  if (n < 0 || world < 1 || chunk <= 0 || chunk % SB || world * chunk < n || !aligned(src, dst))
     return DN_BAD_SHAPE;
-  DN_PAYLOAD_DISPATCH(type, pack_kernel, dim3(grid8(world * chunk / 8)), dim3(256), 0, st, src, dst, n,
-                      world, chunk, scale, amax);
+  const long nsb = world * chunk / SB;
+  DN_PAYLOAD_DISPATCH(type, pack_kernel, dim3(grid_sb(nsb)), dim3(256), 0, st, src, dst, n, nsb,
+                      scale, scaled);
   return dn_launch_status();
 }
 
-DN_API int dn_payload_unpack(const void* src, float* dst, long n, long chunk, float scale, unsigned* amax,
-                             int type, hipStream_t st) {
-  if (n < 0 || chunk <= 0 || chunk % 8 || !aligned(src, dst)) return DN_BAD_SHAPE;
+// the first n elements of a payload of sub-blocks -> fp32 dst
+DN_API int dn_payload_unpack(const void* src, float* dst, long n, float scale, int type,
+                             hipStream_t st) {
+  if (n < 0 || !aligned(src, dst)) return DN_BAD_SHAPE;
   if (n == 0) return DN_OK;
-  DN_PAYLOAD_DISPATCH(type, unpack_kernel, dim3(grid8((n + 7) / 8)), dim3(256), 0, st, src, dst, n, chunk,
-                      scale, amax);
+  const long nsb = (n + SB - 1) / SB;
+  DN_PAYLOAD_DISPATCH(type, unpack_kernel, dim3(grid_sb(nsb)), dim3(256), 0, st, src, dst, n, nsb,
+                      scale);
   return dn_launch_status();
 }
 
+// W rank-blocks of `chunk` elements -> their scaled fp32 sum as one rank-block
 DN_API int dn_payload_rowsum(const void* src, void* dst, int world, long chunk, float scale, int type,
                              hipStream_t st) {
-  if (world < 1 || chunk <= 0 || chunk % 8 || !aligned(src, dst)) return DN_BAD_SHAPE;
-  DN_PAYLOAD_DISPATCH(type, rowsum_kernel, dim3(grid8(chunk / 8)), dim3(256), 0, st, src, dst, world,
-                      chunk / 8, scale);
+  if (world < 1 || chunk <= 0 || chunk % SB || !aligned(src, dst)) return DN_BAD_SHAPE;
+  DN_PAYLOAD_DISPATCH(type, rowsum_kernel, dim3(grid_sb(chunk / SB)), dim3(256), 0, st, src, dst,
+                      world, chunk / SB, scale);
   return dn_launch_status();
 }
+
+// payload elements of `elems` data elements (sub-block headers included; 0 stays 0)
+DN_API long dn_payload_numel(long elems) { return (elems + SB - 1) / SB * SBS; }
+DN_API long dn_payload_subblock() { return SB; }

@@ -11,7 +11,9 @@
 //       order[c * B + b] (or c * B + b without an order) where c = *cursor mod nb.  Nothing in
 //       the step reads the host, so K steps can be captured in one HIP graph.  The cursor is
 //       advanced by the step's Adam launch (optim.hip), never here: every workgroup of this
-//       launch reads it.
+//       launch reads it.  With `sd` the step's dataset row (subject) indices go there too, and
+//       xb may be null: the GEMMs then read the batch rows from the dataset through them
+//       (gemm.hip GemmProb::gx, the Adam-emitted pack at large batch: no batch copy).
 #pragma once
 #include "common.h"
 
@@ -29,6 +31,7 @@ struct StepPrologue {
   const long long* cursor;
   long nb;          // batches per pass over `order` (the cursor wraps)
   int f8, B, gx_bf16;
+  long long* sd;    // optional [B]: the batch's dataset rows (device-fed only)
 };
 
 // the dataset row of sample b at cursor batch c
@@ -70,7 +73,9 @@ __device__ __forceinline__ void prologue_item(const StepPrologue& sp, long i, lo
     reinterpret_cast<f32x4*>(sp.g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else {
     i -= sp.ug;
-    sp.yd[i] = sp.gx ? sp.gy[prologue_row(sp, c, (int)i)] : sp.y[i];
+    const long r = sp.gx ? prologue_row(sp, c, (int)i) : 0;
+    sp.yd[i] = sp.gx ? sp.gy[r] : sp.y[i];
+    if (sp.sd) sp.sd[i] = r;
   }
 }
 
@@ -82,8 +87,9 @@ __device__ __forceinline__ long prologue_cursor(const StepPrologue& sp) {
 static inline int prologue_gather(StepPrologue& sp, const void* gx, int gx_bf16, long row_elems,
                                   const long long* gy, const long long* order, long nb,
                                   const long long* cursor, int B, void* xb, long long* yd, float* g,
-                                  long ng, int* bump) {
-  if (!gx || !gy || !cursor || !xb || !yd || B <= 0 || nb <= 0 || row_elems <= 0) return DN_BAD_SHAPE;
+                                  long ng, int* bump, long long* sd = nullptr) {
+  if (!gx || !gy || !cursor || !(xb || sd) || !yd || B <= 0 || nb <= 0 || row_elems <= 0)
+    return DN_BAD_SHAPE;
   if (row_elems % 8 || ng % 4) return DN_BAD_SHAPE;
   if (((uintptr_t)gx | (uintptr_t)xb | (uintptr_t)g) & 15) return DN_BAD_SHAPE;
   if ((long)B * (row_elems / 8) >= (1L << 31)) return DN_BAD_SHAPE;
@@ -91,7 +97,8 @@ static inline int prologue_gather(StepPrologue& sp, const void* gx, int gx_bf16,
   sp.xb = (bf16*)xb;
   sp.yd = yd;
   sp.g = g;
-  sp.ux = (long)B * (row_elems / 8);
+  sp.ux = xb ? (long)B * (row_elems / 8) : 0;  // no xb: the rows only (sd)
+  sp.sd = sd;
   sp.ug = ng / 4;
   sp.ny = B;
   sp.bump = bump;

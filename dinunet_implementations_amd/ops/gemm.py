@@ -23,14 +23,60 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_float,
                           _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
                           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p,
-                          _lib.c_void_p])
+                          _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p])
 
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
 _lib.register("dn_gemm_dma_on", [])
 _lib.register("dn_gemm_arm_bump", [_lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_gemm_bump_armed", [])
 _lib.register("dn_gemm_grouped", [_lib.c_int] + [_lib.c_void_p] * 19 + [_lib.c_int] * 8
-              + [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p])
+              + [_lib.c_void_p, _lib.c_void_p] + [_lib.c_void_p] * 4 + [_lib.c_void_p])
+
+# Operands read in place from a dataset resident in HBM (csrc/kernels/gemm.hip RowGather): a
+# registered tensor (the device-fed step's static batch buffer, 2-D [B*S, F]) stands for rows
+# X[subj[r // S] * S + r % S] of the dataset X [N*S, F] -- the GEMMs that consume the batch read
+# it through the step's subject indices, so the step needs no batch copy.
+_ROWS = {}
+
+
+class rows_from:
+    """``with rows_from(buf2d, X2d, subj, S):`` GEMMs that take ``buf2d`` as a k-contiguous A or a
+    k-major B read dataset rows instead (the LDS-DMA kernels; ``S >= 64``)."""
+
+    def __init__(self, buf2d: Tensor, X2d: Tensor, subj: Tensor, S: int):
+        self.key = (buf2d.data_ptr(), tuple(buf2d.shape))
+        self.val = (X2d, subj, int(S))
+
+    def __enter__(self):
+        _ROWS[self.key] = self.val
+        return self
+
+    def __exit__(self, *a):
+        _ROWS.pop(self.key, None)
+        return False
+
+
+def _gather_of(t: Tensor):
+    """(X, subj, S) when ``t`` (an operand as passed: rows = its first axis, row-contiguous) is
+    a registered batch buffer, else None."""
+    if not _ROWS or t.dim() != 2 or t.dtype != torch.bfloat16 or not t.is_contiguous():
+        return None
+    return _ROWS.get((t.data_ptr(), tuple(t.shape)))
+
+
+def _gather_args(a: Tensor, b: Tensor, trans_a: bool, trans_b: bool):
+    """(gx, subj, S, op) for the kernel: A's rows when ``a`` is a registered buffer used
+    untransposed (k-contiguous A), B's k rows when ``b`` is one used untransposed (k-major B)."""
+    ga, gb = _gather_of(a), _gather_of(b)
+    if (ga is not None and trans_a) or (gb is not None and trans_b) or (
+            ga is not None and gb is not None):
+        raise ValueError("rows_from: a gathered batch buffer is read as a k-contiguous A or a "
+                         "k-major B only (one per GEMM)")
+    if ga is not None:
+        return ga[0].data_ptr(), ga[1].data_ptr(), ga[2], 1
+    if gb is not None:
+        return gb[0].data_ptr(), gb[1].data_ptr(), gb[2], 2
+    return None, None, 0, 0
 
 # DINUNET_SPLITK_INLAUNCH=1: split-K partials are combined inside the GEMM launch by each
 # tile's last-arriving workgroup (csrc/kernels/gemm.hip splitk_epilogue) instead of by the
@@ -187,7 +233,7 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
               int(out.dtype == torch.bfloat16), out.stride(0), M, N, K, float(alpha), float(beta),
               _lib.ptr(bias), int(relu), _lib.ptr(row_map), tile, sp, _lib.ptr(slab),
               _lib.ptr(mask), mask.stride(0) if mask is not None else 0, _lib.ptr(cnt),
-              _lib.stream())
+              *_gather_args(a, b, trans_a, trans_b), _lib.stream())
     return out
 
 
@@ -375,7 +421,8 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
         return
     n = len(probs)
     arrs = {k: [] for k in ("A", "lda", "B", "ldb", "C", "ldc", "M", "N", "K", "alpha", "beta",
-                            "bias", "rmap", "ncol", "C2", "xcol", "X1", "X2")}
+                            "bias", "rmap", "ncol", "C2", "xcol", "X1", "X2", "GX", "SUBJ", "GS",
+                            "GOP")}
     keep = []
     ta = tb = None
     a_bf = b_bf = c_bf = None
@@ -420,6 +467,9 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
                      ("xcol", xcol), ("X1", _lib.ptr(xs[0]) if xs else None),
                      ("X2", _lib.ptr(xs[1]) if xs else None)):
             arrs[k].append(v)
+        for k, v in zip(("GX", "SUBJ", "GS", "GOP"),
+                        _gather_args(q["a"], q["b"], trans_a, trans_b)):
+            arrs[k].append(v)
         maxk = max(maxk, K)
         t64 += ((M + 63) // 64) * ((N + 63) // 64)
         t128 += ((M + 127) // 128) * ((N + 127) // 128)
@@ -454,7 +504,8 @@ def mm_grouped(problems, trans_a: bool = False, trans_b: bool = False,
               (P * n)(*arrs["X2"]), _lib.ptr(perm), 0,
               int(a_bf), int(b_bf), ta, tb,
               int(c_bf), 0 if tile is None else int(tile), sp, _lib.ptr(slab), _lib.ptr(cnt),
-              _lib.stream())
+              (P * n)(*arrs["GX"]), (P * n)(*arrs["SUBJ"]), (I * n)(*arrs["GS"]),
+              (I * n)(*arrs["GOP"]), _lib.stream())
 
 
 # Plain GEMMs (bf16 operands, no row map) run on csrc/kernels/gemm.hip's LDS-DMA kernel, which

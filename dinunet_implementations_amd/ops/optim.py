@@ -46,7 +46,7 @@ _lib.register("dn_adam_pack", [_lib.c_void_p] * 4 + [_lib.c_long, _lib.c_float, 
                                _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int,
                                _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
                                _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
-                               _lib.c_int, _lib.c_void_p, _lib.c_void_p])
+                               _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_step_record", [_lib.c_void_p, _lib.c_int, _lib.c_void_p])
 
 
@@ -167,9 +167,12 @@ class FusedAdam:
 
     # Adam that also emits the next step's operands (optim.hip adam_pack_kernel) ------------------
     def attach_pack(self, pack, src=None, xb: Optional[torch.Tensor] = None,
-                    yd: Optional[torch.Tensor] = None):
+                    yd: Optional[torch.Tensor] = None, sd: Optional[torch.Tensor] = None,
+                    copy_x: bool = True):
         """Keep ``pack`` (``ops.lstm.PersistentPack``) current from every :meth:`step_pack`, and
-        gather the next batch of ``src`` (``DeviceSource``) into ``xb`` / ``yd`` there too."""
+        gather the next batch of ``src`` (``DeviceSource``) into ``xb`` / ``yd`` there too.
+        ``sd`` (int64 [B + 1]): the next batch's dataset rows go there as well; ``copy_x=False``
+        then skips the batch copy (the GEMMs read the rows in place: ``ops.gemm.rows_from``)."""
         import ctypes
         rows = pack.rows(self.flat)
 
@@ -183,7 +186,9 @@ class FusedAdam:
         tab = (_Seg * max(1, len(rows)))()
         for i, (off, n, kind, d, dst, dst2) in enumerate(rows):
             tab[i] = _Seg(off, n, kind, d, dst, dst2 or None)
-        self._pack = (pack, tab, len(rows), src, xb, yd)
+        if not copy_x and sd is None:
+            raise ValueError("attach_pack: without the batch copy the step needs its row indices")
+        self._pack = (pack, tab, len(rows), src, xb, yd, sd, copy_x)
 
     def step_pack(self, grad_scale: float = 1.0, update: bool = True, gofs: int = 1,
                   record=None):
@@ -193,7 +198,7 @@ class FusedAdam:
         ``cursor + gofs`` gathered.  ``update=False``: images + gather + zeroing only (priming).
         ``record``: a :meth:`StepRecorder.args` struct -- the step's score column and loss go to
         the recorder's rings at the cursor (one more workgroup of the same launch)."""
-        pack, tab, cnt, src, xb, yd = self._pack
+        pack, tab, cnt, src, xb, yd, sd, copy_x = self._pack
         d = self.flat.data
         if self._tdev is None:
             self.sync_device_step()
@@ -201,9 +206,9 @@ class FusedAdam:
         if src is not None:
             gx = [src.X.data_ptr(), src._mode(xb), src.row,
                   src.Y.data_ptr(), _lib.ptr(src.order), src.nb, src.cursor.data_ptr(), src.B,
-                  xb.data_ptr(), yd.data_ptr()]
+                  xb.data_ptr() if copy_x else None, yd.data_ptr(), _lib.ptr(sd)]
         else:
-            gx = [None, 0, 0, None, None, 1, None, 0, None, None]
+            gx = [None, 0, 0, None, None, 1, None, 0, None, None, None]
         _lib.call("dn_adam_pack", d.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
                   self.exp_avg_sq.data_ptr(), d.numel(), self.lr, b1, b2, self.eps,
                   self.weight_decay, grad_scale, self._tdev.data_ptr(), int(update), 1,

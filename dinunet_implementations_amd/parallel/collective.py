@@ -33,15 +33,15 @@ Tensor = torch.Tensor
 
 PAYLOAD_TYPES = {"bf16": (0, torch.bfloat16), "fp16": (1, torch.float16), "fp32": (2, torch.float32)}
 
-_lib.register("dn_payload_amax", [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_payload_pack", [_lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_long,
-                                  _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p])
-_lib.register("dn_payload_unpack", [_lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_float,
-                                    _lib.c_void_p, _lib.c_int, _lib.c_void_p])
+                                  _lib.c_float, _lib.c_int, _lib.c_int, _lib.c_void_p])
+_lib.register("dn_payload_unpack", [_lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_float,
+                                    _lib.c_int, _lib.c_void_p])
 _lib.register("dn_payload_rowsum", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_float,
                                     _lib.c_int, _lib.c_void_p])
 
-HDR = 8  # header elements per block: [e, 0 x 7], the block holds payload(x * 2^e)
+HDR = 8    # header elements per sub-block: [e, 0 x 7], the sub-block holds payload(x * 2^e)
+SB = 2048  # data elements per sub-block (payload.hip): fp16 scales are per sub-block
 
 
 def payload_name(cfg: Optional[dict]) -> str:
@@ -69,64 +69,85 @@ def _scale_exp(amax: float) -> int:
     return max(-100, min(100, e))
 
 
+def payload_numel(elems: int) -> int:
+    """Payload elements holding ``elems`` data elements: whole sub-blocks of [HDR | SB]."""
+    return -(-int(elems) // SB) * (HDR + SB)
+
+
 def blocks_numel(world: int, chunk: int) -> int:
-    return world * (HDR + chunk)
+    """``world`` rank-blocks of ``chunk`` data elements (a multiple of SB) each."""
+    return world * payload_numel(chunk)
+
+
+def chunk_for(n: int, world: int) -> int:
+    """Per-rank data elements of a ``world``-way exchange of ``n``: whole sub-blocks."""
+    return max(SB, -(-int(n) // (SB * world)) * SB)
 
 
 def to_payload(src: Tensor, dst: Tensor, world: int, chunk: int, scale: float = 1.0,
-               amax: Optional[Tensor] = None):
-    """fp32 ``src`` -> ``dst``: ``world`` blocks of [header | chunk] in the payload dtype, zero
-    past ``src``; fp16 blocks scaled by 2^e from ``amax`` (a uint32 word the caller zeroed;
-    :func:`from_payload` zeroes it again)."""
+               scaled: Optional[bool] = None):
+    """fp32 ``src`` -> ``dst``: ``world`` rank-blocks of ``chunk`` elements (a multiple of SB) as
+    sub-blocks of [header | SB] in the payload dtype, zero past ``src``.  fp16 sub-blocks are
+    scaled by 2^e from their own max |x| (``scaled``, default: fp16), computed inside the pack
+    launch (payload.hip)."""
     n = src.numel()
     fp16 = dst.dtype == torch.float16
+    scaled = fp16 if scaled is None else bool(scaled and fp16)
+    if chunk % SB or world * chunk < n or dst.numel() < blocks_numel(world, chunk):
+        raise ValueError(f"to_payload: {n} elements into {world} x {chunk} (sub-blocks of {SB}) "
+                         f"in {dst.numel()}")
     if dst.is_cuda:
-        if fp16 and amax is not None:
-            _lib.call("dn_payload_amax", src.data_ptr(), n, amax.data_ptr(), _lib.stream())
         _lib.call("dn_payload_pack", src.data_ptr(), dst.data_ptr(), n, world, chunk, scale,
-                  amax.data_ptr() if (fp16 and amax is not None) else None, _code(dst.dtype),
-                  _lib.stream())
+                  int(scaled), _code(dst.dtype), _lib.stream())
         return
-    e = _scale_exp(float(src.abs().max())) if (fp16 and amax is not None and n
-                                               and not torch.isnan(src).any()) else 0
-    body = torch.zeros(world * chunk, dtype=torch.float32)
-    body[:n] = src.reshape(-1).float() * (scale * 2.0 ** e)
-    v = dst.view(world, HDR + chunk)
+    nsb = world * chunk // SB
+    body = torch.zeros(nsb * SB, dtype=torch.float32)
+    body[:n] = src.reshape(-1).float()
+    b = body.view(nsb, SB)
+    if scaled:
+        e = torch.tensor([_scale_exp(float(a)) for a in b.abs().max(1).values], dtype=torch.float32)
+    else:
+        e = torch.zeros(nsb)
+    v = dst[:nsb * (HDR + SB)].view(nsb, HDR + SB)
     v[:, :HDR] = 0
-    v[:, 0] = e
-    v[:, HDR:] = body.view(world, chunk).to(dst.dtype)
+    v[:, 0] = e.to(dst.dtype)
+    v[:, HDR:] = (b * (scale * torch.pow(2.0, e))[:, None]).to(dst.dtype)
 
 
-def from_payload(src: Tensor, dst: Tensor, world: int, chunk: int, scale: float = 1.0,
-                 amax: Optional[Tensor] = None):
-    """``world`` payload blocks -> fp32 ``dst`` (each block unscaled by its 2^-e)."""
+def from_payload(src: Tensor, dst: Tensor, world: Optional[int] = None,
+                 chunk: Optional[int] = None, scale: float = 1.0):
+    """The first ``dst.numel()`` data elements of a payload (sub-blocks back to back: one
+    rank-block or several whole ones) -> fp32 ``dst``, each sub-block unscaled by its 2^-e."""
     n = dst.numel()
     if dst.is_cuda:
-        _lib.call("dn_payload_unpack", src.data_ptr(), dst.data_ptr(), n, chunk, scale,
-                  amax.data_ptr() if amax is not None else None, _code(src.dtype), _lib.stream())
+        _lib.call("dn_payload_unpack", src.data_ptr(), dst.data_ptr(), n, scale, _code(src.dtype),
+                  _lib.stream())
         return
-    v = src.view(world, HDR + chunk)
+    nsb = -(-n // SB)
+    v = src[:nsb * (HDR + SB)].view(nsb, HDR + SB)
     un = torch.pow(2.0, -v[:, :1].float())
     body = (v[:, HDR:].float() * un).reshape(-1)[:n]
     dst.reshape(-1).copy_(body * scale if scale != 1.0 else body)
 
 
 def rowsum(src: Tensor, dst: Tensor, world: int, chunk: int, scale: float):
-    """``dst`` (one block) = payload(scale * sum_w unscaled fp32(src[w])) -- fp32 accumulation in
-    rank order, rescaled by the smallest block exponent."""
+    """``dst`` (one rank-block) = payload(scale * sum_w unscaled fp32(src[w])) per sub-block --
+    fp32 accumulation in rank order, rescaled by the sub-block's smallest exponent."""
     if dst.is_cuda:
         _lib.call("dn_payload_rowsum", src.data_ptr(), dst.data_ptr(), world, chunk, scale,
                   _code(dst.dtype), _lib.stream())
         return
-    v = src.view(world, HDR + chunk)
-    es = [int(v[w, 0].float()) for w in range(world)]
-    acc = torch.zeros(chunk, dtype=torch.float32)
+    nsb = chunk // SB
+    v = src[:blocks_numel(world, chunk)].view(world, nsb, HDR + SB)
+    es = v[:, :, 0].float()
+    acc = torch.zeros(nsb, SB, dtype=torch.float32)
     for w in range(world):
-        acc += v[w, HDR:].float() * (2.0 ** -es[w])
-    e = min(es)
-    dst[:HDR] = 0
-    dst[0] = e
-    dst[HDR:] = (acc * (scale * 2.0 ** e)).to(dst.dtype)
+        acc += v[w, :, HDR:].float() * torch.pow(2.0, -es[w])[:, None]
+    e = es.min(0).values
+    out = dst[:nsb * (HDR + SB)].view(nsb, HDR + SB)
+    out[:, :HDR] = 0
+    out[:, 0] = e.to(dst.dtype)
+    out[:, HDR:] = (acc * (scale * torch.pow(2.0, e))[:, None]).to(dst.dtype)
 
 
 class DirectMean:
@@ -139,14 +160,10 @@ class DirectMean:
         self.n = int(n)
         self.code, self.dtype = PAYLOAD_TYPES[payload]
         W = group.world
-        self.chunk = max(8, -(-self.n // (8 * W)) * 8)   # per-rank slice, 16-byte multiple
+        self.chunk = chunk_for(self.n, W)   # per-rank slice: whole sub-blocks
         self.send = torch.zeros(blocks_numel(W, self.chunk), dtype=self.dtype, device=device)
         self.recv = torch.zeros_like(self.send)
-        self.mine = torch.zeros(HDR + self.chunk, dtype=self.dtype, device=device)
-        # fp16: per-site power-of-two block scale from max|g| (payload.hip); the word is zeroed
-        # again by every unpack
-        self.amax = (torch.zeros(1, dtype=torch.int32, device=device)
-                     if self.dtype == torch.float16 else None)
+        self.mine = torch.zeros(payload_numel(self.chunk), dtype=self.dtype, device=device)
 
     def _a2a(self):
         g = self.group
@@ -161,11 +178,11 @@ class DirectMean:
         """``x`` (fp32, ``n`` elements, contiguous) <- scale * mean over sites, on the current
         stream (RCCL orders its collectives after it)."""
         W, c = self.group.world, self.chunk
-        to_payload(x.reshape(-1), self.send, W, c, amax=self.amax)
+        to_payload(x.reshape(-1), self.send, W, c)
         self._a2a()
         rowsum(self.recv, self.mine, W, c, 1.0 / W)
         self.group.all_gather_into(self.send, self.mine)
-        from_payload(self.send, x.reshape(-1), W, c, scale, amax=self.amax)
+        from_payload(self.send, x.reshape(-1), W, c, scale)
         return self.n * self.send.element_size()  # this site's payload
 
 

@@ -32,8 +32,8 @@ from ..ops import _grad as _gradreg
 from ..ops import _lib
 from ..ops import capture as _cap
 from ..ops.optim import FlatParams
-from .collective import (HDR, PAYLOAD_TYPES, DirectMean, from_payload, launch_on, payload_name,
-                         to_payload)
+from .collective import (PAYLOAD_TYPES, SB, DirectMean, from_payload, launch_on, payload_name,
+                         payload_numel, to_payload)
 from .group import SiteGroup
 from .lowrank import EPS as EPS_MGS
 from .lowrank import LowRankTable, _mgs_torch_, dad_factors, orthonormalize_
@@ -341,9 +341,9 @@ class DSGDEngine(Engine):
             buf = self._half_bufs.get(b)
             if buf is None:
                 dt = PAYLOAD_TYPES[self.wire][1]  # one unscaled block: headers sum to 0
-                buf = self._half_bufs[b] = torch.zeros(HDR + -(-(e - s) // 8) * 8, dtype=dt,
+                buf = self._half_bufs[b] = torch.zeros(payload_numel(e - s), dtype=dt,
                                                        device=view.device)
-            to_payload(view, buf, 1, buf.numel() - HDR)
+            to_payload(view, buf, 1, -(-(e - s) // SB) * SB)
             self._handles[b] = self.group.all_reduce(buf, async_op=True)
             self.comm_bytes += (e - s) * buf.element_size()
         else:
@@ -374,7 +374,7 @@ class DSGDEngine(Engine):
             if self.half and not self.direct:
                 s, e = self.buckets[b]
                 buf = self._half_bufs[b]
-                from_payload(buf, self.flat.grad[s:e], 1, buf.numel() - HDR)
+                from_payload(buf, self.flat.grad[s:e])
         self._reset()
         self.last_scale = 1.0 if self.direct else 1.0 / g.world  # the direct exchange leaves the mean
         return self.last_scale
@@ -469,8 +469,10 @@ class RankDADEngine(Engine):
                            if len(self._dense_ranges) > 1 else None)
         self._dense_buf = (torch.empty(self._dense_idx.numel(), dtype=torch.float32, device=dev)
                            if self._dense_idx is not None else None)
-        # 16-byte multiple: the send slot is also the per-rank stride of the 16-bit gather
-        self._send = torch.zeros(-(-max(off, 1) // 8) * 8, dtype=torch.float32, device=dev)
+        # the send slot is also the per-rank stride of the gather: 16-byte multiple, whole payload
+        # sub-blocks when the factors travel in 16 bits
+        pad = SB if (self.half and self.group.distributed) else 8
+        self._send = torch.zeros(-(-max(off, 1) // pad) * pad, dtype=torch.float32, device=dev)
         n = len(self.fast_layers)
         if not n:
             return
@@ -479,9 +481,8 @@ class RankDADEngine(Engine):
                           if self.group.distributed else self._send)
         if self.half and self.group.distributed:
             dt = PAYLOAD_TYPES[self.wire][1]
-            self._send16 = torch.zeros(HDR + self._send.numel(), dtype=dt, device=dev)
-            self._gathered16 = torch.zeros(W * (HDR + self._send.numel()), dtype=dt, device=dev)
-            self._amax = torch.zeros(1, dtype=torch.int32, device=dev)  # fp16 block scale
+            self._send16 = torch.zeros(payload_numel(self._send.numel()), dtype=dt, device=dev)
+            self._gathered16 = torch.zeros(W * self._send16.numel(), dtype=dt, device=dev)
         layers = []
         self._praw = []
         for _, o, out_f, in_f, rr, po, qo in self.fast_layers:
@@ -560,9 +561,9 @@ class RankDADEngine(Engine):
         if g.distributed:
             if self.half:  # factors on the wire in the payload type, reconstructed in fp32
                 n = self._send.numel()
-                to_payload(self._send, self._send16, 1, n, amax=self._amax)
+                to_payload(self._send, self._send16, 1, n)
                 g.all_gather_into(self._gathered16, self._send16)
-                from_payload(self._gathered16, self._gathered, W, n, amax=self._amax)
+                from_payload(self._gathered16, self._gathered)
                 self.comm_bytes += self._send16.numel() * self._send16.element_size()
             else:
                 g.all_gather_into(self._gathered, self._send)

@@ -57,6 +57,18 @@ HEADS = {"ica": ica_forward_loss, "fs": fs_forward_loss}
 # watchdog (hipErrorStreamCaptureUnsupported -> abort).
 CAPTURE_MODE = "thread_local"
 
+
+def _quiesce_collectives(group) -> None:
+    """Before a capture on an RCCL group: let the process group's watchdog retire every finished
+    eager collective first.  It polls their (pooled) completion events every ~100 ms; a pooled
+    event re-recorded by a collective inside the capture while the watchdog still holds the old
+    work aborts the process (hipErrorCapturedEvent: seen right after eager collectives, e.g. the
+    warm-up steps or dsgd_collective=calibrate, and intermittently in the GPU tests)."""
+    if getattr(group, "distributed", False) and getattr(group, "backend", None) == "nccl":
+        import time
+        torch.cuda.synchronize()
+        time.sleep(0.3)
+
 # The LSTM weight repack leaves the graph and rides in the step prologue's launch
 # (DINUNET_DEFER_PACK=0 keeps it captured)
 DEFER_PACK = os.environ.get("DINUNET_DEFER_PACK", "1") != "0"
@@ -65,6 +77,15 @@ DEFER_PACK = os.environ.get("DINUNET_DEFER_PACK", "1") != "0"
 # (DINUNET_SPLIT_AT=stem keeps the encoder-output cut): graph B is then the input-gradient GEMM +
 # the encoder's weight gradients, ~25 us at the headline step instead of ~10
 SPLIT_AT_PROJECTION = os.environ.get("DINUNET_SPLIT_AT", "projection") != "stem"
+
+# Device-fed steps with the Adam-emitted pack read the batch IN PLACE from the HBM-resident
+# dataset at large batch: the Adam writes the next batch's subject indices instead of copying
+# the batch (B*S*C*W bf16: 400 MB at B=2048), and the two GEMMs that consume it -- the encoder
+# forward (A rows) and the encoder weight gradient (B's k rows) -- gather the rows through them
+# (ops.gemm.rows_from, gemm.hip RowGather).  DINUNET_ROWS_FEED=1 / 0 forces it on / off; auto
+# from 256 samples per step
+ROWS_FEED = os.environ.get("DINUNET_ROWS_FEED", "auto")
+ROWS_FEED_MIN_B = 256
 
 # Device-fed single-site steps: the fused Adam rewrites the packed LSTM / encoder operand images
 # from the parameters it updates, zeroes the gradient and gathers the next batch (one launch
@@ -242,6 +263,7 @@ class TrainStep:
         return self.engine.reduce()
 
     def _capture(self, x, y):
+        _quiesce_collectives(self.engine.group)
         sx, sy = self._static_inputs(x, y)
         g = torch.cuda.CUDAGraph()
         prev = getattr(self.engine, "sync_enabled", None)
@@ -414,6 +436,8 @@ class TrainStep:
         # (which advances Adam's step counter and the cursor) ... Adam (update + images + zeroed
         # gradient + NEXT batch); the eager warm-up steps keep the pack launch
         self._apack = None
+        self._dsubj = None
+        self._rows = None
         from ..ops.gemm import PLAIN_BLAS
         # (across sites the update runs after the replays, eagerly: the same launch then)
         # (one gather per step: not with accumulation, whose micro-batches gather each)
@@ -421,12 +445,32 @@ class TrainStep:
                 and not PLAIN_BLAS and self._rides() and hasattr(self.model, "persistent_pack")):
             pp = self.model.persistent_pack(dev)
             if pp is not None:
-                self.opt.attach_pack(pp, src, self._dsx, self._dsy)
+                rows = self._rows_feed_ok(src)
+                if rows:
+                    # [B + 1]: a K tile's second subject index may be read one past the batch
+                    self._dsubj = torch.zeros(src.B + 1, dtype=torch.int64, device=dev)
+                    S = src.sample_shape[0]
+                    self._rows = (self._dsx.view(src.B * S, -1),
+                                  src.X.view(src.X.shape[0] * S, -1), self._dsubj, S)
+                self.opt.attach_pack(pp, src, self._dsx, self._dsy,
+                                     sd=self._dsubj if rows else None, copy_x=not rows)
                 # the device step counter must exist before any capture: created inside one, its
                 # allocation and initial fill would become nodes of the graph, resetting the
                 # counter at every replay
                 self.opt.sync_device_step()
                 self._apack = pp
+
+    def _rows_feed_ok(self, src) -> bool:
+        """Read the batch in place (``ROWS_FEED``)?  A bf16 [N, S, ...] dataset with S >= 64
+        windows per subject (at most two subjects per 64-row K tile) and 16-B window rows."""
+        shp = src.sample_shape
+        ok = (src.X.dtype == torch.bfloat16 and len(shp) >= 2 and shp[0] >= 64
+              and (src.row // shp[0]) % 8 == 0)
+        if ROWS_FEED == "1":
+            if not ok:
+                raise ValueError("DINUNET_ROWS_FEED=1: the dataset cannot be read in place")
+            return True
+        return ok and ROWS_FEED == "auto" and src.B >= ROWS_FEED_MIN_B
 
     def _rides(self) -> bool:
         fn = getattr(self.model, "prologue_rides_pack", None)
@@ -494,10 +538,16 @@ class TrainStep:
             raise RuntimeError("Adam-emitted pack: the forward did not start with the encoder GEMM "
                                "on the persistent operand images")
 
+    def _rows_ctx(self):
+        """The in-place batch rows (``ROWS_FEED``) for every GEMM issued inside -- the encoder
+        forward AND its weight gradient, which a split step issues after the forward context."""
+        from ..ops.gemm import rows_from
+        return rows_from(*self._rows) if self._rows is not None else _NoDefer()
+
     def _dev_body_apack(self):
         """One whole device-fed step in the Adam-emitted-pack form (single site)."""
         sx, sy = self._dsxf, self._dsy
-        with self._apack_forward():
+        with self._rows_ctx(), self._apack_forward():
             out, loss, pred = self._fwd_bwd(sx, sy)
         if self._pre_reduce is not None:
             self._pre_reduce()
@@ -532,7 +582,9 @@ class TrainStep:
         all-reduce between its parts, the reduction, and the update that also emits the next
         step's operands -- everything a replay needs, so K such steps form one graph."""
         if self._apack is not None:
-            out, loss, pred = self._split_backward(self._dsxf, self._dsy, self._apack_forward())
+            with self._rows_ctx():
+                out, loss, pred = self._split_backward(self._dsxf, self._dsy,
+                                                       self._apack_forward())
         else:
             out, loss, pred = self._split_backward(self._dsxf, self._dsy,
                                                    self._dev_prologue(self.opt.device_step()))
@@ -568,6 +620,7 @@ class TrainStep:
         return out, loss, pred
 
     def _dev_capture(self, k: int):
+        _quiesce_collectives(self.engine.group)
         g = torch.cuda.CUDAGraph()
         prev = getattr(self.engine, "sync_enabled", None)
         if prev is not None:
@@ -589,19 +642,22 @@ class TrainStep:
         """Device-fed form of :meth:`_capture_split`: graph A = prologue + forward + backward
         down to the cut (:meth:`_split_fwd_bwd`), graph B = the rest (the all-reduce of every
         non-stem gradient runs between the two replays)."""
+        _quiesce_collectives(self.engine.group)
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         sx, sy = self._dsxf, self._dsy
         self.engine.sync_enabled = False
         try:
-            with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
-                with (self._apack_forward() if self._apack is not None
-                      else self._dev_prologue(None)) as rp:
-                    h, hd, out, loss, pred = self._split_fwd_bwd(sx, sy)
-                if isinstance(rp, ride_pack) and not rp.consumed:
-                    raise RuntimeError("device-fed prologue was not absorbed by the weight pack")
-            with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):
-                if h.requires_grad:
-                    torch.autograd.backward(h, hd.grad)
+            with self._rows_ctx():
+                with torch.cuda.graph(ga, capture_error_mode=CAPTURE_MODE):
+                    with (self._apack_forward() if self._apack is not None
+                          else self._dev_prologue(None)) as rp:
+                        h, hd, out, loss, pred = self._split_fwd_bwd(sx, sy)
+                    if isinstance(rp, ride_pack) and not rp.consumed:
+                        raise RuntimeError("device-fed prologue was not absorbed by the weight "
+                                           "pack")
+                with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=CAPTURE_MODE):
+                    if h.requires_grad:
+                        torch.autograd.backward(h, hd.grad)
         finally:
             self.engine.sync_enabled = True
         self._dgraphs["split"] = (ga, gb, (out, loss, pred), (h, hd))

@@ -627,35 +627,66 @@ def test_gemm_splitk_in_launch_combine_matches_reduce_kernel(splits, monkeypatch
 @pytest.mark.parametrize("payload", ["fp16", "bf16", "fp32"])
 @pytest.mark.parametrize("n,W", [(4099, 3), (4 << 20, 8), (37, 2)])
 def test_payload_kernels_match_torch_layout(payload, n, W):
-    """collective.py kernels vs its torch (CPU) implementation of the same block layout: pack
-    (block scale from amax, header, zero pad), fp32-accumulating row sum, unpack (scalar tail);
-    fp16 site values spanning 1e-5..1e2 keep 11-bit precision through the block scale."""
+    """collective.py kernels vs its torch (CPU) implementation of the same sub-block layout: pack
+    (per-sub-block scale from the sub-block's own max |x| inside the pack launch, headers, zero
+    pad), fp32-accumulating row sum (per-sub-block smallest exponent), unpack (scalar tail);
+    fp16 values spanning 1e-5..1e2 keep 11-bit precision through the sub-block scales, and a
+    sub-block of tiny gradients beside one of large ones keeps its own precision."""
     from dinunet_implementations_amd.parallel import collective as C
     dt = C.PAYLOAD_TYPES[payload][1]
-    chunk = -(-n // (8 * W)) * 8
+    chunk = C.chunk_for(n, W)
     # |x| over 7 decades (fp16's normal range spans 2^29 ~ 5e8 once scaled to the block max)
     x = ((torch.rand(n, device=DEV) + 0.5) * torch.randn(n, device=DEV).sign()
          * torch.logspace(-5, 2, n, device=DEV))
-    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
     send = torch.full((C.blocks_numel(W, chunk),), 7.0, dtype=dt, device=DEV)
-    C.to_payload(x, send, W, chunk, scale=0.5, amax=amax)
+    C.to_payload(x, send, W, chunk, scale=0.5)
     ref = torch.empty(send.numel(), dtype=dt)
-    C.to_payload(x.cpu(), ref, W, chunk, scale=0.5, amax=amax.cpu())
+    C.to_payload(x.cpu(), ref, W, chunk, scale=0.5)
     assert torch.equal(send.cpu(), ref)
-    blocks = torch.randn(W, C.HDR + chunk, device=DEV)
-    blocks[:, :C.HDR] = 0
-    blocks[:, 0] = torch.arange(W) - 1.0 if payload == "fp16" else 0.0
+    nsb = chunk // C.SB
+    blocks = torch.randn(W, nsb, C.HDR + C.SB, device=DEV)
+    blocks[:, :, :C.HDR] = 0
+    if payload == "fp16":
+        blocks[:, :, 0] = (torch.arange(W, device=DEV)[:, None] - 1.0
+                           + torch.arange(nsb, device=DEV)[None, :] % 3)
     blocks = blocks.to(dt).reshape(-1)
-    mine = torch.empty(C.HDR + chunk, dtype=dt, device=DEV)
+    mine = torch.empty(C.payload_numel(chunk), dtype=dt, device=DEV)
     C.rowsum(blocks, mine, W, chunk, 1.0 / W)
-    ref_m = torch.empty(C.HDR + chunk, dtype=dt)
+    ref_m = torch.empty(C.payload_numel(chunk), dtype=dt)
     C.rowsum(blocks.cpu(), ref_m, W, chunk, 1.0 / W)
     assert torch.equal(mine.cpu(), ref_m)
     out = torch.empty(n, device=DEV)
-    C.from_payload(send, out, W, chunk, scale=2.0, amax=amax)
-    assert int(amax.item()) == 0  # reset for the next exchange
+    C.from_payload(send, out, W, chunk, scale=2.0)
     if payload == "fp32":
         assert torch.equal(out, x)
     else:
         r = ((out - x).abs() / x.abs()).max().item()
         assert r <= (2.0 ** -11 if payload == "fp16" else 2.0 ** -8) * 1.01, r
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2])
+def test_gemm_rows_gathered_from_dataset(tile):
+    """RowGather (ops.gemm.rows_from): a registered batch buffer read IN PLACE from the dataset
+    through subject indices -- as the k-contiguous A of the encoder forward and the k-major B of
+    the encoder weight gradient (scalar-loaded subjects per K tile, S >= 64) -- bit-identical to
+    the same GEMMs on the gathered copy."""
+    from dinunet_implementations_amd.ops import gemm as G
+    g = torch.Generator(device=DEV).manual_seed(4)
+    N_, S, F, B, O = 40, 98, 200, 12, 64
+    X = torch.randn(N_ * S, F, device=DEV, generator=g).to(torch.bfloat16)
+    subj = torch.randint(0, N_, (B + 1,), device=DEV, generator=g)
+    rows = (subj[:B, None] * S + torch.arange(S, device=DEV)[None, :]).reshape(-1)
+    xc = X[rows].contiguous()                      # the batch copy
+    buf = torch.zeros_like(xc)                     # the stale static buffer
+    w = torch.randn(O, F, device=DEV, generator=g).to(torch.bfloat16)
+    dy = torch.randn(B * S, O, device=DEV, generator=g).to(torch.bfloat16)
+    ref_y = G.mm(xc, w, trans_b=True, out_dtype=torch.bfloat16, tile=tile)
+    ref_dw = G.mm(dy, xc, trans_a=True, tile=tile, splits=3)
+    with G.rows_from(buf, X, subj, S):
+        y = G.mm(buf, w, trans_b=True, out_dtype=torch.bfloat16, tile=tile)
+        dw = G.mm(dy, buf, trans_a=True, tile=tile, splits=3)
+        gw = torch.zeros(O, F, device=DEV)
+        G.mm_grouped([dict(a=dy, b=buf, out=gw, beta=1.0)], trans_a=True, tile=tile, splits=3)
+        with pytest.raises(ValueError):  # a transposed A cannot be gathered: never read stale rows
+            G.mm(buf, dy, trans_a=True)
+    assert torch.equal(y, ref_y) and torch.equal(dw, ref_dw) and torch.equal(gw, ref_dw)

@@ -694,3 +694,34 @@ def test_fs_device_feed_matches_host_loop(accum):
     feed = _feed_vs_host(sh, sd, X, Y, 16, nb=5, accum=accum, col=-1)
     assert feed.src.width == 66 and sd._dsx.shape == (16, 72) and sd._dsx.dtype == torch.float32
     assert torch.allclose(fh.data, fd.data, rtol=1e-6, atol=1e-7), (fh.data - fd.data).abs().max()
+
+
+@pytest.mark.parametrize("engine,sites", [("dSGD", 1), ("dSGD", "rccl1")])
+def test_device_fed_rows_in_place_matches_batch_copy(engine, sites, monkeypatch, request):
+    """DINUNET_ROWS_FEED: the Adam-emitted pack writes the next batch's subject indices instead
+    of copying the batch, and the encoder forward / weight-gradient GEMMs read the rows in place
+    from the HBM-resident dataset -- the same trajectory, bit for bit, as the batch copy, on one
+    site and on the captured multi-site step."""
+    from dinunet_implementations_amd.runtime import step as step_mod
+    from dinunet_implementations_amd.runtime.feed import DeviceFeed
+    grp = request.getfixturevalue("rccl1") if sites == "rccl1" else None
+    xs, ys = _batches(n=6, B=8, S=70)
+    B = xs.shape[1]
+    X = xs.reshape(-1, *xs.shape[2:]).to(torch.bfloat16)
+    Y = ys.reshape(-1)
+    mk = (lambda: _trainer_cfg(0, engine, grp, {}, use_graph=True)) if grp is not None else (
+        lambda: _trainer(0, engine=engine, use_graph=True))
+    runs = []
+    for mode in ("0", "1"):
+        monkeypatch.setattr(step_mod, "ROWS_FEED", mode)
+        _, f, st = mk()
+        feed = DeviceFeed(st, X, Y, B, 7, col=1, steps_per_graph=4)
+        assert (st._rows is not None) == (mode == "1") and st._apack is not None
+        g = torch.Generator(device="cuda").manual_seed(2)
+        for _ in range(2):
+            order = torch.randint(0, X.shape[0], (7 * B,), device="cuda", generator=g)
+            losses, scores, _ = feed.run_epoch(order)
+        torch.cuda.synchronize()
+        runs.append((f.data.clone(), losses.clone(), scores.clone()))
+    (f0, l0, s0), (f1, l1, s1) = runs
+    assert torch.equal(f0, f1) and torch.equal(l0, l1) and torch.equal(s0, s1)

@@ -82,16 +82,15 @@ def direct_kernels(n: int, world: int, payload: str) -> float:
     import torch
     from dinunet_implementations_amd.parallel import collective as C
     code, dt = C.PAYLOAD_TYPES[payload]
-    chunk = max(8, -(-n // (8 * world)) * 8)
+    chunk = C.chunk_for(n, world)
     x = torch.randn(n, device="cuda")
     send = torch.zeros(C.blocks_numel(world, chunk), dtype=dt, device="cuda")
-    mine = torch.zeros(C.HDR + chunk, dtype=dt, device="cuda")
-    amax = torch.zeros(1, dtype=torch.int32, device="cuda") if dt == torch.float16 else None
+    mine = torch.zeros(C.payload_numel(chunk), dtype=dt, device="cuda")
 
     def run():
-        C.to_payload(x, send, world, chunk, amax=amax)
+        C.to_payload(x, send, world, chunk)
         C.rowsum(send, mine, world, chunk, 1.0 / world)
-        C.from_payload(send, x, world, chunk, 1.0, amax=amax)
+        C.from_payload(send, x, world, chunk, 1.0)
     # device time of the kernels (a graph replay), and separately what issuing them from Python
     # costs per exchange (ctypes launches: the host side of the eager exchange)
     run()
