@@ -11,7 +11,7 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 __host__ __device__ constexpr int rup32(int v) { return (v + 31) & ~31; }
 
 // 32-bit counter hash (Wellons' lowbias32 finaliser over idx ^ key(seed, layer)): two 32-bit
-// multiplies per element.  The former 64-bit splitmix finaliser (six 64-bit multiplies, each a
+// multiplies per hash.  The former 64-bit splitmix finaliser (six 64-bit multiplies, each a
 // chain of quarter-rate 32-bit ones) made the layer-0 dropout the longest phase of the forward.
 __device__ __forceinline__ uint32_t hmix(uint64_t seed, uint32_t layer, uint32_t idx) {
   const uint32_t key = (uint32_t)seed * 0x9E3779B9u ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu ^
@@ -22,11 +22,19 @@ __device__ __forceinline__ uint32_t hmix(uint64_t seed, uint32_t layer, uint32_t
   x ^= x >> 15;
   x *= 0x846CA68Bu;
   x ^= x >> 16;
-  return x >> 8;  // 24 uniform bits
+  return x;
 }
 
+// Keep decision of element (m, k) of a [.][K] activation: one hash serves the element PAIR
+// idx / 2 (16 uniform bits each: low half for even idx, high half for odd), so a lane holding
+// consecutive elements (every kernel's vector loads) hashes once per two -- the quarter-rate
+// multiplies of the layer-0 input dropout were ~2 us of the replicated head's prologue.  Keep
+// probabilities resolve to 2^-16.
 __device__ __forceinline__ bool hkeep(uint64_t seed, int layer, int m, int k, int K, float p) {
-  return (float)hmix(seed, (uint32_t)layer, (uint32_t)(m * K + k)) * (1.f / 16777216.f) >= p;
+  const uint32_t idx = (uint32_t)(m * K + k);
+  const uint32_t h = hmix(seed, (uint32_t)layer, idx >> 1);
+  const uint32_t u = (idx & 1u) ? (h >> 16) : (h & 0xffffu);
+  return (float)u * (1.f / 65536.f) >= p;
 }
 
 // sum over the four lanes holding one accumulator column (l, l^16, l^32, l^48)
