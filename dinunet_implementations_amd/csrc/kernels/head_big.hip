@@ -338,14 +338,17 @@ headb_loss_kernel(BArgs a, const long long* __restrict__ y, float* __restrict__ 
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) ls += __shfl_xor(ls, off);
+  // (only the C real classes: a wave-wide sum is 6 cross-lane steps, 96 for all 16 slots)
 #pragma unroll
   for (int c = 0; c < 16; ++c)
+    if (c < C) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) gs[c] += __shfl_xor(gs[c], off);
+      for (int off = 32; off >= 1; off >>= 1) gs[c] += __shfl_xor(gs[c], off);
+    }
   if (lane == 0) {
     red[wid][16] = ls;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) red[wid][c] = gs[c];
+    for (int c = 0; c < 16; ++c) red[wid][c] = c < C ? gs[c] : 0.f;
   }
   __syncthreads();
   if (tid < 17) {
