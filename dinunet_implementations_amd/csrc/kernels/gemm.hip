@@ -674,18 +674,29 @@ __device__ __forceinline__ bf16x8 dma_frag(const char* img, int r0, int ks, int 
   }
 }
 
+// LDS bytes of gemm_dma_kernel<BM, BN, TA, TB, S>: the S-stage ring or the epilogue staging
+template <int BM, int BN, bool TA, bool TB, int S>
+constexpr int dma_smem() {
+  constexpr int STAGE = DmaImg<BM, !TA>::BYTES + DmaImg<BN, TB>::BYTES;
+  constexpr int EBYTES = 4 * (BM / 2) * (BN / 2 + 4) * 4;
+  return S * STAGE > EBYTES ? S * STAGE : EBYTES;
+}
+
+// s_waitcnt vmcnt(n), 0 <= n < 64 (vmcnt bits [3:0] and [15:14])
+#define DN_VMWAIT(n) __builtin_amdgcn_s_waitcnt(DN_VMCNT0 | ((n) & 15) | (((n) >> 4) << 14))
+
 template <int BM, int BN, bool TA, bool TB, int S>
 __global__ void __launch_bounds__(256)
 gemm_dma_kernel(GemmGroup g) {
-  static_assert(S >= 2 && S <= 4, "ring depth");
+  static_assert(S >= 2 && S <= 8, "ring depth");
   typedef DmaImg<BM, !TA> IA;
   typedef DmaImg<BN, TB> IB;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int ES = WN + 4;                 // fp32 epilogue row stride (per-wave WM x WN block)
-  constexpr int EBYTES = 4 * WM * ES * 4;    // four waves
-  constexpr int SMEM = S * STAGE > EBYTES ? S * STAGE : EBYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  // one dynamic LDS array (dma_smem bytes; a second __shared__ object beside a glds ring can
+  // make hipcc drain vmcnt before LDS reads): the 8-stage ring is 128 KB, past the static limit
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
 
   const int ntiles = g.tile_start[g.n];
   const int bid = (int)blockIdx.x;
@@ -734,9 +745,15 @@ gemm_dma_kernel(GemmGroup g) {
     }
   for (int t = 0; t < nk; ++t) {
     const int ahead = min(D - 1, nk - 1 - t);  // tiles after t already issued
-    if (ahead >= 2) __builtin_amdgcn_s_waitcnt(DN_VMCNT0 | (2 * G));
-    else if (ahead == 1) __builtin_amdgcn_s_waitcnt(DN_VMCNT0 | G);
-    else __builtin_amdgcn_s_waitcnt(DN_VMCNT0);
+    static_assert((D - 1) * G < 64, "vmcnt range");
+    // (an immediate per count: one wave-uniform branch)
+    if (D - 1 >= 6 && ahead >= 6) DN_VMWAIT(6 * G);
+    else if (D - 1 >= 5 && ahead == 5) DN_VMWAIT(5 * G);
+    else if (D - 1 >= 4 && ahead == 4) DN_VMWAIT(4 * G);
+    else if (D - 1 >= 3 && ahead == 3) DN_VMWAIT(3 * G);
+    else if (ahead >= 2) DN_VMWAIT(2 * G);
+    else if (ahead == 1) DN_VMWAIT(G);
+    else DN_VMWAIT(0);
     __builtin_amdgcn_s_barrier();
     if (t + D < nk) {
       char* nxt = smem + ((t + D) % S) * STAGE;
@@ -1132,6 +1149,13 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
 }
 
 static int g_gemm_dma = 1;  // bf16 x bf16 aligned groups take gemm_dma_kernel (A/B switch)
+// largest grid (workgroups) of 64 x 64 tiles that takes the 8-stage ring (DN_GEMM_RING8_MAX; default
+// 0 = off: measured slower at the B = 32 step, encoder 10.2 vs 9.2 us and input gradient 15.5 vs
+// 14.2 -- those K loops are not bound by the tiles in flight, 0.3146 vs 0.3116 ms/step)
+static const long g_ring8_max = [] {
+  const char* e = getenv("DN_GEMM_RING8_MAX");
+  return e ? atol(e) : 0L;
+}();
 
 static int kchunk_for(int K, int& splits) {
   int kchunk = K;
@@ -1162,10 +1186,24 @@ int launch(GemmGroup& g, hipStream_t st) {
     // ring depth: a grid that fills the chip several times over hides the DMA latency with
     // resident workgroups (2 stages, 32 KB at 64x64 -> 5 per CU); a small grid (the B = 32
     // step's ~200-tile GEMMs) needs the deeper 4-stage ring inside each workgroup
-    if (g.vec && g_gemm_dma && BM == 64 && (long)tiles * g.splits < 512)
-      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 4>), grid, dim3(256), 0, st, g);
+    // (DN_GEMM_RING8_MAX: a grid of at most that many workgroups takes the 8-stage ring, 128 KB
+    // of LDS and seven tiles in flight per workgroup)
+    const long wgs = (long)tiles * g.splits;
+    if (g.vec && g_gemm_dma && BM == 64 && wgs <= g_ring8_max) {
+      constexpr int SM = dma_smem<BM, BN, TA, TB, 8>();
+      static bool init = false;
+      if (!init) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_dma_kernel<BM, BN, TA, TB, 8>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, SM);
+        init = true;
+      }
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 8>), grid, dim3(256), SM, st, g);
+    } else if (g.vec && g_gemm_dma && BM == 64 && wgs < 512)
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 4>), grid, dim3(256),
+                         (dma_smem<BM, BN, TA, TB, 4>()), st, g);
     else if (g.vec && g_gemm_dma)
-      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 2>), grid, dim3(256), 0, st, g);
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 2>), grid, dim3(256),
+                         (dma_smem<BM, BN, TA, TB, 2>()), st, g);
     else if (g.vec)
       hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, TAe, TBe, true>), grid, dim3(256), 0, st, g);
     else
