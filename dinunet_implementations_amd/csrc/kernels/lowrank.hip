@@ -123,13 +123,34 @@ struct LrLayer {
 // block of every layer, [layer][8], via dn_lr_set_stamps
 #ifdef LR_STAMPS
 __device__ unsigned long long* lr_stamp_buf;
-#define LR_STAMP(i) do { if (threadIdx.x == 0 && lr_stamp_buf && blockIdx.x == (unsigned)(X.b3 + X.n3 - 1)) { \
+#define LR_STAMP(i) do { if (threadIdx.x == 0 && lr_stamp_buf && bid == X.b3 + X.n3 - 1) { \
   unsigned long long v_; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v_) :: "memory"); \
   lr_stamp_buf[(long)l * 8 + (i)] = v_; } } while (0)
 #else
 #define LR_STAMP(i) do { } while (0)
 #endif
 constexpr int LR_QLDS = 16384;  // floats of Q staged by lr_gq (in * r)
+// Layer lookup by kernel argument: first block (lr_gq: b1, lr_gtp: b3) or first tile (recon) of
+// each of <= LR_KMAX layers of one launch (the host cuts a larger table into launches of
+// LR_KMAX layers).  A search through the device table was a chain of dependent scalar loads, one
+// L2 round trip per layer before any block could start its real loads.
+constexpr int LR_KMAX = 16;
+struct LrIndex {
+  int n;                // layers of this launch
+  int first[LR_KMAX];   // absolute first block / first tile of layer j
+};
+// unrolled selects (a runtime index into the by-value argument would copy it to scratch)
+__device__ __forceinline__ int lr_layer_of(int v, const LrIndex& ix, int* first = nullptr) {
+  int l = 0, f = ix.first[0];
+#pragma unroll
+  for (int j = 1; j < LR_KMAX; ++j) {
+    const bool in = j < ix.n && v >= ix.first[j];
+    l = in ? j : l;
+    f = in ? ix.first[j] : f;
+  }
+  if (first) *first = f;
+  return l;
+}
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -158,6 +179,7 @@ __device__ __forceinline__ void stage_load(f32x4 (&v)[LR_STV], const float* src,
   const int n4 = nf >> 2;
 #pragma unroll
   for (int j = 0; j < LR_STV; ++j) {
+    if (j * 256 >= n4) break;  // uniform: no redundant loads past the end
     const int i = tid + 256 * j;
     v[j] = ((gfloat4*)src)[i < n4 ? i : n4 - 1];
   }
@@ -166,6 +188,7 @@ __device__ __forceinline__ void stage_store(const f32x4 (&v)[LR_STV], float* dst
   const int n4 = nf >> 2;
 #pragma unroll
   for (int j = 0; j < LR_STV; ++j) {
+    if (j * 256 >= n4) break;
     const int i = tid + 256 * j;
     if (i < n4) reinterpret_cast<f32x4*>(dst)[i] = v[j];
   }
@@ -175,51 +198,72 @@ __device__ __forceinline__ void stage_store(const f32x4 (&v)[LR_STV], float* dst
 // PowerSGD error feedback (M = G + err formed on the fly and written back to the gradient buffer),
 // QL = Q staged in LDS (in * r <= LR_QLDS; a generic pointer would make every B read a flat load)
 template <bool VEC, bool ERR, bool QL>
-__device__ __forceinline__ void gq_main(const LrLayer& X, float* qs, float* red, int tid, int w) {
+__device__ __forceinline__ void gq_main(const LrLayer& X, float* qs, float* red, int tid, int w,
+                                        int bid) {
   const int lane = tid & 63, r = X.r, in = X.in;
   const int nq = in * r;
   constexpr bool lds = QL;
   const bool qvec = lds && (nq & 3) == 0;
   f32x4 qv[LR_STV];
   if (qvec) stage_load(qv, X.Qsend, nq, tid);
-  const int row0 = 16 * (blockIdx.x - X.b1);
+  const int row0 = 16 * (bid - X.b1);
   const int c = lane & 15, kr = lane >> 4;
   const int row = row0 + c;
   const bool rv = row < X.out;
   const long roff = (long)(rv ? row : row0) * in;
-  float* gw = X.G + roff;
+  typedef __attribute__((address_space(1))) float wfloat;
+  typedef __attribute__((address_space(1))) f32x4 wfloat4;
+  wfloat* gw = (wfloat*)(X.G + roff);  // global stores: a flat store also counts in lgkmcnt
   gfloat* grow = (gfloat*)(X.G + roff);
   gfloat* erow = (gfloat*)(X.err + (ERR ? roff : 0));
   constexpr int U = 8;
   const int nch = (in + 15) >> 4;
-  // chunk j of this wave = global chunk w + 4 j; its lane run starts at column 16 ch + 4 kr
-  auto load = [&](f32x4 (&v)[U], int j0) {
+  // chunk j of this wave = global chunk w + 4 j; its lane run starts at column 16 ch + 4 kr.
+  // issue: every load of U chunks (G and, for PowerSGD, err) goes out before any is used; fix:
+  // M = G + err, written back, and the out-of-range zeroing.  (With the add and the write-back
+  // inside the load loop hipcc waited for each chunk's loads before issuing the next chunk's:
+  // one L2 round trip per chunk, 13.7 us for the ICA layers.)
+  auto issue = [&](f32x4 (&v)[U], f32x4 (&e)[U], int j0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k0 = 16 * (w + 4 * (j0 + u)) + 4 * kr;
-      f32x4 g;
+      if (VEC) {
+        const int kk = (rv && k0 < in) ? k0 : 0;
+        v[u] = ((gfloat4*)grow)[kk >> 2];
+        if (ERR) e[u] = ((gfloat4*)erow)[kk >> 2];
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int k = k0 + s2, kk = (rv && k < in) ? k : 0;
+          v[u][s2] = grow[kk];
+          if (ERR) e[u][s2] = erow[kk];
+        }
+      }
+    }
+  };
+  auto fix = [&](f32x4 (&v)[U], const f32x4 (&e)[U], int j0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k0 = 16 * (w + 4 * (j0 + u)) + 4 * kr;
       if (VEC) {
         const bool ok = rv && k0 < in;
-        g = ((gfloat4*)grow)[(ok ? k0 : 0) >> 2];
         if (ERR) {
-          g += ((gfloat4*)erow)[(ok ? k0 : 0) >> 2];
-          if (ok) reinterpret_cast<f32x4*>(gw)[k0 >> 2] = g;
+          v[u] += e[u];
+          if (ok) ((wfloat4*)gw)[k0 >> 2] = v[u];
         }
-        g *= ok ? 1.f : 0.f;  // a multiply, not a select: keeps the load unconditional
+        v[u] *= ok ? 1.f : 0.f;  // a multiply, not a select: keeps the load unconditional
       } else {
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
           const int k = k0 + s2;
           const bool ok = rv && k < in;
-          float x = grow[ok ? k : 0];
           if (ERR) {
-            x += erow[ok ? k : 0];
-            if (ok) gw[k] = x;
+            v[u][s2] += e[u][s2];
+            if (ok) gw[k] = v[u][s2];
           }
-          g[s2] = x * (ok ? 1.f : 0.f);
+          v[u][s2] *= ok ? 1.f : 0.f;
         }
       }
-      v[u] = g;
     }
   };
   const float cmask = c < r ? 1.f : 0.f;
@@ -239,9 +283,9 @@ __device__ __forceinline__ void gq_main(const LrLayer& X, float* qs, float* red,
     }
   };
   const int nj = (nch - w + 3) >> 2;  // this wave's chunk count (scalar)
-  f32x4 g0[U], g1[U];
-  load(g0, 0);
-  if (U < nj) load(g1, U);
+  f32x4 g0[U], g1[U], e0[U], e1[U];
+  issue(g0, e0, 0);
+  if (U < nj) issue(g1, e1, U);
   if (qvec) {
     stage_store(qv, qs, nq, tid);
   } else if (lds) {
@@ -250,11 +294,13 @@ __device__ __forceinline__ void gq_main(const LrLayer& X, float* qs, float* red,
   __syncthreads();
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int j = 0; j < nj; j += 2 * U) {
+    fix(g0, e0, j);
     mma(g0, j, acc);
-    if (j + 2 * U < nj) load(g0, j + 2 * U);
+    if (j + 2 * U < nj) issue(g0, e0, j + 2 * U);
     if (j + U >= nj) break;
+    fix(g1, e1, j + U);
     mma(g1, j + U, acc);
-    if (j + 3 * U < nj) load(g1, j + 3 * U);
+    if (j + 3 * U < nj) issue(g1, e1, j + 3 * U);
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[w * 256 + (4 * kr + j) * 16 + c] = acc[j];  // [w][i][c]
@@ -275,15 +321,14 @@ __device__ __forceinline__ void gq_main(const LrLayer& X, float* qs, float* red,
 // B[k][l & 15] = Q[16 ch + 4 (l >> 4) + s][l & 15].  Two rounds of U chunks are in flight at
 // once, issued before Q is staged: one HBM round trip for a 1000-column layer instead of four.
 __global__ void __launch_bounds__(256)
-lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
+lr_gq_kernel(const LrLayer* __restrict__ Ls, LrIndex ix, int it, float tol) {
   __shared__ float qs[LR_QLDS];
   __shared__ float red[4 * 256];
-  int l = 0;
-  while (l + 1 < nl && (int)blockIdx.x >= Ls[l + 1].b1) ++l;
-  const LrLayer& X = Ls[l];
+  const int bid = (int)blockIdx.x + ix.first[0];
+  const LrLayer& X = Ls[lr_layer_of(bid, ix)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform loops, no exec masks
-  const bool lead = blockIdx.x == (unsigned)X.b1 && tid == 0;
+  const bool lead = bid == X.b1 && tid == 0;
   if (it == 0) {
     if (lead) *X.active = 1;
   } else {
@@ -303,7 +348,7 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
   }
   if (lead) *X.iters += 1;  // one writer per layer (its first block's thread 0)
   const bool vec = (X.in & 3) == 0, ql = X.in * X.r <= LR_QLDS;  // uniform per layer
-#define LR_GQ(V, E) (ql ? gq_main<V, E, true>(X, qs, red, tid, w) : gq_main<V, E, false>(X, qs, red, tid, w))
+#define LR_GQ(V, E) (ql ? gq_main<V, E, true>(X, qs, red, tid, w, bid) : gq_main<V, E, false>(X, qs, red, tid, w, bid))
   if (X.err) {
     if (vec) LR_GQ(true, true); else LR_GQ(false, true);
   } else {
@@ -312,25 +357,66 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, int nl, int it, float tol) {
 #undef LR_GQ
 }
 
-// Forward substitution x <- x D^{-1/2} R_s^{-1} for one row held in registers: Rh[k][m] =
-// R_s[k][m] above the diagonal, Rh[k][k] = 1 / R_s[k][k] (0 for a dropped column), zeros below;
-// Sv = D^{-1/2}.  Uniform LDS reads (broadcast); right-looking so the chain per step is one FMA.
-__device__ __forceinline__ void lr_solve_row(float (&x)[LR_MAXR], const float* Rh,
-                                             const float* Sv) {
+// Scaled Cholesky of the fp64 Gram gm (the lr_gtp_kernel factorisation), wave 0, unrolled to the
+// rank bound R >= r (R x R steps instead of LR_MAXR x LR_MAXR): Rh / Sv as lp_solve reads them.
+template <int R>
+__device__ __forceinline__ void lp_chol(const double* gm, float* Rh, float* Sv, int r, int lane) {
+  const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
+  double dmax = di;
 #pragma unroll
-  for (int j = 0; j < LR_MAXR; ++j) x[j] *= Sv[j];
+  for (int o = 1; o < 16; o <<= 1) dmax = fmax(dmax, shfl_d(dmax, lane ^ o));
+  const bool live = lane < r && di > fmax(1e-13 * dmax, 1e-280);
+  const double si = live ? 1.0 / sqrt(di) : 0.0;
+  float sv[R];
 #pragma unroll
-  for (int j = 0; j < LR_MAXR; ++j) {
+  for (int jj = 0; jj < R; ++jj) sv[jj] = rlane((float)si, jj);
+  float av[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj)
+    av[jj] = (lane < r && jj < r) ? (float)(gm[(lane & 15) * 16 + jj] * si) * sv[jj] : 0.f;
+  unsigned dead = ~(unsigned)__ballot(live) & ((1u << r) - 1u);
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const float akk = rlane(av[k], k);
+    const bool dk = ((dead >> k) & 1u) || akk <= 1e-6f;
+    const float inv = dk ? 0.f : __builtin_amdgcn_rsqf(akk);
+    dead |= dk ? 1u << k : 0u;
+    const float rki = av[k] * inv;
+    if (lane < LR_MAXR) Rh[k * LR_MAXR + lane] = lane > k ? rki : (lane == k ? inv : 0.f);
+    const float sk = rki * inv;
+#pragma unroll
+    for (int jj = k + 1; jj < R; ++jj) av[jj] = __builtin_fmaf(-sk, rlane(av[jj], k), av[jj]);
+  }
+  if (lane < LR_MAXR) Sv[lane] = lane < R ? (float)si : 0.f;
+}
+
+// Forward substitution x <- x D^{-1/2} R_s^{-1} for one row held in registers, bounded by R
+// (entries >= R of x stay untouched: zero on entry, never read): Rh[k][m] = R_s[k][m] above the
+// diagonal, Rh[k][k] = 1 / R_s[k][k] (0 for a dropped column), zeros below; Sv = D^{-1/2}.
+// Uniform LDS reads (broadcast); right-looking so the chain per step is one FMA.
+template <int R>
+__device__ __forceinline__ void lp_solve(float (&x)[LR_MAXR], const float* Rh, const float* Sv) {
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) x[jj] *= Sv[jj];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
     float rw[LR_MAXR];
 #pragma unroll
-    for (int q4 = 0; q4 < LR_MAXR / 4; ++q4) {
-      const f32x4 v = reinterpret_cast<const f32x4*>(Rh + j * LR_MAXR)[q4];
+    for (int q4 = 0; q4 < R / 4; ++q4) {
+      const f32x4 v = reinterpret_cast<const f32x4*>(Rh + jj * LR_MAXR)[q4];
       rw[4 * q4] = v[0]; rw[4 * q4 + 1] = v[1]; rw[4 * q4 + 2] = v[2]; rw[4 * q4 + 3] = v[3];
     }
-    x[j] *= rw[j];
+    x[jj] *= rw[jj];
 #pragma unroll
-    for (int m = j + 1; m < LR_MAXR; ++m) x[m] = __builtin_fmaf(-x[j], rw[m], x[m]);
+    for (int mm = jj + 1; mm < R; ++mm) x[mm] = __builtin_fmaf(-x[jj], rw[mm], x[mm]);
   }
+}
+__device__ __forceinline__ void lp_solve_r(float (&x)[LR_MAXR], const float* Rh, const float* Sv,
+                                           int r) {
+  if (r <= 4) lp_solve<4>(x, Rh, Sv);
+  else if (r <= 8) lp_solve<8>(x, Rh, Sv);
+  else if (r <= 12) lp_solve<12>(x, Rh, Sv);
+  else lp_solve<16>(x, Rh, Sv);
 }
 
 // grid = sum of n3, block 256: 16 columns of one layer per block, all rows.  Q[16 cols] =
@@ -343,26 +429,41 @@ __device__ __forceinline__ void lr_solve_row(float (&x)[LR_MAXR], const float* R
 // P[r0 + k][l & 15], k = l >> 4; the 4 waves take interleaved 4-row chunks and meet in LDS.  The
 // commit rides here: the new Q slice replaces Qsend, and the block's ||Q - Q_prev||^2, ||Q||^2
 // go to `norms` for the next lr_gq.
+template <int R>  // rank bound: r <= R in {4, 8, 16} for every layer of the launch
 __global__ void __launch_bounds__(256)
-lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
-  __shared__ float ps[LR_PLDS];
+lr_gtp_kernel(const LrLayer* __restrict__ Ls, LrIndex ix, int it) {
+  __shared__ __attribute__((aligned(16))) float ps[LR_PLDS];
   __shared__ float red[4 * 256];
   __shared__ double gm[256];
   __shared__ double gpart[4 * 256];
   __shared__ __attribute__((aligned(16))) float Rh[LR_MAXR * LR_MAXR];
   __shared__ float Sv[LR_MAXR];
-  int l = 0;
-  while (l + 1 < nl && (int)blockIdx.x >= Ls[l + 1].b3) ++l;
+  const int bid = (int)blockIdx.x + ix.first[0];
+  const int l = lr_layer_of(bid, ix);
   const LrLayer& X = Ls[l];
   if (it > 0 && !*X.active) return;
   LR_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, r = X.r, n = X.out;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform loops, no exec masks
-  const int cb = blockIdx.x - X.b3;
+  const int cb = bid - X.b3;
   const int c = lane & 15, kr = lane >> 4;
   const int col = 16 * cb + c;
   const bool cv = col < X.in;
   gfloat* gcol = (gfloat*)(X.G + (cv ? col : 16 * cb));
+  // P's loads go out first (registers, then LDS): in-order vmcnt lets the LDS staging wait for
+  // them alone while the G column loads behind them are still in flight, so the Gram below runs
+  // under the G loads instead of after them
+  const int n4 = (n * r) >> 2;
+  const bool pvec = ((n * r) & 3) == 0;
+  f32x4 pv[LR_STV];
+  if (pvec) {
+#pragma unroll
+    for (int j = 0; j < LR_STV; ++j)
+      if (j * 256 < n4) {  // uniform: no loads past P's end
+        const int i = tid + 256 * j;
+        pv[j] = ((gfloat4*)X.P)[i < n4 ? i : n4 - 1];
+      }
+  }
   // the first two rounds of this wave's G^T P column loads: in flight from here on (double
   // buffered below -- a load-then-MFMA loop exposed one HBM round trip per round)
   constexpr int U = 16;
@@ -382,55 +483,59 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
     for (int u = 0; u < U; ++u) {
       const int row = rb + 16 * u + kr;
       // rows past n meet a zero A entry; columns past r give H columns the solve ignores
-      const float pv = ps[(row < n ? row : 0) * r + (c < r ? c : 0)] * cmask;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v[u], pv, acc, 0, 0, 0);
+      const float pw = ps[(row < n ? row : 0) * r + (c < r ? c : 0)] * cmask;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v[u], pw, acc, 0, 0, 0);
     }
   };
   const int rb0 = 4 * w;
   load(g0, rb0);
   if (rb0 + 16 * U < n) load(g1, rb0 + 16 * U);
-  if (((n * r) & 3) == 0) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(X.P);
-#pragma unroll 8
-    for (int i = tid; i < n * r / 4; i += 256) reinterpret_cast<f32x4*>(ps)[i] = src[i];
+  if (pvec) {
+#pragma unroll
+    for (int j = 0; j < LR_STV; ++j) {
+      const int i = tid + 256 * j;
+      if (j * 256 < n4 && i < n4) reinterpret_cast<f32x4*>(ps)[i] = pv[j];
+    }
   } else {
     for (int i = tid; i < n * r; i += 256) ps[i] = X.P[i];
   }
   __syncthreads();
   LR_STAMP(1);
-  {  // Gram P^T P on the fp64 matrix cores (fp32 values, exact products): for 16x16x4 f64 lane l
-     // holds A[l & 15][k = l >> 4] = P[row k][col l & 15] and B[k][l & 15] -- the same value
-     // (C: row (l >> 4) + 4 reg, col l & 15 -- the f64 map, not the f32 one).  Wave w takes
-     // every 4th block of 4 rows; the four wave partials are added in a fixed order.  The loop
-     // is uniform (scalar wave id and trip count) with unconditional clamped LDS reads: a
-     // divergent loop made hipcc shuttle the accumulators between AGPRs and VGPRs every
-     // iteration (19k cycles for 768 rows)
+  // Gram P^T P on the fp64 matrix cores (fp32 values, exact products), NG = 16 / RG row groups
+  // packed side by side in the 16 columns (RG = 4 for r <= 4, 8 for r <= 8, else 16): lane l
+  // holds A[i][k] = P[row(g, k)][c'] with i = l & 15 = g RG + c', k = l >> 4, row(g, k) = base +
+  // 4 g + k, and B[k][i] the same value, so C's diagonal RG x RG block g is the Gram of group g's
+  // rows -- one MFMA covers 4 NG rows.  (C map of 16x16x4 f64: row (l >> 4) + 4 reg, col l & 15.)
+  // Wave w takes every 4th block of 4 NG rows; the partials of the waves and groups are added in
+  // a fixed order.  The loop is uniform (scalar wave id and trip count) with unconditional clamped
+  // LDS reads: a divergent loop made hipcc shuttle the accumulators between AGPRs and VGPRs every
+  // iteration (19k cycles for 768 rows)
+  constexpr int RG = R <= 4 ? 4 : R <= 8 ? 8 : 16, NG = 16 / RG, RB = 4 * NG;
+  {
+    const int gi = c / RG, cc = c % RG;
+    const float vmask = cc < r ? 1.f : 0.f;
+    const int ccl = cc < r ? cc : 0;
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    const int iters = (n - 4 * w + 15) / 16;  // scalar trip count: a uniform loop
-    const int cc = c < r ? c : 0;
+    const int iters = (n - RB * w + 4 * RB - 1) / (4 * RB);  // scalar trip count
     int it2 = 0;
-    for (; it2 + 4 <= iters; it2 += 4) {  // four rows' reads in flight per round
+    for (; it2 + 4 <= iters; it2 += 4) {  // four MFMAs' reads in flight per round
       float x[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int row = 4 * w + 16 * (it2 + j) + kr;
-        x[j] = ps[(row < n ? row : 0) * r + cc];  // clamped, unconditional LDS reads
+        const int row = RB * w + 4 * RB * (it2 + j) + 4 * gi + kr;
+        x[j] = ps[(row < n ? row : 0) * r + ccl] * (row < n ? vmask : 0.f);  // clamped reads
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = 4 * w + 16 * (it2 + j) + kr;
-        const double v = (row < n && c < r) ? (double)x[j] : 0.0;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
-      }
+      for (int j = 0; j < 4; ++j)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)x[j], (double)x[j], acc, 0, 0, 0);
     }
     for (; it2 < iters; ++it2) {
-      const int row = 4 * w + 16 * it2 + kr;
-      const float x = ps[(row < n ? row : 0) * r + cc];
-      const double v = (row < n && c < r) ? (double)x : 0.0;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+      const int row = RB * w + 4 * RB * it2 + 4 * gi + kr;
+      const float x = ps[(row < n ? row : 0) * r + ccl] * (row < n ? vmask : 0.f);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)x, (double)x, acc, 0, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) gpart[w * 256 + (kr + 4 * j) * 16 + c] = acc[j];  // f64 C map
+    for (int j = 0; j < 4; ++j) gpart[w * 256 + (kr + 4 * j) * 16 + c] = acc[j];
   }
   LR_STAMP(2);
   {  // H = G[:, 16 cols]^T P, rounds of 16 chunks, two buffers in flight
@@ -447,7 +552,18 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
   }
   __syncthreads();
   LR_STAMP(3);
-  gm[tid] = (gpart[tid] + gpart[256 + tid]) + (gpart[512 + tid] + gpart[768 + tid]);
+  {
+    const int i = tid >> 4, j = tid & 15;
+    double v = 0.0;
+    if (i < RG && j < RG) {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int e = (g * RG + i) * 16 + g * RG + j;
+        v += (gpart[e] + gpart[256 + e]) + (gpart[512 + e] + gpart[768 + e]);
+      }
+    }
+    gm[tid] = v;
+  }
   red[tid] = red[tid] + red[256 + tid] + red[512 + tid] + red[768 + tid];  // H[k][c], own entry
   __syncthreads();
   LR_STAMP(4);
@@ -455,42 +571,10 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
     // wave 0, lane i < r = row i.  Jacobi scaling in fp64: A_s = D^{-1/2} A D^{-1/2} has a unit
     // diagonal (P's columns are ~sigma_i u_i: the scaling removes nearly all of cond(A)), so the
     // Cholesky R_s^T R_s = A_s runs in fp32 on the hardware rsq / FMA units, and
-    // R^{-1} = D^{-1/2} R_s^{-1} is applied by substitution.  A column whose norm vanished
-    // (d_i <= 1e-13 max d) or that is numerically dependent (pivot <= 1e-6 after scaling) is
-    // dropped: its Pn and Q columns are zero.
-    const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
-    double dmax = di;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) dmax = fmax(dmax, shfl_d(dmax, lane ^ o));
-    const bool live = lane < r && di > fmax(1e-13 * dmax, 1e-280);
-    const double si = live ? 1.0 / sqrt(di) : 0.0;
-    float sv[LR_MAXR];  // s_j, uniform (read with v_readlane: no LDS round trip)
-#pragma unroll
-    for (int jj = 0; jj < LR_MAXR; ++jj) sv[jj] = rlane((float)si, jj);
-    float a[LR_MAXR];
-#pragma unroll
-    for (int jj = 0; jj < LR_MAXR; ++jj)
-      a[jj] = (lane < r && jj < r) ? (float)(gm[(lane & 15) * 16 + jj] * si) * sv[jj] : 0.f;
-    unsigned dead = ~(unsigned)__ballot(live) & ((1u << r) - 1u);
-    // right-looking Cholesky, straight line: lane i keeps row i of the (symmetric) trailing
-    // matrix, so R_s[k][i] = A[i][k] / sqrt(A[k][k]) is the lane's OWN a[k] -- no transposed
-    // access -- and row k reaches every lane through v_readlane (k is a compile-time index).
-    // Steps k >= r find a zero pivot and drop out, so there are no rank branches.  (Divergent
-    // `if (lane == k)` blocks and shuffles made this ~17k cycles.)
-#pragma unroll
-    for (int k = 0; k < LR_MAXR; ++k) {
-      const float akk = rlane(a[k], k);
-      const bool dk = ((dead >> k) & 1u) || akk <= 1e-6f;
-      const float inv = dk ? 0.f : __builtin_amdgcn_rsqf(akk);
-      dead |= dk ? 1u << k : 0u;
-      const float rki = a[k] * inv;  // R_s[k][lane] for lane > k (symmetry)
-      if (lane < LR_MAXR) Rh[k * LR_MAXR + lane] = lane > k ? rki : (lane == k ? inv : 0.f);
-      const float sk = rki * inv;    // A[lane][k] / A[k][k]
-#pragma unroll
-      for (int jj = k + 1; jj < LR_MAXR; ++jj)  // rows <= k are finished: garbage there is unread
-        a[jj] = __builtin_fmaf(-sk, rlane(a[jj], k), a[jj]);
-    }
-    if (lane < LR_MAXR) Sv[lane] = (float)si;
+    // R^{-1} = D^{-1/2} R_s^{-1} is applied by substitution (lp_chol / lp_solve, R x R steps).
+    // A column whose norm vanished (d_i <= 1e-13 max d) or that is numerically dependent
+    // (pivot <= 1e-6 after scaling) is dropped: its Pn and Q columns are zero.
+    lp_chol<R>(gm, Rh, Sv, r, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -499,20 +583,25 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
     const int k = 16 * cb + lane;
     float dd = 0.f, qq = 0.f;
     if (lane < 16) {
+      const bool kv = k < X.in;
+      float* qrow = X.Qsend + (long)(kv ? k : 0) * r;
+      float old[R];  // the last commit, loaded before the solve (all at once, clamped)
+#pragma unroll
+      for (int j = 0; j < R; ++j) old[j] = ((gfloat*)qrow)[j < r ? j : 0];
       float x[LR_MAXR];
 #pragma unroll
-      for (int q4 = 0; q4 < LR_MAXR / 4; ++q4) {
+      for (int j = 0; j < LR_MAXR; ++j) x[j] = 0.f;
+#pragma unroll
+      for (int q4 = 0; q4 < R / 4; ++q4) {
         const f32x4 v = reinterpret_cast<const f32x4*>(red + lane * 16)[q4];
         x[4 * q4] = v[0]; x[4 * q4 + 1] = v[1]; x[4 * q4 + 2] = v[2]; x[4 * q4 + 3] = v[3];
       }
-      lr_solve_row(x, Rh, Sv);
-      if (k < X.in) {
-        float* qrow = X.Qsend + (long)k * r;
+      lp_solve<R>(x, Rh, Sv);
+      if (kv) {
 #pragma unroll
-        for (int j = 0; j < LR_MAXR; ++j) {
+        for (int j = 0; j < R; ++j) {
           if (j < r) {
-            const float old = qrow[j];
-            dd += (x[j] - old) * (x[j] - old);
+            dd += (x[j] - old[j]) * (x[j] - old[j]);
             qq += x[j] * x[j];
             qrow[j] = x[j];
           }
@@ -533,31 +622,58 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, int nl, int it) {
     for (int row = tid; row < n; row += 256) {
       float x[LR_MAXR];
 #pragma unroll
-      for (int j = 0; j < LR_MAXR; ++j) x[j] = j < r ? ps[row * r + j] : 0.f;
-      lr_solve_row(x, Rh, Sv);
+      for (int j = 0; j < LR_MAXR; ++j) x[j] = (j < R && j < r) ? ps[row * r + j] : 0.f;
+      lp_solve<R>(x, Rh, Sv);
       float* prow = X.Psend + (long)row * r;
 #pragma unroll
-      for (int j = 0; j < LR_MAXR; ++j)
+      for (int j = 0; j < R; ++j)
         if (j < r) prow[j] = x[j];
     }
   }
 }
 
-// PowerSGD: G <- P Q^T (the compressed update), err <- M - P Q^T (M = G + err from lr_gq)
+// PowerSGD: G <- P Q^T (the compressed update), err <- M - P Q^T (M = G + err from lr_gq), one
+// 16 x 16 output tile per wave on the f32 matrix cores (16x16x4, K = r in chunks of 4; operand
+// lanes as in pi_reconstruct_kernel below).  The tile list is every layer's tiles in order.  The
+// per-thread-element loop it replaced (layer search, 64-bit division and r dependent loads per
+// element) was latency-bound: 14.6 us for the ICA layers.
 __global__ void __launch_bounds__(256)
-lr_recon_ef_kernel(const LrLayer* __restrict__ Ls, const long* __restrict__ starts, int nl,
-                   long total) {
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    int l = 0;
-    while (l + 1 < nl && e >= starts[l + 1]) ++l;
-    const LrLayer& X = Ls[l];
-    const long i = e - starts[l];
-    const int row = (int)(i / X.in), k = (int)(i - (long)row * X.in);
-    float s = 0.f;
-    for (int c = 0; c < X.r; ++c) s += X.Psend[(long)row * X.r + c] * X.Qsend[(long)k * X.r + c];
-    const float m = X.G[i];
-    X.G[i] = s;
-    if (X.err) X.err[i] = m - s;
+lr_recon_ef_kernel(const LrLayer* __restrict__ Ls, LrIndex ix, int ntiles) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kq = lane >> 4;
+  for (int tile = blockIdx.x * 4 + w; tile < ntiles; tile += gridDim.x * 4) {
+    int t0;
+    const LrLayer& X = Ls[lr_layer_of(tile, ix, &t0)];
+    const int tn = (X.in + 15) / 16;
+    const int ti = tile - t0;
+    const int r0 = 16 * (ti / tn), k0 = 16 * (ti % tn);
+    const int prow = r0 + c16, qrow = k0 + c16;
+    const bool pv = prow < X.out, qv = qrow < X.in;
+    const float* p = X.Psend + (long)(pv ? prow : 0) * X.r;
+    const float* q = X.Qsend + (long)(qv ? qrow : 0) * X.r;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < X.r; c += 4) {
+      const int cc = c + kq;
+      const float av = (pv && cc < X.r) ? p[cc] : 0.f;
+      const float bv = (qv && cc < X.r) ? q[cc] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+    const int col = k0 + c16;
+    float m[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = r0 + 4 * kq + j;
+      m[j] = (row < X.out && col < X.in) ? X.G[(long)row * X.in + col] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = r0 + 4 * kq + j;
+      if (row < X.out && col < X.in) {
+        const long i = (long)row * X.in + col;
+        X.G[i] = acc[j];
+        if (X.err) X.err[i] = m[j] - acc[j];
+      }
+    }
   }
 }
 
@@ -736,65 +852,6 @@ __device__ __forceinline__ void lp_publish(__amdgpu_buffer_rsrc_t dst, const flo
   for (int e = q1 + tid; e < e1; e += 256) lp_st1(dst, 4 * e, src[e - e0]);
 }
 
-
-// Scaled Cholesky of the fp64 Gram gm (the lr_gtp_kernel factorisation), wave 0, unrolled to the
-// rank bound R >= r (R x R steps instead of LR_MAXR x LR_MAXR): Rh / Sv as lr_solve_row reads them.
-template <int R>
-__device__ __forceinline__ void lp_chol(const double* gm, float* Rh, float* Sv, int r, int lane) {
-  const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
-  double dmax = di;
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) dmax = fmax(dmax, shfl_d(dmax, lane ^ o));
-  const bool live = lane < r && di > fmax(1e-13 * dmax, 1e-280);
-  const double si = live ? 1.0 / sqrt(di) : 0.0;
-  float sv[R];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) sv[jj] = rlane((float)si, jj);
-  float av[R];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj)
-    av[jj] = (lane < r && jj < r) ? (float)(gm[(lane & 15) * 16 + jj] * si) * sv[jj] : 0.f;
-  unsigned dead = ~(unsigned)__ballot(live) & ((1u << r) - 1u);
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    const float akk = rlane(av[k], k);
-    const bool dk = ((dead >> k) & 1u) || akk <= 1e-6f;
-    const float inv = dk ? 0.f : __builtin_amdgcn_rsqf(akk);
-    dead |= dk ? 1u << k : 0u;
-    const float rki = av[k] * inv;
-    if (lane < LR_MAXR) Rh[k * LR_MAXR + lane] = lane > k ? rki : (lane == k ? inv : 0.f);
-    const float sk = rki * inv;
-#pragma unroll
-    for (int jj = k + 1; jj < R; ++jj) av[jj] = __builtin_fmaf(-sk, rlane(av[jj], k), av[jj]);
-  }
-  if (lane < LR_MAXR) Sv[lane] = lane < R ? (float)si : 0.f;
-}
-
-// lr_solve_row bounded by R (entries >= R of x stay untouched: zero on entry, never read)
-template <int R>
-__device__ __forceinline__ void lp_solve(float (&x)[LR_MAXR], const float* Rh, const float* Sv) {
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) x[jj] *= Sv[jj];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) {
-    float rw[LR_MAXR];
-#pragma unroll
-    for (int q4 = 0; q4 < R / 4; ++q4) {
-      const f32x4 v = reinterpret_cast<const f32x4*>(Rh + jj * LR_MAXR)[q4];
-      rw[4 * q4] = v[0]; rw[4 * q4 + 1] = v[1]; rw[4 * q4 + 2] = v[2]; rw[4 * q4 + 3] = v[3];
-    }
-    x[jj] *= rw[jj];
-#pragma unroll
-    for (int mm = jj + 1; mm < R; ++mm) x[mm] = __builtin_fmaf(-x[jj], rw[mm], x[mm]);
-  }
-}
-__device__ __forceinline__ void lp_solve_r(float (&x)[LR_MAXR], const float* Rh, const float* Sv,
-                                           int r) {
-  if (r <= 4) lp_solve<4>(x, Rh, Sv);
-  else if (r <= 8) lp_solve<8>(x, Rh, Sv);
-  else if (r <= 12) lp_solve<12>(x, Rh, Sv);
-  else lp_solve<16>(x, Rh, Sv);
-}
 
 __global__ void __launch_bounds__(256)
 lr_persist_kernel(LpArgs a) {
@@ -1053,28 +1110,61 @@ DN_API int dn_lr_limits(int* maxr, int* plds, int* qlds) {
   return DN_OK;
 }
 
-// One power iteration / PowerSGD half-round over every layer of the table.
+// One power iteration / PowerSGD half-round over every layer of the table (`layers`: the device
+// table; `host`: the same table in host memory, read for the launch index).  Launches of at most
+// LR_KMAX layers each (one launch for every ICA model).
 //   stage 0: lr_gq (P = G Q; it == 0 re-activates every layer, it > 0 applies dad_tol first)
 //   stage 1: lr_gtp (Pn = P R^{-1} from the fp64 Gram; Q = G^T Pn committed to Qsend)
-DN_API int dn_lr_stage(const void* layers, int nl, int blocks1, int blocks3, int stage, int it,
-                       float tol, hipStream_t st) {
+DN_API int dn_lr_stage(const void* layers, const void* host, int nl, int stage, int it, float tol,
+                       hipStream_t st) {
   if (nl <= 0) return DN_OK;
-  if (nl > 256) return DN_BAD_SHAPE;
+  if (nl > 256 || !host || (stage != 0 && stage != 1)) return DN_BAD_SHAPE;
   const LrLayer* L = (const LrLayer*)layers;
-  if (stage == 0)
-    hipLaunchKernelGGL(lr_gq_kernel, dim3(blocks1), dim3(256), 0, st, L, nl, it, tol);
-  if (stage == 1) hipLaunchKernelGGL(lr_gtp_kernel, dim3(blocks3), dim3(256), 0, st, L, nl, it);
+  const LrLayer* H = (const LrLayer*)host;
+  for (int c0 = 0; c0 < nl; c0 += LR_KMAX) {
+    LrIndex ix{};
+    ix.n = nl - c0 < LR_KMAX ? nl - c0 : LR_KMAX;
+    for (int j = 0; j < ix.n; ++j) ix.first[j] = stage == 0 ? H[c0 + j].b1 : H[c0 + j].b3;
+    const LrLayer& E = H[c0 + ix.n - 1];
+    const int blocks = (stage == 0 ? E.b1 + E.n1 : E.b3 + E.n3) - ix.first[0];
+    if (blocks <= 0) continue;
+    if (stage == 0)
+      hipLaunchKernelGGL(lr_gq_kernel, dim3(blocks), dim3(256), 0, st, L + c0, ix, it, tol);
+    else {
+      int rm = 1;
+      for (int j = 0; j < ix.n; ++j) rm = H[c0 + j].r > rm ? H[c0 + j].r : rm;
+      if (rm <= 4)
+        hipLaunchKernelGGL(lr_gtp_kernel<4>, dim3(blocks), dim3(256), 0, st, L + c0, ix, it);
+      else if (rm <= 8)
+        hipLaunchKernelGGL(lr_gtp_kernel<8>, dim3(blocks), dim3(256), 0, st, L + c0, ix, it);
+      else
+        hipLaunchKernelGGL(lr_gtp_kernel<16>, dim3(blocks), dim3(256), 0, st, L + c0, ix, it);
+    }
+  }
   return dn_launch_status();
 }
 
-// PowerSGD reconstruction + error feedback over every layer (starts: device long[nl] prefix)
-DN_API int dn_lr_recon_ef(const void* layers, const long* starts, int nl, long total,
-                          hipStream_t st) {
-  if (nl <= 0 || total <= 0) return DN_OK;
-  long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(lr_recon_ef_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                     (const LrLayer*)layers, starts, nl, total);
+// PowerSGD reconstruction + error feedback over every layer (`host`: the table in host memory)
+DN_API int dn_lr_recon_ef(const void* layers, const void* host, int nl, hipStream_t st) {
+  if (nl <= 0) return DN_OK;
+  if (nl > 256 || !host) return DN_BAD_SHAPE;
+  const LrLayer* L = (const LrLayer*)layers;
+  const LrLayer* H = (const LrLayer*)host;
+  for (int c0 = 0; c0 < nl; c0 += LR_KMAX) {
+    LrIndex ix{};
+    ix.n = nl - c0 < LR_KMAX ? nl - c0 : LR_KMAX;
+    long t = 0;
+    for (int j = 0; j < ix.n; ++j) {
+      ix.first[j] = (int)t;
+      t += (long)((H[c0 + j].out + 15) / 16) * ((H[c0 + j].in + 15) / 16);
+    }
+    if (t <= 0) continue;
+    if (t > (1L << 30)) return DN_BAD_SHAPE;
+    long blocks = (t + 3) / 4;  // one 16 x 16 tile per wave
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(lr_recon_ef_kernel, dim3((unsigned)blocks), dim3(256), 0, st, L + c0, ix,
+                       (int)t);
+  }
   return dn_launch_status();
 }
 

@@ -19,10 +19,9 @@ from ..ops import _lib
 
 _lib.register("dn_mgs_batched", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
                                   _lib.c_int, _lib.c_float, _lib.c_void_p])
-_lib.register("dn_lr_stage", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_int,
-                              _lib.c_int, _lib.c_float, _lib.c_void_p])
-_lib.register("dn_lr_recon_ef", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long,
-                                 _lib.c_void_p])
+_lib.register("dn_lr_stage", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
+                              _lib.c_float, _lib.c_void_p])
+_lib.register("dn_lr_recon_ef", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p])
 _lib.register("dn_pi_reconstruct", [_lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_long,
                                      _lib.c_int, _lib.c_void_p])
 
@@ -117,7 +116,6 @@ class LowRankTable:
         self.iters = torch.zeros(max(n, 1), dtype=torch.int32, device=device)
         tab = (LrLayer * max(n, 1))()
         b1 = b3 = 0
-        starts = []
         total = 0
         for i, (G, err, P, ps, qs) in enumerate(layers):
             out_f, in_f = G.shape
@@ -138,10 +136,11 @@ class LowRankTable:
             t.out, t.in_, t.r, t.b1, t.n1, t.b3, t.n3 = out_f, in_f, r, b1, n1, b3, n3
             b1 += n1
             b3 += n3
-            starts.append(total)
             total += out_f * in_f
         self.blocks1, self.blocks3, self.total = b1, b3, total
-        self._host_tab = tab  # the persistent launch takes the table by value
+        # the persistent launch takes the table by value; the staged launches read their layer
+        # index (first block / tile per layer, kernel argument) from it
+        self._host_tab = tab
         self.table = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
         # (gram partials, norms, barrier words) of dn_lr_persist: allocated (zeroed) here, never
         # inside a capture
@@ -151,7 +150,6 @@ class LowRankTable:
         self._persist = (torch.zeros(max(n, 1) * mj * 256, dtype=torch.float64, device=device),
                          torch.zeros(max(n, 1) * mj * 2, dtype=torch.float32, device=device),
                          torch.zeros(int(L.dn_lr_persist_words()), dtype=torch.int32, device=device))
-        self.starts = torch.tensor(starts or [0], dtype=torch.int64).to(device)
 
     def persist(self, iters: int, tol: float = 0.0) -> bool:
         """ALL ``iters`` power iterations of every layer in ONE launch (``lr_persist_kernel``:
@@ -182,10 +180,15 @@ class LowRankTable:
         """Cumulative power iterations run per layer (host sync)."""
         return [int(v) for v in self.iters[:self.n].tolist()]
 
+    def host_table(self) -> int:
+        """Address of the host copy of the descriptor table."""
+        import ctypes
+        return ctypes.addressof(self._host_tab)
+
     def _stage(self, stage: int, it: int, tol: float = 0.0):
         if self.n:
-            _lib.call("dn_lr_stage", self.table.data_ptr(), self.n, self.blocks1, self.blocks3,
-                      stage, int(it), float(tol), _lib.stream())
+            _lib.call("dn_lr_stage", self.table.data_ptr(), self.host_table(), self.n, stage,
+                      int(it), float(tol), _lib.stream())
 
     def gq(self, it: int, tol: float = 0.0):
         """P = G Q (PowerSGD: M = G + err first).  Iteration 0 re-activates every layer; later
@@ -200,5 +203,5 @@ class LowRankTable:
     def recon_ef(self):
         """PowerSGD: G <- Psend Qsend^T, err <- M - G (M = G + err left by :meth:`gq`)."""
         if self.n:
-            _lib.call("dn_lr_recon_ef", self.table.data_ptr(), self.starts.data_ptr(), self.n,
-                      self.total, _lib.stream())
+            _lib.call("dn_lr_recon_ef", self.table.data_ptr(), self.host_table(), self.n,
+                      _lib.stream())

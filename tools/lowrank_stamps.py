@@ -26,7 +26,7 @@ def main():
     st = _lib.stream
 
     def stage(s_, it):
-        _lib.call("dn_lr_stage", t.table.data_ptr(), t.n, t.blocks1, t.blocks3, s_, it, 0.0, st())
+        _lib.call("dn_lr_stage", t.table.data_ptr(), t.host_table(), t.n, s_, it, 0.0, st())
     acc = torch.zeros(len(ICA), 7, dtype=torch.float64)
     reps = 20
     for k in range(reps + 3):
