@@ -237,6 +237,7 @@ struct RowGather {
   const long long* subj;     // [rows / gs + 1] dataset subject indices
   int gs;                    // rows per subject
   int op;                    // 1: operand A, 2: operand B
+  int r0;                    // A rows: the problem's row 0 is logical row r0 (a row-range view)
 };
 
 // One GEMM problem of a (possibly grouped) launch.
@@ -272,6 +273,17 @@ struct GemmGroup {
   // next to each other (ops.gemm._xcd_order) and each block is fetched into one XCD's L2
   const int* perm;
 };
+
+// problem of a launch-wide tile / element index: a count over the (monotone) prefix, unrolled so
+// every prefix load issues at once (a search loop was one dependent kernarg load per problem
+// before a workgroup could start its own loads)
+template <typename T>
+__device__ __forceinline__ int group_prob(const GemmGroup& g, const T* start, T v) {
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < GMAX; ++i) pi += (i < g.n && v >= start[i]) ? 1 : 0;
+  return pi;
+}
 
 // the armed bump rides in the next launch of one group only
 __device__ __forceinline__ void group_bump(const GemmGroup& g) {
@@ -414,8 +426,7 @@ gemm_kernel(GemmGroup g) {
   if (slot >= ntiles) return;
   group_bump(g);
   const int gtile = g.perm ? g.perm[slot] : slot;
-  int pi = 0;
-  while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
+  const int pi = group_prob(g, g.tile_start, gtile);
   const GemmProb& P = g.p[pi];
   const TAe* __restrict__ A = reinterpret_cast<const TAe*>(P.A);
   const TBe* __restrict__ B = reinterpret_cast<const TBe*>(P.B);
@@ -573,7 +584,8 @@ struct DmaStream {
   __device__ __forceinline__ void init(const bf16* __restrict__ base, long ld, int row0, int nrows,
                                        int wid, int lane, int unitcol = -1,
                                        const bf16* ggx = nullptr,
-                                       const long long* gsubj = nullptr, int ggs = 1) {
+                                       const long long* gsubj = nullptr, int ggs = 1,
+                                       int ggr0 = 0) {
     ins0 = wid * PW;
     kstep = KCONTIG ? 1 : ld;
     unit = 0;
@@ -595,8 +607,9 @@ struct DmaStream {
         kofs[j] = 8 * ch;
         long row = gr;
         if (subj && gr < nrows) {  // operand row gr -> dataset row (once per workgroup)
-          const int b = gr / gs;
-          row = subj[b] * gs + (gr - b * gs);
+          const int gg = gr + ggr0;
+          const int b = gg / gs;
+          row = subj[b] * gs + (gg - b * gs);
         }
         p[j] = gr < nrows ? base + row * ld + 8 * ch : nullptr;
       } else {
@@ -704,8 +717,7 @@ gemm_dma_kernel(GemmGroup g) {
   if (slot >= ntiles) return;
   group_bump(g);
   const int gtile = g.perm ? g.perm[slot] : slot;
-  int pi = 0;
-  while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
+  const int pi = group_prob(g, g.tile_start, gtile);
   const GemmProb& P = g.p[pi];
   const bf16* __restrict__ A = reinterpret_cast<const bf16*>(P.A);
   const bf16* __restrict__ B = reinterpret_cast<const bf16*>(P.B);
@@ -728,7 +740,8 @@ gemm_dma_kernel(GemmGroup g) {
 
   DmaStream<BM, !TA> sa;
   DmaStream<BN, TB> sb;
-  sa.init(A, P.lda, row0, M, wid, lane, -1, P.rg.op == 1 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
+  sa.init(A, P.lda, row0, M, wid, lane, -1, P.rg.op == 1 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs,
+          P.rg.r0);
   sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol,
           P.rg.op == 2 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
   // S-stage ring, tiles prefetched D = S - 1 ahead: at the top of iteration t this wave waits
@@ -908,8 +921,7 @@ gemm256_kernel(GemmGroup g) {
   if (slot >= ntiles) return;
   group_bump(g);
   const int gtile = g.perm ? g.perm[slot] : slot;
-  int pi = 0;
-  while (pi + 1 < g.n && gtile >= g.tile_start[pi + 1]) ++pi;
+  const int pi = group_prob(g, g.tile_start, gtile);
   const GemmProb& P = g.p[pi];
   const bf16* __restrict__ A = reinterpret_cast<const bf16*>(P.A);
   const bf16* __restrict__ B = reinterpret_cast<const bf16*>(P.B);
@@ -932,7 +944,8 @@ gemm256_kernel(GemmGroup g) {
 
   DmaStream<BM, !TA, NW> sa;
   DmaStream<BN, TB, NW> sb;
-  sa.init(A, P.lda, row0, M, wid, lane, -1, P.rg.op == 1 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
+  sa.init(A, P.lda, row0, M, wid, lane, -1, P.rg.op == 1 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs,
+          P.rg.r0);
   sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol,
           P.rg.op == 2 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
   if (nk > 0) {
@@ -1057,12 +1070,13 @@ gemm256_kernel(GemmGroup g) {
 }
 
 // 4 consecutive outputs of one row: v (already alpha-free split sum) -> epilogue -> vector store
-__device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, int row, int col, f32x4 v) {
+__device__ __forceinline__ void epi_store4(const Epi& epi, void* C, long ldc, int row, int col, f32x4 v,
+                                           long orow = -2) {
   if (epi.xcol >= 0 && col + 3 >= epi.xcol) {  // the column-sum group (xcol % 4 == 0)
     epi_store(epi, C, ldc, row, col, v[0]);
     return;
   }
-  const long orow = epi.row_map ? epi.row_map[row] : row;
+  if (orow == -2) orow = epi.row_map ? epi.row_map[row] : row;  // else: the caller's, loaded early
   if (orow < 0) return;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1105,8 +1119,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
   for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; 4 * i4 < total;
        i4 += (long)gridDim.x * blockDim.x) {
     const long idx0 = 4 * i4;
-    int pi = 0;
-    while (pi + 1 < g.n && idx0 >= g.elem_start[pi + 1]) ++pi;
+    const int pi = group_prob(g, g.elem_start, idx0);
     const GemmProb& P = g.p[pi];
     const long base = g.elem_start[pi];
     const long mn = (long)P.M * P.N;
@@ -1116,6 +1129,10 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
                      ((((uintptr_t)P.C) & 15) == 0) &&
                      ((((uintptr_t)P.slab) & 15) == 0);
     if (vec) {
+      // the output row (and its row-map entry) first: that load then overlaps the slab loads
+      // instead of following them
+      const int row = (int)(idx / P.N), col = (int)(idx - (long)row * P.N);
+      const long orow = P.epi.row_map ? P.epi.row_map[row] : row;
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
       int s = 0;
       for (; s + 4 <= g.splits; s += 4) {  // four slab loads in flight per round
@@ -1131,8 +1148,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmGroup g) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += a[e];
       }
-      const int row = (int)(idx / P.N), col = (int)(idx - (long)row * P.N);
-      epi_store4(P.epi, P.C, P.ldc, row, col, v);
+      epi_store4(P.epi, P.C, P.ldc, row, col, v, orow);
       continue;
     }
 #pragma unroll
@@ -1382,7 +1398,8 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
                    long ldb, void* C, int c_bf16, long ldc, int M, int N, int K, float alpha,
                    float beta, const float* bias, int relu, const int* row_map, int tile,
                    int splits, float* slab, const void* mask, long ldm, int* counters,
-                   const void* gx, const long long* subj, int gs, int gop, hipStream_t st) {
+                   const void* gx, const long long* subj, int gs, int gop, int gr0,
+                   hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return DN_BAD_SHAPE;
   if (splits > 1 && !slab) return DN_BAD_SHAPE;
   GemmGroup g;
@@ -1399,7 +1416,7 @@ DN_API int dn_gemm(const void* A, int a_bf16, int ta, long lda, const void* B, i
   P.slab = g.splits > 1 ? slab : nullptr;
   P.epi = Epi{bias, row_map, alpha, beta, relu, c_bf16, 0, (const bf16*)mask, ldm, nullptr, -1,
               nullptr, nullptr};
-  P.rg = RowGather{(const bf16*)gx, subj, gs, gx ? gop : 0};
+  P.rg = RowGather{(const bf16*)gx, subj, gs, gx ? gop : 0, gx && gop == 1 ? gr0 : 0};
   return run_group(g, a_bf16, b_bf16, ta, tb, tile, st);
 }
 
@@ -1440,7 +1457,7 @@ DN_API int dn_gemm_grouped(int n, const void* const* A, const long* lda, const v
                 xcol ? xcol[i] : -1, X1 ? (float*)X1[i] : nullptr, X2 ? (float*)X2[i] : nullptr};
     P.rg = RowGather{};
     if (GX && GX[i])
-      P.rg = RowGather{(const bf16*)GX[i], (const long long*)SUBJ[i], GS[i], GOP[i]};
+      P.rg = RowGather{(const bf16*)GX[i], (const long long*)SUBJ[i], GS[i], GOP[i], 0};
     if (P.epi.C2 && !P.epi.ncol) return DN_BAD_SHAPE;  // second outputs: column sums only
     if (P.epi.xcol >= 0 && (N[i] != P.epi.xcol + 4 || P.epi.xcol % 8 || !P.epi.X1 || c_bf16 ||
                             P.epi.ncol > 0 || bias[i]))

@@ -179,18 +179,16 @@ __device__ __forceinline__ void stage_load(f32x4 (&v)[LR_STV], const float* src,
   const int n4 = nf >> 2;
 #pragma unroll
   for (int j = 0; j < LR_STV; ++j) {
-    if (j * 256 >= n4) break;  // uniform: no redundant loads past the end
     const int i = tid + 256 * j;
-    v[j] = ((gfloat4*)src)[i < n4 ? i : n4 - 1];
+    if (j * 256 < n4) v[j] = ((gfloat4*)src)[i < n4 ? i : n4 - 1];  // uniform: no loads past the end
   }
 }
 __device__ __forceinline__ void stage_store(const f32x4 (&v)[LR_STV], float* dst, int nf, int tid) {
   const int n4 = nf >> 2;
 #pragma unroll
   for (int j = 0; j < LR_STV; ++j) {
-    if (j * 256 >= n4) break;
     const int i = tid + 256 * j;
-    if (i < n4) reinterpret_cast<f32x4*>(dst)[i] = v[j];
+    if (j * 256 < n4 && i < n4) reinterpret_cast<f32x4*>(dst)[i] = v[j];
   }
 }
 
@@ -458,11 +456,10 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, LrIndex ix, int it) {
   f32x4 pv[LR_STV];
   if (pvec) {
 #pragma unroll
-    for (int j = 0; j < LR_STV; ++j)
-      if (j * 256 < n4) {  // uniform: no loads past P's end
-        const int i = tid + 256 * j;
-        pv[j] = ((gfloat4*)X.P)[i < n4 ? i : n4 - 1];
-      }
+    for (int j = 0; j < LR_STV; ++j) {
+      const int i = tid + 256 * j;
+      if (j * 256 < n4) pv[j] = ((gfloat4*)X.P)[i < n4 ? i : n4 - 1];  // uniform: none past P's end
+    }
   }
   // the first two rounds of this wave's G^T P column loads: in flight from here on (double
   // buffered below -- a load-then-MFMA loop exposed one HBM round trip per round)
@@ -972,22 +969,51 @@ lr_persist_kernel(LpArgs a) {
     lp_barrier(a.sync, l, (++bar) * (unsigned)J, 0x100u + (unsigned)l, a.spin);
     LP_STAMP(sb + 3);
     // ---- phase B: Gram, Cholesky, H = G[:, my cols]^T P, Q[my cols], Psend[my rows] ----
-    if (tid < 128) {  // member partials in a fixed order, 8 loads in flight per round
-      double s0 = 0.0, s1 = 0.0;
-      for (int b0 = 0; b0 < J; b0 += 8) {
-        double2 v[8];
+    // One round of loads for both inputs of the phase: the J partial Grams (rows < r only; thread
+    // t takes double2 entry t & 127 of members [h Jh, h Jh + Jh), h = t >> 7) first, then this
+    // thread's share of P.  The Gram sums wait only for the Gram loads (in-order vmcnt), so wave
+    // 0's Cholesky runs while the P loads are still in flight; P reaches LDS after it.  (Loading
+    // the Grams, then staging P, then factorising was two round trips plus the Cholesky in series.)
+    const int Jh = (J + 1) >> 1, gh = tid >> 7, gp = tid & 127;
+    const bool gload = gp < 8 * r;  // double2 entries of Gram rows 0 .. r-1
+    constexpr int GV = 8, PV = 8;   // registers for 16 members and 8192 floats of P; the rest
+                                    // (larger tables) is loaded after, in series
+    double2 gv[GV];
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          v[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
-              rG, ((b0 + q < J ? b0 + q : 0) * 256 + 2 * tid) * 8, 0, 16));
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (b0 + q < J) { s0 += v[q].x; s1 += v[q].y; }
-      }
-      gm[2 * tid] = s0;
-      gm[2 * tid + 1] = s1;
+    for (int q = 0; q < GV; ++q) {
+      // unconditional, clamped: a per-load branch (or a `break`) made hipcc wait for every load
+      // at the join, or keep gv in LDS
+      const int mb = gh * Jh + q;
+      gv[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+          rG, (((gload && q < Jh && mb < J) ? mb : 0) * 256 + 2 * gp) * 8, 0, 16));
     }
-    lp_stage(stg, rP, (n * r + 3) & ~3, tid);
+    __builtin_amdgcn_sched_barrier(0);  // keep every Gram load ahead of the P loads
+    const int pn4 = (n * r + 3) >> 2;
+    f32x4 pv[PV];
+#pragma unroll
+    for (int q = 0; q < PV; ++q) {
+      const int i = q * 256 + tid;
+      pv[q] = lp_ld4(rP, 16 * (i < pn4 ? i : 0));
+    }
+    {
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int q = 0; q < GV; ++q)
+        if (q < Jh && gh * Jh + q < J) { s0 += gv[q].x; s1 += gv[q].y; }
+      for (int q = GV; q < Jh; ++q) {  // J > 2 GV members
+        const int mb = gh * Jh + q;
+        if (mb < J) {
+          const double2 v = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+              rG, ((gload ? mb : 0) * 256 + 2 * gp) * 8, 0, 16));
+          s0 += v.x;
+          s1 += v.y;
+        }
+      }
+      gpart[gh * 256 + 2 * gp] = s0;
+      gpart[gh * 256 + 2 * gp + 1] = s1;
+    }
+    lp_sync();
+    gm[tid] = (tid < 16 * r) ? gpart[tid] + gpart[256 + tid] : 0.0;
     lp_sync();
     LP_STAMP(sb + 4);
     if (w == 0) {  // scaled Cholesky of the Gram, wave 0, unrolled to the rank bound
@@ -996,6 +1022,14 @@ lr_persist_kernel(LpArgs a) {
       else if (r <= 12) lp_chol<12>(gm, Rh, Sv, r, lane);
       else lp_chol<16>(gm, Rh, Sv, r, lane);
     }
+#pragma unroll
+    for (int q = 0; q < PV; ++q) {
+      const int i = q * 256 + tid;
+      if (q * 256 < pn4 && i < pn4) reinterpret_cast<f32x4*>(stg)[i] = pv[q];
+    }
+    if (pn4 > PV * 256)  // larger P: the rest in series
+      lp_stage(stg + 4 * PV * 256, lp_rsrc(X.P + 4 * PV * 256), 4 * (pn4 - PV * 256), tid);
+    lp_sync();  // P staged, Rh / Sv visible
     LP_STAMP(sb + 8);
     {  // H = G[:, my cols]^T P on the matrix cores (the WB waves of a column block meet in red)
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};

@@ -23,7 +23,8 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_float,
                           _lib.c_float, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
                           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p,
-                          _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p])
+                          _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
+                          _lib.c_void_p])
 
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
 _lib.register("dn_gemm_dma_on", [])
@@ -228,13 +229,61 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
     if mask is not None:
         if (mask.dtype != torch.bfloat16 or tuple(mask.shape) != (M, N) or mask.stride(1) != 1):
             raise ValueError("mm mask must be a row-contiguous bf16 [M, N] tensor")
+    gargs = _gather_args(a, b, trans_a, trans_b)
+    tail = _tail_rows(M, N, K, tile, sp) if slab is None else None
+    Mm = M if tail is None else tail
     _lib.call("dn_gemm", A.data_ptr(), int(A.dtype == torch.bfloat16), ta, lda, B.data_ptr(),
               int(B.dtype == torch.bfloat16), tb, ldb, out.data_ptr(),
-              int(out.dtype == torch.bfloat16), out.stride(0), M, N, K, float(alpha), float(beta),
+              int(out.dtype == torch.bfloat16), out.stride(0), Mm, N, K, float(alpha), float(beta),
               _lib.ptr(bias), int(relu), _lib.ptr(row_map), tile, sp, _lib.ptr(slab),
               _lib.ptr(mask), mask.stride(0) if mask is not None else 0, _lib.ptr(cnt),
-              *_gather_args(a, b, trans_a, trans_b), _lib.stream())
+              *gargs, 0, _lib.stream())
+    if tail is not None:
+        # the rows of the launch's last, mostly idle round of 256 x 256 tiles as a row-range view
+        # (operand / output / mask / row-map pointers offset, gathered rows through r0) on
+        # 64 x 64 tiles: sixteen times the workgroups, so the round fills the CUs it would idle
+        r0 = tail
+        Mt = M - r0
+        ea, eo = A.element_size(), out.element_size()
+        a_ptr = A.data_ptr() + (r0 * ea if ta else r0 * lda * ea)
+        if gargs[3] == 1:  # A's rows are gathered: the kernel maps view row r to r0 + r
+            a_ptr = A.data_ptr()
+        _lib.call("dn_gemm", a_ptr, int(A.dtype == torch.bfloat16), ta, lda, B.data_ptr(),
+                  int(B.dtype == torch.bfloat16), tb, ldb, out.data_ptr() + r0 * out.stride(0) * eo,
+                  int(out.dtype == torch.bfloat16), out.stride(0), Mt, N, K, float(alpha),
+                  float(beta), _lib.ptr(bias), int(relu),
+                  (row_map.data_ptr() + 4 * r0) if row_map is not None else None, 0, 1, None,
+                  (mask.data_ptr() + r0 * mask.stride(0) * 2) if mask is not None else None,
+                  mask.stride(0) if mask is not None else 0, None, *gargs, r0, _lib.stream())
     return out
+
+
+# DINUNET_GEMM_TAIL=0: no row-range tail split of 256 x 256 launches (A/B switch)
+GEMM_TAIL = __import__("os").environ.get("DINUNET_GEMM_TAIL", "1") == "1"
+
+
+def _tail_rows(M: int, N: int, K: int, tile: int, sp: int):
+    """First row ``r0`` of a tail launch when a one-split launch of 256 x 256 tiles (one
+    workgroup per CU) would end in a round of at most a quarter of the CUs: rows ``r0:`` then run
+    as a second launch of 64 x 64 tiles (B = 2048 ICA step: the encoder and input-gradient GEMMs
+    have 784 row tiles on 256 CUs = 3 full rounds + 16 tiles, a fourth round for 2 % of the
+    work; split along K instead, the tail's slab traffic and reduce cost about what the round
+    did).  None: launch as is."""
+    if not (GEMM_TAIL and tile == 2 and sp == 1 and K >= 512):
+        return None
+    tn = -(-N // 256)
+    tm = -(-M // 256)
+    tiles = tm * tn
+    if tiles <= _NCU:
+        return None
+    rem = tiles % _NCU
+    if rem == 0 or 4 * rem > _NCU:
+        return None
+    tail_m = -(-rem // tn)
+    r0 = (tm - tail_m) * 256
+    if r0 <= 0 or r0 >= M:
+        return None
+    return r0
 
 
 _ONES = {}

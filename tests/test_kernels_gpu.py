@@ -690,3 +690,61 @@ def test_gemm_rows_gathered_from_dataset(tile):
         with pytest.raises(ValueError):  # a transposed A cannot be gathered: never read stale rows
             G.mm(buf, dy, trans_a=True)
     assert torch.equal(y, ref_y) and torch.equal(dw, ref_dw) and torch.equal(gw, ref_dw)
+
+
+@pytest.mark.parametrize("case", ["mask", "bias_relu", "gather", "trans_a"])
+def test_gemm256_tail_rows_split(case):
+    """A 256 x 256 launch whose last round would hold a few tiles runs those rows as a row-range
+    view on 64 x 64 tiles (ops.gemm._tail_rows): the fp32 reference with every epilogue (mask,
+    bias + ReLU, bf16 out), with gathered A rows (RowGather r0) and a transposed A; the rows
+    before the tail are the same launch as without the split."""
+    from dinunet_implementations_amd.ops import gemm as G
+    g = torch.Generator(device=DEV).manual_seed(7)
+    M, N, K = 256 * 257 + 40, 256, 512      # 258 row tiles: the tail is rows 65536..
+    assert G._tail_rows(M, N, K, 2, 1) == 256 * 256
+    if case == "gather":
+        S, F = 98, K
+        n_subj = -(-M // S)
+        X = torch.randn((n_subj + 3) * S, F, device=DEV, generator=g).to(torch.bfloat16)
+        subj = torch.randperm(n_subj + 3, device=DEV, generator=g)[:n_subj + 1]
+        rows = (subj[:n_subj, None] * S + torch.arange(S, device=DEV)[None, :]).reshape(-1)[:M]
+        a_ref = X[rows].contiguous()
+        w = torch.randn(N, K, device=DEV, generator=g).to(torch.bfloat16)
+        bias = torch.randn(N, device=DEV, generator=g)
+        ref = torch.relu(a_ref.float() @ w.float().t() + bias)
+        buf = torch.zeros(n_subj * S, F, device=DEV, dtype=torch.bfloat16)[:M]
+        with G.rows_from(buf, X, subj, S):
+            out = G.mm(buf, w, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16, tile=2)
+        G.GEMM_TAIL = False
+        try:
+            plain = G.mm(a_ref, w, trans_b=True, bias=bias, relu=True, out_dtype=torch.bfloat16,
+                         tile=2)
+        finally:
+            G.GEMM_TAIL = True
+        assert rel(out, ref) < 1e-2 and rel(out, plain) < 1e-2
+        return
+    a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    b = torch.randn(K, N, device=DEV, generator=g).to(torch.bfloat16)
+    kw = {}
+    ref = a.float() @ b.float()
+    if case == "mask":
+        y = torch.relu(torch.randn(M, N, device=DEV, generator=g)).to(torch.bfloat16)
+        kw = dict(mask=y, out_dtype=torch.bfloat16)
+        ref = ref * (y.float() > 0)
+    elif case == "bias_relu":
+        bias = torch.randn(N, device=DEV, generator=g)
+        kw = dict(bias=bias, relu=True, out_dtype=torch.bfloat16)
+        ref = torch.relu(ref + bias)
+    elif case == "trans_a":
+        a = a.t().contiguous().t()  # a column-major view: A read transposed
+        kw = dict(out_dtype=torch.float32)
+    out = G.mm(a, b, tile=2, **kw)
+    G.GEMM_TAIL = False
+    try:
+        plain = G.mm(a, b, tile=2, **kw)
+    finally:
+        G.GEMM_TAIL = True
+    assert rel(out, ref) < 1e-2
+    head = 256 * 256
+    assert torch.equal(out[:head], plain[:head])  # rows before the tail: the same launch
+    assert rel(out[head:], plain[head:]) < 1e-2
