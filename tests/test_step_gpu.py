@@ -453,6 +453,40 @@ def test_powersgd_device_matches_reference_math():
             assert torch.allclose(x, y, rtol=1e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("rank", [4, 8, 16])
+def test_powersgd_device_many_layers_and_ranks(rank):
+    """More matrices than one low-rank launch indexes (20 > LR_KMAX = 16: the host cuts the table
+    into launches of 16 layers) and every rank bound of lr_gtp (4, 8, 16): the device PowerSGD
+    equals the torch-op algorithm over 2 steps of error feedback."""
+    import torch.nn as nn
+    from dinunet_implementations_amd.ops import FlatParams
+    from dinunet_implementations_amd.parallel import PowerSGDEngine
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    grp = SiteGroup(device=torch.device("cuda"))
+
+    def model():
+        torch.manual_seed(5)
+        dims = [96, 80, 64, 72, 96] * 4 + [96]
+        return nn.Sequential(*[nn.Linear(dims[i], dims[i + 1]) for i in range(20)]).cuda()
+    ma, mb = model(), model()
+    fa, fb = FlatParams(ma.parameters()), FlatParams(mb.parameters())
+    ea = PowerSGDEngine(ma, fa, grp, {"powersgd_rank": rank})
+    eb = PowerSGDEngine(mb, fb, grp, {"powersgd_rank": rank, "powersgd_device": False})
+    assert ea.fast and not eb.fast and len(ea.mats) == 20
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for _ in range(2):
+        gr = torch.randn(fa.grad.shape, device="cuda", generator=g)
+        fa.grad.copy_(gr)
+        fb.grad.copy_(gr)
+        ea.reduce()
+        eb.reduce()
+        torch.cuda.synchronize()
+        assert torch.allclose(fa.grad, fb.grad, rtol=1e-3, atol=1e-4), \
+            (fa.grad - fb.grad).abs().max()
+        for x, y in zip(ea.err, eb.err):
+            assert torch.allclose(x, y, rtol=1e-3, atol=1e-4)
+
+
 def test_powersgd_step_graph_matches_eager():
     xs, ys = _batches()
     _, fe, se = _trainer(0, engine="powerSGD", use_graph=False)

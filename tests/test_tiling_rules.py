@@ -82,3 +82,26 @@ def test_lstm_launchers_refuse_inconsistent_buffers():
                          None, 0, 1, None) == BAD
     assert L.dn_lstm_fwd(None, None, None, 32, 98, 192, 2, None, None, ctypes.c_void_p(16),
                          None, 1.0, None, None, None, 0, 1, None) == BAD
+
+
+def test_tail_rows_cut_only_a_mostly_idle_last_round():
+    """ops.gemm._tail_rows: a one-split 256 x 256 launch whose last round would fill at most a
+    quarter of the CUs runs those rows as a second launch (r0 = first tail row, a tile boundary);
+    full rounds, larger last rounds, split launches and other tiles launch as they are."""
+    from dinunet_implementations_amd.ops import gemm
+    ncu = gemm._NCU
+    M = 2048 * 98                                   # B = 2048 ICA rows: 784 row tiles
+    r0 = gemm._tail_rows(M, 256, 1536, 2, 1)
+    assert r0 == (784 - 784 % ncu) * 256 and r0 % 256 == 0
+    assert gemm._tail_rows(M, 1536, 256, 2, 1) is None      # projection: last round 37.5 % full
+    assert gemm._tail_rows(M, 256, 1536, 1, 1) is None      # not the 256 x 256 kernel
+    assert gemm._tail_rows(M, 256, 1536, 2, 4) is None      # split-K launches keep their slabs
+    assert gemm._tail_rows(256 * ncu * 3, 256, 1536, 2, 1) is None  # whole rounds
+    assert gemm._tail_rows(256 * 100, 256, 1536, 2, 1) is None      # one partial round only
+    assert gemm._tail_rows(M, 256, 128, 2, 1) is None       # short K: not worth a launch
+    old = gemm.GEMM_TAIL
+    try:
+        gemm.GEMM_TAIL = False
+        assert gemm._tail_rows(M, 256, 1536, 2, 1) is None
+    finally:
+        gemm.GEMM_TAIL = old
