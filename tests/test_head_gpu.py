@@ -93,7 +93,7 @@ def _compare(mods_fused, mods_ref, fused_fn, x, y, log_out, train=True, emulate=
     return xf, xr
 
 
-@pytest.mark.parametrize("B", [32, 7, 50, 65, 300, 2048])
+@pytest.mark.parametrize("B", [32, 7, 50, 65, 300, 2048, 5000])
 def test_ica_head_train_matches_modules(B):
     torch.manual_seed(0)
     head = _ica_head(p=0.0).to(DEV).train()
