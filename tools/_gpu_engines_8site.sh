@@ -10,7 +10,7 @@ for s in ${SEEDS:-0 1}; do
     port=$((port + 1))
     DINUNET_BACKEND=gloo timeout -k 10 ${RUNLIMIT:-280} python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
       --master-addr 127.0.0.1 --master-port $port tools/bench_time_to_auc.py --engine $e --cohort hard \
-      --signal 0.35 --subjects ${SUBJ:-384} --val 128 --batch 32 --max-steps ${STEPS:-600} --eval-every 50 \
+      --effect 0.35 --subjects ${SUBJ:-384} --val 128 --batch 32 --max-steps ${STEPS:-600} --eval-every 50 \
       --target 0.99 --full --seed $s > gpurun_out/e8_${e}_$s.log 2>&1 || { tail -30 gpurun_out/e8_${e}_$s.log; exit 3; }
     echo "{\"engine\": \"$e\", \"seed\": $s, \"sites\": 8, \"run\": $(grep '^{' gpurun_out/e8_${e}_$s.log | tail -1)}" >> $out
     python - "$out" <<'PY'
