@@ -1173,6 +1173,15 @@ static const long g_ring8_max = [] {
   return e ? atol(e) : 0L;
 }();
 
+// largest grid (exclusive) of 64 x 64 tiles that takes the 4-stage ring (DN_GEMM_RING4_MAX, default
+// 512: from there two workgroups per CU hold the 2-stage ring's tile in flight each; the B = 32
+// step's grouped weight gradients, 568 workgroups, took 26.7 vs 21.1 us on the 4-stage ring,
+// 0.3181-0.3192 vs 0.3107-0.3110 ms/step)
+static const long g_ring4_max = [] {
+  const char* e = getenv("DN_GEMM_RING4_MAX");
+  return e ? atol(e) : 512L;
+}();
+
 static int kchunk_for(int K, int& splits) {
   int kchunk = K;
   if (splits > 1) {
@@ -1214,7 +1223,7 @@ int launch(GemmGroup& g, hipStream_t st) {
         init = true;
       }
       hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 8>), grid, dim3(256), SM, st, g);
-    } else if (g.vec && g_gemm_dma && BM == 64 && wgs < 512)
+    } else if (g.vec && g_gemm_dma && BM == 64 && wgs < g_ring4_max)
       hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, 4>), grid, dim3(256),
                          (dma_smem<BM, BN, TA, TB, 4>()), st, g);
     else if (g.vec && g_gemm_dma)
