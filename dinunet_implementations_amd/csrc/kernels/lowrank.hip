@@ -357,7 +357,10 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, LrIndex ix, int it, float tol) {
 
 // Scaled Cholesky of the fp64 Gram gm (the lr_gtp_kernel factorisation), wave 0, unrolled to the
 // rank bound R >= r (R x R steps instead of LR_MAXR x LR_MAXR): Rh / Sv as lp_solve reads them.
-template <int R>
+// ALLW: every wave of the workgroup runs it (the same values: a benign LDS race) with branch-free
+// stores -- lanes >= LR_MAXR write the pad past Rh's LR_MAXR^2 entries / Sv's LR_MAXR, so the
+// factorisation shares a basic block with the caller's MFMAs and can issue under them
+template <int R, bool ALLW = false>
 __device__ __forceinline__ void lp_chol(const double* gm, float* Rh, float* Sv, int r, int lane) {
   const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
   double dmax = di;
@@ -380,14 +383,24 @@ __device__ __forceinline__ void lp_chol(const double* gm, float* Rh, float* Sv, 
     const float inv = dk ? 0.f : __builtin_amdgcn_rsqf(akk);
     dead |= dk ? 1u << k : 0u;
     const float rki = av[k] * inv;
-    if (lane < LR_MAXR) Rh[k * LR_MAXR + lane] = lane > k ? rki : (lane == k ? inv : 0.f);
+    const float rv = lane > k ? rki : (lane == k ? inv : 0.f);
+    if constexpr (ALLW)
+      Rh[lane < LR_MAXR ? k * LR_MAXR + lane : LR_MAXR * LR_MAXR + lane - LR_MAXR] = rv;
+    else if (lane < LR_MAXR)
+      Rh[k * LR_MAXR + lane] = rv;
     const float sk = rki * inv;
 #pragma unroll
     for (int jj = k + 1; jj < R; ++jj) av[jj] = __builtin_fmaf(-sk, rlane(av[jj], k), av[jj]);
   }
-  if (lane < LR_MAXR) Sv[lane] = lane < R ? (float)si : 0.f;
+  if constexpr (ALLW)
+    Sv[lane] = lane < R ? (float)si : 0.f;
+  else if (lane < LR_MAXR)
+    Sv[lane] = lane < R ? (float)si : 0.f;
 }
 
+// lp_chol<R, true> cut into its preamble and its R elimination steps, for a caller that
+// interleaves the steps with independent MFMAs by hand (the compiler kept the whole chain ahead
+// of them); same arithmetic, same stores
 // Forward substitution x <- x D^{-1/2} R_s^{-1} for one row held in registers, bounded by R
 // (entries >= R of x stay untouched: zero on entry, never read): Rh[k][m] = R_s[k][m] above the
 // diagonal, Rh[k][k] = 1 / R_s[k][k] (0 for a dropped column), zeros below; Sv = D^{-1/2}.
@@ -408,13 +421,6 @@ __device__ __forceinline__ void lp_solve(float (&x)[LR_MAXR], const float* Rh, c
 #pragma unroll
     for (int mm = jj + 1; mm < R; ++mm) x[mm] = __builtin_fmaf(-x[jj], rw[mm], x[mm]);
   }
-}
-__device__ __forceinline__ void lp_solve_r(float (&x)[LR_MAXR], const float* Rh, const float* Sv,
-                                           int r) {
-  if (r <= 4) lp_solve<4>(x, Rh, Sv);
-  else if (r <= 8) lp_solve<8>(x, Rh, Sv);
-  else if (r <= 12) lp_solve<12>(x, Rh, Sv);
-  else lp_solve<16>(x, Rh, Sv);
 }
 
 // grid = sum of n3, block 256: 16 columns of one layer per block, all rows.  Q[16 cols] =
@@ -850,6 +856,7 @@ __device__ __forceinline__ void lp_publish(__amdgpu_buffer_rsrc_t dst, const flo
 }
 
 
+template <int R>  // rank bound: r <= R in {4, 8, 12, 16} for every layer of the launch
 __global__ void __launch_bounds__(256)
 lr_persist_kernel(LpArgs a) {
   __shared__ __attribute__((aligned(16))) float stg[LP_LDS];        // Q (phase A) / P (phase B)
@@ -858,8 +865,8 @@ lr_persist_kernel(LpArgs a) {
   __shared__ float qold[LP_RB * 16 * LR_MAXR];  // my Q rows of the last commit
   __shared__ double gpart[4 * 256];
   __shared__ double gm[256];
-  __shared__ __attribute__((aligned(16))) float Rh[LR_MAXR * LR_MAXR];
-  __shared__ float Sv[LR_MAXR];
+  __shared__ __attribute__((aligned(16))) float Rh[LR_MAXR * LR_MAXR + 64 - LR_MAXR];
+  __shared__ float Sv[64];
   __shared__ float dq[2 * 4];
   const int l = blockIdx.x & (LP_MAXL - 1), j = blockIdx.x / LP_MAXL;
   if (l >= a.nl || j >= a.L[l].J) return;
@@ -1016,11 +1023,10 @@ lr_persist_kernel(LpArgs a) {
     gm[tid] = (tid < 16 * r) ? gpart[tid] + gpart[256 + tid] : 0.0;
     lp_sync();
     LP_STAMP(sb + 4);
-    if (w == 0) {  // scaled Cholesky of the Gram, wave 0, unrolled to the rank bound
-      if (r <= 4) lp_chol<4>(gm, Rh, Sv, r, lane);
-      else if (r <= 8) lp_chol<8>(gm, Rh, Sv, r, lane);
-      else if (r <= 12) lp_chol<12>(gm, Rh, Sv, r, lane);
-      else lp_chol<16>(gm, Rh, Sv, r, lane);
+    // R = 16: wave 0 factorises ahead of the P staging (every wave's copy beside the MFMAs would
+    // spill at that bound)
+    if constexpr (R > 12) {
+      if (w == 0) lp_chol<R>(gm, Rh, Sv, r, lane);
     }
 #pragma unroll
     for (int q = 0; q < PV; ++q) {
@@ -1029,9 +1035,12 @@ lr_persist_kernel(LpArgs a) {
     }
     if (pn4 > PV * 256)  // larger P: the rest in series
       lp_stage(stg + 4 * PV * 256, lp_rsrc(X.P + 4 * PV * 256), 4 * (pn4 - PV * 256), tid);
-    lp_sync();  // P staged, Rh / Sv visible
+    lp_sync();  // P staged
     LP_STAMP(sb + 8);
-    {  // H = G[:, my cols]^T P on the matrix cores (the WB waves of a column block meet in red)
+    {  // H = G[:, my cols]^T P on the matrix cores (the WB waves of a column block meet in red),
+       // with the scaled Cholesky of the Gram (every wave, identical values) in the same block:
+       // its readlane / VALU chain issues between the MFMAs instead of ahead of them in wave 0
+      if constexpr (R <= 12) lp_chol<R, true>(gm, Rh, Sv, r, lane);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < LP_GV; ++i) {
@@ -1060,6 +1069,7 @@ lr_persist_kernel(LpArgs a) {
       red[cb * WB * 256 + o] = v;
     }
     lp_sync();
+    LP_STAMP(sb + 9);
     float dd = 0.f, qq = 0.f;
     if (tid < ncol) {  // wave 0: one Q row per lane, H[col][:] D^{-1/2} R_s^{-1}
       const int cb = tid >> 4, i = tid & 15;
@@ -1068,7 +1078,7 @@ lr_persist_kernel(LpArgs a) {
       for (int e = 0; e < LR_MAXR; ++e) old[e] = e < r ? qold[tid * r + e] : 0.f;
 #pragma unroll
       for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? red[cb * WB * 256 + i * 16 + e] : 0.f;
-      lp_solve_r(x, Rh, Sv, r);
+      lp_solve<R>(x, Rh, Sv);
 #pragma unroll
       for (int e = 0; e < LR_MAXR; ++e) {
         if (e < r) {
@@ -1108,7 +1118,7 @@ lr_persist_kernel(LpArgs a) {
         const int row = 16 * rb0 + tid;
 #pragma unroll
         for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? stg[row * r + e] : 0.f;
-        lp_solve_r(x, Rh, Sv, r);
+        lp_solve<R>(x, Rh, Sv);
 #pragma unroll
         for (int e = 0; e < LR_MAXR; ++e)
           if (e < r) X.Psend[(long)row * r + e] = x[e];
@@ -1264,9 +1274,18 @@ DN_API int dn_lr_persist(const void* host_layers, int nl, int iters, float tol, 
   a.spin = dn_spin_limit(LP_SPIN);
   // members of a layer meet at barriers: every workgroup must be resident at once (else the
   // staged kernels, DN_UNSUPPORTED)
-  if (!dn_fits_resident(reinterpret_cast<const void*>(lr_persist_kernel), LP_MAXL * jmax, 256, 0))
+  int rmax = 1;
+  for (int l = 0; l < nl; ++l) rmax = a.L[l].X.r > rmax ? a.L[l].X.r : rmax;
+  const void* kfn = rmax <= 4 ? reinterpret_cast<const void*>(lr_persist_kernel<4>)
+                  : rmax <= 8 ? reinterpret_cast<const void*>(lr_persist_kernel<8>)
+                  : rmax <= 12 ? reinterpret_cast<const void*>(lr_persist_kernel<12>)
+                               : reinterpret_cast<const void*>(lr_persist_kernel<16>);
+  if (!dn_fits_resident(kfn, LP_MAXL * jmax, 256, 0))
     return DN_UNSUPPORTED;
-  hipLaunchKernelGGL(lr_persist_kernel, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
+  if (rmax <= 4) hipLaunchKernelGGL(lr_persist_kernel<4>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
+  else if (rmax <= 8) hipLaunchKernelGGL(lr_persist_kernel<8>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
+  else if (rmax <= 12) hipLaunchKernelGGL(lr_persist_kernel<12>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(lr_persist_kernel<16>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
   return dn_launch_status();
 }
 

@@ -24,6 +24,9 @@ ALLOWED = {
     # BR = 16 backward with a per-step output gradient (sequence-output mode, batch > 512 only;
     # the ICA model's temporal-mean mode does not spill)
     r"lstm_bwd_kernelILi192ELi16ELb1E": 96,
+    # rank-dAD's one-launch power iteration at rank bound 16 (ranks 13-16 only; the compspec
+    # default rank 10 takes the spill-free bound-12 kernel)
+    r"lr_persist_kernelILi16E": 64,
 }
 
 

@@ -3,7 +3,8 @@
 (lowrank.hip lr_persist_kernel), member 0 of every layer, ICA-LSTM headline geometry; plus the
 launch time by events.  Per iteration: A = Q staged + P = G Q, pub = P / Gram partials published,
 bar1 = first barrier, gram = partial sums + P staged, chol+H = Cholesky + G^T P, solve = Q rows /
-Psend published, bar2 = second barrier (us)."""
+Psend published (hsum: the G^T P partial sums of the column blocks first), bar2 = second
+barrier (us)."""
 import ctypes
 import os
 import sys
@@ -54,7 +55,7 @@ def main():
             d = lambda a_, b_: (row[sb + b_] - row[sb + a_]) / 100  # noqa: E731
             out.append(f"it{it} A={d(0, 1):.2f} pub={d(1, 2):.2f} bar1={d(2, 3):.2f} "
                        f"gram={d(3, 4):.2f} chol={d(4, 8):.2f} H={d(8, 5):.2f} "
-                       f"solve={d(5, 6):.2f} bar2={d(6, 7):.2f}")
+                       f"hsum={d(5, 9):.2f} solve={d(9, 6):.2f} bar2={d(6, 7):.2f}")
         print(" | ".join(out))
 
 
