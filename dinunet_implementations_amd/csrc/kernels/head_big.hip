@@ -125,17 +125,23 @@ __device__ __forceinline__ void bn_affine(const BArgs& a, const BLayer& P, const
   t = 0.f;
   if (!P.bn) return;
   const bool train = a.train != 0;
+  // the affine parameters and running statistics are loaded with the partials, not after the
+  // merge (each was one more dependent round trip before the first chunk)
+  const float gk = P.gamma[k], bk = P.beta[k];
+  const bool upd = leader && train && P.bn == 2;
+  const float rm0 = (upd || !(P.bn == 1 || train)) ? P.rmean[k] : 0.f;
+  const float rv0 = (upd || !(P.bn == 1 || train)) ? P.rvar[k] : 0.f;
   float mean, rstd;
   if (P.bn == 1 || train) {
     const F2* part = reinterpret_cast<const F2*>(ws + P.part_off);
     float cnt = 0.f, m2 = 0.f;
     mean = 0.f;
-    for (int r8 = 0; r8 < a.nrb; r8 += 8) {  // 8 partial loads in flight, merged in order
-      F2 qs[8];
+    for (int r8 = 0; r8 < a.nrb; r8 += 16) {  // 16 partial loads in flight, merged in order
+      F2 qs[16];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qs[i] = part[(long)min(r8 + i, a.nrb - 1) * P.out + k];
+      for (int i = 0; i < 16; ++i) qs[i] = part[(long)min(r8 + i, a.nrb - 1) * P.out + k];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 16; ++i) {
         const int rb = r8 + i;
         if (rb < a.nrb) {
           const float nb = (float)min(RB, a.B - rb * RB);
@@ -152,19 +158,18 @@ __device__ __forceinline__ void bn_affine(const BArgs& a, const BLayer& P, const
     rstd = rsqrtf(var + P.eps);
     if (leader) {
       reinterpret_cast<F2*>(wsw + P.stat_off)[k] = F2{mean, rstd};
-      if (train && P.bn == 2) {
+      if (upd) {
         const float mo = P.momentum;
-        P.rmean[k] = (1.f - mo) * P.rmean[k] + mo * mean;
-        P.rvar[k] = (1.f - mo) * P.rvar[k] +
-                    mo * var * ((float)a.B / (float)(a.B > 1 ? a.B - 1 : 1));
+        P.rmean[k] = (1.f - mo) * rm0 + mo * mean;
+        P.rvar[k] = (1.f - mo) * rv0 + mo * var * ((float)a.B / (float)(a.B > 1 ? a.B - 1 : 1));
       }
     }
   } else {
-    mean = P.rmean[k];
-    rstd = rsqrtf(P.rvar[k] + P.eps);
+    mean = rm0;
+    rstd = rsqrtf(rv0 + P.eps);
   }
-  s = P.gamma[k] * rstd;
-  t = P.beta[k] - mean * s;
+  s = gk * rstd;
+  t = bk - mean * s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -189,10 +194,26 @@ headb_fwd_kernel(BArgs a, int l, const float* __restrict__ x, long ldx,
   long ld = ldx;
   bool prelu = false;
   if (l > 0) {
-    const BLayer& P = a.L[l - 1];
-    src = reinterpret_cast<const float*>(ws + P.z_off);
+    src = reinterpret_cast<const float*>(ws + a.L[l - 1].z_off);
     ld = K;
-    prelu = P.relu != 0;
+    prelu = a.L[l - 1].relu != 0;
+  }
+  const int sr = tid >> 4, sq = (tid & 15) * 4;  // staging: 16 rows x 16 column quads per pass
+  // two chunks of raw input / weight values in registers ahead of the MFMAs, the first two issued
+  // before the BatchNorm prologue (they do not depend on it): at one chunk of prefetch the loop
+  // was a chain of K / 64 global round trips (21.6 us for the 768-wide layer at B = 2048).
+  float va0[4][4], vw0[4][4], va1[4][4], vw1[4][4];
+  auto load_chunk = [&](int kc, float (&va)[4][4], float (&vw)[4][4]) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      load4<VX>(src, ld, r0 + sr + 16 * p, kc + sq, B, K, va[p]);
+      load4<VW>(L.W, K, n0 + sr + 16 * p, kc + sq, N, K, vw[p]);
+    }
+  };
+  load_chunk(0, va0, vw0);
+  if (TB < K) load_chunk(TB, va1, vw1);
+  if (l > 0) {
+    const BLayer& P = a.L[l - 1];
     const bool leader = blockIdx.x == 0 && blockIdx.y == 0;
     for (int k = tid; k < K; k += BNT) {
       float s, t;
@@ -204,20 +225,8 @@ headb_fwd_kernel(BArgs a, int l, const float* __restrict__ x, long ldx,
   }
   bf16* aimg = reinterpret_cast<bf16*>(ws + L.a_off);
   const bool wimg = train && blockIdx.y == 0;
-  const int sr = tid >> 4, sq = (tid & 15) * 4;  // staging: 16 rows x 16 column quads per pass
   f32x4 acc[4] = {};
-  // chunk kc+TB's raw input / weight values are loaded into registers before chunk kc's MFMAs
-  // (one chunk of prefetch): the loop is a chain of global round trips otherwise
-  float va[4][4], vw[4][4];
-  auto load_chunk = [&](int kc) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      load4<VX>(src, ld, r0 + sr + 16 * p, kc + sq, B, K, va[p]);
-      load4<VW>(L.W, K, n0 + sr + 16 * p, kc + sq, N, K, vw[p]);
-    }
-  };
-  load_chunk(0);
-  for (int kc = 0; kc < K; kc += TB) {
+  auto stage = [&](int kc, const float (&va)[4][4], const float (&vw)[4][4]) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int row = sr + 16 * p, gr = r0 + row, k = kc + sq;
@@ -241,8 +250,8 @@ headb_fwd_kernel(BArgs a, int l, const float* __restrict__ x, long ldx,
       if (wimg && gr < B && k < L.S_a) *reinterpret_cast<bf16x4*>(aimg + (long)gr * L.S_a + k) = b4;
       *reinterpret_cast<bf16x4*>(Wt + row * LS + sq) = to_bf4(vw[p]);
     }
-    __syncthreads();
-    if (kc + TB < K) load_chunk(kc + TB);
+  };
+  auto mma = [&]() {
 #pragma unroll
     for (int ks = 0; ks < TB; ks += 32) {
       const int kk = ks + 8 * (lane >> 4);
@@ -253,6 +262,18 @@ headb_fwd_kernel(BArgs a, int l, const float* __restrict__ x, long ldx,
         acc[mt] = mfma16(av, bw, acc[mt]);
       }
     }
+  };
+  for (int kc = 0; kc < K; kc += 2 * TB) {
+    stage(kc, va0, vw0);
+    __syncthreads();
+    if (kc + 2 * TB < K) load_chunk(kc + 2 * TB, va0, vw0);
+    mma();
+    __syncthreads();
+    if (kc + TB >= K) break;
+    stage(kc + TB, va1, vw1);
+    __syncthreads();
+    if (kc + 3 * TB < K) load_chunk(kc + 3 * TB, va1, vw1);
+    mma();
     __syncthreads();
   }
   const int n = n0 + 16 * wid + (lane & 15);
@@ -299,6 +320,16 @@ headb_loss_kernel(BArgs a, const long long* __restrict__ y, float* __restrict__ 
   const float* Z = reinterpret_cast<const float*>(ws + L.z_off);
   float* g = reinterpret_cast<float*>(ws + a.g_off);
   const bool train = a.train != 0;
+  // the seed and the BatchNorm step counters are read here, not after the reductions: the tail
+  // of this one-workgroup launch was a chain of dependent global round trips
+  unsigned long long seed = 0ull;
+  long long nbt[BMAXL];
+  if (tid == 0 && train) {
+    seed = rng ? *rng : 0ull;
+#pragma unroll
+    for (int l = 0; l < BMAXL; ++l)
+      nbt[l] = (l < a.nl && a.L[l].bn == 2 && a.L[l].nbt) ? *a.L[l].nbt : 0;
+  }
   float ls = 0.f;
   float gs[16];
 #pragma unroll
@@ -361,11 +392,11 @@ headb_loss_kernel(BArgs a, const long long* __restrict__ y, float* __restrict__ 
     }
   }
   if (tid == 0 && train) {
-    const unsigned long long seed = rng ? *rng : 0ull;
     *reinterpret_cast<unsigned long long*>(ws) = seed;
     if (rng) *rng = seed + 1ull;
-    for (int l = 0; l < a.nl; ++l)
-      if (a.L[l].bn == 2 && a.L[l].nbt) *a.L[l].nbt += 1;
+#pragma unroll
+    for (int l = 0; l < BMAXL; ++l)
+      if (l < a.nl && a.L[l].bn == 2 && a.L[l].nbt) *a.L[l].nbt = nbt[l] + 1;
   }
 }
 
@@ -383,24 +414,28 @@ headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws) {
   float* cr = cf + 2 * N;
   F2* cs = reinterpret_cast<F2*>(cf + 3 * N);
   for (int c = tid; c < N; c += BNT) {
+    // everything this column needs is loaded before the partial sums are merged
+    const F2 st = stat[c];
+    const float gmc = L.gamma[c];
+    const float gg0 = blockIdx.x == 0 ? L.ggamma[c] : 0.f;
+    const float gb0 = blockIdx.x == 0 ? L.gbeta[c] : 0.f;
     float s1 = 0.f, s2 = 0.f;
-    for (int r8 = 0; r8 < a.nrb; r8 += 8) {  // 8 partial loads in flight, summed in order
-      F2 qs[8];
+    for (int r8 = 0; r8 < a.nrb; r8 += 16) {  // 16 partial loads in flight, summed in order
+      F2 qs[16];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qs[i] = part2[(long)min(r8 + i, a.nrb - 1) * N + c];
+      for (int i = 0; i < 16; ++i) qs[i] = part2[(long)min(r8 + i, a.nrb - 1) * N + c];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 16; ++i)
         if (r8 + i < a.nrb) {
           s1 += qs[i].x;
           s2 += qs[i].y;
         }
     }
     if (blockIdx.x == 0) {
-      L.ggamma[c] += s2;
-      L.gbeta[c] += s1;
+      L.ggamma[c] = gg0 + s2;
+      L.gbeta[c] = gb0 + s1;
     }
-    const F2 st = stat[c];
-    cA[c] = L.gamma[c] * st.y;
+    cA[c] = gmc * st.y;
     cm[c] = st.x;
     cr[c] = st.y;
     cs[c] = F2{s1 / (float)B, s2 / (float)B};
@@ -417,10 +452,10 @@ headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws) {
     const float A = cA[cc], m = cm[cc], rs = cr[cc];
     const F2 q = cs[cc];
     float sum = 0.f;
-    // rows in groups of 16 with every load of a group issued before its first use: a thread
+    // rows in groups of 32 with every load of a group issued before its first use: a thread
     // walks 64 rows of one column, and one dependent L2 round trip per row made this launch
-    // ~30 us at B = 2048
-    constexpr int RG = 16;
+    // ~30 us at B = 2048 (12.7 us at groups of 16)
+    constexpr int RG = 32;
     for (int rg = 0; rg < cnt; rg += RG) {
       float zv[RG], dv[RG];
 #pragma unroll
@@ -463,27 +498,42 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
   const int kb = job % nkb;
   const int k0 = kb * TB;
 
-  // rows [r0, r0 + RB) x columns [c0, c0 + TB) of dZ_l into T0 (bf16, zero outside)
-  auto stage_dz = [&](int r0, int c0, bool write_img) {
+  // rows [r0, r0 + RB) x columns [c0, c0 + TB) of dZ_l (bf16, zero outside): loaded into
+  // registers one chunk ahead of the MFMAs (load_dz), written to T0 when the chunk is staged
+  // (put_dz).  Both loops below were a chain of one global round trip per 64-wide chunk.
+  struct DzRegs {
+    float f[4][4];
+    bf16x4 h[4];
+  };
+  auto load_dz = [&](int r0, int c0, DzRegs& d) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int gr = r0 + sr + 16 * p, c = c0 + sq;
+      if constexpr (LAST) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = gr < B && c + e < N;
+          const float q = g[ok ? (long)gr * N + c + e : 0];
+          d.f[p][e] = ok ? q * gscale : 0.f;
+        }
+      } else {
+        const bool ok = gr < B && c < L.S_z;
+        const bf16x4 q = *reinterpret_cast<const bf16x4*>(dz + (ok ? (long)gr * L.S_z + c : 0));
+        const bf16x4 zero = {};
+        d.h[p] = ok ? q : zero;
+      }
+    }
+  };
+  auto put_dz = [&](int r0, int c0, const DzRegs& d, bool write_img) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int row = sr + 16 * p, gr = r0 + row, c = c0 + sq;
       bf16x4 b4;
       if constexpr (LAST) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bool ok = gr < B && c + e < N;
-          const float q = g[ok ? (long)gr * N + c + e : 0];
-          v[e] = ok ? q * gscale : 0.f;
-        }
-        b4 = to_bf4(v);
+        b4 = to_bf4(d.f[p]);
         if (write_img && gr < B && c < L.S_z) *reinterpret_cast<bf16x4*>(dz + (long)gr * L.S_z + c) = b4;
       } else {
-        const bool ok = gr < B && c < L.S_z;
-        const bf16x4 q = *reinterpret_cast<const bf16x4*>(dz + (ok ? (long)gr * L.S_z + c : 0));
-        const bf16x4 zero = {};
-        b4 = ok ? q : zero;
+        b4 = d.h[p];
       }
       *reinterpret_cast<bf16x4*>(T0 + row * LS + sq) = b4;
     }
@@ -492,17 +542,27 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
   if (dA_job) {
     const int rb = job / nkb, r0 = rb * RB;
     f32x4 acc[4] = {};
+    DzRegs dr;
+    float wv[4][4];
+    auto load_w = [&](int nc) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) load4<VW>(L.W, K, nc + sr + 16 * p, k0 + sq, N, K, wv[p]);
+    };
+    load_dz(r0, 0, dr);
+    load_w(0);
     for (int nc = 0; nc < N; nc += TB) {
-      stage_dz(r0, nc, LAST && kb == 0);
+      put_dz(r0, nc, dr, LAST && kb == 0);
 #pragma unroll
       for (int p = 0; p < 4; ++p) {  // T1[k][n] = W[nc + n][k0 + k]
         const int nl_ = sr + 16 * p;
-        float v[4];
-        load4<VW>(L.W, K, nc + nl_, k0 + sq, N, K, v);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) T1[(sq + e) * LS + nl_] = (bf16)v[e];
+        for (int e = 0; e < 4; ++e) T1[(sq + e) * LS + nl_] = (bf16)wv[p][e];
       }
       __syncthreads();
+      if (nc + TB < N) {  // (a load left in flight at the end holds the epilogue's registers)
+        load_dz(r0, nc + TB, dr);
+        load_w(nc + TB);
+      }
 #pragma unroll
       for (int ks = 0; ks < TB; ks += 32) {
         const int kk = ks + 8 * (lane >> 4);
@@ -583,17 +643,29 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
   const int rb0 = sp * a.nrb / RS, rb1 = (sp + 1) * a.nrb / RS;
   const bf16* aimg = reinterpret_cast<const bf16*>(ws + L.a_off);
   f32x4 acc[4] = {};
-  for (int r0 = rb0 * RB; r0 < rb1 * RB; r0 += RB) {
-    stage_dz(r0, n0, false);
+  DzRegs dr;
+  bf16x4 av4[4];
+  auto load_a = [&](int r0) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const int row = sr + 16 * p, gr = r0 + row, c = k0w + sq;
+      const int gr = r0 + sr + 16 * p, c = k0w + sq;
       const bool ok = gr < B && c < L.S_a;
       const bf16x4 q = *reinterpret_cast<const bf16x4*>(aimg + (ok ? (long)gr * L.S_a + c : 0));
       const bf16x4 zero = {};
-      *reinterpret_cast<bf16x4*>(T1 + row * LS + sq) = ok ? q : zero;
+      av4[p] = ok ? q : zero;
     }
+  };
+  load_dz(rb0 * RB, n0, dr);
+  load_a(rb0 * RB);
+  for (int r0 = rb0 * RB; r0 < rb1 * RB; r0 += RB) {
+    put_dz(r0, n0, dr, false);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) *reinterpret_cast<bf16x4*>(T1 + (sr + 16 * p) * LS + sq) = av4[p];
     __syncthreads();
+    if (r0 + RB < rb1 * RB) {
+      load_dz(r0 + RB, n0, dr);
+      load_a(r0 + RB);
+    }
 #pragma unroll
     for (int ks = 0; ks < RB; ks += 32) {
       const bf16x8 bf = tr_frag(T1, LS, 16 * wid, ks, lane);
@@ -622,12 +694,12 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
     } else {
       const float* dbp = reinterpret_cast<const float*>(ws + L.dbp_off);
       db = 0.f;
-      for (int r8 = 0; r8 < a.nrb; r8 += 8) {  // 8 loads in flight, summed in order
-        float qs[8];
+      for (int r8 = 0; r8 < a.nrb; r8 += 16) {  // 16 loads in flight, summed in order
+        float qs[16];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) qs[i] = dbp[(long)min(r8 + i, a.nrb - 1) * N + n];
+        for (int i = 0; i < 16; ++i) qs[i] = dbp[(long)min(r8 + i, a.nrb - 1) * N + n];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 16; ++i)
           if (r8 + i < a.nrb) db += qs[i];
       }
     }

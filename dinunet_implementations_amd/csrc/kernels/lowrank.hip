@@ -398,9 +398,6 @@ __device__ __forceinline__ void lp_chol(const double* gm, float* Rh, float* Sv, 
     Sv[lane] = lane < R ? (float)si : 0.f;
 }
 
-// lp_chol<R, true> cut into its preamble and its R elimination steps, for a caller that
-// interleaves the steps with independent MFMAs by hand (the compiler kept the whole chain ahead
-// of them); same arithmetic, same stores
 // Forward substitution x <- x D^{-1/2} R_s^{-1} for one row held in registers, bounded by R
 // (entries >= R of x stay untouched: zero on entry, never read): Rh[k][m] = R_s[k][m] above the
 // diagonal, Rh[k][k] = 1 / R_s[k][k] (0 for a dropped column), zeros below; Sv = D^{-1/2}.
