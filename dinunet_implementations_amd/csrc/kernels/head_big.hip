@@ -72,6 +72,7 @@ struct BLayer {
   long part2_off;  // F2 [nrb][out] per-row-block (sum dy, sum dy xhat)
   long dz_off;   // bf16 [B][S_z] d loss / d Z
   long dbp_off;  // fp32 [nrb][out] per-row-block column sums of dZ (bias gradient)
+  long dwp_off;  // fp32 [rs][out][in] row-split partial weight gradients of this layer
 };
 
 struct BArgs {
@@ -79,7 +80,35 @@ struct BArgs {
   int nl, B, nrb, train, log_out;
   long g_off;   // fp32 [B][C] p - onehot
   long gs_off;  // fp32 [16] its column sums
-  long dwp_off; // fp32 [rs][out][in] row-split partial weight gradients (one layer at a time)
+};
+
+// gW of layer l += its RS row-split partials, added in split order (deterministic); workgroup
+// `bid` of `nb`.  Run by the extra workgroups of the NEXT backward launch (each layer has its own
+// partials, so layer l-1's kernels do not overwrite them), or by headb_dw_reduce_kernel for the
+// first layer: a launch of its own is ~4.7 us of floor for a few microseconds of loads.
+__device__ __forceinline__ void dw_reduce_body(const BArgs& a, int l, const char* ws, int RS,
+                                               int bid, int nb) {
+  const BLayer& L = a.L[l];
+  const long NK = (long)L.out * L.in;
+  const float* part = reinterpret_cast<const float*>(ws + L.dwp_off);
+  for (long e = bid * 256L + threadIdx.x; e < NK; e += (long)nb * 256) {
+    float v = 0.f;
+    for (int s8 = 0; s8 < RS; s8 += 8) {  // 8 split loads in flight, added in split order
+      float qs[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qs[i] = part[min(s8 + i, RS - 1) * NK + e];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (s8 + i < RS) v += qs[i];
+    }
+    L.gW[e] += v;
+  }
+}
+
+// a pending reduce riding on a launch: layer rl (< 0: none) with rs splits, in the launch's
+// workgroups from r0 on
+struct RedJob {
+  int rl, rs, r0;
 };
 
 // Row splits of one layer's dW reduction: enough (tile, split) jobs for ~2 per CU, each split at
@@ -403,7 +432,11 @@ headb_loss_kernel(BArgs a, const long long* __restrict__ y, float* __restrict__ 
 // ---------------------------------------------------------------------------------------------
 // BatchNorm backward of layer l: dZ_l from dy_l and the merged column sums.
 __global__ void __launch_bounds__(BNT)
-headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws) {
+headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws, RedJob rj) {
+  if (rj.rl >= 0 && (int)blockIdx.x >= rj.r0) {
+    dw_reduce_body(a, rj.rl, ws, rj.rs, blockIdx.x - rj.r0, gridDim.x - rj.r0);
+    return;
+  }
   extern __shared__ float cf[];  // [4][N]: gamma rstd, mean, rstd, (sum dy) / B | (sum dy xhat) / B
   const BLayer& L = a.L[l];
   const int N = L.out, B = a.B, tid = threadIdx.x;
@@ -482,7 +515,11 @@ headb_bn_bwd_kernel(BArgs a, int l, char* __restrict__ ws) {
 template <bool LAST, bool VW>
 __global__ void __launch_bounds__(BNT)
 headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict__ dloss,
-                 float* __restrict__ dx, long lddx, int nA, int RS) {
+                 float* __restrict__ dx, long lddx, int nA, int RS, RedJob rj) {
+  if (rj.rl >= 0 && (int)blockIdx.x >= rj.r0) {
+    dw_reduce_body(a, rj.rl, ws, rj.rs, blockIdx.x - rj.r0, gridDim.x - rj.r0);
+    return;
+  }
   __shared__ __attribute__((aligned(16))) bf16 T0[RB * LS];
   __shared__ __attribute__((aligned(16))) bf16 T1[RB * LS];
   const BLayer& L = a.L[l];
@@ -675,7 +712,7 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
     __syncthreads();
   }
   const int k = k0w + 16 * wid + (lane & 15);
-  float* part = reinterpret_cast<float*>(ws + a.dwp_off) + (long)sp * N * K;
+  float* part = reinterpret_cast<float*>(ws + L.dwp_off) + (long)sp * N * K;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -707,24 +744,10 @@ headb_bwd_kernel(BArgs a, int l, char* __restrict__ ws, const float* __restrict_
   }
 }
 
-// gW of layer l += the RS row-split partials, added in split order (deterministic)
+// the first layer's reduce (nothing of the head runs after it)
 __global__ void __launch_bounds__(256)
 headb_dw_reduce_kernel(BArgs a, int l, const char* __restrict__ ws, int RS) {
-  const BLayer& L = a.L[l];
-  const long NK = (long)L.out * L.in;
-  const float* part = reinterpret_cast<const float*>(ws + a.dwp_off);
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < NK; e += (long)gridDim.x * 256) {
-    float v = 0.f;
-    for (int s8 = 0; s8 < RS; s8 += 8) {  // 8 split loads in flight, added in split order
-      float qs[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) qs[i] = part[min(s8 + i, RS - 1) * NK + e];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (s8 + i < RS) v += qs[i];
-    }
-    L.gW[e] += v;
-  }
+  dw_reduce_body(a, l, ws, RS, blockIdx.x, gridDim.x);
 }
 
 struct BPlan {
@@ -800,15 +823,13 @@ static bool bplan(int nl, const int* dims, const int* flags, const float* drops,
   off = al256(off + 4L * B * dims[nl]);
   a.gs_off = off;
   off = al256(off + 4L * 16);
-  long dwp = 0;
   for (int l = 0; l < nl; ++l) {
-    const BLayer& L = a.L[l];
+    BLayer& L = a.L[l];
     const int nkb = (L.in + TB - 1) / TB, nW = ((L.out + TB - 1) / TB) * nkb;
-    const long need = (long)dw_splits(nW, a.nrb) * L.out * L.in;
-    dwp = dwp > need ? dwp : need;
+    const int rs = dw_splits(nW, a.nrb);
+    L.dwp_off = off;
+    if (rs > 1) off = al256(off + 4L * rs * L.out * L.in);
   }
-  a.dwp_off = off;
-  off = al256(off + 4L * dwp);
   p.ws_bytes = off;
   return true;
 }
@@ -869,32 +890,51 @@ int headb_bwd(int nl, const int* dims, const int* flags, const float* drops, con
   }
   p.a.train = 1;
   p.a.log_out = 0;
+  RedJob pend{-1, 0, 0};  // the previous layer's reduce, carried by the next launch
+  long pend_blocks = 0;
+  auto take = [&](int r0, unsigned& grid) {
+    RedJob r = pend;
+    if (r.rl >= 0) {
+      r.r0 = r0;
+      grid += (unsigned)pend_blocks;
+    }
+    pend = RedJob{-1, 0, 0};
+    return r;
+  };
   for (int l = nl - 1; l >= 0; --l) {
     const BLayer& L = p.a.L[l];
-    if (l < nl - 1 && L.bn)
-      hipLaunchKernelGGL(headb_bn_bwd_kernel, dim3(p.a.nrb), dim3(BNT), 20 * L.out, st, p.a, l,
-                         (char*)ws);
+    if (l < nl - 1 && L.bn) {
+      unsigned g = (unsigned)p.a.nrb;
+      const RedJob rj = take(p.a.nrb, g);
+      hipLaunchKernelGGL(headb_bn_bwd_kernel, dim3(g), dim3(BNT), 20 * L.out, st, p.a, l,
+                         (char*)ws, rj);
+    }
     const int nkb = (L.in + TB - 1) / TB;
     const int nA = (l > 0 || dx) ? p.a.nrb * nkb : 0;
     const int nWt = ((L.out + TB - 1) / TB) * nkb;
     const int RS = dw_splits(nWt, p.a.nrb);
     const int nW = nWt * RS;
     const bool vw = L.in % 4 == 0;
-    const dim3 grid(nA + nW);
+    unsigned g = (unsigned)(nA + nW);
+    const RedJob rj = take(nA + nW, g);
+    const dim3 grid(g);
     if (l == nl - 1) {
-      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<true, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
-      else hipLaunchKernelGGL((headb_bwd_kernel<true, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
+      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<true, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS, rj);
+      else hipLaunchKernelGGL((headb_bwd_kernel<true, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS, rj);
     } else {
-      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<false, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
-      else hipLaunchKernelGGL((headb_bwd_kernel<false, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS);
+      if (vw) hipLaunchKernelGGL((headb_bwd_kernel<false, true>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS, rj);
+      else hipLaunchKernelGGL((headb_bwd_kernel<false, false>), grid, dim3(BNT), 0, st, p.a, l, (char*)ws, dloss, dx, lddx, nA, RS, rj);
     }
     if (RS > 1) {
       const long NK = (long)L.out * L.in;
       long blocks = (NK + 255) / 256;
       if (blocks > 1024) blocks = 1024;
-      hipLaunchKernelGGL(headb_dw_reduce_kernel, dim3((unsigned)blocks), dim3(BNT), 0, st, p.a, l,
-                         (const char*)ws, RS);
+      pend = RedJob{l, RS, 0};
+      pend_blocks = blocks;
     }
   }
+  if (pend.rl >= 0)
+    hipLaunchKernelGGL(headb_dw_reduce_kernel, dim3((unsigned)pend_blocks), dim3(BNT), 0, st, p.a,
+                       pend.rl, (const char*)ws, pend.rs);
   return dn_launch_status();
 }
