@@ -49,7 +49,9 @@ def test_lstm_backward_rows_tile_the_forward_padding():
             bf = int(L.dn_lstm_rows_per_wg(B, hd))
             bb = int(L.dn_lstm_rows_per_wg_bwd(B, hd))
             padded = -(-B // bf) * bf
-            assert -(-B // bb) * bb <= padded, (hd, B, bf, bb)
+            # the backward reads the forward's cell states with its own padded batch as the
+            # direction stride (lstm.hip bwd_recur): the two paddings must be EQUAL
+            assert -(-B // bb) * bb == padded, (hd, B, bf, bb)
     assert int(L.dn_lstm_rows_per_wg(2048, 192)) == 4 and int(L.dn_lstm_rows_per_wg_bwd(2048, 192)) == 8
     assert int(L.dn_lstm_rows_per_wg_bwd(1024, 192)) == 8
     assert int(L.dn_lstm_rows_per_wg_bwd(2044, 192)) == 4  # not a multiple of 8: same as forward
