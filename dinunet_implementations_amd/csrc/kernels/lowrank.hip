@@ -410,7 +410,7 @@ __device__ __forceinline__ void lp_solve(float (&x)[LR_MAXR], const float* Rh, c
   for (int jj = 0; jj < R; ++jj) {
     float rw[LR_MAXR];
 #pragma unroll
-    for (int q4 = 0; q4 < R / 4; ++q4) {
+    for (int q4 = 0; q4 < (R + 3) / 4; ++q4) {  // (entries >= R read, never used)
       const f32x4 v = reinterpret_cast<const f32x4*>(Rh + jj * LR_MAXR)[q4];
       rw[4 * q4] = v[0]; rw[4 * q4 + 1] = v[1]; rw[4 * q4 + 2] = v[2]; rw[4 * q4 + 3] = v[3];
     }
@@ -592,9 +592,10 @@ lr_gtp_kernel(const LrLayer* __restrict__ Ls, LrIndex ix, int it) {
 #pragma unroll
       for (int j = 0; j < LR_MAXR; ++j) x[j] = 0.f;
 #pragma unroll
-      for (int q4 = 0; q4 < R / 4; ++q4) {
+      for (int q4 = 0; q4 < (R + 3) / 4; ++q4) {
         const f32x4 v = reinterpret_cast<const f32x4*>(red + lane * 16)[q4];
-        x[4 * q4] = v[0]; x[4 * q4 + 1] = v[1]; x[4 * q4 + 2] = v[2]; x[4 * q4 + 3] = v[3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[4 * q4 + e] = 4 * q4 + e < R ? v[e] : 0.f;
       }
       lp_solve<R>(x, Rh, Sv);
       if (kv) {
@@ -1275,12 +1276,14 @@ DN_API int dn_lr_persist(const void* host_layers, int nl, int iters, float tol, 
   for (int l = 0; l < nl; ++l) rmax = a.L[l].X.r > rmax ? a.L[l].X.r : rmax;
   const void* kfn = rmax <= 4 ? reinterpret_cast<const void*>(lr_persist_kernel<4>)
                   : rmax <= 8 ? reinterpret_cast<const void*>(lr_persist_kernel<8>)
+                  : rmax <= 10 ? reinterpret_cast<const void*>(lr_persist_kernel<10>)
                   : rmax <= 12 ? reinterpret_cast<const void*>(lr_persist_kernel<12>)
                                : reinterpret_cast<const void*>(lr_persist_kernel<16>);
   if (!dn_fits_resident(kfn, LP_MAXL * jmax, 256, 0))
     return DN_UNSUPPORTED;
   if (rmax <= 4) hipLaunchKernelGGL(lr_persist_kernel<4>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
   else if (rmax <= 8) hipLaunchKernelGGL(lr_persist_kernel<8>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
+  else if (rmax <= 10) hipLaunchKernelGGL(lr_persist_kernel<10>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
   else if (rmax <= 12) hipLaunchKernelGGL(lr_persist_kernel<12>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(lr_persist_kernel<16>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
   return dn_launch_status();
