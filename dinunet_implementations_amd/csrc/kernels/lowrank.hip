@@ -854,7 +854,11 @@ __device__ __forceinline__ void lp_publish(__amdgpu_buffer_rsrc_t dst, const flo
 }
 
 
-template <int R>  // rank bound: r <= R in {4, 8, 12, 16} for every layer of the launch
+// R: rank bound, r <= R in {4, 8, 10, 12, 16} for every layer of the launch.  EX: every layer's
+// rank IS R (the default: one rank for all layers), so r is a compile-time constant and every
+// `e < r` below folds away -- with a run-time r the per-entry predicates were hoisted out of the
+// iteration loop and spilled (hundreds of SGPRs parked in VGPR lanes, reloaded per use).
+template <int R, bool EX>
 __global__ void __launch_bounds__(256)
 lr_persist_kernel(LpArgs a) {
   __shared__ __attribute__((aligned(16))) float stg[LP_LDS];        // Q (phase A) / P (phase B)
@@ -873,7 +877,7 @@ lr_persist_kernel(LpArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, kr = lane >> 4;
-  const int n = X.out, m = X.in, r = X.r, J = Y.J;
+  const int n = X.out, m = X.in, r = EX ? R : X.r, J = Y.J;
   const int cc = c < r ? c : 0;
   const float cmask = c < r ? 1.f : 0.f;
   // my row slice (phase A): row blocks [rb0, rb1), chunks (rb, ch) dealt to waves w, w+4, ...
@@ -1071,20 +1075,29 @@ lr_persist_kernel(LpArgs a) {
     float dd = 0.f, qq = 0.f;
     if (tid < ncol) {  // wave 0: one Q row per lane, H[col][:] D^{-1/2} R_s^{-1}
       const int cb = tid >> 4, i = tid & 15;
+      // unconditional clamped loads + selects, R (not LR_MAXR) entries: an `e < r ? load : 0`
+      // per entry compiled to a branch and a separate LDS wait each (predicates spilled to VGPR
+      // lanes), ~2 us of the phase
       float old[LR_MAXR], x[LR_MAXR];
 #pragma unroll
-      for (int e = 0; e < LR_MAXR; ++e) old[e] = e < r ? qold[tid * r + e] : 0.f;
+      for (int e = 0; e < LR_MAXR; ++e) old[e] = x[e] = 0.f;
 #pragma unroll
-      for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? red[cb * WB * 256 + i * 16 + e] : 0.f;
+      for (int e = 0; e < R; ++e) {
+        const float o = qold[tid * r + (e < r ? e : r - 1)];
+        const float h = red[cb * WB * 256 + i * 16 + e];
+        old[e] = e < r ? o : 0.f;
+        x[e] = e < r ? h : 0.f;
+      }
       lp_solve<R>(x, Rh, Sv);
 #pragma unroll
-      for (int e = 0; e < LR_MAXR; ++e) {
-        if (e < r) {
-          dd += (x[e] - old[e]) * (x[e] - old[e]);
-          qq += x[e] * x[e];
-          mine[tid * r + e] = x[e];
-        }
+      for (int e = 0; e < R; ++e) {
+        const float d = e < r ? x[e] - old[e] : 0.f, q = e < r ? x[e] : 0.f;
+        dd += d * d;
+        qq += q * q;
       }
+#pragma unroll
+      for (int e = 0; e < R; ++e)
+        if (e < r) mine[tid * r + e] = x[e];
     }
     dd = wave_sum(dd);
     qq = wave_sum(qq);
@@ -1115,10 +1128,15 @@ lr_persist_kernel(LpArgs a) {
         float x[LR_MAXR];
         const int row = 16 * rb0 + tid;
 #pragma unroll
-        for (int e = 0; e < LR_MAXR; ++e) x[e] = e < r ? stg[row * r + e] : 0.f;
+        for (int e = 0; e < LR_MAXR; ++e) x[e] = 0.f;
+#pragma unroll
+        for (int e = 0; e < R; ++e) {
+          const float v = stg[row * r + (e < r ? e : r - 1)];
+          x[e] = e < r ? v : 0.f;
+        }
         lp_solve<R>(x, Rh, Sv);
 #pragma unroll
-        for (int e = 0; e < LR_MAXR; ++e)
+        for (int e = 0; e < R; ++e)
           if (e < r) X.Psend[(long)row * r + e] = x[e];
       }
       break;
@@ -1272,20 +1290,23 @@ DN_API int dn_lr_persist(const void* host_layers, int nl, int iters, float tol, 
   a.spin = dn_spin_limit(LP_SPIN);
   // members of a layer meet at barriers: every workgroup must be resident at once (else the
   // staged kernels, DN_UNSUPPORTED)
-  int rmax = 1;
-  for (int l = 0; l < nl; ++l) rmax = a.L[l].X.r > rmax ? a.L[l].X.r : rmax;
-  const void* kfn = rmax <= 4 ? reinterpret_cast<const void*>(lr_persist_kernel<4>)
-                  : rmax <= 8 ? reinterpret_cast<const void*>(lr_persist_kernel<8>)
-                  : rmax <= 10 ? reinterpret_cast<const void*>(lr_persist_kernel<10>)
-                  : rmax <= 12 ? reinterpret_cast<const void*>(lr_persist_kernel<12>)
-                               : reinterpret_cast<const void*>(lr_persist_kernel<16>);
+  int rmax = 1, rmin = 1 << 30;
+  for (int l = 0; l < nl; ++l) {
+    rmax = a.L[l].X.r > rmax ? a.L[l].X.r : rmax;
+    rmin = a.L[l].X.r < rmin ? a.L[l].X.r : rmin;
+  }
+  const int rb = rmax <= 4 ? 4 : rmax <= 8 ? 8 : rmax <= 10 ? 10 : rmax <= 12 ? 12 : 16;
+  const bool ex = rmin == rmax && rmax == rb;
+  const void* kfn = nullptr;
+  void (*kl)(LpArgs) = nullptr;
+#define LP_PICK(RB_)                                                              \
+  if (rb == RB_) kl = ex ? lr_persist_kernel<RB_, true> : lr_persist_kernel<RB_, false>;
+  LP_PICK(4) LP_PICK(8) LP_PICK(10) LP_PICK(12) LP_PICK(16)
+#undef LP_PICK
+  kfn = reinterpret_cast<const void*>(kl);
   if (!dn_fits_resident(kfn, LP_MAXL * jmax, 256, 0))
     return DN_UNSUPPORTED;
-  if (rmax <= 4) hipLaunchKernelGGL(lr_persist_kernel<4>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
-  else if (rmax <= 8) hipLaunchKernelGGL(lr_persist_kernel<8>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
-  else if (rmax <= 10) hipLaunchKernelGGL(lr_persist_kernel<10>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
-  else if (rmax <= 12) hipLaunchKernelGGL(lr_persist_kernel<12>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(lr_persist_kernel<16>, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(kl, dim3(LP_MAXL * jmax), dim3(256), 0, st, a);
   return dn_launch_status();
 }
 

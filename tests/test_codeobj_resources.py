@@ -24,9 +24,10 @@ ALLOWED = {
     # BR = 16 backward with a per-step output gradient (sequence-output mode, batch > 512 only;
     # the ICA model's temporal-mean mode does not spill)
     r"lstm_bwd_kernelILi192ELi16ELb1E": 96,
-    # rank-dAD's one-launch power iteration at rank bound 16 (ranks 13-16 only; the compspec
-    # default rank 10 takes the spill-free bound-12 kernel)
-    r"lr_persist_kernelILi16E": 64,
+    # rank-dAD's one-launch power iteration at rank bound 16 with MIXED per-layer ranks (some
+    # layer above 12; one rank for all layers takes the spill-free exact-rank kernels, the
+    # compspec default rank 10 among them)
+    r"lr_persist_kernelILi16ELb0E": 192,
 }
 
 
