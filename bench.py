@@ -66,9 +66,10 @@ def parse():
                     help="site-loop cohort size (split 0.8/0.1/0.1)")
     ap.add_argument("--tta-epochs", type=int, default=30)
     ap.add_argument("--collective", default="auto",
-                    choices=["auto", "allreduce", "direct", "calibrate"],
-                    help="dSGD site-mean form (dsgd_collective); calibrate = time both, keep the "
-                         "faster")
+                    choices=["auto", "allreduce", "direct", "peer", "calibrate"],
+                    help="site-mean form (dsgd_collective): RCCL all-reduce, RCCL all-to-all "
+                         "exchange, the IPC peer exchange (parallel/peer.py), or calibrate = time "
+                         "the captured all-reduce and peer exchange, keep the faster")
     ap.add_argument("--loopback-rccl", action="store_true",
                     help="one GPU, but through a one-rank RCCL group marked distributed: the "
                          "N > 1 step (split backward, bucketed all-reduce, captured collectives) "
@@ -254,9 +255,9 @@ def main():
             "final_loss": round(loss, 5),
             # N > 1 code path: collectives captured inside the K-step graphs (runtime.step)
             "comm_graph": bool(getattr(step, "comm_graph", False)),
-            "collective": ((getattr(engine, "calibration", None)
-                            or ("direct" if engine.direct else "allreduce"))
-                           if args.engine == "dSGD" else None),
+            "collective": (getattr(engine, "calibration", None)
+                           or ("peer" if engine.peer else
+                               "direct" if getattr(engine, "direct", False) else "allreduce")),
             "split_backward": bool(getattr(step, "split", False)),
             **({"dad_iters_per_step": iters} if iters is not None else {}),
             # HBM high-water mark of the run (allocator view: model, optimizer state, activations,

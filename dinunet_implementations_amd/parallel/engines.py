@@ -41,6 +41,9 @@ from .lowrank import LowRankTable, _mgs_torch_, dad_factors, orthonormalize_
 Tensor = torch.Tensor
 
 
+COLLECTIVES = ("auto", "allreduce", "direct", "peer", "calibrate")
+
+
 class Engine:
     name = "base"
 
@@ -55,16 +58,48 @@ class Engine:
         self.half = self.wire != "fp32"
         self.comm_bytes = 0  # payload bytes this site sent in the last reduce (observability)
         self._means: Dict[Tuple[int, int], DirectMean] = {}
+        # ``dsgd_collective``: the site-mean form of every engine -- "allreduce" (RCCL / gloo),
+        # "direct" (all-to-all + fp32 sum + all-gather through the process group), "peer" (the
+        # IPC-mapped HBM exchange of parallel/peer.py: kernels only, captured in the step's
+        # graph on any backend), "auto" (peer for 16-bit wires on GPU sites -- the fp32-sum form
+        # the reference's 16-bit payloads need, captured -- else all-reduce), "calibrate"
+        # (dSGD: measured; the low-rank engines take auto's choice)
+        coll = str(self.cfg.get("dsgd_collective", "auto"))
+        if coll not in COLLECTIVES:
+            raise ValueError(f"dsgd_collective {coll!r}: expected one of {', '.join(COLLECTIVES)}")
+        self.collective = coll
+        self.peer = self._want_peer(coll)
+
+    def _peer_ok(self) -> bool:
+        from . import peer as _peer
+        return _peer.available(self.group, self.flat.grad.device)
+
+    def _want_peer(self, coll: str) -> bool:
+        if not self.group.distributed:
+            return False
+        if coll == "peer":
+            if not self._peer_ok():
+                raise ValueError("dsgd_collective='peer' needs GPU sites and the kernel library "
+                                 f"(at most 16 sites); device {self.flat.grad.device}")
+            return True
+        return coll in ("auto", "calibrate") and self.half and self._peer_ok()
 
     # collective path -------------------------------------------------------------------------
     @property
     def capturable(self) -> bool:
         """Can the step capture this engine's collectives in its HIP graph
-        (``runtime.step.TrainStep.comm_graph``)?  Not when a site-mean goes through the direct
-        exchange (16-bit wires, ``collective.DirectMean``): RCCL's all-to-all captured from the
-        exchange's own stream crashes at capture end (``tools/diag/capture_collectives.py``
-        a2a_side, RCCL 2.26.6), so those steps keep host-issued collectives."""
-        return not self.half
+        (``runtime.step.TrainStep.comm_graph``)?  Always with the peer exchange (its kernels are
+        ordinary launches on the step's stream, whatever the process group); with RCCL for the
+        fp32 all-reduce; not for host collectives (gloo) nor for RCCL's all-to-all exchange
+        (captured from the exchange's own stream it crashed at capture end,
+        ``tools/diag/capture_collectives.py`` a2a_side, RCCL 2.26.6)."""
+        if not self.group.distributed or self.peer:
+            return True
+        return self.group.backend == "nccl" and not self.half
+
+    def _peer_mean(self, tag, n: int):
+        from . import peer as _peer
+        return _peer.mean(self.group, self.flat.grad.device, n, self.wire, (self.name,) + tuple(tag))
 
     def step_context(self):
         return contextlib.nullcontext()
@@ -99,18 +134,33 @@ class Engine:
             dm = self._means[key] = DirectMean(self.group, n, self.wire, device)
         return dm
 
-    def _allreduce_mean_(self, buf: Tensor):
-        """In-place mean over sites, honouring ``precision_bits`` / ``payload_dtype``: a 16-bit
-        payload goes through the direct exchange (fp32 accumulation, collective.DirectMean)."""
+    def _allreduce_mean_(self, buf: Tensor, tag=("mean",)):
+        """In-place mean over sites, honouring ``precision_bits`` / ``payload_dtype``: the peer
+        exchange when selected (``tag`` names the exchange region: exchanges that may be in
+        flight together need their own), else a 16-bit payload goes through the direct exchange
+        (fp32 accumulation, collective.DirectMean) and fp32 through the all-reduce."""
         g = self.group
         if not g.distributed:
             return
-        if self.half:
+        if self.peer:
+            self.comm_bytes += self._peer_mean(tag, buf.numel()).run_(buf)
+        elif self.half:
             self.comm_bytes += self._direct(("mean", buf.numel()), buf.numel(), buf.device).run_(buf)
         else:
             g.all_reduce(buf)
             buf.mul_(1.0 / g.world)
             self.comm_bytes += buf.numel() * 4
+
+
+class _PeerWork:
+    """``Work``-like handle of a pushed peer exchange: ``wait()`` issues its reduce + unpack on
+    the current stream."""
+
+    def __init__(self, pm, view: Tensor, scale: float = 1.0):
+        self.pm, self.view, self.scale = pm, view, scale
+
+    def wait(self):
+        self.pm.finish(self.view, self.scale)
 
 
 # =============================================================================================
@@ -156,19 +206,19 @@ class DSGDEngine(Engine):
             self._expected[self._param_bucket[id(p)]] += 1
         self._handles: Dict[int, object] = {}
         self._half_bufs: Dict[int, Tensor] = {}
-        # ``dsgd_collective``: "direct" = all_to_all + fp32 sum + all_gather (collective.py) on a
-        # comm stream of its own; "allreduce" = one RCCL all-reduce per bucket (a 16-bit payload
-        # is then SUMMED in 16 bits inside RCCL); "auto" = direct for 16-bit payloads;
-        # "calibrate" = whichever of the two measures faster on this job's buckets and links
-        coll = str(self.cfg.get("dsgd_collective", "auto"))
-        if coll not in ("auto", "direct", "allreduce", "calibrate"):
-            raise ValueError(f"dsgd_collective {coll!r}: expected auto, direct, allreduce or "
-                             "calibrate")
+        # ``dsgd_collective``: "peer" = the IPC-mapped HBM exchange (peer.py: push / fp32 sum /
+        # push back, captured in the step graph); "direct" = all_to_all + fp32 sum + all_gather
+        # (collective.py) on a comm stream of its own; "allreduce" = one RCCL all-reduce per
+        # bucket (a 16-bit payload is then SUMMED in 16 bits inside RCCL); "auto" = peer for
+        # 16-bit payloads on GPU sites (direct off the GPU), all-reduce for fp32; "calibrate" =
+        # whichever captured form measures faster on this job's buckets and links
+        coll = self.collective
         self.calibration: Optional[dict] = None
         if coll == "calibrate":
             coll = self._calibrate()
-        self.direct = coll == "direct" or (coll == "auto" and self.half)
-        if self.half and not self.direct and self.wire == "fp16":
+            self.peer = coll == "peer"
+        self.direct = (not self.peer) and (coll == "direct" or (coll == "auto" and self.half))
+        if self.half and not self.direct and not self.peer and self.wire == "fp16":
             # RCCL sums an all-reduce buffer in its own type: unscaled fp16 would flush
             # gradients below ~6e-8 and overflow past 65504 in the sum over sites, and a
             # per-site block scale cannot be summed.  The 16-bit all-reduce therefore ships
@@ -196,49 +246,54 @@ class DSGDEngine(Engine):
 
     @property
     def capturable(self) -> bool:
-        return not self.direct  # all-reduce buckets (fp32, or the 16-bit all-reduce) capture
+        # the peer exchange always; RCCL all-reduce buckets (fp32, or the 16-bit all-reduce)
+        if not self.group.distributed or self.peer:
+            return True
+        return self.group.backend == "nccl" and not self.direct
 
     def _calibrate(self) -> str:
-        """``dsgd_collective="calibrate"``: time both site-mean forms on THIS job's buckets and
-        links and keep the faster -- the choice the link model of ``profiles/r4_comm_model.md``
-        could only predict (it depends on per-hop latency and link rates nobody had measured).
+        """``dsgd_collective="calibrate"``: time the site-mean forms the step can run on THIS
+        job's buckets and links and keep the faster -- the choice the link model of
+        ``profiles/r4_comm_model.md`` could only predict (per-hop latency and link rates).
 
-        Both forms are timed host-issued over every bucket: the RCCL all-reduce and the direct
-        exchange (all-to-all + fp32 sum + all-gather, ``collective.DirectMean``).  The step then
-        captures the all-reduce in its HIP graph (``TrainStep.comm_graph``), which only removes
-        host time from it, so a tie or a near-tie still favours the all-reduce.  (A capture here,
-        at process-group start, aborted RCCL's watchdog on an event recorded in the capturing
-        stream, ``hipErrorCapturedEvent``.)  The per-form times are max-reduced over the sites, so every site takes the same decision
-        from the same numbers; the record lands in ``self.calibration`` (``logs.json``
-        ``dsgd_collective``).  ``dsgd_calibrate_reps`` (default 10) timed repetitions."""
+        Each candidate is timed in the form the step will run it: the bucket sequence captured
+        in a HIP graph and replayed (``TrainStep.comm_graph`` captures the collectives into the
+        step), except an all-reduce over a host backend (gloo), which the step issues from the
+        host and which is timed so.  Candidates: the all-reduce and the peer exchange
+        (``parallel.peer``, GPU sites).  Only forms with the SAME arithmetic compete: a 16-bit
+        wire takes the fp32-sum exchange without a race (peer on GPU sites, else direct) --
+        RCCL's all-reduce would sum 16-bit partials, so a timing could change the training
+        numerics.  The per-form times are max-reduced over the sites, so every site takes the
+        same decision from the same numbers; the record lands in ``self.calibration``
+        (``logs.json`` ``dsgd_collective``).  ``dsgd_calibrate_reps`` (default 10) timed
+        replays."""
         import time as _time
         g = self.group
         sizes = [e - s for s, e in self.buckets]
         if not g.distributed:
             self.calibration = {"choice": "allreduce", "reason": "one site: no collective"}
             return "allreduce"
-        if self.half and self.wire == "fp16":
-            self.calibration = {"choice": "direct",
-                                "reason": "fp16 wire: only the direct exchange sums in fp32"}
-            return "direct"
+        peer_ok = self._peer_ok()
+        if self.half:
+            choice = "peer" if peer_ok else "direct"
+            self.calibration = {"choice": choice, "wire": self.wire,
+                                "reason": "16-bit wire: only the exchange sums in fp32"}
+            return choice
         dev = self.flat.grad.device
         cuda = dev.type == "cuda"
         reps = max(1, int(self.cfg.get("dsgd_calibrate_reps", 10)))
         sync = torch.cuda.synchronize if cuda else (lambda: None)
-        wdt = PAYLOAD_TYPES[self.wire][1] if self.half else torch.float32
-        ar_bufs = [torch.zeros(n, dtype=wdt, device=dev) for n in sizes]
-        dm_bufs = [torch.zeros(n, dtype=torch.float32, device=dev) for n in sizes]
-        means = [self._direct((s, e), e - s, dev) for s, e in self.buckets]
+        bufs = [torch.zeros(n, dtype=torch.float32, device=dev) for n in sizes]
 
         def allreduce():
-            for b in ar_bufs:
+            for b in bufs:
                 g.all_reduce(b)
 
-        def direct():
-            for dm, b in zip(means, dm_bufs):
-                dm.run_(b)
+        def peer():
+            for (s, e), b in zip(self.buckets, bufs):
+                self._peer_mean(("bucket", s, e), e - s).run_(b)
 
-        def timed(fn):
+        def host_timed(fn):
             for _ in range(2):
                 fn()
             sync()
@@ -249,20 +304,35 @@ class DSGDEngine(Engine):
             sync()
             return (_time.perf_counter() - t0) / reps * 1e6
 
-        t = torch.tensor([timed(allreduce), timed(direct)], dtype=torch.float64,
-                         device=dev if g.backend == "nccl" else "cpu")
-        g.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_ar, t_dm = (float(v) for v in t.cpu())
-        if g.backend == "nccl":
-            # let RCCL's watchdog retire the calibration's finished collectives before anything
-            # captures: it polls their (pooled) events every ~100 ms, and a pooled event reused
-            # by a captured collective while the watchdog still holds the old work aborts the
-            # process (hipErrorCapturedEvent, seen on the bench's first capture after this)
+        def graph_timed(fn):
+            fn()  # eager once (RCCL communicator / peer regions set up outside the capture)
             sync()
-            _time.sleep(0.5)
-        choice = "direct" if t_dm < t_ar else "allreduce"
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+                fn()
+            gr.replay()
+            sync()
+            g.barrier()
+            t0 = _time.perf_counter()
+            for _ in range(reps):
+                gr.replay()
+            sync()
+            t = (_time.perf_counter() - t0) / reps * 1e6
+            g.barrier()
+            del gr
+            return t
+
+        rccl_graph = cuda and g.backend == "nccl"
+        times = [graph_timed(allreduce) if rccl_graph else host_timed(allreduce),
+                 graph_timed(peer) if peer_ok else float("inf")]
+        t = torch.tensor(times, dtype=torch.float64, device=dev if g.backend == "nccl" else "cpu")
+        g.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_ar, t_peer = (float(v) for v in t.cpu())
+        choice = "peer" if t_peer < t_ar else "allreduce"
         self.calibration = {"choice": choice, "allreduce_us": round(t_ar, 2),
-                            "direct_us": round(t_dm, 2), "form": "host-issued",
+                            "peer_us": round(t_peer, 2) if peer_ok else None,
+                            "allreduce_form": "captured" if rccl_graph else "host-issued",
+                            "peer_form": "captured" if peer_ok else "unavailable",
                             "bucket_elems": sizes, "sites": g.world, "reps": reps,
                             "wire": self.wire}
         return choice
@@ -333,7 +403,14 @@ class DSGDEngine(Engine):
             self.comm_bytes = 0
         s, e = self.buckets[b]
         view = self.flat.grad[s:e]
-        if self.direct:
+        if self.peer:
+            # push now (no wait: the peers' data travel under the rest of the backward), reduce
+            # + unpack when reduce() waits, in bucket order
+            pm = self._peer_mean(("bucket", s, e), e - s)
+            pm.start(view)
+            self._handles[b] = _PeerWork(pm, view)
+            self.comm_bytes += pm.bytes_sent
+        elif self.direct:
             dm = self._direct((s, e), e - s, view.device)
             self._handles[b] = launch_on(self._comm_stream, lambda: dm.run_(view))
             self.comm_bytes += dm.n * dm.send.element_size()
@@ -371,12 +448,13 @@ class DSGDEngine(Engine):
         self._drain()
         for b, h in self._handles.items():
             h.wait()
-            if self.half and not self.direct:
+            if self.half and not self.direct and not self.peer:
                 s, e = self.buckets[b]
                 buf = self._half_bufs[b]
                 from_payload(buf, self.flat.grad[s:e])
         self._reset()
-        self.last_scale = 1.0 if self.direct else 1.0 / g.world  # the direct exchange leaves the mean
+        # the exchanges leave the mean, the all-reduce the sum
+        self.last_scale = 1.0 if (self.direct or self.peer) else 1.0 / g.world
         return self.last_scale
 
     def close(self):
@@ -530,11 +608,37 @@ class RankDADEngine(Engine):
         ``dad_tol`` stop decided on the device: no host sync, HIP-graph capturable."""
         if not self.fast or not self.fast_layers:
             return
+        self._dense_start()  # (peer) the dense part travels under the power iteration
         if self._persist_ok and self._table.persist(max(1, self.iters), self.tol):
             return  # every iteration in one launch (lr_persist_kernel)
         for it in range(max(1, self.iters)):
             self._table.gq(it, self.tol)
             self._table.orth_gtp(it)
+
+    def _dense_view(self) -> Tensor:
+        """The dense (dSGD-mean) part of the gradient as one contiguous fp32 range: the flat
+        range itself, or gathered into ``_dense_buf`` (scatter back with ``_dense_back``)."""
+        grad = self.flat.grad
+        if self._dense_idx is None:
+            a, b = self._dense_ranges[0]
+            return grad[a:b]
+        torch.index_select(grad, 0, self._dense_idx, out=self._dense_buf)
+        return self._dense_buf
+
+    def _dense_back(self, buf: Tensor):
+        if self._dense_idx is not None:
+            self.flat.grad.index_copy_(0, self._dense_idx, buf)
+
+    def _dense_start(self):
+        """Peer exchange: push the dense part right after the backward (no wait), so it crosses
+        the links while the power iteration runs; ``_fast_reduce`` finishes it."""
+        self._dense_pending = None
+        if not (self.peer and self.group.distributed and self._dense_ranges):
+            return
+        buf = self._dense_view()
+        pm = self._peer_mean(("dense",), buf.numel())
+        pm.start(buf)
+        self._dense_pending = (pm, buf)
 
     def power_iterations(self) -> Optional[List[int]]:
         """Cumulative power iterations each factorised layer ran on the device (``dad_tol``
@@ -547,19 +651,27 @@ class RankDADEngine(Engine):
         g = self.group
         W = g.world
         self.comm_bytes = 0
-        if g.distributed and self._dense_ranges:
-            grad = self.flat.grad
-            if self._dense_idx is None:
-                a, b = self._dense_ranges[0]
-                self._allreduce_mean_(grad[a:b])
-            else:
-                torch.index_select(grad, 0, self._dense_idx, out=self._dense_buf)
-                self._allreduce_mean_(self._dense_buf)
-                grad.index_copy_(0, self._dense_idx, self._dense_buf)
+        # (not consumed: a pre_reduce captured in a graph pushes at every replay, and every
+        # reduction after it finishes that push)
+        pend = getattr(self, "_dense_pending", None)
+        if pend is not None:  # pushed before the power iteration (peer)
+            pm, buf = pend
+            pm.finish(buf)
+            self._dense_back(buf)
+            self.comm_bytes += pm.bytes_sent
+        elif g.distributed and self._dense_ranges:
+            buf = self._dense_view()
+            self._allreduce_mean_(buf, tag=("dense",))
+            self._dense_back(buf)
         if not self.fast_layers:
             return 1.0
         if g.distributed:
-            if self.half:  # factors on the wire in the payload type, reconstructed in fp32
+            if self.peer:  # one-sided writes into every site's gather slot (fp32 out)
+                from . import peer as _peer
+                pg = _peer.gather(g, self.flat.grad.device, self._send.numel(), self.wire,
+                                  ("rankDAD", "factors"))
+                self.comm_bytes += pg.run(self._send, self._gathered, self._send.numel())
+            elif self.half:  # factors on the wire in the payload type, reconstructed in fp32
                 n = self._send.numel()
                 to_payload(self._send, self._send16, 1, n)
                 g.all_gather_into(self._gathered16, self._send16)
@@ -778,19 +890,29 @@ class PowerSGDEngine(Engine):
         g = self.group
         W = g.world
         self.comm_bytes = 0
+        dense_pm = None
         if g.distributed:
             dense = self._dense_pack()
-            self._allreduce_mean_(dense)
-            self._dense_unpack(dense)
+            if self.peer and self.fast and self.mats and dense.numel():
+                # the peer exchange: push the dense part now, finish it after the P / Q rounds
+                dense_pm = self._peer_mean(("dense",), dense.numel())
+                dense_pm.start(dense)
+            else:
+                self._allreduce_mean_(dense, tag=("dense",))
+                self._dense_unpack(dense)
         if not self.mats:
             return 1.0
         if self.fast:
             if not factorized:
                 self.pre_reduce()
-            self._allreduce_mean_(self._pbuf)   # round 1: P (mean over sites)
-            self._table.orth_gtp(0)             # orthonormalise P, Q = M^T P
-            self._allreduce_mean_(self._qbuf)   # round 2: Q (mean); also the next warm start
-            self._table.recon_ef()              # G = P Q^T, err = M - G
+            self._allreduce_mean_(self._pbuf, tag=("P",))  # round 1: P (mean over sites)
+            self._table.orth_gtp(0)                         # orthonormalise P, Q = M^T P
+            self._allreduce_mean_(self._qbuf, tag=("Q",))  # round 2: Q (mean); next warm start
+            self._table.recon_ef()                          # G = P Q^T, err = M - G
+            if dense_pm is not None:
+                dense_pm.finish(dense)
+                self._dense_unpack(dense)
+                self.comm_bytes += dense_pm.bytes_sent
             return 1.0
         Ms = []
         for (p, rows, cols, r), e in zip(self.mats, self.err):

@@ -184,13 +184,18 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
     be = backend or os.environ.get("DINUNET_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
     pg = None
     loopback = bool(loopback and world == 1)
-    if loopback:
-        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    # every collective's completion events are its own: with torch's event cache a pooled event
+    # the process group's watchdog still polls could be re-recorded by a collective inside a
+    # graph capture, and the watchdog's next query aborts the process (hipErrorCapturedEvent)
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     if world > 1 or loopback:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = dict(backend=be, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
+            if loopback:
+                kw["store"] = dist.HashStore()  # one rank: an in-process store, no TCP port
+            else:
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if be == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
@@ -199,15 +204,6 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
                        backend=be if (world > 1 or loopback) else None, pg=pg, loopback=loopback)
     _GROUP.gpu_shared = _gpu_shared(_GROUP)
     return _GROUP
-
-
-def _free_port() -> int:
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _gpu_shared(g: SiteGroup) -> Optional[bool]:

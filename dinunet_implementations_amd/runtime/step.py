@@ -58,16 +58,25 @@ HEADS = {"ica": ica_forward_loss, "fs": fs_forward_loss}
 CAPTURE_MODE = "thread_local"
 
 
+def _engine_capturable(engine) -> bool:
+    cap = getattr(engine, "capturable", None)
+    if cap is None:  # an engine without the property: RCCL collectives capture, host ones not
+        return engine.group.backend == "nccl"
+    return bool(cap)
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 def _quiesce_collectives(group) -> None:
-    """Before a capture on an RCCL group: let the process group's watchdog retire every finished
-    eager collective first.  It polls their (pooled) completion events every ~100 ms; a pooled
-    event re-recorded by a collective inside the capture while the watchdog still holds the old
-    work aborts the process (hipErrorCapturedEvent: seen right after eager collectives, e.g. the
-    warm-up steps or dsgd_collective=calibrate, and intermittently in the GPU tests)."""
+    """Before a capture on an RCCL group: every eager collective issued so far has finished on
+    the device.  (The process group's completion events are never pooled -- ``init_sites`` turns
+    off torch's event cache, ``TORCH_NCCL_CUDA_EVENT_CACHE=0`` -- so an event the watchdog still
+    polls is never re-recorded inside a capture: the hipErrorCapturedEvent abort a pooled event
+    caused, seen right after eager collectives, cannot happen.)"""
     if getattr(group, "distributed", False) and getattr(group, "backend", None) == "nccl":
-        import time
         torch.cuda.synchronize()
-        time.sleep(0.3)
 
 # The LSTM weight repack leaves the graph and rides in the step prologue's launch
 # (DINUNET_DEFER_PACK=0 keeps it captured)
@@ -148,11 +157,11 @@ class TrainStep:
             env = os.environ.get("DINUNET_SPLIT_GRAPH", "")
             split = can_split and (engine.group.distributed if env == "" else env == "1")
         self.split = bool(split and can_split)
-        # collectives inside the captured step: RCCL only (gloo collectives are host calls)
+        # collectives inside the captured step: the engine says whether its site-means can be
+        # captured (the peer exchange on any backend, RCCL's all-reduce; not host collectives)
         grp = engine.group
         self.comm_graph = bool(CAPTURE_COMM and self.use_graph and grp.distributed
-                               and grp.backend == "nccl" and self.accum == 1
-                               and getattr(engine, "capturable", True))
+                               and self.accum == 1 and _engine_capturable(engine))
         self.split_at = None  # "projection" | "stem", set at capture
         self._first_buckets = engine.split_buckets(list(model.stem_parameters())) if self.split else []
         self.graph_b = None
@@ -246,8 +255,7 @@ class TrainStep:
         if self.accum == 1:
             return self._graph_opt_ok()
         g = self.engine.group
-        comm = (not g.distributed) or (CAPTURE_COMM and g.backend == "nccl"
-                                       and getattr(self.engine, "capturable", True))
+        comm = (not g.distributed) or (CAPTURE_COMM and _engine_capturable(self.engine))
         return comm and isinstance(self.opt, ops.FusedAdam) and self.flat.data.is_cuda
 
     def _graph_opt_ok(self) -> bool:
@@ -503,7 +511,11 @@ class TrainStep:
         for k in range(A):
             bump = self.opt.device_step() if (graph_opt and k == 0) else None
             grad = self.flat.grad if k == 0 else self.flat.grad[:0]
-            if sync is not None and not graph_opt:
+            if sync is not None and not graph_opt and not _capturing():
+                # eager only: a captured body without the update keeps the collectives off
+                # (_dev_capture disabled them) and the engine's reduction after the replay
+                # launches every bucket -- enabling them here would issue host or uncapturable
+                # collectives inside the capture
                 self.engine.sync_enabled = k == A - 1
             with self._dev_prologue(bump, grad) as rp:
                 out, loss, pred = self._fwd_bwd(sx, sy)

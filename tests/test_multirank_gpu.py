@@ -62,6 +62,35 @@ CASES = [
          "--oracle", "--grad-tol", "1e-6", "--oracle-tol", "0.4"]),
     (2, ["--engine", "powerSGD", "--precision", "32", "--feed", "device", "--oracle",
          "--grad-tol", "1e-6", "--oracle-tol", "0.25"]),
+    # the peer exchange (parallel/peer.py): real cross-process device traffic through IPC-mapped
+    # HBM INSIDE the captured step (comm_graph on the gloo group too: kernels only), every engine
+    # and wire against the fp64 oracle; 16-bit wires take it by default (auto)
+    (2, ["--engine", "dSGD", "--precision", "32", "--collective", "peer", "--oracle"]),
+    (2, ["--engine", "dSGD", "--precision", "32", "--collective", "peer", "--feed", "device",
+         "--oracle"]),
+    # (4 sites, fp32: the first-step gradient matches the fp64 mean to 3.4e-8 -- peer and gloo
+    # all-reduce alike -- and Adam amplifies the fp32 sum-order difference to a 5.0-5.4e-2
+    # update error after 8 steps for both, profiles/r6_peer_oracle_w4.jsonl)
+    (4, ["--engine", "dSGD", "--precision", "32", "--collective", "peer", "--oracle",
+         "--oracle-tol", "0.15", "--grad-tol", "1e-7"]),
+    (4, ["--engine", "dSGD", "--precision", "32", "--collective", "peer", "--feed", "device",
+         "--oracle", "--oracle-tol", "0.15"]),
+    (2, ["--engine", "dSGD", "--precision", "16", "--collective", "peer", "--payload", "bf16",
+         "--oracle", "--oracle-tol", "0.3", "--grad-tol", "6e-3"]),
+    (2, ["--engine", "rankDAD", "--precision", "32", "--collective", "peer", "--dad-tol", "0",
+         "--oracle", "--grad-tol", "1e-6", "--oracle-tol", "0.4"]),
+    (2, ["--engine", "rankDAD", "--precision", "16", "--dad-tol", "0", "--feed", "device",
+         "--oracle", "--oracle-tol", "0.5"]),
+    (2, ["--engine", "powerSGD", "--precision", "32", "--collective", "peer", "--oracle",
+         "--grad-tol", "1e-6", "--oracle-tol", "0.25"]),
+    (2, ["--engine", "powerSGD", "--precision", "16", "--feed", "device", "--oracle",
+         "--oracle-tol", "0.35"]),
+    # device-fed accumulation (local_iterations = 2): host collectives after the replay (gloo
+    # all-reduce: the captured micro-batches keep them off) and the captured peer exchange
+    (2, ["--engine", "dSGD", "--precision", "32", "--feed", "device", "--accum", "2",
+         "--oracle"]),
+    (2, ["--engine", "dSGD", "--precision", "16", "--feed", "device", "--accum", "2",
+         "--oracle", "--oracle-tol", "0.3"]),
 ]
 
 
@@ -89,6 +118,10 @@ def test_replicas_bit_identical(world, args):
         if "device" not in args:  # (device-fed: the fused Adam zeroes the gradient it consumes)
             assert "grad_rel_err" in res, res
     assert res["graph"] and res["world"] == world
-    if "device" in args and "dSGD" in args:  # the bench path: the update emits the next
-        assert res["adam_pack"] and res["split"], res  # step's operands
+    if "device" in args and "dSGD" in args and "--accum" not in args:  # the bench path: the
+        assert res["adam_pack"] and res["split"], res  # update emits the next step's operands
+    if "peer" in args or ("16" in args and "allreduce" not in args):  # the peer exchange, captured
+        assert res["peer"] and (res["comm_graph"] or "--accum" in args), res
+        if "--accum" not in args or "device" in args:  # (host-fed accumulation: eager update)
+            assert res["captured_update"], res
     assert r.returncode == 0, r.stderr[-3000:]

@@ -185,17 +185,23 @@ def test_comm_graph_device_fed_matches_single_site(rccl1, apack, monkeypatch):
 
 @pytest.mark.parametrize("engine,cfg,captured", [
     ("dSGD", {}, True),
-    ("dSGD", {"precision_bits": "16"}, False),          # direct fp16 exchange: host-issued
+    ("dSGD", {"precision_bits": "16"}, True),           # fp16 wire: the peer exchange (auto)
+    ("dSGD", {"dsgd_collective": "peer"}, True),
+    ("dSGD", {"precision_bits": "16", "dsgd_collective": "direct"}, False),  # RCCL all-to-all
     ("dSGD", {"precision_bits": "16", "dsgd_collective": "allreduce", "payload_dtype": "bf16"},
      True),
     ("rankDAD", {}, True),
+    ("rankDAD", {"precision_bits": "16"}, True),
+    ("rankDAD", {"dsgd_collective": "peer"}, True),
     ("powerSGD", {}, True),
+    ("powerSGD", {"precision_bits": "16"}, True),
 ])
 def test_comm_graph_matches_host_issued_collectives(rccl1, engine, cfg, captured, monkeypatch):
-    """Every engine with a capturable wire: the step with its collectives captured in the K-step
-    graph gives the trajectory of the uncaptured multi-site step (DINUNET_CAPTURE_COMM=0:
-    host-issued collectives between / after the replays, eager update).  The direct 16-bit
-    exchange (RCCL all-to-all) keeps host-issued collectives (Engine.capturable)."""
+    """Every engine and wire: the step with its collectives captured in the K-step graph gives
+    the trajectory of the uncaptured multi-site step (DINUNET_CAPTURE_COMM=0: host-issued
+    collectives between / after the replays, eager update).  16-bit wires default to the peer
+    exchange (kernels only: captured); only an explicit RCCL all-to-all exchange
+    (``dsgd_collective=direct``) keeps host-issued collectives (Engine.capturable)."""
     from dinunet_implementations_amd.runtime import step as step_mod
     xs, ys = _batches(n=8)
     n = 12

@@ -123,7 +123,8 @@ def main():
     ap.add_argument("--oracle", action="store_true", help="compare with the fp64-mean oracle")
     ap.add_argument("--oracle-tol", type=float, default=1e-3)
     ap.add_argument("--payload", default=None, help="payload_dtype (fp16 | bf16 | fp32)")
-    ap.add_argument("--collective", default="auto", help="dsgd_collective (auto | direct | allreduce)")
+    ap.add_argument("--collective", default="auto",
+                    help="dsgd_collective (auto | direct | allreduce | peer | calibrate)")
     ap.add_argument("--dad-tol", type=float, default=None,
                     help="dad_tol (the rank-dAD oracle replays a fixed iteration count: pass 0)")
     ap.add_argument("--grad-tol", type=float, default=None,
@@ -187,8 +188,8 @@ def main():
 
     g_first = None
     if a.feed == "device":
-        if a.ragged or a.accum != 1:
-            raise SystemExit("--feed device takes neither --ragged nor --accum")
+        if a.ragged:
+            raise SystemExit("--feed device does not take --ragged")
         from dinunet_implementations_amd.ops import DeviceSource
         xs, ys = zip(*[(x, y) for _, x, y in site_batches(grp.rank)])
         src = DeviceSource(torch.cat(xs).to(torch.bfloat16), torch.cat(ys), a.batch)
@@ -209,6 +210,10 @@ def main():
            "accum": a.accum, "ragged": a.ragged, "graph": step.graph is not None or bool(getattr(step, "_dgraphs", None)),
            "split": bool(step.split), "steps": opt.step_count, "max_abs_diff": maxdiff,
            "feed": a.feed, "adam_pack": getattr(step, "_apack", None) is not None,
+           "peer": bool(getattr(eng, "peer", False)), "comm_graph": bool(step.comm_graph),
+           "captured_update": bool(step.graph_opt or any(
+               v[2] is True for v in getattr(step, "_dgraphs", {}).values()
+               if isinstance(v, tuple) and len(v) == 3)),
            "param_sum": float(mine.double().sum())}
     if a.oracle:
         ok_o = torch.zeros(1, dtype=torch.float64, device=dev)
