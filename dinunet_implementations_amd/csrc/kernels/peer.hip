@@ -135,7 +135,12 @@ struct PxArgs {
   long dstride;              // gather: dst elements between sites
   long timeout;              // wait limit in s_memrealtime ticks (100 MHz)
   int W, me, scaled;
-  float scale;               // reduce: * scale (1/W); unpack / gcollect: * scale
+  float scale;               // unpack / gcollect: * scale
+  float scale_red;           // reduce: * scale_red (1/W: the mean)
+  int mode;                  // bit 0: release = store drain only (every payload byte is an
+                             // uncached store: no L2 line to write back); bit 1: no acquire
+                             // invalidate, the payload is read with system-scope (sc0 sc1) loads;
+                             // bit 2: waits done by a preceding px_wait_kernel launch
 };
 
 typedef __attribute__((address_space(1))) unsigned px_gu32;
@@ -147,8 +152,10 @@ __device__ __forceinline__ unsigned px_get(unsigned* f) {
   return __hip_atomic_load((px_gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// lane 0: wait until *f == 1 (bounded), then clear it; a timeout sets the error word to `code`
+// lane 0: wait until *f == 1 (bounded), then clear it; a timeout sets the error word to `code`.
+// mode bit 2: the flags were already taken by a one-workgroup wait launch (px_wait_kernel)
 __device__ __forceinline__ void px_take(unsigned* f, const PxArgs& a, unsigned code) {
+  if (a.mode & 4) return;
   const long t0 = (long)__builtin_amdgcn_s_memrealtime();
   while (px_get(f) != 1u) {
     if ((long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
@@ -161,19 +168,60 @@ __device__ __forceinline__ void px_take(unsigned* f, const PxArgs& a, unsigned c
 }
 
 // every storing wave drains its stores, the workgroup meets, lane 0 releases at system scope
-__device__ __forceinline__ void px_drain_release() {
+// (mode bit 0: the drain is the release -- the payload went to uncached memory)
+__device__ __forceinline__ void px_drain_release(int mode) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (threadIdx.x == 0 && !(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
-// lane 0 acquired (after its waits): the workgroup follows
-__device__ __forceinline__ void px_acquire_join() {
-  if (threadIdx.x == 0) {
+// lane 0 acquired (after its waits): the workgroup follows (mode bit 1: no invalidate, every
+// payload load is a system-scope load, px_ldw8)
+__device__ __forceinline__ void px_acquire_join(int mode) {
+  if (threadIdx.x == 0 && !(mode & 2)) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+}
+
+typedef __attribute__((ext_vector_type(4))) unsigned px_u32x4;
+
+// 8 payload elements at wire element offset `at` + 8 * i8 of a peer-written region: plain loads
+// after an acquire, or system-scope (sc0 sc1) buffer loads (mode bit 1)
+template <int T>
+__device__ __forceinline__ void px_ldw8(const void* base, long at, long i8, int mode,
+                                        float (&o)[8]) {
+  const char* p = wptr<T>(const_cast<void*>(base), at);
+  if (!(mode & 2)) {
+    ld8<T>(p, i8, o);
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(p), 0,
+                                                                     0x7fffffff, 0x00020000);
+  if constexpr (T == PT_F32) {
+    const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(32 * i8), 0, 17));
+    const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(32 * i8 + 16), 0, 17));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { o[k] = a[k]; o[4 + k] = b[k]; }
+  } else {
+    const typename Wire<T>::v8 v = __builtin_bit_cast(
+        typename Wire<T>::v8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(16 * i8), 0, 17));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (float)v[k];
+  }
+}
+
+// the sub-block header (element 0 = its exponent) of a peer-written region
+template <int T>
+__device__ __forceinline__ int px_ldexp(const void* base, long at, int mode) {
+  if (!(mode & 2)) return (int)ld1<T>(base, at);
+  const char* p = wptr<T>(const_cast<void*>(base), at);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(p), 0,
+                                                                     0x7fffffff, 0x00020000);
+  const unsigned u = __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 17);
+  if constexpr (T == PT_F32) return (int)__uint_as_float(u);
+  else return (int)(float)__builtin_bit_cast(typename Wire<T>::s, (unsigned short)(u & 0xffff));
 }
 
 // fp32 x[e0 .. e0 + 8) (zeros past n) -> scaled sub-block element values, exponent of the
@@ -226,52 +274,58 @@ __global__ void __launch_bounds__(256) px_push_kernel(PxArgs a) {
   const int e = px_load_scaled<T>(a.src, d * a.chunk + (long)s * SB + 8 * threadIdx.x, a.n,
                                   a.scaled, o, wm);
   px_store_sb<T>(a.inbox[d], ((long)a.me * nsbc + s) * SBS, e, o);
-  px_drain_release();
+  px_drain_release(a.mode);
   if (threadIdx.x == 0) px_set(a.flags[d] + (long)s * a.W + a.me, 1u);
 }
 
+// sub-block s of MY chunk: wait for every site's push, fp32 sum in site order, into every site's
+// gather slot
 template <int T>
-__global__ void __launch_bounds__(256) px_reduce_kernel(PxArgs a) {
-  const int s = blockIdx.x, W = a.W;
+__device__ __forceinline__ void px_reduce_task(const PxArgs& a, int s) {
+  const int W = a.W;
   const long nsbc = a.chunk / SB;
   if (threadIdx.x == 0)
     for (int w = 0; w < W; ++w) px_take(a.flags[a.me] + (long)s * W + w, a, 0x100u | (unsigned)w);
-  px_acquire_join();
+  px_acquire_join(a.mode);
   const void* in = a.inbox[a.me];
+  int ew[PX_MAXW];
   int emin = 1 << 20;
-  for (int w = 0; w < W; ++w) emin = min(emin, (int)ld1<T>(in, ((long)w * nsbc + s) * SBS));
+  for (int w = 0; w < W; ++w) {
+    ew[w] = px_ldexp<T>(in, ((long)w * nsbc + s) * SBS, a.mode);
+    emin = min(emin, ew[w]);
+  }
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v[8];
   for (int w = 0; w < W; ++w) {  // site order: every replica sums the same way
     const long at = ((long)w * nsbc + s) * SBS;
-    const float un = exp2i(-(int)ld1<T>(in, at));
-    ld8<T>(wptr<T>(const_cast<void*>(in), at), 1 + threadIdx.x, v);
+    const float un = exp2i(-ew[w]);
+    px_ldw8<T>(in, at, 1 + threadIdx.x, a.mode, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] += v[k] * un;
   }
-  const float sc = a.scale * exp2i(emin);
+  const float sc = a.scale_red * exp2i(emin);
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] *= sc;
   const long at = ((long)a.me * nsbc + s) * SBS;
   for (int j = 0; j < W; ++j) px_store_sb<T>(a.gath[j], at, emin, acc);
-  px_drain_release();
+  px_drain_release(a.mode);
   if (threadIdx.x == 0)
     for (int j = 0; j < W; ++j) px_set(a.flags[j] + nsbc * W + (long)a.me * nsbc + s, 1u);
 }
 
+// owner d's sub-block s of the mean -> my fp32 range
 template <int T>
-__global__ void __launch_bounds__(256) px_unpack_kernel(PxArgs a) {
-  const int s = blockIdx.x, d = blockIdx.y;
+__device__ __forceinline__ void px_unpack_task(const PxArgs& a, int d, int s) {
   const long nsbc = a.chunk / SB;
   if (threadIdx.x == 0)
     px_take(a.flags[a.me] + nsbc * a.W + (long)d * nsbc + s, a, 0x200u | (unsigned)d);
-  px_acquire_join();
+  px_acquire_join(a.mode);
   const long at = ((long)d * nsbc + s) * SBS;
   const void* g = a.gath[a.me];
-  const float sc = a.scale * exp2i(-(int)ld1<T>(g, at));
+  const float sc = a.scale * exp2i(-px_ldexp<T>(g, at, a.mode));
   const long e0 = d * a.chunk + (long)s * SB + 8 * threadIdx.x;
   if (e0 >= a.n) return;
   float o[8];
-  ld8<T>(wptr<T>(const_cast<void*>(g), at), 1 + threadIdx.x, o);
+  px_ldw8<T>(g, at, 1 + threadIdx.x, a.mode, o);
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] *= sc;
   if (e0 + 8 <= a.n) {
@@ -281,6 +335,44 @@ __global__ void __launch_bounds__(256) px_unpack_kernel(PxArgs a) {
     for (int k = 0; k < 8; ++k)
       if (e0 + k < a.n) a.dst[e0 + k] = o[k];
   }
+}
+
+template <int T>
+__global__ void __launch_bounds__(256) px_reduce_kernel(PxArgs a) { px_reduce_task<T>(a, blockIdx.x); }
+
+template <int T>
+__global__ void __launch_bounds__(256) px_unpack_kernel(PxArgs a) {
+  px_unpack_task<T>(a, blockIdx.y, blockIdx.x);
+}
+
+// ---- separate waits -------------------------------------------------------------------------
+// When site processes SHARE a GPU (the one-GPU rehearsal), a launch whose every workgroup waits
+// holds a wave slot on many CUs while it waits -- and a peer's persistent LSTM workgroup, which
+// needs a whole CU's registers, then finds no CU, so the peer never reaches the push being waited
+// for (cross-process deadlock broken only by the timeout: seen at 4 sites on one GPU).  There, each
+// wait is its own ONE-workgroup launch ahead of the data launch (mode bit 2): it polls a
+// contiguous range [lo, hi) of my flag words until every word is 1, clears them, and acquires;
+// the data launch then runs without waiting.  One site per GPU (production) keeps the waits
+// inside the data launches (one launch fewer per phase).
+__global__ void __launch_bounds__(256) px_wait_kernel(unsigned* f, long lo, long hi, unsigned* err,
+                                                      long timeout, unsigned code) {
+  const long t0 = (long)__builtin_amdgcn_s_memrealtime();
+  bool late = false;
+  for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    while (px_get(f + i) != 1u) {
+      if ((long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+        late = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (late) break;
+    px_set(f + i, 0u);
+  }
+  if (late) px_set(err, code);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
 }
 
 // ---- factor all-gather --------------------------------------------------------------------------
@@ -293,11 +385,11 @@ __global__ void __launch_bounds__(256) px_gpush_kernel(PxArgs a) {
   const int s = blockIdx.x, d = blockIdx.y, W = a.W;
   const long nsb = a.chunk / SB;
   if (threadIdx.x == 0) px_take(a.flags[a.me] + W * nsb + (long)d * nsb + s, a, 0x300u | (unsigned)d);
-  px_acquire_join();
+  px_acquire_join(a.mode);
   float o[8];
   const int e = px_load_scaled<T>(a.src, (long)s * SB + 8 * threadIdx.x, a.n, a.scaled, o, wm);
   px_store_sb<T>(a.gath[d], ((long)a.me * nsb + s) * SBS, e, o);
-  px_drain_release();
+  px_drain_release(a.mode);
   if (threadIdx.x == 0) px_set(a.flags[d] + (long)a.me * nsb + s, 1u);
 }
 
@@ -306,14 +398,14 @@ __global__ void __launch_bounds__(256) px_gcollect_kernel(PxArgs a) {
   const int s = blockIdx.x, w = blockIdx.y, W = a.W;
   const long nsb = a.chunk / SB;
   if (threadIdx.x == 0) px_take(a.flags[a.me] + (long)w * nsb + s, a, 0x400u | (unsigned)w);
-  px_acquire_join();
+  px_acquire_join(a.mode);
   const long at = ((long)w * nsb + s) * SBS;
   const void* g = a.gath[a.me];
-  const float sc = a.scale * exp2i(-(int)ld1<T>(g, at));
+  const float sc = a.scale * exp2i(-px_ldexp<T>(g, at, a.mode));
   const long e0 = (long)s * SB + 8 * threadIdx.x;
   float o[8];
   if (e0 < a.n) {
-    ld8<T>(wptr<T>(const_cast<void*>(g), at), 1 + threadIdx.x, o);
+    px_ldw8<T>(g, at, 1 + threadIdx.x, a.mode, o);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] *= sc;
     float* out = a.dst + (long)w * a.dstride;
@@ -326,7 +418,7 @@ __global__ void __launch_bounds__(256) px_gcollect_kernel(PxArgs a) {
     }
   }
   // every lane has read the slot: return its credit to the writer
-  px_drain_release();
+  px_drain_release(a.mode);
   if (threadIdx.x == 0) px_set(a.flags[w] + W * nsb + (long)a.me * nsb + s, 1u);
 }
 
@@ -394,6 +486,13 @@ DN_API int dn_peer_fill_u32(unsigned* p, unsigned v, long count) {
   return DN_OK;
 }
 
+// diagnostics: copy `bytes` of arena memory to the host (flag-state dumps after a timeout)
+DN_API int dn_peer_peek(const void* src, void* host, long bytes) {
+  if (!src || !host || bytes < 0) return DN_BAD_SHAPE;
+  return hipMemcpy(host, src, (size_t)bytes, hipMemcpyDeviceToHost) == hipSuccess ? DN_OK
+                                                                                   : DN_LAUNCH_FAILED;
+}
+
 DN_API long dn_peer_args_size() { return (long)sizeof(PxArgs); }
 
 #define DN_PX_DISPATCH(T, KERNEL, ...)                                                           \
@@ -411,6 +510,26 @@ static bool px_ok(const PxArgs& a) {
   for (int w = 0; w < a.W; ++w)
     if (!a.inbox[w] || !a.gath[w] || !a.flags[w]) return false;
   return (((uintptr_t)a.src | (uintptr_t)a.dst) & 15) == 0;
+}
+
+// the one-workgroup wait of `phase` (1 reduce, 2 unpack, 3 gpush, 4 gcollect) for my flag words
+DN_API int dn_peer_wait(const PxArgs* args, int phase, hipStream_t st) {
+  if (!args) return DN_BAD_SHAPE;
+  const PxArgs& a = *args;
+  if (!px_ok(a)) return DN_BAD_SHAPE;
+  const long t = g_dn_spin_limit == 0 ? 0 : g_dn_peer_timeout_ms * 100000L;
+  const long nsb = a.chunk / SB, W = a.W;
+  long lo, hi;
+  switch (phase) {
+    case 1: lo = 0, hi = nsb * W; break;                 // rs flags of my chunk
+    case 2: lo = nsb * W, hi = 2 * nsb * W; break;       // ag flags of every owner
+    case 3: lo = W * nsb, hi = 2 * W * nsb; break;       // gather credits
+    case 4: lo = 0, hi = W * nsb; break;                 // gather data
+    default: return DN_BAD_SHAPE;
+  }
+  hipLaunchKernelGGL(px_wait_kernel, dim3(1), dim3(256), 0, st, a.flags[a.me], lo, hi, a.err, t,
+                     (unsigned)(phase << 8) | 0xffu);
+  return dn_launch_status();
 }
 
 // phase: 0 push, 1 reduce, 2 unpack (site-mean); 3 gpush, 4 gcollect (gather)

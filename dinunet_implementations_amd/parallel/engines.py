@@ -230,8 +230,17 @@ class DSGDEngine(Engine):
             self.wire = "bf16"
         self._comm_stream = (torch.cuda.Stream(device=flat.grad.device)
                              if self.direct and group.distributed and flat.grad.is_cuda else None)
+        self._peer_build()
         self._hooks = []
         self._delivered = set()
+        if self.peer:
+            # no pushes from autograd's gradient hooks: they run in the autograd thread, on a
+            # stream that need not be the step's, and the peer exchange reuses its slots safely
+            # only when every push is stream-ordered after the previous exchange's finish
+            # (replicas diverged with hook-issued pushes in eager side-stream steps).  The
+            # captured step pushes the body bucket between its backward parts itself
+            # (launch_bucket); eager steps push every bucket in reduce().
+            self.overlap = False
         if self.overlap:
             # autograd fires a parameter's post-accumulate hook even when its producer returned
             # no gradient for it -- which is what the fused ops do: they accumulate into .grad
@@ -306,7 +315,8 @@ class DSGDEngine(Engine):
 
         def graph_timed(fn):
             fn()  # eager once (RCCL communicator / peer regions set up outside the capture)
-            sync()
+            from ..runtime.step import _quiesce_collectives
+            _quiesce_collectives(g)  # every eager collective retired by the watchdog first
             gr = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gr, capture_error_mode="thread_local"):
                 fn()
@@ -389,7 +399,15 @@ class DSGDEngine(Engine):
             self._expected[self._param_bucket[id(p)]] += 1
         self._half_bufs.clear()
         self._reset()
+        self._peer_build()
         return list(range(len(body)))
+
+    def _peer_build(self):
+        """The peer exchange of every bucket, built now (arena regions and the IPC handle
+        exchange are host work, never inside a capture; every site builds in the same order)."""
+        if self.peer:
+            for s, e in self.buckets:
+                self._peer_mean(("bucket", s, e), e - s)
 
     def launch_bucket(self, b: int):
         """Mark bucket ``b`` ready and start every ready bucket up to it, in order (RCCL stream
@@ -446,6 +464,10 @@ class DSGDEngine(Engine):
             return 1.0
         self._ready = [True] * len(self.buckets)
         self._drain()
+        if self.peer:  # every pushed bucket's reduce + unpack, in bucket order, fused launches
+            from . import peer as _peer
+            _peer.finish_many([(h.pm, h.view, h.scale) for h in self._handles.values()])
+            self._handles.clear()
         for b, h in self._handles.items():
             h.wait()
             if self.half and not self.direct and not self.peer:
@@ -573,6 +595,11 @@ class RankDADEngine(Engine):
             G = self.flat.grad[o:o + out_f * in_f].view(out_f, in_f)
             layers.append((G, None, praw, self._send[po:po + out_f * rr].view(out_f, rr), qsend))
         self._table = LowRankTable(layers, dev)
+        if self.peer:  # the exchanges, built outside any capture (peer.PeerArena)
+            from . import peer as _peer
+            if self._dense_ranges:
+                self._peer_mean(("dense",), sum(b - a for a, b in self._dense_ranges))
+            _peer.gather(self.group, dev, self._send.numel(), self.wire, ("rankDAD", "factors"))
 
         class PiRecon(ctypes.Structure):
             _fields_ = [("G", ctypes.c_void_p), ("P", ctypes.c_void_p), ("Q", ctypes.c_void_p),
@@ -859,6 +886,12 @@ class PowerSGDEngine(Engine):
             layers.append((G, E, P, Ps, Q))
             po, qo, eo = po + rw * r, qo + c * r, eo + rw * c
         self._table = LowRankTable(layers, dev)
+        if self.peer:  # the exchanges, built outside any capture (peer.PeerArena)
+            nd = sum(n for _, n in self.dense_segs)
+            if nd:
+                self._peer_mean(("dense",), nd)
+            self._peer_mean(("P",), self._pbuf.numel())
+            self._peer_mean(("Q",), self._qbuf.numel())
 
     def pre_reduce(self):
         """M = G + err and the local P = M Q of every matrix (one launch, graph-capturable)."""

@@ -132,6 +132,13 @@ def resolve_device(gpus=None, local_rank: int = 0, world: int = 1, backend: Opti
     if not ids:
         return torch.device("cpu")
     k = ids[0]
+    if len(ids) > 1:
+        # the reference's GUI offers "GPU IDs to use Eg. [0], [0, 1]" (assets/coinstac-gui.png):
+        # one MI355X (288 GB HBM) holds a whole site here, so the extra ids are not used -- say so
+        # instead of dropping them silently
+        import warnings
+        warnings.warn(f"gpus={ids}: a site runs on ONE GPU (GPU {k}); the other ids "
+                      f"{ids[1:]} are not used (one site = one MI355X)", RuntimeWarning)
     if not n_devices:
         import warnings
         warnings.warn(f"gpus={ids} but no GPU is visible: the site runs on the CPU", RuntimeWarning)

@@ -45,6 +45,7 @@ _lib.register("dn_peer_open", [_lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_peer_close", [_lib.c_void_p])
 _lib.register("dn_peer_fill_u32", [_lib.c_void_p, ctypes.c_uint, _lib.c_long])
 _lib.register("dn_peer_launch", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p])
+_lib.register("dn_peer_wait", [_lib.c_void_p, _lib.c_int, _lib.c_void_p])
 _lib.register("dn_peer_set_timeout_ms", [_lib.c_long])
 
 PUSH, REDUCE, UNPACK, GPUSH, GCOLLECT = range(5)
@@ -59,7 +60,16 @@ class _PxArgs(ctypes.Structure):
                 ("dst", ctypes.c_void_p), ("err", ctypes.c_void_p), ("n", ctypes.c_long),
                 ("chunk", ctypes.c_long), ("dstride", ctypes.c_long), ("timeout", ctypes.c_long),
                 ("W", ctypes.c_int), ("me", ctypes.c_int), ("scaled", ctypes.c_int),
-                ("scale", ctypes.c_float)]
+                ("scale", ctypes.c_float), ("scale_red", ctypes.c_float), ("mode", ctypes.c_int)]
+
+
+# hand-off form (peer.hip PxArgs.mode): bit 0 = release by store drain only, bit 1 = system-scope
+# payload loads instead of an acquire invalidate.  Default 2: every payload byte is read with
+# system-scope loads from uncached memory, so the acquire's invalidate buys nothing (loopback step
+# 0.3643 -> 0.3564 ms, profiles/r6_peer_mode_ab.jsonl).  The release keeps the L2 write-back the
+# memory model prescribes at system scope (bit 0 drops it: 0.3574 ms, not the default -- the drain
+# alone is not specified to order a store against a later store from another agent).
+MODE = int(os.environ.get("DINUNET_PEER_MODE", "2"))
 
 
 def available(group, device) -> bool:
@@ -84,6 +94,12 @@ class PeerArena:
         self._chunks: List[tuple] = []  # (local base, [site bases], bytes)
         self._used = 0
         self._cache: Dict[tuple, object] = {}
+        # waits as one-workgroup launches of their own when site processes share this GPU (a
+        # waiting data launch there can starve a peer's whole-CU kernels: peer.hip px_wait_kernel);
+        # DINUNET_PEER_WAIT=inline|launch forces one form
+        forced = os.environ.get("DINUNET_PEER_WAIT", "")
+        self.wait_launch = (forced == "launch") if forced in ("inline", "launch") else bool(
+            getattr(group, "gpu_shared", False))
         # sticky error word of every wait on this site (normal device memory)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         ms = os.environ.get("DINUNET_PEER_TIMEOUT_MS")
@@ -92,6 +108,11 @@ class PeerArena:
         _ARENAS.add(self)
 
     def _new_chunk(self, nbytes: int):
+        if torch.cuda.is_current_stream_capturing():
+            # the allocation, its zero fill and the handle exchange are host work: an exchange
+            # must first run (or be built) outside a capture -- the engines build theirs eagerly
+            raise RuntimeError("peer exchange: a new arena region was requested inside a HIP "
+                               "graph capture; build the exchange before capturing")
         nbytes = max(ARENA_BYTES, -(-nbytes // ALIGN) * ALIGN)
         with torch.cuda.device(self.device):
             p = ctypes.c_void_p()
@@ -172,16 +193,20 @@ class _Exchange:
         self.code, self.dtype = PAYLOAD_TYPES[wire]
         self.scaled = 1 if wire == "fp16" else 0
 
-    def _args(self, inbox, gath, flags, src, dst, n, chunk, dstride=0, scale=1.0):
-        a = _PxArgs()
+    def _args(self, inbox, gath, flags, src, dst, n, chunk, dstride=0, scale=1.0, a=None):
+        a = _PxArgs() if a is None else a
         for w in range(self.ar.W):
             a.inbox[w], a.gath[w], a.flags[w] = inbox[w], gath[w], flags[w]
         a.src, a.dst, a.err = src, dst, self.ar.err.data_ptr()
         a.n, a.chunk, a.dstride = int(n), int(chunk), int(dstride)
         a.W, a.me, a.scaled, a.scale = self.ar.W, self.ar.me, self.scaled, float(scale)
+        a.scale_red = 1.0 / self.ar.W
+        a.mode = MODE | (4 if self.ar.wait_launch else 0)
         return a
 
     def _launch(self, args, phase):
+        if self.ar.wait_launch and phase != PUSH:  # the phase's wait, as a launch of its own
+            _lib.call("dn_peer_wait", ctypes.byref(args), phase, _lib.stream())
         _lib.call("dn_peer_launch", ctypes.byref(args), phase, self.code, _lib.stream())
 
 
@@ -208,14 +233,16 @@ class PeerMean(_Exchange):
         self._launch(self._args(self.inbox, self.gath, self.flags, x.data_ptr(), 0, self.n,
                                 self.chunk), PUSH)
 
-    def finish(self, x: torch.Tensor, scale: float = 1.0):
+    def finish_args(self, x: torch.Tensor, scale: float = 1.0, into=None):
         if x.numel() != self.n or x.dtype != torch.float32 or not x.is_contiguous():
             raise ValueError(f"PeerMean.finish: {self.n} contiguous fp32 elements expected")
-        red = self._args(self.inbox, self.gath, self.flags, 0, 0, self.n, self.chunk,
-                         scale=1.0 / self.ar.W)
-        self._launch(red, REDUCE)
-        self._launch(self._args(self.inbox, self.gath, self.flags, 0, x.data_ptr(), self.n,
-                                self.chunk, scale=scale), UNPACK)
+        return self._args(self.inbox, self.gath, self.flags, 0, x.data_ptr(), self.n, self.chunk,
+                          scale=scale, a=into)
+
+    def finish(self, x: torch.Tensor, scale: float = 1.0):
+        """Reduce my chunk (waits for every site's push) and unpack every owner's mean into
+        ``x`` (waits for the owners' reduce)."""
+        finish_many([(self, x, scale)])
 
     def run_(self, x: torch.Tensor, scale: float = 1.0) -> int:
         """``x`` <- scale * mean over sites, on the current stream; returns bytes this site sent."""
@@ -255,6 +282,18 @@ class PeerGather(_Exchange):
         return self.bytes_sent
 
 
+def finish_many(items) -> None:
+    """Reduce + unpack of several pushed exchanges ``[(PeerMean, x, scale), ...]`` in the given
+    order (every site must pass the same sequence): two launches per exchange.  (One launch for
+    reduce + unpack of several exchanges -- the blocks' own reduce tasks first, then unpack tasks
+    waiting on the peers' -- timed out intermittently on a shared GPU while the separate
+    launches never did: ``profiles/r6_peer_fused_index.jsonl``; not kept.)"""
+    for pm, x, scale in items:
+        a = pm.finish_args(x, scale)
+        pm._launch(a, REDUCE)
+        pm._launch(a, UNPACK)
+
+
 def mean(group, device, n: int, wire: str, tag) -> PeerMean:
     ar = arena(group, device)
     return ar.get(("mean", tag, int(n), wire), lambda: PeerMean(ar, n, wire))
@@ -263,6 +302,27 @@ def mean(group, device, n: int, wire: str, tag) -> PeerMean:
 def gather(group, device, m: int, wire: str, tag) -> PeerGather:
     ar = arena(group, device)
     return ar.get(("gather", tag, int(m), wire), lambda: PeerGather(ar, m, wire))
+
+
+_lib.register("dn_peer_peek", [_lib.c_void_p, _lib.c_void_p, _lib.c_long])
+
+
+def flag_state(ex) -> dict:
+    """Diagnostics: the set flag words of an exchange in THIS site's arena (after a timeout:
+    which wait never saw its flag)."""
+    import numpy as np
+    W = ex.ar.W
+    if isinstance(ex, PeerMean):
+        n = 2 * W * ex.nsbc
+    else:
+        n = 2 * W * ex.nsb
+    buf = np.zeros(n, dtype=np.uint32)
+    _lib.call("dn_peer_peek", ex.flags[ex.ar.me], buf.ctypes.data, 4 * n)
+    half = n // 2
+    return {"kind": type(ex).__name__, "words": n,
+            "set_first_half": [int(i) for i in np.nonzero(buf[:half])[0][:16]],
+            "set_second_half": [int(i) for i in np.nonzero(buf[half:])[0][:16]],
+            "nsub": ex.nsbc if isinstance(ex, PeerMean) else ex.nsb}
 
 
 def errors(reset: bool = True) -> List[tuple]:

@@ -1,31 +1,30 @@
 """The training step of one site: forward, loss, backward, aggregation, optimizer.
 
-The launch-bound part (encoder GEMM, persistent LSTM, classifier, loss head, full backward,
-gradient zeroing) is captured once into a HIP graph and replayed every step; gradient
-aggregation (RCCL collectives) and the single fused Adam launch run after the replay, because the
-optimizer's bias-correction scalars change every step and collective capture is not needed for a
-handful of bucketed all-reduces.  Engines whose reduction needs host-side logic (rank-dAD,
-PowerSGD) or that capture activations run eagerly.
+Everything launch-bound (encoder GEMM, persistent LSTM, classifier, loss head, full backward) is
+captured into HIP graphs and replayed.  With one site the fused Adam update is captured too (its
+step number and bias corrections live on the device): a host-fed step is one prologue launch +
+one replay, and device-fed runs (``bind`` / ``run``) replay graphs of K whole steps with no host
+work between them.
 
-Before each replay ONE prologue launch converts the batch into the graph's static (bf16) input,
-copies the labels and zeroes the flat gradient.  With a single site the fused Adam update is
-captured too (its step number lives on the device), so a step is prologue + one replay.
+Before each host-fed replay ONE prologue launch converts the batch into the graph's static
+(bf16) input, copies the labels and zeroes the flat gradient.
 
-Split backward (dSGD across sites): the model's ``stem`` (ICA: the encoder) produces the LAST
+Across sites (``comm_graph``, default) the engine's collectives are captured in the same graph:
+the two backward parts, the bucket exchanges between them, the engine's reduction and the fused
+Adam form ONE captured step, and device-fed runs replay K-step graphs exactly as at one site.  An
+engine says whether its site-means can be captured (``Engine.capturable``): always with the peer
+exchange (``parallel/peer.py``, kernels on the step's stream, any process-group backend), with
+RCCL for the all-reduce; host collectives (gloo all-reduce) and RCCL's all-to-all exchange
+cannot, and those steps (or ``DINUNET_CAPTURE_COMM=0``) replay two graphs A / B with the
+collectives and the update issued from the host between and after the replays.
+
+Split backward (across sites): the model's ``stem`` (ICA: the encoder) produces the LAST
 gradients of the backward, so the backward is issued in two parts cut at the LSTM input
 projection when the model provides ``proj_stem`` (part A ends with every LSTM and head gradient
 final; part B = the input-gradient GEMM + the encoder's weight gradients), else at the stem
-output.  The all-reduce of every non-stem gradient starts on RCCL's stream between the parts and
-runs under part B; only the small stem bucket's all-reduce is exposed.
-
-Multi-site steps over RCCL capture their collectives (``comm_graph``, default; RCCL supports
-stream capture): the two backward parts, the bucket all-reduces on RCCL's stream (a forked
-branch of the graph, joined before the update), the engine's reduction and the fused Adam are
-ONE captured step, and device-fed runs replay graphs of K whole steps exactly as at one site --
-no host work, no graph boundary and no eager launch between steps.  Without it
-(``DINUNET_CAPTURE_COMM=0``, or the gloo backend, whose collectives are host calls) the parts
-are two graphs A / B with the collectives and the update issued from the host between and
-after the replays.
+output.  The exchange of every non-stem gradient starts between the parts (RCCL: on its own
+stream; peer: the push, whose data cross the links while part B runs) and only the small stem
+bucket's exchange is exposed.
 """
 from __future__ import annotations
 
@@ -71,12 +70,20 @@ def _capturing() -> bool:
 
 def _quiesce_collectives(group) -> None:
     """Before a capture on an RCCL group: every eager collective issued so far has finished on
-    the device.  (The process group's completion events are never pooled -- ``init_sites`` turns
-    off torch's event cache, ``TORCH_NCCL_CUDA_EVENT_CACHE=0`` -- so an event the watchdog still
-    polls is never re-recorded inside a capture: the hipErrorCapturedEvent abort a pooled event
-    caused, seen right after eager collectives, cannot happen.)"""
+    the device AND the process group's watchdog has retired it.  The watchdog polls the
+    completion event of every eager collective it holds; one it still held when a capture
+    re-recorded that event aborted the process (hipErrorCapturedEvent, ``profiles/
+    r6_captured_event_abort.txt``: right after eager collectives, e.g. the warm-up steps or
+    dsgd_collective=calibrate).  ``ProcessGroup._wait_for_pending_works`` returns once the
+    watchdog's list is empty -- a condition, not a guessed delay (the round-5 form slept 0.3 s).
+    ``init_sites`` also turns off torch's completion-event cache
+    (``TORCH_NCCL_CUDA_EVENT_CACHE=0``), so no pooled event is shared between works."""
     if getattr(group, "distributed", False) and getattr(group, "backend", None) == "nccl":
         torch.cuda.synchronize()
+        pg = getattr(group, "pg", None)
+        if pg is not None and hasattr(pg, "_wait_for_pending_works"):
+            pg._wait_for_pending_works()
+
 
 # The LSTM weight repack leaves the graph and rides in the step prologue's launch
 # (DINUNET_DEFER_PACK=0 keeps it captured)

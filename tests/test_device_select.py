@@ -19,7 +19,8 @@ def test_gpus_empty_means_cpu():
 
 def test_gpus_list_picks_the_first_id():
     assert resolve_device([1], local_rank=0, n_devices=8) == torch.device("cuda", 1)
-    assert resolve_device([2, 3], local_rank=0, n_devices=8) == torch.device("cuda", 2)
+    with pytest.warns(RuntimeWarning, match="not used"):  # extra ids are reported, not dropped
+        assert resolve_device([2, 3], local_rank=0, n_devices=8) == torch.device("cuda", 2)
     assert resolve_device(5, local_rank=0, n_devices=8) == torch.device("cuda", 5)
 
 

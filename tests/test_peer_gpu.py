@@ -14,12 +14,15 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world,wire", [(2, "all"), (4, "fp16")])
-def test_peer_exchange_multiprocess(world, wire):
+@pytest.mark.parametrize("world,wire,wait", [(2, "all", "launch"), (4, "fp16", "launch"),
+                                             (4, "all", "inline")])
+def test_peer_exchange_multiprocess(world, wire, wait):
+    """``wait``: the waits as one-workgroup launches of their own (what sites sharing a GPU use)
+    or inside the data launches (one site per GPU, production; safe here: no other kernels)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from mp_util import free_port
     env = dict(os.environ, DINUNET_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2",
-               DINUNET_PEER_TIMEOUT_MS="20000")
+               DINUNET_PEER_TIMEOUT_MS="20000", DINUNET_PEER_WAIT=wait)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
            str(world), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tools", "peer_check.py"), "--wire", wire, "--reps", "3"]

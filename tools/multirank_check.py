@@ -201,9 +201,22 @@ def main():
             g_first = (flat.grad.double() * getattr(eng, "last_scale", 1.0)).clone()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    if getattr(eng, "peer", False):  # a timed-out wait of the peer exchange (sticky error words)
+        from dinunet_implementations_amd.parallel import peer as _peer
+        errs = grp.all_gather_object([(a.me, a.error()) for a in _peer.arenas()])
+        if any(code for site in errs for _, code in site):  # which flags were left set
+            dump = [(str(k), _peer.flag_state(ex)) for a_ in _peer.arenas()
+                    for k, ex in a_._cache.items()]
+            for r_, d_ in enumerate(grp.all_gather_object(dump)):
+                if grp.rank == 0:
+                    print(f"# site {r_} flags: {d_}", file=sys.stderr, flush=True)
+    else:
+        errs = None
     mine = flat.data.detach().cpu()
     allp = grp.all_gather(mine)
     same = all(torch.equal(p, allp[0]) for p in allp)
+    if errs is not None and any(code for site in errs for _, code in site):
+        same = False  # a timed-out wait: that step used incomplete data
     maxdiff = max(float((p - allp[0]).abs().max()) for p in allp)
     res = {"ok": bool(same), "world": grp.world, "engine": a.engine, "precision": a.precision,
            "payload": eng.wire, "collective": a.collective,
@@ -214,7 +227,7 @@ def main():
            "captured_update": bool(step.graph_opt or any(
                v[2] is True for v in getattr(step, "_dgraphs", {}).values()
                if isinstance(v, tuple) and len(v) == 3)),
-           "param_sum": float(mine.double().sum())}
+           "param_sum": float(mine.double().sum()), "peer_errors": errs}
     if a.oracle:
         ok_o = torch.zeros(1, dtype=torch.float64, device=dev)
         if grp.rank == 0:

@@ -107,6 +107,23 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         us = t0.elapsed_time(t1) * 1e3 / max(1, a.time)
+        # two exchanges pushed back to back, finished by ONE fused launch (the dSGD buckets)
+        n2 = a.n // 3 + 77
+        pm2 = peer.mean(grp, dev, n2, wire, ("check2", wire))
+        y1, y2 = torch.empty(a.n, device=dev), torch.empty(n2, device=dev)
+        y1.copy_(site_data(11, me, a.n))
+        y2.copy_(site_data(12, me, n2))
+        pm.start(y1)
+        pm2.start(y2)
+        peer.finish_many([(pm, y1, 1.0), (pm2, y2, 1.0)])
+        torch.cuda.synchronize()
+        for step_, out_, n_ in ((11, y1, a.n), (12, y2, n2)):
+            xs_ = [site_data(step_, r, n_).double() for r in range(W)]
+            ref = sum(xs_) / W
+            mag = sum(v.abs() for v in xs_) / W
+            worst = max(worst, float(((out_.cpu().double() - ref).abs() / mag.clamp_min(1e-38)).max()))
+            outs = grp.all_gather(out_.cpu())
+            same = same and all(torch.equal(t, outs[0]) for t in outs)
         err_word = pm.ar.error()
         ok = worst <= TOL[wire] and same and gerr <= TOL[wire] and err_word == 0
         res[wire] = {"mean_rel_err": worst, "replicas_identical": same, "gather_rel_err": gerr,
