@@ -159,6 +159,47 @@ DN_API int dn_relu_bwd_colsum(const void* dy, const void* y, void* dym, float* d
 }
 
 // in-kernel wait limit (common.h): < 0 restores every kernel's default
+// fp32 -> bf16 images of up to 8 tensors in one launch (the replicated head's weight images when
+// no Adam-emitted operand pack keeps them current: ops.head.HeadSpec.own_images)
+constexpr int CAST_MAX = 8;
+struct CastGroup {
+  const float* src[CAST_MAX];
+  bf16* dst[CAST_MAX];
+  long n[CAST_MAX];
+  long off[CAST_MAX + 1];  // prefix of n (elements)
+  int count;
+};
+
+__global__ void __launch_bounds__(256) cast_group_kernel(CastGroup g) {
+  const long total = g.off[g.count];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    int t = 0;
+#pragma unroll
+    for (int k = 1; k < CAST_MAX; ++k)
+      if (k < g.count && i >= g.off[k]) t = k;
+    const long j = i - g.off[t];
+    g.dst[t][j] = (bf16)g.src[t][j];
+  }
+}
+
+DN_API int dn_cast_bf16_group(const float* const* src, bf16* const* dst, const long* n, int count,
+                              hipStream_t st) {
+  if (count < 1 || count > CAST_MAX || !src || !dst || !n) return DN_BAD_SHAPE;
+  CastGroup g{};
+  g.count = count;
+  for (int k = 0; k < count; ++k) {
+    if (!src[k] || !dst[k] || n[k] < 0) return DN_BAD_SHAPE;
+    g.src[k] = src[k], g.dst[k] = dst[k], g.n[k] = n[k];
+    g.off[k + 1] = g.off[k] + n[k];
+  }
+  const long total = g.off[count];
+  if (total == 0) return DN_OK;
+  const long blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(cast_group_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256),
+                     0, st, g);
+  return dn_launch_status();
+}
+
 int g_dn_spin_limit = -1;
 DN_API int dn_set_spin_limit(int polls) {
   g_dn_spin_limit = polls < 0 ? -1 : polls;

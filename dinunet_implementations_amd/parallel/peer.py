@@ -329,6 +329,8 @@ def errors(reset: bool = True) -> List[tuple]:
     """``[(site, code, what)]`` of every arena whose error word is set (then cleared)."""
     out = []
     for ar in arenas():
+        if not ar._chunks:  # never exchanged anything (or closed)
+            continue
         code = ar.error()
         if code:
             out.append((ar.me, code, f"{PHASES.get(code >> 8, 'wait')} on site {code & 0xff}"))

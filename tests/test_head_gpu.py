@@ -256,9 +256,10 @@ def test_fs_backward_exact_given_forward_state(B):
 @pytest.mark.parametrize("one_launch", [True, False])
 def test_fused_forward_backward_chain_matches_two_phase(one_launch, monkeypatch):
     """With a d(loss) hint the forward runs the backward too: either the WHOLE head step in one
-    launch (csrc/kernels/head_step.hip) or the output-gradient chain with dW / dX left to the
-    backward launch.  Both are bitwise the unfused three-phase result (same reduction orders,
-    same bf16 rounding points)."""
+    launch (csrc/kernels/head_rep.hip on the head's own bf16 weight images, cast right before:
+    no Adam-emitted pack here) or the output-gradient chain with dW / dX left to the backward
+    launch.  Both are bitwise the unfused three-phase result (same reduction orders, same bf16
+    rounding points)."""
     from dinunet_implementations_amd.ops import head as H
     monkeypatch.setattr(H, "_HEAD_STEP", one_launch)
     torch.manual_seed(0)
@@ -315,18 +316,18 @@ class _Imgs:
 
 
 def _step_vs_classic(mods, x, y, log_out, reps=1, rep=False):
-    """Run the head with the one-launch step (``rep``: the replicated-forward kernel
-    head_rep.hip, else head_step.hip) and the three-launch path from identical state; return both
-    results (outputs, dx, grads, buffers)."""
+    """Run the head with the one-launch step (head_rep.hip; ``rep``: on weight images handed in
+    like the fused Adam's persistent pack, else on the head's own images cast right before the
+    launch) and the three-launch path from identical state; return both results (outputs, dx,
+    grads, buffers)."""
     from dinunet_implementations_amd.ops import head as H
     ref_mods = [copy.deepcopy(m) for m in mods]
     one = torch.ones((), device=DEV)
     res = []
     seed0 = None
     for flag, ms in ((True, mods), (False, ref_mods)):
-        old, old_rep = H._HEAD_STEP, H._HEAD_REP
+        old = H._HEAD_STEP
         H._HEAD_STEP = flag
-        H._HEAD_REP = rep
         try:
             spec = H.HeadSpec(ms)
             r = spec.rng(x.device)  # both paths draw the same dropout masks
@@ -347,18 +348,23 @@ def _step_vs_classic(mods, x, y, log_out, reps=1, rep=False):
             res.append((out.clone(), loss.clone(), pred.clone(), xi.grad.clone(),
                         [p.grad.clone() for p in params], [b.clone() for b in bufs], spec))
         finally:
-            H._HEAD_STEP, H._HEAD_REP = old, old_rep
+            H._HEAD_STEP = old
     return res
 
 
 @pytest.mark.parametrize("B,p", [(32, 0.0), (17, 0.0), (32, 0.25), (2, 0.0)])
-def test_head_step_one_launch_ica_bitwise(B, p):
+def test_head_one_launch_own_images_ica_bitwise(B, p):
+    """Steps without the Adam-emitted pack (host-fed, eager): the replicated head on its own
+    bf16 images (one cast launch of the fp32 weights right before) equals the three-launch path
+    bitwise -- the form round 5's hand-off head (head_step.hip, deleted) served."""
+    from dinunet_implementations_amd.ops import head as H
     torch.manual_seed(11)
     mods = list(_ica_head(p=p).to(DEV).train())
     x = torch.randn(B, 384, device=DEV)
     y = torch.randint(0, 2, (B,), device=DEV)
+    n0 = H.REP_LAUNCHES
     a, b = _step_vs_classic(mods, x, y, log_out=False, reps=3)
-    assert int(a[-1].sync(torch.device(DEV))[160].item()) == 0  # no hand-off timed out
+    assert H.REP_LAUNCHES == n0 + 3, "the replicated head did not run"
     for u, v in zip(a[:4], b[:4]):
         assert torch.equal(u, v)
     for u, v in zip(a[4], b[4]):
@@ -368,14 +374,18 @@ def test_head_step_one_launch_ica_bitwise(B, p):
 
 
 @pytest.mark.parametrize("B,dropout_in", [(16, ()), (32, ()), (9, (1,))])
-def test_head_step_one_launch_fs_bitwise(B, dropout_in):
+def test_head_one_launch_fs_outside_envelope_bitwise(B, dropout_in):
+    """The FS MSANNet (66 input features: not a multiple of the replicated head's 16-B rows) is
+    outside the one-launch envelope: asking for it runs the three-launch path, bitwise the same."""
+    from dinunet_implementations_amd.ops import head as H
     torch.manual_seed(12)
     net = _fs_head(dropout_in=dropout_in).to(DEV).train()
     mods = [m for blk in net.layers for m in blk] + [net.fc_out]
     x = torch.rand(B, 66, device=DEV)
     y = torch.randint(0, 2, (B,), device=DEV)
+    n0 = H.REP_LAUNCHES
     a, b = _step_vs_classic(mods, x, y, log_out=True, reps=2)
-    assert int(a[-1].sync(torch.device(DEV))[160].item()) == 0
+    assert H.REP_LAUNCHES == n0
     for u, v in zip(a[:4], b[:4]):
         assert torch.equal(u, v)
     for u, v in zip(a[4], b[4]):
@@ -385,8 +395,9 @@ def test_head_step_one_launch_fs_bitwise(B, dropout_in):
 @pytest.mark.parametrize("B,p", [(32, 0.0), (17, 0.0), (32, 0.25), (2, 0.0), (32, 0.5)])
 def test_head_rep_one_launch_ica_bitwise(B, p):
     """The replicated-forward head (head_rep.hip: every workgroup runs the whole forward and
-    output-gradient chain, no hand-off) equals the three-launch path bitwise: outputs, loss,
-    argmax, d input, every parameter gradient; running statistics to an ulp."""
+    output-gradient chain, no hand-off) on pack-provided images equals the three-launch path
+    bitwise: outputs, loss, argmax, d input, every parameter gradient; running statistics to an
+    ulp."""
     from dinunet_implementations_amd.ops import head as H
     torch.manual_seed(11)
     mods = list(_ica_head(p=p).to(DEV).train())
@@ -454,14 +465,14 @@ def test_head_rep_graph_replay_fresh_masks():
     assert torch.isfinite(x.grad).all()
 
 
-def test_head_step_one_launch_graph_replay_and_epochs(monkeypatch):
-    """Captured in a HIP graph and replayed 200 times (with eager launches in between): the
-    monotonic-epoch hand-offs stay consistent (no timeout, epoch == launches) and the replayed
-    result equals the eager one from the same state."""
+def test_head_own_images_graph_replay_and_epochs():
+    """Own-image head captured in a HIP graph (the weight cast and the replicated head both in
+    the graph) and replayed 200 times with eager launches in between: the done counter resets
+    every launch, the dropout seed advances once per launch, and the weights each replay reads
+    are the CURRENT ones (a changed weight changes the replayed loss)."""
     from dinunet_implementations_amd.ops import head as H
-    monkeypatch.setattr(H, "_HEAD_REP", False)
     torch.manual_seed(13)
-    mods = list(_ica_head(p=0.25).to(DEV).train())
+    mods = list(_ica_head(p=0.0).to(DEV).train())
     spec = H.HeadSpec(mods)
     x = torch.randn(32, 384, device=DEV, requires_grad=True)
     y = torch.randint(0, 2, (32,), device=DEV)
@@ -475,10 +486,13 @@ def test_head_step_one_launch_graph_replay_and_epochs(monkeypatch):
 
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
+    n0 = H.REP_LAUNCHES
     with torch.cuda.stream(s):
         for _ in range(3):
             run()
     torch.cuda.current_stream().wait_stream(s)
+    assert H.REP_LAUNCHES == n0 + 3
+    seed0 = int(spec.rng(x.device).item())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         sl = run()
@@ -487,7 +501,12 @@ def test_head_step_one_launch_graph_replay_and_epochs(monkeypatch):
         if i % 50 == 0:
             run()
     torch.cuda.synchronize()
-    sync = spec.sync(torch.device(DEV))
-    assert int(sync[160].item()) == 0
-    assert int(sync[0].item()) == 3 + 200 + 4  # one epoch per launch
+    assert int(spec.rng(x.device).item()) == seed0 + 200 + 4
+    assert int(spec.sync(x.device)[192].item()) == 0
     assert torch.isfinite(sl).all() and torch.isfinite(x.grad).all()
+    before = float(sl)
+    with torch.no_grad():
+        spec.layers[-1].linear.weight.mul_(3.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(sl) != before, "the replay read stale weight images"

@@ -9,30 +9,22 @@ from dinunet_implementations_amd.parallel.group import SiteGroup, _gpu_shared
 from dinunet_implementations_amd.runtime import health
 
 
-class _Spec:
-    def __init__(self):
-        self._sync = torch.zeros(256, dtype=torch.int32)
-
-
-class _M(torch.nn.Module):
-    def __init__(self):
-        super().__init__()
-        self._head = _Spec()
-
-
-def test_error_words_raise_and_reset():
-    m = _M()
-    eng = types.SimpleNamespace(_table=types.SimpleNamespace(
+def test_error_words_raise_and_reset(monkeypatch):
+    from dinunet_implementations_amd.parallel import peer
+    eng = types.SimpleNamespace(peer=True, _table=types.SimpleNamespace(
         _persist=(None, None, torch.zeros(8 * 64 + 1, dtype=torch.int32))))
-    health.check([m], eng)  # all clear
-    m._head._sync[health.HEAD_ERR_WORD] = 3
+    ar = types.SimpleNamespace(me=1, _chunks=[1], err=torch.zeros(1, dtype=torch.int32))
+    ar.error = lambda: int(ar.err.item())
+    monkeypatch.setattr(peer, "arenas", lambda: [ar])
+    health.check([], eng)  # all clear
     eng._table._persist[2][-1] = 0x203
+    ar.err[0] = 0x100
     with pytest.raises(health.HandoffError) as e:
-        health.check([m], eng, "in epoch 4")
+        health.check([], eng, "in epoch 4")
     msg = str(e.value)
-    assert "head_step code 0x3" in msg and "A1 hand-off" in msg
     assert "lr_persist code 0x203" in msg and "layer 3 Q barrier" in msg and "epoch 4" in msg
-    health.check([m], eng)  # the words were cleared
+    assert "peer_exchange code 0x100" in msg and "reduce-scatter wait" in msg and "site 0" in msg
+    health.check([], eng)  # the words were cleared
 
 
 class _FakeGroup(SiteGroup):

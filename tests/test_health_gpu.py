@@ -1,7 +1,7 @@
-"""Negative controls of the persistent-kernel hand-off check (runtime.health) on the GPU: with the
-in-kernel poll limit forced to 0 every hand-off wait of the one-launch head and every barrier of
-the one-launch rank-dAD iteration gives up at once; the check must then raise -- on the kernels
-directly and through the production site loop -- and stay quiet with the default limit."""
+"""Negative controls of the in-kernel wait check (runtime.health) on the GPU: with the poll limit
+forced to 0 every barrier of the one-launch rank-dAD iteration and every peer-exchange wait that
+finds its flag unset gives up at once; the check must then raise -- on the kernels directly and
+through the production site loop -- and stay quiet with the default limit."""
 import pytest
 import torch
 
@@ -25,22 +25,6 @@ def _step(engine="dSGD"):
     return m, st, x, y
 
 
-def test_head_step_timeout_raises(spin_zero, monkeypatch):
-    from dinunet_implementations_amd.ops import head as H
-    monkeypatch.setattr(H, "_HEAD_REP", False)  # head_step.hip: the head with hand-offs
-    health = spin_zero
-    m, st, x, y = _step()
-    st(x, y)
-    torch.cuda.synchronize()
-    assert m._head is not None and m._head._sync is not None, "one-launch head did not run"
-    with pytest.raises(health.HandoffError, match="head_step"):
-        health.check([m], st.engine)
-    health.set_spin_limit(-1)
-    st(x, y)
-    torch.cuda.synchronize()
-    health.check([m], st.engine)  # default limit: no timeout
-
-
 def test_rankdad_barrier_timeout_raises(spin_zero):
     health = spin_zero
     m, st, x, y = _step("rankDAD")
@@ -56,39 +40,61 @@ def test_rankdad_barrier_timeout_raises(spin_zero):
     health.check([m], eng)
 
 
-def test_site_loop_fails_on_timed_out_handoff(tmp_path, spin_zero, monkeypatch):
-    from dinunet_implementations_amd.ops import head as H
-    monkeypatch.setattr(H, "_HEAD_REP", False)  # head_step.hip: the head with hand-offs
+def test_peer_wait_timeout_raises(spin_zero):
+    """A reduce whose push never ran (no site wrote its flag) gives up at once under the zero
+    limit and says so; after that a complete exchange runs clean and exact."""
+    from dinunet_implementations_amd.parallel import peer
+    from dinunet_implementations_amd.parallel.group import SiteGroup
+    health = spin_zero
+    grp = SiteGroup(device=torch.device("cuda", 0), loopback=True)
+    pm = peer.mean(grp, grp.device, 5000, "fp32", ("health",))
+    x = torch.randn(5000, device="cuda")
+    pm.finish(x)  # no push: the reduce-scatter wait cannot be satisfied
+    torch.cuda.synchronize()
+    eng = type("E", (), {"peer": True})()
+    with pytest.raises(health.HandoffError, match="peer_exchange.*reduce-scatter"):
+        health.check([], eng)
+    health.set_spin_limit(-1)
+    y = torch.randn(5000, device="cuda")
+    ref = y.clone()
+    pm.run_(y)  # one site: the mean is the value itself
+    torch.cuda.synchronize()
+    health.check([], eng)
+    assert torch.equal(y, ref)
+
+
+def test_site_loop_fails_on_timed_out_wait(tmp_path, spin_zero):
     from test_runtime_gpu import _ica_root, _run_site
     root = _ica_root(tmp_path)
     with pytest.raises(spin_zero.HandoffError):
-        _run_site(root, str(tmp_path / "out"), {"epochs": 2, "batch_size": 8})
+        _run_site(root, str(tmp_path / "out"), {"epochs": 2, "batch_size": 8,
+                                                "agg_engine": "rankDAD", "dad_reduction_rank": 4})
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
-@pytest.mark.parametrize("engine", ["rankDAD", "dSGD"])
-def test_persistent_kernels_beside_busy_cus(engine, use_graph, monkeypatch):
-    """the persistent launches -- rank-dAD's one-launch power iteration
-    (``lr_persist_kernel``) and the hand-off head (``head_step.hip``) -- on the multi-site path
-    (one-rank RCCL group: ``_persist_ok`` true, collectives issued) while 64 CUs are held by
-    collective-sized workgroups on a side stream, as RCCL's channel kernels hold them during a
-    transfer: no in-kernel wait may time out and training must match the undisturbed run."""
+@pytest.mark.parametrize("engine,cfg", [("rankDAD", {}), ("dSGD", {"dsgd_collective": "peer"})])
+def test_waiting_kernels_beside_busy_cus(engine, cfg, use_graph, monkeypatch):
+    """the launches that wait -- rank-dAD's one-launch power iteration
+    (``lr_persist_kernel``) and the peer exchange -- on the multi-site path (one-rank RCCL group:
+    ``_persist_ok`` true, collectives issued) while 64 CUs are held by collective-sized
+    workgroups on a side stream, as RCCL's channel kernels hold them during a transfer: no
+    in-kernel wait may time out and training must match the undisturbed run."""
     import torch.distributed as dist
-    from dinunet_implementations_amd.ops import head as H
     from dinunet_implementations_amd.runtime import health
     from test_step_gpu import _OneRankGroup, _batches, _free_port, _trainer
     import os
-    monkeypatch.setattr(H, "_HEAD_REP", False)  # head_step.hip: the head with hand-offs
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
         grp = _OneRankGroup(dist.group.WORLD)
         xs, ys = _batches()
-        ma, fa, sa = _trainer(0, engine=engine, group=grp, use_graph=use_graph)
-        mb, fb, sb = _trainer(0, engine=engine, group=grp, use_graph=use_graph)
+        ma, fa, sa = _trainer(0, engine=engine, group=grp, use_graph=use_graph, cfg=cfg)
+        mb, fb, sb = _trainer(0, engine=engine, group=grp, use_graph=use_graph, cfg=cfg)
         if engine == "rankDAD":
             assert sb.engine._persist_ok, "the persistent power iteration must be on"
+        else:
+            assert sb.engine.peer, "the peer exchange must be on"
         side = torch.cuda.Stream()
         for i in range(xs.shape[0]):
             sa(xs[i], ys[i])
@@ -99,7 +105,6 @@ def test_persistent_kernels_beside_busy_cus(engine, use_graph, monkeypatch):
                 health.occupy_cus(64, 3000)
             sb(xs[i], ys[i])
         torch.cuda.synchronize()
-        assert mb._head is not None and mb._head._sync is not None, "hand-off head did not run"
         health.check([mb], sb.engine)
         assert torch.equal(fa.data, fb.data)
     finally:

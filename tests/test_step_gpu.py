@@ -28,7 +28,7 @@ def _trainer(seed, engine="dSGD", group=None, **kw):
     flat = FlatParams(m.parameters())
     opt = FusedAdam(flat, lr=1e-3)
     grp = group or SiteGroup(device=torch.device("cuda"))
-    eng = make_engine(engine, m, flat, grp, {"precision_bits": "32"})
+    eng = make_engine(engine, m, flat, grp, {"precision_bits": "32", **kw.pop("cfg", {})})
     return m, flat, TrainStep(m, flat, opt, eng, task="ica", **kw)
 
 
