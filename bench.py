@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--tta-subjects", type=int, default=2560,
                     help="site-loop cohort size (split 0.8/0.1/0.1)")
     ap.add_argument("--tta-epochs", type=int, default=30)
-    ap.add_argument("--collective", default="auto",
+    ap.add_argument("--collective", default="calibrate",
                     choices=["auto", "allreduce", "direct", "peer", "calibrate"],
                     help="site-mean form (dsgd_collective): RCCL all-reduce, RCCL all-to-all "
                          "exchange, the IPC peer exchange (parallel/peer.py), or calibrate = time "

@@ -22,6 +22,7 @@ all-reduce SUM in place and folds ``1/world`` into the fused Adam launch).
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -283,16 +284,20 @@ class DSGDEngine(Engine):
             self.calibration = {"choice": "allreduce", "reason": "one site: no collective"}
             return "allreduce"
         peer_ok = self._peer_ok()
-        if self.half:
-            choice = "peer" if peer_ok else "direct"
-            self.calibration = {"choice": choice, "wire": self.wire,
-                                "reason": "16-bit wire: only the exchange sums in fp32"}
-            return choice
         dev = self.flat.grad.device
         cuda = dev.type == "cuda"
         reps = max(1, int(self.cfg.get("dsgd_calibrate_reps", 10)))
         sync = torch.cuda.synchronize if cuda else (lambda: None)
         bufs = [torch.zeros(n, dtype=torch.float32, device=dev) for n in sizes]
+        if self.half:
+            note = None
+            if peer_ok:
+                peer_ok, note = self._peer_verify(bufs)
+            choice = "peer" if peer_ok else "direct"
+            self.calibration = {"choice": choice, "wire": self.wire,
+                                "reason": "16-bit wire: only the exchange sums in fp32"
+                                          + (f"; peer {note}" if note else "")}
+            return choice
 
         def allreduce():
             for b in bufs:
@@ -333,6 +338,9 @@ class DSGDEngine(Engine):
             return t
 
         rccl_graph = cuda and g.backend == "nccl"
+        peer_note = None
+        if peer_ok:
+            peer_ok, peer_note = self._peer_verify(bufs)
         times = [graph_timed(allreduce) if rccl_graph else host_timed(allreduce),
                  graph_timed(peer) if peer_ok else float("inf")]
         t = torch.tensor(times, dtype=torch.float64, device=dev if g.backend == "nccl" else "cpu")
@@ -342,10 +350,49 @@ class DSGDEngine(Engine):
         self.calibration = {"choice": choice, "allreduce_us": round(t_ar, 2),
                             "peer_us": round(t_peer, 2) if peer_ok else None,
                             "allreduce_form": "captured" if rccl_graph else "host-issued",
-                            "peer_form": "captured" if peer_ok else "unavailable",
+                            "peer_form": "captured" if peer_ok else (peer_note or "unavailable"),
                             "bucket_elems": sizes, "sites": g.world, "reps": reps,
                             "wire": self.wire}
         return choice
+
+    def _peer_verify(self, bufs) -> Tuple[bool, Optional[str]]:
+        """Before the peer exchange may compete in ``calibrate``: run it once on every bucket with
+        known values (site r sends (r + 1) * v, v small integers: every sum exact) under a short
+        wait limit and check the mean and the error words on EVERY site -- a machine whose IPC
+        mapping or cross-GPU flags misbehave keeps the all-reduce instead of training on a broken
+        exchange.  Returns (usable, reason when not)."""
+        from . import peer as _peer
+        g = self.group
+        note = None
+        ok = True
+        _lib.call("dn_peer_set_timeout_ms", 2000)
+        try:
+            for (s, e), b in zip(self.buckets, bufs):
+                v = (torch.arange(e - s, device=b.device, dtype=torch.float32) % 7) + 1.0
+                b.copy_(v * float(g.rank + 1))
+                self._peer_mean(("bucket", s, e), e - s).run_(b)
+            torch.cuda.synchronize()
+            want = (g.world + 1) / 2.0
+            for (s, e), b in zip(self.buckets, bufs):
+                v = (torch.arange(e - s, device=b.device, dtype=torch.float32) % 7) + 1.0
+                if not torch.allclose(b, v * want, rtol=1e-6, atol=0):
+                    ok, note = False, "failed verification (wrong mean)"
+            errs = _peer.errors()
+            if errs:
+                ok, note = False, f"failed verification (wait timed out: {errs[0][2]})"
+        except RuntimeError as ex:  # e.g. the IPC mapping refused
+            ok, note = False, f"failed verification ({type(ex).__name__}: {ex})"[:200]
+        finally:
+            ms = os.environ.get("DINUNET_PEER_TIMEOUT_MS")
+            _lib.call("dn_peer_set_timeout_ms", int(ms) if ms else -1)
+        flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64,
+                            device=self.flat.grad.device if g.backend == "nccl" else "cpu")
+        g.all_reduce(flag, op=dist.ReduceOp.MIN)  # one site's failure disqualifies it everywhere
+        if flag.item() < 0.5 and ok:
+            ok, note = False, "failed verification on another site"
+        for b in bufs:
+            b.zero_()
+        return ok, note
 
     def _marker(self, pid: int):
         def hook(g):

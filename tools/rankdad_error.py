@@ -20,6 +20,7 @@ iterations, a bad warm start, an early ``dad_tol`` stop).
 Trajectories (``--modes``), all from the same init and the same site batches:
   dsgd      the exact mean (the dSGD update);
   rankdad   the engine's reconstruction for every factorised Linear, dense mean elsewhere;
+  rankdad_tol0  the same with every power iteration run (``dad_tol`` 0: no early stop);
   svd       mean of the per-site truncated SVDs (the rank-r optimum) -- accuracy of ideal rank r.
 Global validation AUC every ``--eval-every`` steps.  Prints one JSON line.
 
@@ -55,7 +56,7 @@ def main():
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--effect", type=float, default=0.35)
-    ap.add_argument("--modes", default="dsgd,rankdad,svd")
+    ap.add_argument("--modes", default="dsgd,rankdad,rankdad_tol0,svd")
     a = ap.parse_args()
 
     from dinunet_implementations_amd.data.synthetic import ica_cohort_hard
@@ -81,12 +82,15 @@ def main():
            "dad_num_pow_iters": a.iters, "dad_tol": a.tol}
 
     def run(mode):
+        mcfg = dict(cfg)
+        if mode == "rankdad_tol0":  # every power iteration, no dad_tol early stop
+            mcfg["dad_tol"] = 0.0
         torch.manual_seed(a.seed)
         model = ICALstm(input_size=256, hidden_size=384, num_comps=C, window_size=Wn).to(dev).train()
         flat = FlatParams(model.parameters())
         opt = FusedAdam(flat, lr=a.lr)
         grp = SiteGroup(device=dev)
-        engs = [make_engine("rankDAD", model, flat, grp, dict(cfg)) for _ in range(a.sites)]
+        engs = [make_engine("rankDAD", model, flat, grp, dict(mcfg)) for _ in range(a.sites)]
         layers = engs[0].fast_layers  # (module, flat offset, out, in, r, send P off, send Q off)
         names = {id(m): n for n, m in model.named_modules()}
         gens = [torch.Generator(device=dev).manual_seed(7 + s + 100 * a.seed) for s in range(a.sites)]
@@ -115,7 +119,7 @@ def main():
                 flat.zero_grad()
                 _, loss, _ = model.forward_loss(Xt[idx], Yt[idx])
                 loss.backward()
-                if mode == "rankdad" or step % a.svd_every == 0:
+                if mode.startswith("rankdad") or step % a.svd_every == 0:
                     engs[s].pre_reduce()  # the production power iteration on this site's G_s
                 gs.append(flat.grad.clone())
             gmean = torch.stack(gs).mean(0)
@@ -124,7 +128,7 @@ def main():
             for m, o, out_f, in_f, r, po, qo in layers:
                 name = names[id(m)]
                 exact = gmean[o:o + out_f * in_f].view(out_f, in_f).double()
-                need_engine = mode == "rankdad" or analyse
+                need_engine = mode.startswith("rankdad") or analyse
                 if need_engine:
                     rec = torch.zeros_like(exact)
                     for e in engs:
@@ -132,18 +136,16 @@ def main():
                         Q = e._send[qo:qo + in_f * r].view(in_f, r).double()
                         rec += P @ Q.t()
                     rec /= a.sites
-                    if mode == "rankdad":
+                    if mode.startswith("rankdad"):
                         upd[o:o + out_f * in_f] = rec.reshape(-1).float()
                     err_hist[name].append(float((rec - exact).norm() / exact.norm().clamp_min(1e-30)))
                 if mode == "svd" or analyse:
-                    rec2 = torch.zeros_like(exact)
-                    tails = []
-                    for g in gs:
-                        G = g[o:o + out_f * in_f].view(out_f, in_f).double()
-                        U, S, Vh = torch.linalg.svd(G, full_matrices=False)
-                        rec2 += (U[:, :r] * S[:r]) @ Vh[:r]
-                        tails.append(float((S[r:] ** 2).sum() / (S ** 2).sum().clamp_min(1e-300)))
-                    rec2 /= a.sites
+                    # every site's G at once (batched SVD), the truncation in fp64
+                    Gs = torch.stack([g[o:o + out_f * in_f].view(out_f, in_f) for g in gs])
+                    U, S, Vh = torch.linalg.svd(Gs, full_matrices=False)
+                    U, S, Vh = U.double(), S.double(), Vh.double()
+                    rec2 = torch.einsum("sik,sk,skj->ij", U[:, :, :r], S[:, :r], Vh[:, :r]) / a.sites
+                    tails = ((S[:, r:] ** 2).sum(1) / (S ** 2).sum(1).clamp_min(1e-300)).tolist()
                     if mode == "svd":
                         upd[o:o + out_f * in_f] = rec2.reshape(-1).float()
                     if analyse:
