@@ -64,12 +64,14 @@ class _PxArgs(ctypes.Structure):
 
 
 # hand-off form (peer.hip PxArgs.mode): bit 0 = release by store drain only, bit 1 = system-scope
-# payload loads instead of an acquire invalidate.  Default 2: every payload byte is read with
-# system-scope loads from uncached memory, so the acquire's invalidate buys nothing (loopback step
-# 0.3643 -> 0.3564 ms, profiles/r6_peer_mode_ab.jsonl).  The release keeps the L2 write-back the
-# memory model prescribes at system scope (bit 0 drops it: 0.3574 ms, not the default -- the drain
-# alone is not specified to order a store against a later store from another agent).
-MODE = int(os.environ.get("DINUNET_PEER_MODE", "2"))
+# payload loads instead of an acquire invalidate.  Default 3: every byte a peer reads -- payload
+# and flag words -- is an uncached store / a system-scope load, so the full system fences' L2
+# write-back and invalidate touch nothing the exchange uses; the release is each storing wave's
+# vmcnt(0) drain (the completion the memory model's system release waits for after its
+# write-back).  Loopback fp16 step 0.3643 (fences) -> 0.3564 (bit 1) -> 0.3497-0.3502 ms (both),
+# the multi-process peer and oracle suites pass with it (profiles/r6_peer_mode_ab.jsonl,
+# profiles/r6_peer_mode3.jsonl); DINUNET_PEER_MODE=0 restores the fences.
+MODE = int(os.environ.get("DINUNET_PEER_MODE", "3"))
 
 
 def available(group, device) -> bool:
