@@ -231,6 +231,15 @@ class DSGDEngine(Engine):
             self.wire = "bf16"
         self._comm_stream = (torch.cuda.Stream(device=flat.grad.device)
                              if self.direct and group.distributed and flat.grad.is_cuda else None)
+        # the peer exchange takes the whole gradient as ONE exchange after the backward, and the
+        # step keeps its backward in one piece (``prefers_split``, runtime.step): the split's
+        # extra launches (a second grouped weight-gradient launch and split-K reduce, ~15 us) and a
+        # second exchange's three launches cost more than pushing the body bucket early hides
+        # (loopback fp16 step: profiles/r6_peer_unsplit_ab.jsonl).  The RCCL all-reduce keeps the
+        # split: its buckets run on RCCL's own stream, truly under the encoder backward.
+        self.prefers_split = not self.peer
+        if self.peer and len(self.buckets) > 1 and bool(self.cfg.get("peer_one_bucket", True)):
+            self._set_buckets([(self.buckets[-1][0], self.buckets[0][1])])
         self._peer_build()
         self._hooks = []
         self._delivered = set()
@@ -292,7 +301,10 @@ class DSGDEngine(Engine):
         if self.half:
             note = None
             if peer_ok:
-                peer_ok, note = self._peer_verify(bufs)
+                prange = [(self.buckets[-1][0], self.buckets[0][1])]
+                peer_ok, note = self._peer_verify(
+                    [torch.zeros(prange[0][1] - prange[0][0], dtype=torch.float32, device=dev)],
+                    prange)
             choice = "peer" if peer_ok else "direct"
             self.calibration = {"choice": choice, "wire": self.wire,
                                 "reason": "16-bit wire: only the exchange sums in fp32"
@@ -303,8 +315,12 @@ class DSGDEngine(Engine):
             for b in bufs:
                 g.all_reduce(b)
 
+        # the peer exchange as the step would run it: ONE exchange of the whole gradient
+        prange = [(self.buckets[-1][0], self.buckets[0][1])]
+        pbufs = [torch.zeros(prange[0][1] - prange[0][0], dtype=torch.float32, device=dev)]
+
         def peer():
-            for (s, e), b in zip(self.buckets, bufs):
+            for (s, e), b in zip(prange, pbufs):
                 self._peer_mean(("bucket", s, e), e - s).run_(b)
 
         def host_timed(fn):
@@ -340,7 +356,7 @@ class DSGDEngine(Engine):
         rccl_graph = cuda and g.backend == "nccl"
         peer_note = None
         if peer_ok:
-            peer_ok, peer_note = self._peer_verify(bufs)
+            peer_ok, peer_note = self._peer_verify(pbufs, prange)
         times = [graph_timed(allreduce) if rccl_graph else host_timed(allreduce),
                  graph_timed(peer) if peer_ok else float("inf")]
         t = torch.tensor(times, dtype=torch.float64, device=dev if g.backend == "nccl" else "cpu")
@@ -355,7 +371,7 @@ class DSGDEngine(Engine):
                             "wire": self.wire}
         return choice
 
-    def _peer_verify(self, bufs) -> Tuple[bool, Optional[str]]:
+    def _peer_verify(self, bufs, ranges) -> Tuple[bool, Optional[str]]:
         """Before the peer exchange may compete in ``calibrate``: run it once on every bucket with
         known values (site r sends (r + 1) * v, v small integers: every sum exact) under a short
         wait limit and check the mean and the error words on EVERY site -- a machine whose IPC
@@ -367,13 +383,13 @@ class DSGDEngine(Engine):
         ok = True
         _lib.call("dn_peer_set_timeout_ms", 2000)
         try:
-            for (s, e), b in zip(self.buckets, bufs):
+            for (s, e), b in zip(ranges, bufs):
                 v = (torch.arange(e - s, device=b.device, dtype=torch.float32) % 7) + 1.0
                 b.copy_(v * float(g.rank + 1))
                 self._peer_mean(("bucket", s, e), e - s).run_(b)
             torch.cuda.synchronize()
             want = (g.world + 1) / 2.0
-            for (s, e), b in zip(self.buckets, bufs):
+            for (s, e), b in zip(ranges, bufs):
                 v = (torch.arange(e - s, device=b.device, dtype=torch.float32) % 7) + 1.0
                 if not torch.allclose(b, v * want, rtol=1e-6, atol=0):
                     ok, note = False, "failed verification (wrong mean)"
@@ -437,7 +453,15 @@ class DSGDEngine(Engine):
                                                         for p, o, _ in segs):
             raise ValueError("stem parameters must occupy one contiguous flat range")
         body = [r for r in ((s1, self.flat.numel), (0, s0)) if r[1] > r[0]]
-        self.buckets = body + [(s0, s1)]
+        self._set_buckets(body + [(s0, s1)])
+        self._peer_build()
+        return list(range(len(body)))
+
+    def _set_buckets(self, ranges):
+        """New contiguous bucket ranges (covering every parameter); per-parameter bookkeeping
+        rebuilt to match."""
+        segs = list(self.flat.segments())
+        self.buckets = list(ranges)
         self._param_bucket = {}
         for p, o, _ in segs:
             self._param_bucket[id(p)] = next(i for i, (a, b) in enumerate(self.buckets) if a <= o < b)
@@ -446,8 +470,6 @@ class DSGDEngine(Engine):
             self._expected[self._param_bucket[id(p)]] += 1
         self._half_bufs.clear()
         self._reset()
-        self._peer_build()
-        return list(range(len(body)))
 
     def _peer_build(self):
         """The peer exchange of every bucket, built now (arena regions and the IPC handle

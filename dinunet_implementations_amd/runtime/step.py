@@ -162,7 +162,9 @@ class TrainStep:
                      and hasattr(engine, "split_buckets"))
         if split is None:
             env = os.environ.get("DINUNET_SPLIT_GRAPH", "")
-            split = can_split and (engine.group.distributed if env == "" else env == "1")
+            split = can_split and ((engine.group.distributed
+                                    and getattr(engine, "prefers_split", True))
+                                   if env == "" else env == "1")
         self.split = bool(split and can_split)
         # collectives inside the captured step: the engine says whether its site-means can be
         # captured (the peer exchange on any backend, RCCL's all-reduce; not host collectives)

@@ -119,7 +119,9 @@ def test_replicas_bit_identical(world, args):
             assert "grad_rel_err" in res, res
     assert res["graph"] and res["world"] == world
     if "device" in args and "dSGD" in args and "--accum" not in args:  # the bench path: the
-        assert res["adam_pack"] and res["split"], res  # update emits the next step's operands
+        assert res["adam_pack"], res  # update emits the next step's operands
+        # split backward with the all-reduce; the peer exchange runs the whole step unsplit
+        assert res["split"] == (not res["peer"]), res
     if "peer" in args or ("16" in args and "allreduce" not in args):  # the peer exchange, captured
         assert res["peer"] and (res["comm_graph"] or "--accum" in args), res
         if "--accum" not in args or "device" in args:  # (host-fed accumulation: eager update)
