@@ -130,7 +130,8 @@ __device__ __forceinline__ void wait_count(int* ctr, int need) {
 #ifndef BWD_RG
 #define BWD_RG 4
 #endif
-// LSTM_FLAGS: forward step hand-off through LDS counters (1) or a workgroup barrier (0);
+// LSTM_FLAGS: forward step hand-off through LDS counters (1; 2: with each producer group's h
+// fragments read in one round) or a workgroup barrier (0);
 // LSTM_PRIO: wave priority raised over the gate phase (the step's critical path) when > 0
 #ifndef LSTM_FLAGS
 #define LSTM_FLAGS 0
@@ -387,15 +388,26 @@ fwd_recur(const bf16* xp,                  // [B*S][ndir][4*HD] permuted cols, n
         hball[ks] = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // LSTM_FLAGS == 2: the flag hand-off with each producer group's h fragments read together
+    // right after its counter is seen (2 k-steps per read round instead of one read per k-step)
+    constexpr bool GRP = LSTM_FLAGS == 2 && !STREAM && UG == 1 && NLM == 0;
+    bf16x8 hg[2];
 #pragma unroll
     for (int ks = 0; ks < (STREAM ? 0 : KS); ++ks) {
       if constexpr (LSTM_FLAGS) {
-        if (ks % (2 * UG) == 0) wait_count(&hcnt[ks / (2 * UG)], 4 * t);
+        if (ks % (2 * UG) == 0) {
+          wait_count(&hcnt[ks / (2 * UG)], 4 * t);
+          if constexpr (GRP) {
+            hg[0] = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
+            hg[1] = *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * (ks + 1) + 8 * q]);
+          }
+        }
       }
       // unmasked (exec-masking made the compiler branch and drain lgkmcnt before every MFMA):
       // lanes of padded columns re-read a valid row, see above
       const bf16x8 hb = HB_ALL ? hball[HB_ALL ? ks : 0]
-                               : *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
+                      : GRP ? hg[ks & 1]
+                            : *reinterpret_cast<const bf16x8*>(&hbuf[cur][n % BR][32 * ks + 8 * q]);
 #pragma unroll
       for (int mt = 0; mt < NRM; ++mt) acc[mt] = mfma16(wf[mt][ks], hb, acc[mt]);
 #pragma unroll

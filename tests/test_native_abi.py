@@ -35,3 +35,15 @@ def test_registered_arities_match_c_declarations():
         elif len(argtypes) != csigs[name]:
             bad[name] = f"ctypes {len(argtypes)} vs C {csigs[name]}"
     assert not bad, bad
+
+
+def test_peer_exchange_argument_block_matches_library():
+    """``parallel.peer._PxArgs`` (ctypes) and peer.hip's PxArgs must agree byte for byte: the
+    launcher copies the block into the kernel arguments."""
+    import ctypes
+    from dinunet_implementations_amd.ops import _lib
+    if not _lib.native_available():
+        pytest.skip("kernel library not built")
+    from dinunet_implementations_amd.parallel import peer
+    assert ctypes.sizeof(peer._PxArgs) == int(_lib.lib().dn_peer_args_size())
+    assert int(_lib.lib().dn_peer_handle_size()) == 64
