@@ -68,8 +68,8 @@ class _PxArgs(ctypes.Structure):
 # and flag words -- is an uncached store / a system-scope load, so the full system fences' L2
 # write-back and invalidate touch nothing the exchange uses; the release is each storing wave's
 # vmcnt(0) drain (the completion the memory model's system release waits for after its
-# write-back).  Loopback fp16 step 0.3643 (fences) -> 0.3564 (bit 1) -> 0.3497-0.3502 ms (both),
-# the multi-process peer and oracle suites pass with it (profiles/r6_peer_mode_ab.jsonl,
+# write-back).  Loopback fp16 step (split form) 0.3643 (fences) -> 0.3564 (bit 1) -> 0.3497-0.3502
+# ms (both; one unsplit exchange since: 0.3255, profiles/r6_peer_unsplit_ab.jsonl), the multi-process peer and oracle suites pass with it (profiles/r6_peer_mode_ab.jsonl,
 # profiles/r6_peer_mode3.jsonl); DINUNET_PEER_MODE=0 restores the fences.
 MODE = int(os.environ.get("DINUNET_PEER_MODE", "3"))
 

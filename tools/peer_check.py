@@ -107,7 +107,7 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         us = t0.elapsed_time(t1) * 1e3 / max(1, a.time)
-        # two exchanges pushed back to back, finished by ONE fused launch (the dSGD buckets)
+        # two exchanges pushed back to back, then finished together (peer.finish_many)
         n2 = a.n // 3 + 77
         pm2 = peer.mean(grp, dev, n2, wire, ("check2", wire))
         y1, y2 = torch.empty(a.n, device=dev), torch.empty(n2, device=dev)
