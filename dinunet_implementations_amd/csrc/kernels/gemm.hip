@@ -18,8 +18,6 @@
 // * Epilogue: bias add, ReLU, accumulate (beta), fp32 or bf16 store, optional row permutation
 //   (used to emit LSTM gate-permuted rows straight into the reference [i|f|o|g] layout).
 #include "common.h"
-#include <stdlib.h>
-#include <string.h>
 
 namespace {
 
@@ -559,9 +557,9 @@ __device__ __forceinline__ int sw_km128(int k) { return (((k >> 1) & 1) | (((k >
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <int ROWS, bool KCONTIG, int NW = 4, int BK = 64>
+template <int ROWS, bool KCONTIG, int NW = 4>
 struct DmaImg {
-  static constexpr int BYTES = ROWS * BK * 2;    // one BK-deep K tile
+  static constexpr int BYTES = ROWS * 64 * 2;    // one 64-deep K tile
   static constexpr int PER_WAVE = BYTES / 1024 / NW;  // 1 KB DMA instructions per wave
 };
 
@@ -569,13 +567,9 @@ struct DmaImg {
 // source pointers fixed for the whole K loop (row / column part and swizzle folded in once; a K
 // tile only adds its k offset).  A lane whose row (column) is out of range keeps a null pointer
 // and reads the zero page; the k range is checked per tile (K % 8 == 0: chunks are all in or out).
-// BK = 32 (gemm256_kernel's deep rings): k-contiguous images are [rows][32 k] (64-B rows, slot =
-// chunk ^ ((row >> 2) & 3): again 16 distinct bank quads per 16-row fragment read); k-major
-// images are the first 32 k-rows of the 64-deep layout.
-template <int ROWS, bool KCONTIG, int NW = 4, int BK = 64>
+template <int ROWS, bool KCONTIG, int NW = 4>
 struct DmaStream {
-  static_assert(BK == 64 || BK == 32, "K tile depth");
-  static constexpr int PW = DmaImg<ROWS, KCONTIG, NW, BK>::PER_WAVE;
+  static constexpr int PW = DmaImg<ROWS, KCONTIG, NW>::PER_WAVE;
   const bf16* p[PW];
   int kofs[PW];  // the chunk's k offset within the tile
   long kstep;    // elements per unit of k
@@ -607,8 +601,8 @@ struct DmaStream {
     for (int j = 0; j < PW; ++j) {
       const int ins = ins0 + j;
       if constexpr (KCONTIG) {
-        const int r = BK == 64 ? ins * 8 + (lane >> 3) : ins * 16 + (lane >> 2);
-        const int ch = BK == 64 ? (lane & 7) ^ sw_kc(r) : (lane & 3) ^ ((r >> 2) & 3);
+        const int r = ins * 8 + (lane >> 3);
+        const int ch = (lane & 7) ^ sw_kc(r);
         const int gr = row0 + r;
         kofs[j] = 8 * ch;
         long row = gr;
@@ -636,7 +630,7 @@ struct DmaStream {
     }
   }
   __device__ __forceinline__ void issue(int k0, int K, char* img) const {
-    if (!KCONTIG && subj) {  // k rows k0 .. k0 + BK - 1 span at most two subjects (gs >= 64)
+    if (!KCONTIG && subj) {  // k rows k0 .. k0 + 63 span at most two subjects (gs >= 64)
       typedef const __attribute__((address_space(4))) long long csubj;
       const int b0 = __builtin_amdgcn_readfirstlane(k0 / gs);
       const long long s0 = ((csubj*)subj)[b0], s1 = ((csubj*)subj)[b0 + 1];
@@ -674,13 +668,9 @@ __device__ __forceinline__ s16x4 tr16_asm(const char* p) {
 }
 
 // 16x32 MFMA operand fragment (operand rows r0 .. r0 + 15, k = 32 ks .. +31) from a DMA image
-template <int ROWS, bool KCONTIG, int BK = 64>
+template <int ROWS, bool KCONTIG>
 __device__ __forceinline__ bf16x8 dma_frag(const char* img, int r0, int ks, int lane) {
-  if constexpr (KCONTIG && BK == 32) {
-    const int r = r0 + (lane & 15);
-    const int ch = lane >> 4;
-    return *reinterpret_cast<const bf16x8*>(img + r * 64 + 16 * (ch ^ ((r >> 2) & 3)));
-  } else if constexpr (KCONTIG) {
+  if constexpr (KCONTIG) {
     const int r = r0 + (lane & 15);
     const int ch = 4 * ks + (lane >> 4);
     return *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * (ch ^ sw_kc(r)));
@@ -914,20 +904,16 @@ gemm_dma_kernel(GemmGroup g) {
 // path in four passes of 32 rows per wave (the ring's 128 KB cannot hold eight 128 x 64 fp32
 // blocks at once), into C (bias / ReLU / mask / beta) or, split-K, raw into the fp32 slab that
 // gemm_splitk_reduce combines (which also applies row maps and the virtual ones column).
-// S stages of BK-deep K tiles (S x BK: 2 x 64 = the two 64 KB stages above, or 4 x 32 / 5 x 32: the
-// same 128 / 160 KB holding three / four tiles in flight -- DINUNET_G256_RING)
-template <int S, int BK>
-constexpr int g256_smem() { return S * (256 * BK * 2) * 2; }
+constexpr int G256_SMEM = 2 * (256 * 64 * 2) * 2;  // two stages of A + B images
 
-template <bool TA, bool TB, int S, int BK>
+template <bool TA, bool TB>
 __global__ void __launch_bounds__(512)
 gemm256_kernel(GemmGroup g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr int BM = 256, BN = 256, NW = 8, WM = 128, WN = 64, FM = WM / 16, FN = WN / 16;
-  typedef DmaImg<BM, !TA, NW, BK> IA;
-  typedef DmaImg<BN, TB, NW, BK> IB;
+  typedef DmaImg<BM, !TA, NW> IA;
+  typedef DmaImg<BN, TB, NW> IB;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
-  static_assert(S * STAGE >= 8 * 32 * (WN + 4) * 4, "epilogue staging fits the ring");
 
   const int ntiles = g.tile_start[g.n];
   const int bid = (int)blockIdx.x;
@@ -948,7 +934,7 @@ gemm256_kernel(GemmGroup g) {
   const int row0 = (tile / tiles_n) * BM, col0 = (tile % tiles_n) * BN;
   const int kbeg = blockIdx.z * P.kchunk;
   const int kend = min(K, kbeg + P.kchunk);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -956,44 +942,32 @@ gemm256_kernel(GemmGroup g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  DmaStream<BM, !TA, NW, BK> sa;
-  DmaStream<BN, TB, NW, BK> sb;
+  DmaStream<BM, !TA, NW> sa;
+  DmaStream<BN, TB, NW> sb;
   sa.init(A, P.lda, row0, M, wid, lane, -1, P.rg.op == 1 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs,
           P.rg.r0);
   sb.init(B, P.ldb, col0, P.epi.xcol >= 0 ? P.epi.xcol : N, wid, lane, P.epi.xcol,
           P.rg.op == 2 ? P.rg.gx : nullptr, P.rg.subj, P.rg.gs);
-  // the ring of gemm_dma_kernel: tiles prefetched D = S - 1 ahead, a counted vmcnt wait for
-  // tile t (the glds of the tiles after it stay in flight), one barrier, refill the stage that
-  // iteration t-1 read
-  constexpr int D = S - 1;
-  constexpr int GW = DmaStream<BM, !TA, NW, BK>::PW + DmaStream<BN, TB, NW, BK>::PW;
-  static_assert((D - 1) * GW < 64, "vmcnt range");
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (d < nk) {
-      sa.issue(kbeg + BK * d, kend, smem + d * STAGE);
-      sb.issue(kbeg + BK * d, kend, smem + d * STAGE + IA::BYTES);
-    }
+  if (nk > 0) {
+    sa.issue(kbeg, kend, smem);
+    sb.issue(kbeg, kend, smem + IA::BYTES);
+  }
   for (int t = 0; t < nk; ++t) {
-    const int ahead = min(D - 1, nk - 1 - t);  // tiles after t already issued
-    if (D - 1 >= 3 && ahead >= 3) DN_VMWAIT(3 * GW);
-    else if (D - 1 >= 2 && ahead == 2) DN_VMWAIT(2 * GW);
-    else if (D - 1 >= 1 && ahead == 1) DN_VMWAIT(GW);
-    else __builtin_amdgcn_s_waitcnt(DN_VMCNT0);  // this wave's share of tile t has landed
-    __builtin_amdgcn_s_barrier();                // ... every wave's; stage (t-1) % S is free again
-    if (t + D < nk) {
-      char* nxt = smem + ((t + D) % S) * STAGE;
-      sa.issue(kbeg + BK * (t + D), kend, nxt);
-      sb.issue(kbeg + BK * (t + D), kend, nxt + IA::BYTES);
+    __builtin_amdgcn_s_waitcnt(DN_VMCNT0);  // this wave's share of tile t has landed
+    __builtin_amdgcn_s_barrier();           // ... every wave's; stage (t+1)&1 is free again
+    if (t + 1 < nk) {
+      char* nxt = smem + ((t + 1) & 1) * STAGE;
+      sa.issue(kbeg + 64 * (t + 1), kend, nxt);
+      sb.issue(kbeg + 64 * (t + 1), kend, nxt + IA::BYTES);
     }
-    const char* cur = smem + (t % S) * STAGE;
+    const char* cur = smem + (t & 1) * STAGE;
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
+    for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = dma_frag<BN, TB, BK>(cur + IA::BYTES, wn * WN + 16 * j, ks, lane);
+      for (int j = 0; j < FN; ++j) bfr[j] = dma_frag<BN, TB>(cur + IA::BYTES, wn * WN + 16 * j, ks, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = dma_frag<BM, !TA, BK>(cur, wm * WM + 16 * i, ks, lane);
+      for (int i = 0; i < FM; ++i) af[i] = dma_frag<BM, !TA>(cur, wm * WM + 16 * i, ks, lane);
       if constexpr (TA || !TB) {  // asm transposed reads: retire them before the MFMAs
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
@@ -1271,42 +1245,16 @@ int launch(GemmGroup& g, hipStream_t st) {
   return dn_launch_status();
 }
 
-template <bool TA, bool TB, int S, int BK>
-static void launch256_r(GemmGroup& g, int tiles, hipStream_t st) {
-  constexpr int smem_bytes = g256_smem<S, BK>();
-  static bool init = false;
-  if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm256_kernel<TA, TB, S, BK>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem_bytes);
-    init = true;
-  }
-  hipLaunchKernelGGL((gemm256_kernel<TA, TB, S, BK>), dim3((tiles + 7) / 8 * 8, 1, g.splits),
-                     dim3(512), smem_bytes, st, g);
-}
-
-// ring of the 256 x 256 kernel: 0 = 2 x 64, 1 = 4 x 32, 2 = 5 x 32 (DINUNET_G256_RING = 2x64 |
-// 4x32 | 5x32 at the first launch; dn_gemm256_set_ring switches it, for the A/B tests)
-static int g_g256_ring = -1;
-static int g256_ring() {
-  if (g_g256_ring < 0) {
-    const char* e = getenv("DINUNET_G256_RING");
-    g_g256_ring = (e && !strcmp(e, "4x32")) ? 1 : (e && !strcmp(e, "5x32")) ? 2 : 0;
-  }
-  return g_g256_ring;
-}
-DN_API int dn_gemm256_set_ring(int r) {
-  if (r < 0 || r > 2) return DN_BAD_SHAPE;
-  g_g256_ring = r;
-  return DN_OK;
-}
-DN_API int dn_gemm256_ring() { return g256_ring(); }
-
 template <bool TA, bool TB>
 static void launch256_t(GemmGroup& g, int tiles, hipStream_t st) {
-  const int r = g256_ring();
-  if (r == 1) launch256_r<TA, TB, 4, 32>(g, tiles, st);
-  else if (r == 2) launch256_r<TA, TB, 5, 32>(g, tiles, st);
-  else launch256_r<TA, TB, 2, 64>(g, tiles, st);
+  static bool init = false;
+  if (!init) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm256_kernel<TA, TB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G256_SMEM);
+    init = true;
+  }
+  hipLaunchKernelGGL((gemm256_kernel<TA, TB>), dim3((tiles + 7) / 8 * 8, 1, g.splits), dim3(512),
+                     G256_SMEM, st, g);
 }
 
 // 256 x 256 tiles (tile 2): bf16 operands on the LDS-DMA contract, split-K through the reduce

@@ -27,8 +27,6 @@ _lib.register("dn_gemm", [_lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_long, _l
                           _lib.c_void_p])
 
 _lib.register("dn_gemm_set_dma", [_lib.c_int])
-_lib.register("dn_gemm256_set_ring", [_lib.c_int])
-_lib.register("dn_gemm256_ring", [])
 _lib.register("dn_gemm_dma_on", [])
 _lib.register("dn_gemm_arm_bump", [_lib.c_void_p, _lib.c_void_p])
 _lib.register("dn_gemm_bump_armed", [])
@@ -208,15 +206,6 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
             out.copy_(res.to(out.dtype))
             return out
         return res.to(out_dtype)
-    if (PANEL and out is None and M >= PANEL_MIN_M and _panel_ok(a, b, trans_a, trans_b, out_dtype,
-                                                                bias, relu, alpha, beta, row_map,
-                                                                splits, tile, mask)):
-        c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
-        rc = _lib.lib().dn_panel_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
-                                      c.data_ptr(), c.stride(0), M, N, K, PANEL_NCOL,
-                                      _lib.stream())
-        if rc == 0:
-            return c
     A, ta, lda = _layout(A, True)
     B, tb, ldb = _layout(B, False)
     if out is None:
@@ -267,37 +256,6 @@ def mm(a: Tensor, b: Tensor, trans_a: bool = False, trans_b: bool = False,
                   (mask.data_ptr() + r0 * mask.stride(0) * 2) if mask is not None else None,
                   mask.stride(0) if mask is not None else 0, None, *gargs, r0, _lib.stream())
     return out
-
-
-# Row-panel kernel (csrc/kernels/panel.hip) for ``A W^T`` with K <= 256 and a bf16 output -- the
-# LSTM input projection -- from PANEL_MIN_M rows: a persistent workgroup keeps its 128-row block of
-# A in LDS across every column of the output and stores straight from the accumulators, where the
-# 256 x 256 tile kernel re-reads A per column tile and serialises each short tile's DMA prologue
-# and staged epilogue.  DINUNET_PANEL=0 keeps the tile kernel (A/B switch); DINUNET_PANEL_NCOL
-# forces the columns per work item (0: automatic).
-PANEL = __import__("os").environ.get("DINUNET_PANEL", "1") != "0"
-PANEL_MIN_M = int(__import__("os").environ.get("DINUNET_PANEL_MIN_M", "16384"))
-PANEL_NCOL = int(__import__("os").environ.get("DINUNET_PANEL_NCOL", "0"))
-_lib.register("dn_panel_gemm", [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_long,
-                                _lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_int, _lib.c_int,
-                                _lib.c_int, _lib.c_void_p])
-
-
-def _panel_ok(a: Tensor, b: Tensor, trans_a: bool, trans_b: bool, out_dtype, bias, relu, alpha,
-              beta, row_map, splits, tile, mask) -> bool:
-    """Does ``mm(a, b, trans_b=True, out_dtype=bf16)`` meet dn_panel_gemm's contract?"""
-    if not (trans_b and not trans_a and out_dtype == torch.bfloat16 and bias is None and not relu
-            and alpha == 1.0 and beta == 0.0 and row_map is None and splits is None
-            and tile is None and mask is None and a.is_cuda):
-        return False
-    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
-        return False
-    K, N = a.shape[1], b.shape[0]
-    if K not in (64, 128, 256) or N % 128 or a.stride(1) != 1 or b.stride(1) != 1:
-        return False
-    if a.stride(0) % 8 or b.stride(0) % 8 or a.data_ptr() % 16 or b.data_ptr() % 16:
-        return False
-    return _gather_of(a) is None and _gather_of(b) is None
 
 
 # DINUNET_GEMM_TAIL=0: no row-range tail split of 256 x 256 launches (A/B switch)

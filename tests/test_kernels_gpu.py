@@ -748,69 +748,3 @@ def test_gemm256_tail_rows_split(case):
     head = 256 * 256
     assert torch.equal(out[:head], plain[:head])  # rows before the tail: the same launch
     assert rel(out[head:], plain[head:]) < 1e-2
-
-
-@pytest.mark.parametrize("K,N,ncol,M", [(256, 1536, 0, 128 * 300 + 37), (256, 1536, 128, 3136),
-                                        (256, 1536, 384, 20000), (128, 512, 256, 5000),
-                                        (64, 384, 0, 999)])
-def test_panel_gemm_matches_tile_gemm(K, N, ncol, M):
-    """Row-panel projection kernel (csrc/kernels/panel.hip): C = A W^T in bf16 against the fp32
-    reference, ragged row blocks (rows >= M dropped by the buffer stores), every column-group width,
-    and bitwise against the 256 x 256 tile kernel (the same MFMA dot products in the same k
-    order); the sentinel past M is untouched."""
-    from dinunet_implementations_amd.ops import _lib
-    from dinunet_implementations_amd.ops import gemm as G
-    g = torch.Generator(device=DEV).manual_seed(11)
-    a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
-    buf = torch.full((M + 128, N), 7.0, device=DEV, dtype=torch.bfloat16)
-    rc = _lib.lib().dn_panel_gemm(a.data_ptr(), K, w.data_ptr(), K, buf.data_ptr(), N, M, N, K,
-                                  ncol, _lib.stream())
-    assert rc == 0
-    out = buf[:M]
-    ref = a.float() @ w.float().t()
-    assert rel(out, ref) < 1e-2
-    assert bool((buf[M:] == 7.0).all())
-    tile = G.mm(a, w, trans_b=True, out_dtype=torch.bfloat16, tile=2 if M >= 4096 else 0)
-    assert torch.equal(out, tile)
-    # through mm(): taken from PANEL_MIN_M rows
-    old = G.PANEL_MIN_M
-    G.PANEL_MIN_M = 1
-    try:
-        assert torch.equal(G.mm(a, w, trans_b=True, out_dtype=torch.bfloat16), out)
-    finally:
-        G.PANEL_MIN_M = old
-
-
-@pytest.mark.parametrize("ring", [1, 2])
-def test_gemm256_deep_rings_bitwise(ring):
-    """The 256 x 256 kernel's deep rings (4 x 32 / 5 x 32 K tiles, DINUNET_G256_RING) against the
-    2 x 64 ring: every operand layout, ragged M / N / K, split-K slabs, bias / ReLU / bf16
-    epilogue -- the same MFMA sequence in the same k order, so bitwise equal; and the fp32
-    reference."""
-    from dinunet_implementations_amd.ops import _lib
-    from dinunet_implementations_amd.ops import gemm as G
-    L = _lib.lib()
-    g = torch.Generator(device=DEV).manual_seed(5)
-    cases = [(70000, 256, 1000, False, False, {}), (65600, 300, 512, False, True,
-              dict(bias=torch.randn(300, device=DEV, generator=g), relu=True,
-                   out_dtype=torch.bfloat16)),
-             (256, 1536, 100352, True, False, dict(splits=4)), (2048, 256, 65536, True, True, {})]
-    try:
-        for M, N, K, ta, tb, kw in cases:
-            a = torch.randn(*((K, M) if ta else (M, K)), device=DEV, generator=g).to(torch.bfloat16)
-            b = torch.randn(*((N, K) if tb else (K, N)), device=DEV, generator=g).to(torch.bfloat16)
-            assert L.dn_gemm256_set_ring(0) == 0
-            base = G.mm(a, b, trans_a=ta, trans_b=tb, tile=2, **kw)
-            assert L.dn_gemm256_set_ring(ring) == 0
-            out = G.mm(a, b, trans_a=ta, trans_b=tb, tile=2, **kw)
-            torch.cuda.synchronize()
-            A_ = a.float().t() if ta else a.float()
-            B_ = b.float().t() if tb else b.float()
-            ref = A_ @ B_
-            if "bias" in kw:
-                ref = torch.relu(ref + kw["bias"])
-            assert rel(out, ref) < 1e-2, (M, N, K, ta, tb)
-            assert torch.equal(out, base), (M, N, K, ta, tb)
-    finally:
-        L.dn_gemm256_set_ring(0)
