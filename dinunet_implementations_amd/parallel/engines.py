@@ -98,6 +98,13 @@ class Engine:
             return True
         return self.group.backend == "nccl" and not self.half
 
+    @property
+    def pre_capturable(self) -> bool:
+        """May the step capture :meth:`pre_reduce` (the local factorisation) in its graph?  Not
+        when it starts with a collective of its own (rank-dAD's site mean over several GPUs per
+        site, a host-issued collective on gloo): the step then runs it after the replay."""
+        return True
+
     def _peer_mean(self, tag, n: int):
         from . import peer as _peer
         return _peer.mean(self.group, self.flat.grad.device, n, self.wire, (self.name,) + tuple(tag))
@@ -606,6 +613,15 @@ class RankDADEngine(Engine):
             self._init_fast()
 
     # ---- gradient-space path ---------------------------------------------------------------
+    @property
+    def pre_capturable(self) -> bool:
+        return self.group.replicas <= 1
+
+    @property
+    def capturable(self) -> bool:
+        # the site mean of several GPUs per site runs in reduce(), outside the graph
+        return self.group.replicas <= 1 and Engine.capturable.fget(self)
+
     def _init_fast(self):
         """Device tables of the factorisation kernels (csrc/kernels/lowrank.hip): per large
         Linear, its gradient view, the warm-start / candidate Q, and the P and Q slots of the
@@ -704,6 +720,9 @@ class RankDADEngine(Engine):
         ``dad_tol`` stop decided on the device: no host sync, HIP-graph capturable."""
         if not self.fast or not self.fast_layers:
             return
+        # several GPUs per site: the site's gradient (mean over its replicas) is what the site
+        # factorises; its replicas then compute identical factors
+        self.group.site_mean_(self.flat.grad)
         self._dense_start()  # (peer) the dense part travels under the power iteration
         if self._persist_ok and self._table.persist(max(1, self.iters), self.tol):
             return  # every iteration in one launch (lr_persist_kernel)
@@ -819,10 +838,14 @@ class RankDADEngine(Engine):
     def local_factors(self):
         """[(module, mode, X, Y)] with mode 'exact' (X=Delta, Y=A) or 'lowrank' (X=P, Y=Q)."""
         res = []
+        k = self.group.replicas
         for m, A, D in self._layer_inputs():
             if self._exact(A, D):
                 res.append((m, "exact", D, A))
             else:
+                if k > 1:  # the site's gradient: its replicas' rows, G = sum_r D_r^T A_r / k
+                    D = self.group.site_all_gather_varlen(D) / k
+                    A = self.group.site_all_gather_varlen(A)
                 P, Q = dad_factors(D, A, self.rank, self.iters, self.tol)
                 res.append((m, "lowrank", P, Q))
         return res

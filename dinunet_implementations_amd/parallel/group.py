@@ -1,4 +1,6 @@
-"""Site group: one process per GPU, each GPU plays one COINSTAC site (rank == site index).
+"""Site group: one process per GPU, each GPU plays one COINSTAC site (rank == site index), or --
+a site input listing several GPUs (``gpus: [0, 1]``) -- ``replicas`` consecutive ranks share one
+site (rank = site * replicas + replica).
 
 The reference routes every update through a remote aggregator over files + JSON (star topology,
 SURVEY.md Â§2.4).  Here all sites form one ``torch.distributed`` process group â€” backend ``nccl``
@@ -6,6 +8,14 @@ SURVEY.md Â§2.4).  Here all sites form one ``torch.distributed`` process group â
 tests â€” and every "remote" reduction is a collective whose result every rank holds.  Decisions
 the remote used to make (best epoch, early stop) are computed redundantly and identically on all
 ranks from collectively-reduced inputs.
+
+Intra-site data parallelism (the reference GUI's "GPU IDs to use, e.g. [0, 1]",
+``datasets/icalstm/inputspec.json:6-10``): the replicas of a site hold disjoint shards of the
+site's splits (``runtime.site.FederatedSite``) and each trains on ``batch_size / replicas`` rows of
+every batch.  Every site has the same replica count, so the engines' mean over ALL ranks is the
+mean over sites of each site's full-batch gradient (dSGD exactly: equal shard sizes); rank-dAD
+first forms the site gradient on ``site_pg`` (``SiteGroup.site_mean_``) so that each site factorises
+its own gradient, and its replicas contribute identical factors.
 """
 from __future__ import annotations
 
@@ -32,6 +42,11 @@ class SiteGroup:
     # a one-rank RCCL group that still takes every collective code path (``init_sites(loopback=
     # True)``, ``bench.py --loopback-rccl``): times the N > 1 step on one GPU
     loopback: bool = False
+    # processes (GPUs) per site and this process's index among its site's; site_pg = the
+    # process group of this site's replicas (None at one replica)
+    replicas: int = 1
+    replica: int = 0
+    site_pg: Any = None
 
     @property
     def distributed(self) -> bool:
@@ -40,6 +55,38 @@ class SiteGroup:
     @property
     def is_master(self) -> bool:
         return self.rank == 0
+
+    @property
+    def site(self) -> int:
+        """This process's site index (the data directory ``local<site>``)."""
+        return self.rank // max(1, self.replicas)
+
+    @property
+    def sites(self) -> int:
+        return self.world // max(1, self.replicas)
+
+    def site_mean_(self, t: torch.Tensor) -> torch.Tensor:
+        """In place: the mean of ``t`` over this site's replicas (identity at one replica)."""
+        if self.replicas > 1 and self.site_pg is not None:
+            dist.all_reduce(t, group=self.site_pg)
+            t.div_(self.replicas)
+        return t
+
+    def site_all_gather_varlen(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate variable-length tensors over this site's replicas (replica order)."""
+        if self.replicas <= 1 or self.site_pg is None:
+            return t
+        n = torch.tensor([t.shape[0]], device=t.device, dtype=torch.long)
+        ns = [torch.empty_like(n) for _ in range(self.replicas)]
+        dist.all_gather(ns, n, group=self.site_pg)
+        sizes = [int(v.item()) for v in ns]
+        mx = max(sizes)
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if t.shape[0]:
+            pad[:t.shape[0]] = t
+        parts = [torch.empty_like(pad) for _ in range(self.replicas)]
+        dist.all_gather(parts, pad, group=self.site_pg)
+        return torch.cat([p[:s] for p, s in zip(parts, sizes)], 0)
 
     # ---- thin collective helpers (no-ops at world 1) ----------------------------------------
     def barrier(self):
@@ -112,16 +159,18 @@ _GROUP: Optional[SiteGroup] = None
 
 
 def resolve_device(gpus=None, local_rank: int = 0, world: int = 1, backend: Optional[str] = None,
-                   n_devices: Optional[int] = None) -> torch.device:
+                   n_devices: Optional[int] = None, replica: int = 0,
+                   replicas: int = 1) -> torch.device:
     """The device of a site from its ``gpus`` input (the reference's "GPU IDs to use",
     ``datasets/icalstm/inputspec.json:6-10``: site 0 -> ``[0]``, site 1 -> ``[1]``;
     ``datasets/test_fsl/inputspec.json:15-17``: ``[]`` = CPU-only FreeSurfer sites).
 
     * ``None`` (not given): this rank's GPU (``LOCAL_RANK``) when one exists, else the CPU;
     * ``[]``: the CPU, as the reference;
-    * ``[k, ...]``: GPU ``k`` (one site = one MI355X: further ids are not used).  With RCCL every
-      site needs its own GPU, so ``k`` must equal ``LOCAL_RANK`` (one process per GPU); a site
-      listing another GPU is a configuration conflict and raises."""
+    * ``[k, ...]``: GPU ``k`` -- with ``replicas`` processes per site, replica ``i`` takes
+      ``ids[i]`` (a site's data-parallel replicas, one process per GPU); ids beyond the replicas
+      are not used (warned).  With RCCL every process needs its own GPU, so the id must equal
+      ``LOCAL_RANK``; a site listing another GPU is a configuration conflict and raises."""
     if n_devices is None:
         n_devices = torch.cuda.device_count() if torch.cuda.is_available() else 0
     if gpus is None:
@@ -131,14 +180,16 @@ def resolve_device(gpus=None, local_rank: int = 0, world: int = 1, backend: Opti
     ids = [int(g) for g in gpus]
     if not ids:
         return torch.device("cpu")
-    k = ids[0]
-    if len(ids) > 1:
+    replicas = max(1, int(replicas))
+    k = ids[replica] if replica < len(ids) else ids[0]
+    if len(ids) > replicas:
         # the reference's GUI offers "GPU IDs to use Eg. [0], [0, 1]" (assets/coinstac-gui.png):
-        # one MI355X (288 GB HBM) holds a whole site here, so the extra ids are not used -- say so
-        # instead of dropping them silently
+        # a site uses one GPU per replica process (run.py --site-gpus / a uniform gpus length),
+        # so ids beyond the replicas are not used -- say so instead of dropping them silently
         import warnings
-        warnings.warn(f"gpus={ids}: a site runs on ONE GPU (GPU {k}); the other ids "
-                      f"{ids[1:]} are not used (one site = one MI355X)", RuntimeWarning)
+        warnings.warn(f"gpus={ids}: a site runs on {replicas} GPU(s) ({ids[:replicas]}, one "
+                      f"process each); the other ids {ids[replicas:]} are not used "
+                      f"(launch {len(ids)} processes per site to use them)", RuntimeWarning)
     if not n_devices:
         import warnings
         warnings.warn(f"gpus={ids} but no GPU is visible: the site runs on the CPU", RuntimeWarning)
@@ -158,8 +209,13 @@ def resolve_device(gpus=None, local_rank: int = 0, world: int = 1, backend: Opti
 
 
 def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
-               timeout_s: Optional[int] = None, gpus=None, loopback: bool = False) -> SiteGroup:
+               timeout_s: Optional[int] = None, gpus=None, loopback: bool = False,
+               replicas: int = 1) -> SiteGroup:
     """Initialise from torchrun-style env vars; world 1 when they are absent.
+
+    ``replicas``: processes per site (intra-site data parallelism, see the module docstring):
+    ranks ``s * replicas .. s * replicas + replicas - 1`` are site ``s``; WORLD_SIZE must be a
+    multiple.  Each site's replicas get their own process group (``site_pg``).
 
     ``loopback`` (world 1 only): build a one-rank process group anyway (RCCL on a GPU) and mark
     the group distributed, so every collective of the multi-site step runs -- and is captured --
@@ -175,6 +231,10 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    replicas = max(1, int(replicas))
+    if world % replicas:
+        raise ValueError(f"WORLD_SIZE={world} is not a multiple of the {replicas} processes "
+                         f"(GPUs) per site")
     if device == "cpu":
         dev = torch.device("cpu")
     elif device not in (None, "", "auto", "cuda"):
@@ -183,7 +243,7 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
         # the site input's `gpus` picks the device (None: this rank's GPU); with RCCL it must
         # be GPU LOCAL_RANK
         be0 = backend or os.environ.get("DINUNET_BACKEND") or "nccl"
-        dev = resolve_device(gpus, local, world, be0)
+        dev = resolve_device(gpus, local, world, be0, replica=rank % replicas, replicas=replicas)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     # DINUNET_BACKEND=gloo rehearses the multi-site GPU path with several ranks on ONE GPU
@@ -207,8 +267,17 @@ def init_sites(backend: Optional[str] = None, device: Optional[str] = None,
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
         pg = dist.group.WORLD
+    site_pg = None
+    if replicas > 1 and world > 1:
+        # every rank creates every site's group, in site order (new_group is collective)
+        for s in range(world // replicas):
+            g = dist.new_group(list(range(s * replicas, (s + 1) * replicas)))
+            if s == rank // replicas:
+                site_pg = g
     _GROUP = SiteGroup(rank=rank, world=world, local_rank=local, device=dev,
-                       backend=be if (world > 1 or loopback) else None, pg=pg, loopback=loopback)
+                       backend=be if (world > 1 or loopback) else None, pg=pg, loopback=loopback,
+                       replicas=replicas if world > 1 else 1, replica=rank % replicas,
+                       site_pg=site_pg)
     _GROUP.gpu_shared = _gpu_shared(_GROUP)
     return _GROUP
 

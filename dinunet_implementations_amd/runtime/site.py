@@ -121,14 +121,14 @@ class FederatedSite:
         self.Trainer, self.Dataset, self.DataHandle = trainer_cls, dataset_cls, datahandle_cls
         self.state = state
         self.out_dir = out_dir
-        self.site = site_name or f"local{group.rank}"
+        self.site = site_name or f"local{group.site}"
         self.device = group.device
         self.verbose = verbose
         self.task_id = str(cfg.get("task_id"))
 
     # ---------------------------------------------------------------------------------------
     def log(self, *a):
-        if self.verbose:
+        if self.verbose and self.group.replica == 0:
             print(f"[{self.site}]", *a, flush=True)
 
     def _global_max(self, v: int) -> int:
@@ -137,14 +137,31 @@ class FederatedSite:
         return int(t.item())
 
     def _datasets(self, split: Dict[str, List[Any]]) -> Dict[str, Tuple[torch.Tensor, torch.Tensor]]:
+        """The site's splits on this process's device; with several processes per site
+        (``group.replicas``) this replica's shard of each: rows ``replica::replicas`` of the
+        site's (identically made) splits, so the replicas' shards are disjoint and cover it."""
         cache = self.cfg
         out = {}
+        k, r = self.group.replicas, self.group.replica
         for key in ("train", "validation", "test"):
             ds = self.Dataset(cache=cache, state=self.state, mode=key)
             if split.get(key):
                 ds.add(split[key])
-            out[key] = ds.materialize(self.device)
+            X, y = ds.materialize(self.device)
+            if k > 1:
+                X, y = X[r::k].contiguous(), y[r::k].contiguous()
+            out[key] = (X, y)
         return out
+
+    def _batch_size(self, cfg: Dict[str, Any]) -> int:
+        """Rows per step on this process: the site's ``batch_size`` split over its replicas."""
+        bs = int(cfg.get("batch_size", 16))
+        k = self.group.replicas
+        if k > 1:
+            if bs % k:
+                raise ValueError(f"batch_size {bs} does not split over the site's {k} GPUs")
+            bs //= k
+        return bs
 
     def _loader(self, X, y, key: str, batch_size: int, seed: int) -> DeviceLoader:
         dl_args = (self.cfg.get("dataloader_args") or {}).get(key, {})
@@ -191,7 +208,7 @@ class FederatedSite:
                       fold_dir: str, seed: int, logs: Dict[str, Any], tag: str = "",
                       start_epoch: int = 1, best: Optional[Dict[str, Any]] = None,
                       resume: Optional[Dict[str, Any]] = None):
-        bs = int(cfg.get("batch_size", 16))
+        bs = self._batch_size(cfg)
         li = max(1, int(cfg.get("local_iterations", 1)))
         tr = self._loader(*data["train"], "train", bs, seed)
         va = self._loader(*data["validation"], "validation", bs, seed)
@@ -388,6 +405,9 @@ class FederatedSite:
         return DeviceFeed(step, X, tr.labels, bs, steps, col=col)
 
     def _pretrain(self, trainer: NNTrainer, data, fold_dir: str, seed: int, logs: Dict[str, Any]):
+        if self.group.replicas > 1:
+            raise NotImplementedError("pretrain with several GPUs per site: the pretraining "
+                                      "site trains alone (one process)")
         sizes = self.group.all_gather_object(int(data["train"][0].shape[0]))
         src = max(range(len(sizes)), key=lambda r: (sizes[r], -r))
         logs["pretrain_site"] = f"local{src}"
@@ -461,12 +481,16 @@ class FederatedSite:
     def run_fold(self, fold: int, split: Dict[str, List[Any]]) -> Dict[str, Any]:
         cfg = self.cfg
         t_fold = time.time()
-        fdir = L.fold_dir(self.out_dir, self.site, self.task_id, fold)
-        seed = site_seed(cfg, self.group.rank) + 7919 * fold
+        g = self.group
+        # a site's replicas write their own logs / checkpoints (their loaders differ) beside it
+        fdir = L.fold_dir(self.out_dir, self.site if g.replica == 0 else
+                          f"{self.site}_replica{g.replica}", self.task_id, fold)
+        seed = site_seed(cfg, g.site) + 7919 * fold + 104729 * g.replica
         data = self._datasets(split)
         logs: Dict[str, Any] = {
             "task_id": self.task_id, "agg_engine": cfg.get("agg_engine"), "fold": fold,
-            "site": self.site, "rank": self.group.rank, "num_sites": self.group.world,
+            "site": self.site, "rank": self.group.rank, "num_sites": self.group.sites,
+            "gpus_per_site": self.group.replicas,
             "log_header": cfg.get("log_header"), "mode": cfg.get("mode"),
             "split_sizes": {k: int(v[1].shape[0]) for k, v in data.items()},
             "device": str(self.device),
@@ -509,7 +533,7 @@ class FederatedSite:
             if hasattr(engine, "close"):
                 engine.close()
             trainer.load_checkpoint(os.path.join(fdir, "checkpoint_best.pt"))
-        te = self._loader(*data["test"], "test", int(cfg.get("batch_size", 16)), seed)
+        te = self._loader(*data["test"], "test", self._batch_size(cfg), seed)
         r = self.global_eval(trainer, te)
         logs["test_metrics"] = L.test_row(r["loss"], r["scores"])
         logs["local_test_metrics"] = L.test_row(r["local_loss"], r["local_scores"])
@@ -523,7 +547,7 @@ class FederatedSite:
             rlogs = {k: v for k, v in logs.items() if not k.startswith("local_")}
             rlogs["remote_iter_duration"] = logs.get("local_iter_duration", [])  # NB.ipynb:860
             rlogs["site"] = "remote"
-            rlogs["sites"] = [f"local{i}" for i in range(self.group.world)]
+            rlogs["sites"] = [f"local{i}" for i in range(self.group.sites)]
             L.write_logs(rdir, rlogs)
             L.write_test_metrics(rdir, [logs["test_metrics"]])
             L.zip_results(rdir, os.path.join(rdir, f"{self.task_id}_fold_{fold}_results.zip"))
@@ -532,10 +556,12 @@ class FederatedSite:
         return logs
 
     def run(self) -> List[Dict[str, Any]]:
-        set_seed(site_seed(self.cfg, self.group.rank))
+        # replicas of a site make identical splits (explicit site seed), which _datasets then
+        # shards; their dropout streams differ
+        set_seed(site_seed(self.cfg, self.group.site) + 104729 * self.group.replica)
         handle = self.DataHandle(cache=self.cfg, state=self.state)
         files = handle.list_files()
-        splits = make_splits(files, self.cfg, site_seed(self.cfg, self.group.rank),
+        splits = make_splits(files, self.cfg, site_seed(self.cfg, self.group.site),
                              base=self.state.get("baseDirectory", "."))
         nfolds = self._global_max(len(splits))
         if nfolds != len(splits):

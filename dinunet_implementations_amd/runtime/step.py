@@ -146,6 +146,8 @@ class TrainStep:
         # (PowerSGD's error feedback and rank-dAD's warm start would otherwise be applied to
         # every partial gradient), so it then runs eagerly inside engine.reduce()
         pre = getattr(engine, "pre_reduce", None) if engine.name != "dSGD" else None
+        if not getattr(engine, "pre_capturable", True):
+            pre = None  # (engine.reduce() runs it after the replay)
         self._pre_reduce = pre if self.accum == 1 else None
         self._pre_any = pre  # device-fed accumulated steps capture it after the last micro-batch
         self.eager_warmup = eager_warmup

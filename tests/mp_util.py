@@ -16,7 +16,7 @@ def free_port() -> int:
     return p
 
 
-def _entry(rank, world, port, fn, args, outdir):
+def _entry(rank, world, port, fn, args, outdir, replicas=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     os.environ.setdefault("OMP_NUM_THREADS", "2")
@@ -26,7 +26,7 @@ def _entry(rank, world, port, fn, args, outdir):
     res = None
     grp = None
     try:
-        grp = init_sites(backend="gloo", device="cpu")
+        grp = init_sites(backend="gloo", device="cpu", replicas=replicas)
         res = ("ok", fn(grp, *args))
     except Exception:  # pragma: no cover - surfaced by the parent
         res = ("err", traceback.format_exc())
@@ -46,22 +46,23 @@ def _entry(rank, world, port, fn, args, outdir):
     os._exit(0)
 
 
-def run_world(fn, world, *args, _retry=True):
+def run_world(fn, world, *args, _retry=True, replicas=1):
+    """Run ``fn(grp, *args)`` on ``world`` gloo ranks (``replicas`` processes per site)."""
     try:
-        return _run_world(fn, world, *args)
+        return _run_world(fn, world, *args, replicas=replicas)
     except AssertionError as e:
         # free_port() -> bind is racy against other processes on the host: retry once on a
         # rendezvous port collision, never on a real failure
         if _retry and ("Address already in use" in str(e) or "EADDRINUSE" in str(e)):
-            return run_world(fn, world, *args, _retry=False)
+            return run_world(fn, world, *args, _retry=False, replicas=replicas)
         raise
 
 
-def _run_world(fn, world, *args):
+def _run_world(fn, world, *args, replicas=1):
     outdir = tempfile.mkdtemp()
     # spawn (not fork): the pytest parent has live OpenMP/autograd threads; workers must be
     # module-level functions of an importable test module
-    mp.start_processes(_entry, args=(world, free_port(), fn, args, outdir), nprocs=world,
+    mp.start_processes(_entry, args=(world, free_port(), fn, args, outdir, replicas), nprocs=world,
                        join=True, start_method="spawn")
     out, errs = [], []
     for r in range(world):

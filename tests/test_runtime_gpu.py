@@ -107,3 +107,39 @@ def test_fs_site_device_feed_matches_host_feed(fs_data_root, tmp_path):
         assert abs(a[0] - b[0]) < 2e-4 and abs(a[1] - b[1]) < 2e-3, (dev["train_log"], host["train_log"])
     for a, b in zip(dev["validation_log"], host["validation_log"]):
         assert abs(a[0] - b[0]) < 2e-4 and abs(a[1] - b[1]) < 2e-3
+
+
+@pytest.mark.parametrize("engine", ["dSGD", "rankDAD"])
+def test_ica_two_sites_two_gpus_each_on_one_gpu(tmp_path, engine):
+    """Several GPUs per site (``run.py --site-gpus 2``, parallel.group): 2 sites x 2 processes
+    -- launched as the driver launches a node, rehearsed on the one GPU over gloo -- train the ICA
+    model with the fused kernels on sharded splits; every process ends with bit-identical
+    parameters (check_replicas), one global test decision, logs per site and replica."""
+    import subprocess
+    import sys
+    from dinunet_implementations_amd.data.synthetic import make_ica_sites
+    root = make_ica_sites(str(tmp_path / "ica"), sites=2, subjects=(64, 64), comps=16, T=120,
+                          window_size=10, window_stride=10, hidden_size=64, input_size=32)
+    out = str(tmp_path / "out")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DINUNET_BACKEND="gloo", PYTHONPATH=repo, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           "4", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m",
+           "dinunet_implementations_amd.run", "--data-path", root, "--out", out,
+           "--site-gpus", "2", "--set", "epochs=2", "--set", "batch_size=8", "--set",
+           f"agg_engine={engine}", "--set", "dad_reduction_rank=4", "--set",
+           "check_replicas=true"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    logs = {}
+    for name in ("local0", "local0_replica1", "local1", "local1_replica1", "remote"):
+        p = os.path.join(out, name)
+        f = next(os.path.join(d, x) for d, _, fs in os.walk(p) for x in fs if x == "logs.json")
+        with open(f) as fh:
+            logs[name] = json.load(fh)
+    tm = {n: l["test_metrics"] for n, l in logs.items()}
+    assert len({json.dumps(v) for v in tm.values()}) == 1, tm  # one global decision
+    for n in ("local0", "local0_replica1", "local1", "local1_replica1"):
+        assert all(logs[n]["replica_check"]), n
+        assert logs[n]["gpus_per_site"] == 2 and logs[n]["num_sites"] == 2
+    assert logs["local0"]["split_sizes"]["train"] + logs["local0_replica1"]["split_sizes"]["train"] > 0
