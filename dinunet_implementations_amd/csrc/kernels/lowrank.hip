@@ -689,38 +689,47 @@ struct PiRecon {
 // rank-dAD: G = sum over the W sites of P_s Q_s^T / W for every layer, one 16 x 16 output tile
 // per wave on the f32 matrix cores (16x16x4, K = r in chunks of 4 per site: lane l feeds
 // A[l & 15][k] = P_s[r0 + (l & 15)][c + k] and B[k][l & 15] = Q_s[k0 + (l & 15)][c + k],
-// k = l >> 4).  The tile list is every layer's tiles in order; the per-thread-element loop it
-// replaced was latency-bound (17 us for the ICA layers).
+// k = l >> 4).  The tile list is every layer's tiles in order; a tile's layer comes from the
+// host-made tile prefix in the kernel arguments (no walk over the device table), and every
+// factor load of a site issues before its MFMAs (r <= 16: four k chunks; a loop of load ->
+// MFMA per chunk was one memory round trip each).
+constexpr int PR_MAXL = 16;
+struct PrIndex {
+  long tstart[PR_MAXL + 1];  // first tile of each layer; tstart[n] = all tiles
+  int n;
+};
+
 __global__ void __launch_bounds__(256)
-pi_reconstruct_kernel(const PiRecon* __restrict__ R, int n, long total, long stride, int W, float inv_w) {
+pi_reconstruct_kernel(const PiRecon* __restrict__ R, PrIndex ix, long stride, int W, float inv_w) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
-  long ntiles = 0;
-  for (int l = 0; l < n; ++l) ntiles += (long)((R[l].out + 15) / 16) * ((R[l].in + 15) / 16);
+  const long ntiles = ix.tstart[ix.n];
   for (long tile = blockIdx.x * 4L + w; tile < ntiles; tile += (long)gridDim.x * 4) {
     int l = 0;
-    long t0 = 0;
-    for (;; ++l) {
-      const long nt = (long)((R[l].out + 15) / 16) * ((R[l].in + 15) / 16);
-      if (tile < t0 + nt || l + 1 == n) break;
-      t0 += nt;
-    }
+#pragma unroll
+    for (int j = 1; j < PR_MAXL; ++j) l += (j < ix.n && tile >= ix.tstart[j]) ? 1 : 0;
     const PiRecon& X = R[l];
+    const int r = X.r;
     const int tn = (X.in + 15) / 16;
-    const int ti = (int)(tile - t0);
+    const int ti = (int)(tile - ix.tstart[l]);
     const int r0 = 16 * (ti / tn), k0 = 16 * (ti % tn);
     const int prow = r0 + c16, qrow = k0 + c16;
     const bool pv = prow < X.out, qv = qrow < X.in;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < W; ++s) {
-      const float* p = X.P + (long)s * stride + (long)(pv ? prow : 0) * X.r;
-      const float* q = X.Q + (long)s * stride + (long)(qv ? qrow : 0) * X.r;
-      for (int c = 0; c < X.r; c += 4) {
-        const int cc = c + kq;
-        const float av = (pv && cc < X.r) ? p[cc] : 0.f;
-        const float bv = (qv && cc < X.r) ? q[cc] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+      const float* p = X.P + (long)s * stride + (long)(pv ? prow : 0) * r;
+      const float* q = X.Q + (long)s * stride + (long)(qv ? qrow : 0) * r;
+      float av[4], bv[4];
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {  // clamped loads, selected: all eight in flight at once
+        const int cc = 4 * c4 + kq, ci = cc < r ? cc : r - 1;
+        const float a = p[ci], b = q[ci];
+        av[c4] = (pv && cc < r) ? a : 0.f;
+        bv[c4] = (qv && cc < r) ? b : 0.f;
       }
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        if (4 * c4 < r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c4], bv[c4], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -854,6 +863,40 @@ __device__ __forceinline__ void lp_publish(__amdgpu_buffer_rsrc_t dst, const flo
 }
 
 
+// LP_BF16X3 (default 1): the G Q and G^T P products of the power iteration on bf16 matrix cores
+// with each fp32 operand split into hi + lo bf16 parts (hi*hi + hi*lo + lo*hi, fp32 accumulation:
+// ~1e-5 relative per product, far below the rank-r truncation the factors exist for): three
+// 16x16x32 MFMAs per 32-deep chunk instead of eight dependent 16x16x4 f32 ones.  0: fp32 MFMAs.
+#ifndef LP_BF16X3
+#define LP_BF16X3 1
+#endif
+__device__ __forceinline__ void lp_split8(const float* v, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bf16 h = (bf16)v[e];
+    hi[e] = h;
+    lo[e] = (bf16)(v[e] - (float)h);
+  }
+}
+__device__ __forceinline__ f32x4 lp_mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                          const bf16x8& bl, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);  // small terms first
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+// every 64-B line of the (1+ KB) argument block requested in one round at entry: the layer's
+// fields are then scalar-cache hits instead of a chain of dependent argument loads
+__device__ __forceinline__ void lp_warm_kernargs() {
+  constexpr int LINES = (int)((sizeof(LpArgs) + 63) / 64);
+  typedef const __attribute__((address_space(4))) unsigned cu32;
+  cu32* kp = (cu32*)__builtin_amdgcn_kernarg_segment_ptr();
+  unsigned acc = 0;
+#pragma unroll
+  for (int i = 0; i < LINES; ++i) acc += kp[16 * i];
+  asm volatile("" ::"s"(acc));
+}
+
 // R: rank bound, r <= R in {4, 8, 10, 12, 16} for every layer of the launch.  EX: every layer's
 // rank IS R (the default: one rank for all layers), so r is a compile-time constant and every
 // `e < r` below folds away -- with a run-time r the per-entry predicates were hoisted out of the
@@ -870,8 +913,10 @@ lr_persist_kernel(LpArgs a) {
   __shared__ __attribute__((aligned(16))) float Rh[LR_MAXR * LR_MAXR + 64 - LR_MAXR];
   __shared__ float Sv[64];
   __shared__ float dq[2 * 4];
+  lp_warm_kernargs();
   const int l = blockIdx.x & (LP_MAXL - 1), j = blockIdx.x / LP_MAXL;
   if (l >= a.nl || j >= a.L[l].J) return;
+  LP_STAMP(60);  // entry (the span before stamp 0: argument loads, G load issue)
   const LpLayer& Y = a.L[l];
   const LrLayer& X = Y.X;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -891,6 +936,38 @@ lr_persist_kernel(LpArgs a) {
   const int WA = 4 / Y.rb_per, rbw = w / WA, chw = w % WA;
   const int WB = 4 / Y.cb_per, cbw = w / WB, rlw = w % WB;
   gfloat* G = (gfloat*)X.G;
+#if LP_BF16X3
+  // 32-deep chunks: lane (c, kr) holds G[row c][32 q + 8 kr .. + 7] (phase A, q = chw + WA i)
+  // and G[32 q + 8 kr .. + 7][col c] (phase B, q = rlw + WB i), split into bf16 hi / lo
+  constexpr int NQ = LP_GV / 2;
+  bf16x8 gah[NQ], gal[NQ], gbh[NQ], gbl[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int row = 16 * (rb0 + rbw) + c;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // m % 4 == 0: a 4-run never straddles m
+      const int k0 = 32 * (chw + WA * i) + 8 * kr + 4 * h;
+      const bool ok = rb0 + rbw < rb1 && row < n && k0 < m;
+      const f32x4 t = ((gfloat4*)(G + (long)(ok ? row : 0) * m))[(ok ? k0 : 0) >> 2] * (ok ? 1.f : 0.f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
+    }
+    lp_split8(v, gah[i], gal[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int col = 16 * (cb0 + cbw) + c;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int row = 32 * (rlw + WB * i) + 8 * kr + e;
+      const bool ok = cb0 + cbw < cb1 && row < n && col < m;
+      v[e] = G[(ok ? (long)row * m + col : 0)] * (ok ? 1.f : 0.f);
+    }
+    lp_split8(v, gbh[i], gbl[i]);
+  }
+#else
   f32x4 ga[LP_GV], gb[LP_GV];
 #pragma unroll
   for (int i = 0; i < LP_GV; ++i) {
@@ -908,6 +985,7 @@ lr_persist_kernel(LpArgs a) {
       gb[i][s2] = G[(ok ? (long)row * m + col : 0)] * (ok ? 1.f : 0.f);
     }
   }
+#endif
   LP_STAMP(0);
   const __amdgpu_buffer_rsrc_t rP = lp_rsrc(X.P), rQ = lp_rsrc(X.Qsend);
   const __amdgpu_buffer_rsrc_t rG = lp_rsrc(Y.gram), rN = lp_rsrc(Y.norms);
@@ -923,6 +1001,22 @@ lr_persist_kernel(LpArgs a) {
     const int ncol = min(m, 16 * cb1) - 16 * cb0;
     for (int e = tid; e < ncol * r; e += 256) qold[e] = stg[16 * cb0 * r + e];  // my Q rows now
     {
+#if LP_BF16X3
+      f32x4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // two chains
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        float bq[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 32 * (chw + WA * i) + 8 * kr + e;
+          bq[e] = stg[(k < m ? k : 0) * r + cc] * cmask;  // k >= m meets a zero A entry
+        }
+        bf16x8 bh, bl;
+        lp_split8(bq, bh, bl);
+        acc2[i & 1] = lp_mfma3(gah[i], gal[i], bh, bl, acc2[i & 1]);
+      }
+      const f32x4 acc = acc2[0] + acc2[1];
+#else
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < LP_GV; ++i) {
@@ -936,6 +1030,7 @@ lr_persist_kernel(LpArgs a) {
         for (int s2 = 0; s2 < 4; ++s2)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[i][s2], bq[s2], acc, 0, 0, 0);
       }
+#endif
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[w * 256 + (4 * kr + e) * 16 + c] = acc[e];
     }
@@ -1043,6 +1138,22 @@ lr_persist_kernel(LpArgs a) {
        // with the scaled Cholesky of the Gram (every wave, identical values) in the same block:
        // its readlane / VALU chain issues between the MFMAs instead of ahead of them in wave 0
       if constexpr (R <= 12) lp_chol<R, true>(gm, Rh, Sv, r, lane);
+#if LP_BF16X3
+      f32x4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        float pv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int row = 32 * (rlw + WB * i) + 8 * kr + e;
+          pv[e] = stg[(row < n ? row : 0) * r + cc] * cmask;
+        }
+        bf16x8 ph, pl;
+        lp_split8(pv, ph, pl);
+        acc2[i & 1] = lp_mfma3(gbh[i], gbl[i], ph, pl, acc2[i & 1]);
+      }
+      const f32x4 acc = acc2[0] + acc2[1];
+#else
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < LP_GV; ++i) {
@@ -1056,6 +1167,7 @@ lr_persist_kernel(LpArgs a) {
         for (int s2 = 0; s2 < 4; ++s2)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(gb[i][s2], pv[s2], acc, 0, 0, 0);
       }
+#endif
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[w * 256 + (4 * kr + e) * 16 + c] = acc[e];
     }
@@ -1152,6 +1264,7 @@ lr_persist_kernel(LpArgs a) {
       __hip_atomic_store(d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  LP_STAMP(61);  // exit of member 0 (Psend stored)
 }
 
 }  // namespace
@@ -1228,15 +1341,28 @@ DN_API int dn_lr_recon_ef(const void* layers, const void* host, int nl, hipStrea
   return dn_launch_status();
 }
 
-// G_l = sum over W sites of P_s Q_s^T / W for every layer; `stride` = send-buffer length.
-DN_API int dn_pi_reconstruct(const void* recon, int n, long total, long stride, int W,
-                             hipStream_t st) {
+// G_l = sum over W sites of P_s Q_s^T / W for every layer; `stride` = send-buffer length;
+// `recon` the device table, `host` the same table in host memory (read for the tile prefix).
+DN_API int dn_pi_reconstruct(const void* recon, const void* host, int n, long total, long stride,
+                             int W, hipStream_t st) {
   if (n <= 0 || total <= 0) return DN_OK;
-  long blocks = (total / 256 + 3) / 4;  // ~one 16 x 16 tile per wave
+  if (n > PR_MAXL || !host) return DN_BAD_SHAPE;
+  const PiRecon* H = (const PiRecon*)host;
+  PrIndex ix{};
+  ix.n = n;
+  long t = 0;
+  for (int l = 0; l < n; ++l) {
+    if (H[l].r < 1 || H[l].r > 16) return DN_BAD_SHAPE;
+    ix.tstart[l] = t;
+    t += (long)((H[l].out + 15) / 16) * ((H[l].in + 15) / 16);
+  }
+  ix.tstart[n] = t;
+  for (int l = n + 1; l <= PR_MAXL; ++l) ix.tstart[l] = t;
+  long blocks = (t + 3) / 4;  // one 16 x 16 tile per wave
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(pi_reconstruct_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                     (const PiRecon*)recon, n, total, stride, W, 1.f / (float)W);
+                     (const PiRecon*)recon, ix, stride, W, 1.f / (float)W);
   return dn_launch_status();
 }
 

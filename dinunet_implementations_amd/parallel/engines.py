@@ -22,6 +22,7 @@ all-reduce SUM in place and folds ``1/world`` into the fused Adam launch).
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -703,6 +704,7 @@ class RankDADEngine(Engine):
             c.out, c.inn, c.r, c.start = out_f, in_f, rr, start
             start += out_f * in_f
         self._recon_total = start
+        self._rec_host = rec  # (the launcher reads the tile prefix from the host copy)
         self._rec = torch.frombuffer(bytearray(bytes(rec)), dtype=torch.uint8).to(dev)
 
     def state_dict(self):
@@ -796,7 +798,8 @@ class RankDADEngine(Engine):
                 g.all_gather_into(self._gathered, self._send)
                 self.comm_bytes += self._send.numel() * 4
         # every layer's G = [P_1..P_W][Q_1..Q_W]^T / W in one launch
-        _lib.call("dn_pi_reconstruct", self._rec.data_ptr(), len(self.fast_layers),
+        _lib.call("dn_pi_reconstruct", self._rec.data_ptr(), ctypes.addressof(self._rec_host),
+                  len(self.fast_layers),
                   self._recon_total, self._send.numel(), W if g.distributed else 1, _lib.stream())
         return 1.0
 

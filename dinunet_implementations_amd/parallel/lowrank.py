@@ -22,8 +22,8 @@ _lib.register("dn_mgs_batched", [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _l
 _lib.register("dn_lr_stage", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
                               _lib.c_float, _lib.c_void_p])
 _lib.register("dn_lr_recon_ef", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p])
-_lib.register("dn_pi_reconstruct", [_lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_long,
-                                     _lib.c_int, _lib.c_void_p])
+_lib.register("dn_pi_reconstruct", [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long,
+                                     _lib.c_long, _lib.c_int, _lib.c_void_p])
 
 EPS = 1e-8
 

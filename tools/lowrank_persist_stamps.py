@@ -57,6 +57,14 @@ def main():
                        f"gram={d(3, 4):.2f} chol={d(4, 8):.2f} H={d(8, 5):.2f} "
                        f"hsum={d(5, 9):.2f} solve={d(9, 6):.2f} bar2={d(6, 7):.2f}")
         print(" | ".join(out))
+    # whole-launch span on the global clock: first member-0 entry to last member-0 exit, and
+    # per layer entry -> stamp 0 (argument loads, G load issue) and last barrier -> exit
+    ent = [v[l][60] for l in range(t.n)]
+    ext = [v[l][61] for l in range(t.n)]
+    print(f"member-0 span: entries within {(max(ent) - min(ent)) / 100:.2f} us, first entry -> "
+          f"last exit {(max(ext) - min(ent)) / 100:.2f} us; per layer entry->stamp0 " +
+          " ".join(f"{(v[l][0] - v[l][60]) / 100:.2f}" for l in range(t.n)) +
+          "; last bar2->exit " + " ".join(f"{(v[l][61] - v[l][48]) / 100:.2f}" for l in range(t.n)))
 
 
 if __name__ == "__main__":
