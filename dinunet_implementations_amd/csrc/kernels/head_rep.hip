@@ -203,6 +203,7 @@ head_rep_kernel(RepArgs a, const float* __restrict__ x, long ldx, const long lon
   // ---- stores into LDS ----------------------------------------------------------------------
   if (tid < RMP)
     reinterpret_cast<int*>(smem + a.t_y)[tid] = (int)(yv < 0 ? -1 : (yv > 0x7fffffffll ? 0x7fffffff : yv));
+  RSTAMP(10);
   {
     const float p0 = L0.drop;
     const float inv = p0 > 0.f ? 1.f / (1.f - p0) : 1.f;
@@ -222,6 +223,7 @@ head_rep_kernel(RepArgs a, const float* __restrict__ x, long ldx, const long lon
       }
     }
   }
+  RSTAMP(11);
 #pragma unroll
   for (int u = 0; u < RWU; ++u) {
     const int wd = a.wjob[wid + RNW * u];
@@ -233,6 +235,7 @@ head_rep_kernel(RepArgs a, const float* __restrict__ x, long ldx, const long lon
         *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(smem + L.w_lds) + nn * L.SW + kk) = wv[u];
     }
   }
+  RSTAMP(12);
 #pragma unroll
   for (int u = 0; u < RPU; ++u) {
     const int pd = a.pjob[wid + RNW * u];
@@ -249,6 +252,7 @@ head_rep_kernel(RepArgs a, const float* __restrict__ x, long ldx, const long lon
       *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(smem + a.t_wc) + (i * L0.Np + nr) * RWCS +
                                  8 * q) = wcv[i];
   }
+  RSTAMP(13);
   load_w0(2);
   rlds_barrier();
   RSTAMP(2);

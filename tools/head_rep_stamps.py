@@ -2,7 +2,9 @@
 """Phase stamps of the replicated-forward head (csrc/kernels/head_rep.hip, s_memrealtime, 100 MHz),
 workgroup 0, in us from its start: 1 W0 rows requested, 2 prologue (image, narrow weights,
 parameters) in LDS, 3 layer 0 + A1, 4 narrow forward, 5 loss, 6 output-gradient chain, 7 dZ0,
-8 dW tiles written, 9 dX written; plus the launch time by HIP events (python included).
+8 dW tiles written, 9 dX written; prologue detail 10 labels stored, 11 input image stored, 12
+narrow weight images stored, 13 parameter vectors stored (wave 0; the barrier after 13 waits for
+the slowest wave); plus the launch time by HIP events (python included).
 
 usage: python tools/head_rep_stamps.py [B] [dropout]"""
 import os
