@@ -690,17 +690,18 @@ struct PiRecon {
 // per wave on the f32 matrix cores (16x16x4, K = r in chunks of 4 per site: lane l feeds
 // A[l & 15][k] = P_s[r0 + (l & 15)][c + k] and B[k][l & 15] = Q_s[k0 + (l & 15)][c + k],
 // k = l >> 4).  The tile list is every layer's tiles in order; a tile's layer comes from the
-// host-made tile prefix in the kernel arguments (no walk over the device table), and every
+// host-made tile prefix and layer records in the kernel arguments (no device table), and every
 // factor load of a site issues before its MFMAs (r <= 16: four k chunks; a loop of load ->
 // MFMA per chunk was one memory round trip each).
 constexpr int PR_MAXL = 16;
 struct PrIndex {
   long tstart[PR_MAXL + 1];  // first tile of each layer; tstart[n] = all tiles
   int n;
+  PiRecon L[PR_MAXL];        // the layer records themselves (kernel arguments: no table load)
 };
 
 __global__ void __launch_bounds__(256)
-pi_reconstruct_kernel(const PiRecon* __restrict__ R, PrIndex ix, long stride, int W, float inv_w) {
+pi_reconstruct_kernel(PrIndex ix, long stride, int W, float inv_w) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
   const long ntiles = ix.tstart[ix.n];
@@ -708,7 +709,7 @@ pi_reconstruct_kernel(const PiRecon* __restrict__ R, PrIndex ix, long stride, in
     int l = 0;
 #pragma unroll
     for (int j = 1; j < PR_MAXL; ++j) l += (j < ix.n && tile >= ix.tstart[j]) ? 1 : 0;
-    const PiRecon& X = R[l];
+    const PiRecon& X = ix.L[l];
     const int r = X.r;
     const int tn = (X.in + 15) / 16;
     const int ti = (int)(tile - ix.tstart[l]);
@@ -1353,6 +1354,7 @@ DN_API int dn_pi_reconstruct(const void* recon, const void* host, int n, long to
   long t = 0;
   for (int l = 0; l < n; ++l) {
     if (H[l].r < 1 || H[l].r > 16) return DN_BAD_SHAPE;
+    ix.L[l] = H[l];
     ix.tstart[l] = t;
     t += (long)((H[l].out + 15) / 16) * ((H[l].in + 15) / 16);
   }
@@ -1361,8 +1363,9 @@ DN_API int dn_pi_reconstruct(const void* recon, const void* host, int n, long to
   long blocks = (t + 3) / 4;  // one 16 x 16 tile per wave
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(pi_reconstruct_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                     (const PiRecon*)recon, ix, stride, W, 1.f / (float)W);
+  (void)recon;  // (the device copy of the table: kept in the interface, the records ride in ix)
+  hipLaunchKernelGGL(pi_reconstruct_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ix, stride,
+                     W, 1.f / (float)W);
   return dn_launch_status();
 }
 
