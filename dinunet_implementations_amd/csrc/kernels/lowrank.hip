@@ -362,20 +362,31 @@ lr_gq_kernel(const LrLayer* __restrict__ Ls, LrIndex ix, int it, float tol) {
 // factorisation shares a basic block with the caller's MFMAs and can issue under them
 template <int R, bool ALLW = false>
 __device__ __forceinline__ void lp_chol(const double* gm, float* Rh, float* Sv, int r, int lane) {
-  const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
-  double dmax = di;
+  // the diagonal by broadcast LDS reads in every lane (no cross-lane max / readlane rounds); the
+  // scaling D^{-1/2} only preconditions the factorisation (R = R_s D^{1/2} whatever positive D
+  // is used, and lp_solve applies the same Sv), so the hardware fp64 rsq serves
+  double dg[R];
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) dmax = fmax(dmax, shfl_d(dmax, lane ^ o));
-  const bool live = lane < r && di > fmax(1e-13 * dmax, 1e-280);
-  const double si = live ? 1.0 / sqrt(di) : 0.0;
+  for (int i = 0; i < R; ++i) dg[i] = i < r ? gm[i * 17] : 0.0;
+  double dmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) dmax = fmax(dmax, dg[i]);
+  const double floor_d = fmax(1e-13 * dmax, 1e-280);
   float sv[R];
+  unsigned dead = 0;
 #pragma unroll
-  for (int jj = 0; jj < R; ++jj) sv[jj] = rlane((float)si, jj);
+  for (int jj = 0; jj < R; ++jj) {
+    const bool lj = jj < r && dg[jj] > floor_d;
+    sv[jj] = lj ? (float)__builtin_amdgcn_rsq(dg[jj]) : 0.f;
+    dead |= (jj < r && !lj) ? 1u << jj : 0u;
+  }
+  const double di = lane < r ? gm[(lane & 15) * 17] : 0.0;
+  const bool live = lane < r && di > floor_d;
+  const double si = live ? __builtin_amdgcn_rsq(di) : 0.0;
   float av[R];
 #pragma unroll
   for (int jj = 0; jj < R; ++jj)
     av[jj] = (lane < r && jj < r) ? (float)(gm[(lane & 15) * 16 + jj] * si) * sv[jj] : 0.f;
-  unsigned dead = ~(unsigned)__ballot(live) & ((1u << r) - 1u);
 #pragma unroll
   for (int k = 0; k < R; ++k) {
     const float akk = rlane(av[k], k);
