@@ -181,6 +181,13 @@ def resolve_device(gpus=None, local_rank: int = 0, world: int = 1, backend: Opti
     if not ids:
         return torch.device("cpu")
     replicas = max(1, int(replicas))
+    if replicas > 1 and len(ids) < replicas:
+        # (run.py --site-gpus k over site inputs that list one GPU each): every process of the
+        # site takes its own GPU, as without a list
+        import warnings
+        warnings.warn(f"gpus={ids} lists fewer GPUs than the site's {replicas} processes: each "
+                      f"process uses its own GPU (LOCAL_RANK)", RuntimeWarning)
+        return torch.device("cuda", local_rank % n_devices) if n_devices else torch.device("cpu")
     k = ids[replica] if replica < len(ids) else ids[0]
     if len(ids) > replicas:
         # the reference's GUI offers "GPU IDs to use Eg. [0], [0, 1]" (assets/coinstac-gui.png):

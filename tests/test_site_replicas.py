@@ -85,6 +85,9 @@ def test_replicas_per_site_rule_and_device_choice():
         warnings.simplefilter("error")  # the listed ids are all used: no warning
         assert resolve_device([2, 3], local_rank=3, n_devices=8, replica=1,
                               replicas=2) == torch.device("cuda", 3)
+    with pytest.warns(RuntimeWarning, match="own GPU"):  # --site-gpus over one-GPU inputs
+        assert resolve_device([1], local_rank=3, n_devices=8, replica=1,
+                              replicas=2) == torch.device("cuda", 3)
     with pytest.warns(RuntimeWarning, match="not used"):
         assert resolve_device([2, 3, 4], local_rank=2, n_devices=8, replica=0,
                               replicas=2) == torch.device("cuda", 2)
