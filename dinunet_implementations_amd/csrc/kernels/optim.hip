@@ -119,6 +119,53 @@ __device__ __forceinline__ void pack_store(const PackPlan& pl, const PackSeg& sg
   }
 }
 
+// 4 consecutive elements j0 .. j0 + 3 of one segment (j0 % 4 == 0, j0 + 3 < sg.n): one index
+// decode per thread and one 8-byte store wherever the destination keeps them consecutive (the
+// cast images, W_ih rows, the W_hh row image; the transposed W_hh image stays per element) --
+// per element, each with its integer divisions and a 2-byte store, the packing was ~6.4 of the
+// launch's 14.5 us at B = 32 (profiles/r6_adam_pack_probe.txt).  Same values as pack_store.
+__device__ __forceinline__ void pack_store4(const PackPlan& pl, const PackSeg& sg, int j0,
+                                            const f32x4& v) {
+  const int GP = 4 * pl.HD;
+  bf16x4 h;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) h[e] = (bf16)v[e];
+  const bool a8 = (((uintptr_t)sg.dst) & 7) == 0;
+  switch (sg.kind) {
+    case PK_CAST:
+      if (a8) {
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(sg.dst) + j0) = h;
+        return;
+      }
+      break;
+    case PK_WIH:
+      if (a8 && (pl.I & 3) == 0) {
+        const int row = j0 / pl.I, k = j0 - row * pl.I;
+        const int g = row / pl.Hd, u = row - g * pl.Hd;
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(sg.dst) +
+                                   (long)(sg.d * GP + 4 * u + g) * pl.I + k) = h;
+        return;
+      }
+      break;
+    case PK_WHH:
+      if (a8 && pl.HD <= 192 && (pl.Hd & 3) == 0 && (pl.HD & 3) == 0) {
+        const int row = j0 / pl.Hd, k = j0 - row * pl.Hd;
+        const int g = row / pl.Hd, u = row - g * pl.Hd, m = 4 * u + g;
+        const int base = sg.d * GP * pl.HD;
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(sg.dst) + base + m * pl.HD + k) = h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          reinterpret_cast<bf16*>(sg.dst2)[base + (k + e) * GP + m] = h[e];
+        return;
+      }
+      break;
+    default:
+      break;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) pack_store(pl, sg, j0 + e, v[e]);
+}
+
 // Per-step train-metric record of a device-fed epoch (runtime.feed.DeviceFeed): the step's score
 // column out[b][col] (ICA: prob[:, 1], reference comps/icalstm/__init__.py:64-65) and its loss
 // land in rings indexed by the batch cursor, so an epoch of K-step graph replays yields the exact
@@ -199,9 +246,13 @@ adam_pack_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
     if (s < pl.cnt && e0 >= pl.s[s].off) {
       const PackSeg& sg = pl.s[s];
       const int j0 = (int)(e0 - sg.off);
+      if (j0 + 4 <= sg.n) {
+        pack_store4(pl, sg, j0, pp);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (j0 + e < sg.n) pack_store(pl, sg, j0 + e, pp[e]);
+        for (int e = 0; e < 4; ++e)
+          if (j0 + e < sg.n) pack_store(pl, sg, j0 + e, pp[e]);
+      }
     }
   }
 }
